@@ -1,0 +1,126 @@
+"""ctypes binding of libf110.so (the C ABI in include/f110.h).
+
+Loads the in-tree library; there is no CPU fallback: if the library or a
+gfx950 device is missing, the calls fail loudly with the library's error.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from . import _build
+
+_P = ctypes.c_void_p
+_D = ctypes.POINTER(ctypes.c_double)
+
+
+class F110Params(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in
+                ("mu", "C_Sf", "C_Sr", "lf", "lr", "h", "m", "I", "s_min", "s_max", "sv_min", "sv_max",
+                 "v_switch", "a_max", "v_min", "v_max", "width", "length", "lidar_max")]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class F110Config(ctypes.Structure):
+    _fields_ = [("n_envs", ctypes.c_int32), ("n_agents", ctypes.c_int32), ("n_beams", ctypes.c_int32),
+                ("theta_dis", ctypes.c_int32), ("integrator", ctypes.c_int32), ("ego_idx", ctypes.c_int32),
+                ("autoreset", ctypes.c_int32), ("_pad", ctypes.c_int32), ("fov", ctypes.c_double),
+                ("eps", ctypes.c_double), ("max_range", ctypes.c_double), ("time_step", ctypes.c_double),
+                ("lidar_dist", ctypes.c_double), ("ttc_thresh", ctypes.c_double),
+                ("noise_std", ctypes.c_double), ("env_offset", ctypes.c_int64), ("seed", ctypes.c_uint64)]
+
+
+class F110Outputs(ctypes.Structure):
+    _fields_ = [("obs", _P), ("scans", _P), ("scans_f64", _P), ("collisions", _P), ("terminated", _P),
+                ("was_reset", _P), ("lap_times", _P), ("lap_counts", _P), ("sim_time", _P)]
+
+
+INTEGRATOR_RK4 = 1
+INTEGRATOR_EULER = 2
+
+EXPORTS = [
+    "f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config", "f110_edt_k",
+    "f110_create", "f110_destroy", "f110_reset", "f110_step", "f110_get_state", "f110_set_state",
+    "f110_scan_batch", "f110_dynamics_batch", "f110_read_counters", "f110_reset_counters",
+    "f110_host_tables", "f110_host_beam_indices",
+]
+
+_lib = None
+
+
+class F110Error(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def load(build_if_missing: bool = True):
+    """Load libf110.so (building it with hipcc if it is missing/stale)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = _build.LIB
+    if build_if_missing:
+        try:
+            _build.build()
+        except Exception as exc:  # pragma: no cover - toolchain missing
+            if not os.path.exists(path):
+                raise F110Error(f"libf110.so is missing and could not be built: {exc}") from exc
+    if not os.path.exists(path):
+        raise F110Error(f"libf110.so not found at {path}; run f110_gymnasium_ros2_jazzy_amd._build.build()")
+    try:  # share torch's HIP runtime (same SONAME) when torch is present
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    L = ctypes.CDLL(path)
+    i32, i64, u64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+    L.f110_abi_version.restype = ctypes.c_int
+    L.f110_last_error.restype = ctypes.c_char_p
+    L.f110_default_params.argtypes = [ctypes.POINTER(F110Params)]
+    L.f110_default_config.argtypes = [ctypes.POINTER(F110Config)]
+    L.f110_edt_k.argtypes = [_P, i32, i32, _P]
+    L.f110_create.argtypes = [ctypes.POINTER(_P), i32, ctypes.POINTER(F110Config), ctypes.POINTER(F110Params),
+                              _P, i32, i32, ctypes.c_double, _D, _P, i32]
+    L.f110_destroy.argtypes = [_P]
+    L.f110_reset.argtypes = [_P, _P, _P, ctypes.POINTER(F110Outputs), _P]
+    L.f110_step.argtypes = [_P, _P, ctypes.POINTER(F110Outputs), _P]
+    L.f110_get_state.argtypes = [_P, _P, _P, _P, _P]
+    L.f110_set_state.argtypes = [_P, _P, _P, _P, _P]
+    L.f110_scan_batch.argtypes = [_P, _P, i64, _P, _P, _P, _P]
+    L.f110_dynamics_batch.argtypes = [_P, _P, _P, _P, i64, _P]
+    L.f110_read_counters.argtypes = [_P, ctypes.POINTER(u64), ctypes.POINTER(u64), _P]
+    L.f110_reset_counters.argtypes = [_P, _P]
+    L.f110_host_tables.argtypes = [i32, i32, ctypes.c_double, ctypes.POINTER(F110Params), _P, _P, _P, _P, _P]
+    L.f110_host_beam_indices.argtypes = [ctypes.c_double, ctypes.c_double, i32, i32, _P]
+    L.f110_host_beam_indices.restype = ctypes.c_int
+    for name in EXPORTS:
+        if name not in ("f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config",
+                        "f110_host_tables"):
+            getattr(L, name).restype = ctypes.c_int
+    if L.f110_abi_version() != 1:
+        raise F110Error("libf110.so ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = "") -> int:
+    if rc < 0:
+        msg = load().f110_last_error()
+        raise F110Error(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+    return rc
+
+
+def default_params() -> F110Params:
+    p = F110Params()
+    load().f110_default_params(ctypes.byref(p))
+    return p
+
+
+def default_config() -> F110Config:
+    c = F110Config()
+    load().f110_default_config(ctypes.byref(c))
+    return c

@@ -1,0 +1,520 @@
+// f110_capi.cpp — host side of libf110.so: the C ABI declared in include/f110.h.
+//
+// Cold path (once per map): exact EDT (Felzenszwalb-Huttenlocher lower
+// envelopes, integer arithmetic), the reference's trig tables, device buffers.
+// Hot path: f110_step / f110_reset fill a StepArgs and enqueue ONE kernel
+// (k_env_step) on the caller's stream; no allocation, no synchronisation.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "f110_internal.h"
+
+using namespace f110;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail(F110_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+}  // namespace
+
+struct f110_ctx {
+    int device = 0;
+    f110_config cfg{};
+    f110_params p{};
+    int H = 0, W = 0;
+    double res = 0, origin[3] = {0, 0, 0};
+    double inc = 0, beam_incr = 0;
+    int n_spawn = 0;
+    // device buffers
+    double *dt = nullptr, *sines = nullptr, *cosines = nullptr, *angles = nullptr, *beam_cos = nullptr,
+           *side = nullptr, *spawn = nullptr;
+    double *st = nullptr, *sb = nullptr, *start = nullptr, *sim_time = nullptr;
+    int32_t *scnt = nullptr, *toggles = nullptr;
+    uint8_t *near_start = nullptr, *pending = nullptr;
+    float *lap_times = nullptr, *lap_counts = nullptr;
+    uint64_t *episode = nullptr, *nstep = nullptr;
+    unsigned long long *ctr = nullptr;
+    std::vector<void *> allocs;
+
+    template <class T>
+    hipError_t alloc(T **p, size_t n) {
+        void *q = nullptr;
+        hipError_t e = hipMalloc(&q, n * sizeof(T) > 0 ? n * sizeof(T) : 16);
+        if (e != hipSuccess) return e;
+        e = hipMemset(q, 0, n * sizeof(T) > 0 ? n * sizeof(T) : 16);
+        allocs.push_back(q);
+        *p = reinterpret_cast<T *>(q);
+        return e;
+    }
+};
+
+// ----------------------------------------------------------------- tables --
+// Host computation of the reference's lookup tables, exactly as NumPy does it
+// (each sin/cos called separately: glibc sincos() differs in the last bit).
+static double (*volatile g_sin)(double) = ::sin;  // volatile: keep sin/cos separate calls
+static double (*volatile g_cos)(double) = ::cos;
+
+extern "C" void f110_host_tables(int32_t theta_dis, int32_t n_beams, double fov, const f110_params *p, double *sines,
+                      double *cosines, double *angles, double *beam_cos, double *side) {
+    // ScanSimulator2D.__init__, laser_models.py:379-381: linspace(0, 2pi, theta_dis)
+    const double stop = 2.0 * kPi;
+    const double step = stop / (double)(theta_dis - 1);
+    for (int i = 0; i < theta_dis; ++i) {
+        double th = (i == theta_dis - 1) ? stop : (double)i * step;
+        if (sines) sines[i] = g_sin(th);
+        if (cosines) cosines[i] = g_cos(th);
+    }
+    // RaceCar.__init__, base_classes.py:122-158
+    const double incr = fov / (double)(n_beams - 1);
+    const double dist_sides = p->width / 2.;
+    const double dist_fr = (p->lf + p->lr) / 2.;
+    for (int i = 0; i < n_beams; ++i) {
+        double angle = -fov / 2. + (double)i * incr;
+        if (angles) angles[i] = angle;
+        if (beam_cos) beam_cos[i] = g_cos(angle);
+        double to_side, to_fr;
+        if (angle > 0) {
+            if (angle < kPi / 2) {
+                to_side = dist_sides / g_sin(angle);
+                to_fr = dist_fr / g_cos(angle);
+            } else {
+                to_side = dist_sides / g_cos(angle - kPi / 2.);
+                to_fr = dist_fr / g_sin(angle - kPi / 2.);
+            }
+        } else {
+            if (angle > -kPi / 2) {
+                to_side = dist_sides / g_sin(-angle);
+                to_fr = dist_fr / g_cos(-angle);
+            } else {
+                to_side = dist_sides / g_cos(-angle - kPi / 2);
+                to_fr = dist_fr / g_sin(-angle - kPi / 2);
+            }
+        }
+        if (side) side[i] = to_fr < to_side ? to_fr : to_side;  // Python min()
+    }
+}
+
+// Host evaluation of the beam-index runs (tests the run construction on CPU).
+extern "C" int f110_host_beam_indices(double yaw, double fov, int32_t theta_dis, int32_t n_beams,
+                                      double *theta_index_out) {
+    const double inc = (double)theta_dis * (fov / (double)(n_beams - 1)) / (2. * kPi);
+    BeamRun runs[kMaxSeg];
+    double t0 = first_theta_index(yaw, fov, theta_dis);
+    int n = build_beam_runs(t0, inc, theta_dis, n_beams, runs, kMaxSeg);
+    if (n < 0) return fail(F110_E_INVALID, "beam index runs exceed kMaxSeg");
+    for (int b = 0; b < n_beams; ++b) theta_index_out[b] = beam_theta_index(runs, n, b);
+    return n;
+}
+
+// ---------------------------------------------------------------- EDT ----
+// 1-D lower envelope of parabolas y = (x - q)^2 + f[q] over the finite sites,
+// compared as exact rationals (Felzenszwalb & Huttenlocher 2012).
+namespace {
+constexpr int64_t kInf = INT64_MAX / 4;
+
+void edt_1d(const int64_t *f, int n, int64_t *d, int *v, int64_t *zn, int64_t *zd) {
+    int k = -1;
+    for (int q = 0; q < n; ++q) {
+        if (f[q] >= kInf) continue;
+        while (k >= 0) {
+            int p = v[k];
+            // intersection of parabolas q and p: s = N / D
+            int64_t N = (f[q] + (int64_t)q * q) - (f[p] + (int64_t)p * p);
+            int64_t D = 2 * (int64_t)(q - p);
+            if (k == 0) break;
+            // drop p if s(q,p) <= z[k] = zn[k]/zd[k]
+            if ((__int128)N * zd[k] <= (__int128)zn[k] * D) {
+                --k;
+            } else {
+                break;
+            }
+        }
+        ++k;
+        v[k] = q;
+        if (k > 0) {
+            int p = v[k - 1];
+            zn[k] = (f[q] + (int64_t)q * q) - (f[p] + (int64_t)p * p);
+            zd[k] = 2 * (int64_t)(q - p);
+        }
+    }
+    if (k < 0) {
+        for (int x = 0; x < n; ++x) d[x] = kInf;
+        return;
+    }
+    int j = 0;
+    for (int x = 0; x < n; ++x) {
+        // advance while z[j+1] < x
+        while (j < k && (__int128)zn[j + 1] < (__int128)x * zd[j + 1]) ++j;
+        int64_t dx = x - v[j];
+        d[x] = dx * dx + f[v[j]];
+    }
+}
+}  // namespace
+
+extern "C" int f110_edt_k(const uint8_t *free_mask, int32_t H, int32_t W, uint32_t *k_out) {
+    if (!free_mask || !k_out || H <= 0 || W <= 0) return fail(F110_E_INVALID, "f110_edt_k: bad arguments");
+    const size_t N = (size_t)H * W;
+    std::vector<int64_t> g(N);
+    bool any = false;
+    // pass 1: squared distance along each column to the nearest occupied cell
+    std::vector<int64_t> col(H), out(H);
+    std::vector<int> v(H > W ? H : W);
+    std::vector<int64_t> zn((H > W ? H : W) + 1), zd((H > W ? H : W) + 1);
+    for (int c = 0; c < W; ++c) {
+        for (int r = 0; r < H; ++r) {
+            bool occ = free_mask[(size_t)r * W + c] == 0;
+            col[r] = occ ? 0 : kInf;
+            any = any || occ;
+        }
+        edt_1d(col.data(), H, out.data(), v.data(), zn.data(), zd.data());
+        for (int r = 0; r < H; ++r) g[(size_t)r * W + c] = out[r];
+    }
+    if (!any) return fail(F110_E_INVALID, "f110_edt_k: map has no occupied cell (EDT undefined)");
+    // pass 2: rows
+    std::vector<int64_t> row(W), rout(W);
+    for (int r = 0; r < H; ++r) {
+        for (int c = 0; c < W; ++c) row[c] = g[(size_t)r * W + c];
+        edt_1d(row.data(), W, rout.data(), v.data(), zn.data(), zd.data());
+        for (int c = 0; c < W; ++c) {
+            if (rout[c] > 0xFFFFFFFFll) return fail(F110_E_INVALID, "f110_edt_k: distance overflows uint32");
+            k_out[(size_t)r * W + c] = (uint32_t)rout[c];
+        }
+    }
+    return F110_OK;
+}
+
+// ---------------------------------------------------------------- misc ----
+extern "C" int f110_abi_version(void) { return F110_ABI_VERSION; }
+extern "C" const char *f110_last_error(void) { return g_err.c_str(); }
+
+extern "C" void f110_default_params(f110_params *p) {
+    // f110_env.py:132-156
+    p->mu = 1.0489;
+    p->C_Sf = 4.718;
+    p->C_Sr = 5.4562;
+    p->lf = 0.15875;
+    p->lr = 0.17145;
+    p->h = 0.074;
+    p->m = 3.74;
+    p->I = 0.04712;
+    p->s_min = -0.4189;
+    p->s_max = 0.4189;
+    p->sv_min = -3.2;
+    p->sv_max = 3.2;
+    p->v_switch = 7.319;
+    p->a_max = 9.51;
+    p->v_min = 0.00000001;
+    p->v_max = 20.0;
+    p->width = 0.31;
+    p->length = 0.58;
+    p->lidar_max = 30.0;
+}
+
+extern "C" void f110_default_config(f110_config *c) {
+    std::memset(c, 0, sizeof(*c));
+    c->n_envs = 1;
+    c->n_agents = 2;            // f110_env.py:159-162
+    c->n_beams = 1080;          // base_classes.py:69
+    c->theta_dis = 2000;        // laser_models.py:360
+    c->integrator = F110_INTEGRATOR_RK4;  // f110_env.py:176-179
+    c->ego_idx = 0;
+    c->autoreset = 0;
+    c->fov = 4.7;
+    c->eps = 0.0001;
+    c->max_range = 30.0;
+    c->time_step = 0.01;
+    c->lidar_dist = 0.0;
+    c->ttc_thresh = 0.005;
+    c->noise_std = 0.01;
+    c->env_offset = 0;
+    c->seed = 42;               // f110_env.py:110-113
+}
+
+static bool is_gfx950(int dev) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+static MapView map_view(const f110_ctx *c) {
+    MapView m;
+    m.dt = c->dt;
+    m.H = c->H;
+    m.W = c->W;
+    m.n = (int64_t)c->H * c->W;
+    m.res = c->res;
+    m.ox = c->origin[0];
+    m.oy = c->origin[1];
+    m.oc = std::cos(c->origin[2]);  // laser_models.py:421-422 (np.sin/np.cos of the yaml yaw)
+    m.os = std::sin(c->origin[2]);
+    m.wres = (double)c->W * c->res;
+    m.hres = (double)c->H * c->res;
+    return m;
+}
+
+static int use_device(const f110_ctx *c) {
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != c->device) HIP_TRY(hipSetDevice(c->device));
+    return F110_OK;
+}
+
+extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cfg, const f110_params *params,
+                           const uint32_t *edt_k, int32_t H, int32_t W, double resolution, const double origin[3],
+                           const double *spawn_poses, int32_t n_spawn) {
+    if (!out || !cfg || !params || !edt_k || !origin) return fail(F110_E_INVALID, "f110_create: null argument");
+    *out = nullptr;
+    const f110_config &C = *cfg;
+    if (C.n_envs <= 0 || C.n_agents <= 0 || C.n_agents > kMaxAgents)
+        return fail(F110_E_INVALID, "f110_create: n_envs must be > 0 and 1 <= n_agents <= 8");
+    if (C.n_beams < 2 || C.theta_dis < 2 || H <= 0 || W <= 0 || !(resolution > 0))
+        return fail(F110_E_INVALID, "f110_create: bad sensor/map dimensions");
+    if (!(C.fov > 0) || !(C.fov < 2 * kPi))
+        return fail(F110_E_INVALID, "f110_create: fov must be in (0, 2*pi) (one index wrap per scan)");
+    if (C.ego_idx < 0 || C.ego_idx >= C.n_agents) return fail(F110_E_INVALID, "f110_create: bad ego_idx");
+    if (C.integrator != F110_INTEGRATOR_RK4 && C.integrator != F110_INTEGRATOR_EULER)
+        return fail(F110_E_INVALID, "f110_create: Invalid Integrator Specified (base_classes.py:399)");
+    if (C.autoreset && (!spawn_poses || n_spawn <= 0))
+        return fail(F110_E_INVALID, "f110_create: autoreset needs a spawn pose table");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(F110_E_NODEVICE, "f110_create: no HIP device visible");
+    if (device < 0 || device >= ndev) return fail(F110_E_NODEVICE, "f110_create: device index out of range");
+    if (!is_gfx950(device)) return fail(F110_E_NODEVICE, "f110_create: device is not gfx950 (MI355X)");
+    HIP_TRY(hipSetDevice(device));
+
+    f110_ctx *c = new f110_ctx();
+    c->device = device;
+    c->cfg = C;
+    c->p = *params;
+    c->H = H;
+    c->W = W;
+    c->res = resolution;
+    for (int i = 0; i < 3; ++i) c->origin[i] = origin[i];
+    c->inc = (double)C.theta_dis * (C.fov / (double)(C.n_beams - 1)) / (2. * kPi);  // laser_models.py:367-368
+    c->beam_incr = C.fov / (double)(C.n_beams - 1);
+    c->n_spawn = n_spawn;
+    const size_t EA = (size_t)C.n_envs * C.n_agents;
+
+    auto cleanup = [&](int code, const std::string &msg) {
+        for (void *q : c->allocs) (void)hipFree(q);
+        delete c;
+        return fail(code, msg);
+    };
+#define ALLOC(ptr, n)                                                        \
+    do {                                                                     \
+        hipError_t e_ = c->alloc(&(ptr), (n));                               \
+        if (e_ != hipSuccess) return cleanup(F110_E_ALLOC, std::string("hipMalloc " #ptr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+    const size_t N = (size_t)H * W;
+    ALLOC(c->dt, N);
+    ALLOC(c->sines, (size_t)C.theta_dis);
+    ALLOC(c->cosines, (size_t)C.theta_dis);
+    ALLOC(c->angles, (size_t)C.n_beams);
+    ALLOC(c->beam_cos, (size_t)C.n_beams);
+    ALLOC(c->side, (size_t)C.n_beams);
+    ALLOC(c->st, 7 * EA);
+    ALLOC(c->sb, 2 * EA);
+    ALLOC(c->scnt, EA);
+    ALLOC(c->start, 3 * EA);
+    ALLOC(c->toggles, EA);
+    ALLOC(c->near_start, EA);
+    ALLOC(c->lap_times, EA);
+    ALLOC(c->lap_counts, EA);
+    ALLOC(c->sim_time, (size_t)C.n_envs);
+    ALLOC(c->pending, (size_t)C.n_envs);
+    ALLOC(c->episode, (size_t)C.n_envs);
+    ALLOC(c->nstep, (size_t)C.n_envs);
+    ALLOC(c->ctr, 2);
+    if (spawn_poses && n_spawn > 0) ALLOC(c->spawn, (size_t)n_spawn * C.n_agents * 3);
+#undef ALLOC
+
+    // dt = res * EDT (get_dt, laser_models.py:52) — bit-exact from the integer k.
+    std::vector<double> dt(N);
+    for (size_t i = 0; i < N; ++i) dt[i] = resolution * std::sqrt((double)edt_k[i]);
+    std::vector<double> s(C.theta_dis), co(C.theta_dis), an(C.n_beams), bc(C.n_beams), sd(C.n_beams);
+    f110_host_tables(C.theta_dis, C.n_beams, C.fov, params, s.data(), co.data(), an.data(), bc.data(), sd.data());
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipMemcpy(c->dt, dt.data(), N * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(c->sines, s.data(), s.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(c->cosines, co.data(), co.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(c->angles, an.data(), an.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(c->beam_cos, bc.data(), bc.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(c->side, sd.data(), sd.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess && c->spawn)
+        e = hipMemcpy(c->spawn, spawn_poses, (size_t)n_spawn * C.n_agents * 3 * sizeof(double),
+                      hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) return cleanup(F110_E_HIP, std::string("f110_create upload: ") + hipGetErrorString(e));
+    size_t lds = step_lds_bytes(C.n_agents, C.n_beams);
+    if (lds > 160 * 1024) return cleanup(F110_E_INVALID, "f110_create: n_agents*n_beams too large for LDS");
+    e = prepare_env_step(lds);
+    if (e != hipSuccess) return cleanup(F110_E_HIP, std::string("f110_create: LDS attribute: ") + hipGetErrorString(e));
+    *out = c;
+    return F110_OK;
+}
+
+extern "C" int f110_destroy(f110_ctx *ctx) {
+    if (!ctx) return F110_OK;
+    (void)hipSetDevice(ctx->device);
+    for (void *q : ctx->allocs) (void)hipFree(q);
+    delete ctx;
+    return F110_OK;
+}
+
+static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
+    StepArgs a{};
+    a.map = map_view(c);
+    a.sines = c->sines;
+    a.cosines = c->cosines;
+    a.angles = c->angles;
+    a.beam_cos = c->beam_cos;
+    a.side = c->side;
+    a.p = c->p;
+    a.E = c->cfg.n_envs;
+    a.A = c->cfg.n_agents;
+    a.B = c->cfg.n_beams;
+    a.theta_dis = c->cfg.theta_dis;
+    a.integrator = c->cfg.integrator;
+    a.ego = c->cfg.ego_idx;
+    a.autoreset = c->cfg.autoreset;
+    a.fov = c->cfg.fov;
+    a.eps = c->cfg.eps;
+    a.max_range = c->cfg.max_range;
+    a.dt = c->cfg.time_step;
+    a.lidar_dist = c->cfg.lidar_dist;
+    a.ttc_thresh = c->cfg.ttc_thresh;
+    a.noise_std = c->cfg.noise_std;
+    a.inc = c->inc;
+    a.beam_incr = c->beam_incr;
+    a.seed = c->cfg.seed;
+    a.env_offset = c->cfg.env_offset;
+    a.st = c->st;
+    a.sb = c->sb;
+    a.scnt = c->scnt;
+    a.start = c->start;
+    a.toggles = c->toggles;
+    a.near_start = c->near_start;
+    a.lap_times = c->lap_times;
+    a.lap_counts = c->lap_counts;
+    a.sim_time = c->sim_time;
+    a.pending = c->pending;
+    a.episode = c->episode;
+    a.nstep = c->nstep;
+    a.spawn = c->spawn;
+    a.n_spawn = c->n_spawn;
+    if (out) a.out = *out;
+    a.ctr = c->ctr;
+    return a;
+}
+
+extern "C" int f110_reset(f110_ctx *ctx, const double *poses, const uint8_t *env_mask, const f110_outputs *out,
+                          void *stream) {
+    if (!ctx || !poses) return fail(F110_E_INVALID, "f110_reset: null argument");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    StepArgs a = make_step_args(ctx, out);
+    a.mode = 1;
+    a.reset_poses = poses;
+    a.reset_mask = env_mask;
+    HIP_TRY(launch_env_step(a, (hipStream_t)stream));
+    return F110_OK;
+}
+
+extern "C" int f110_step(f110_ctx *ctx, const float *actions, const f110_outputs *out, void *stream) {
+    if (!ctx || !actions) return fail(F110_E_INVALID, "f110_step: null argument");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    StepArgs a = make_step_args(ctx, out);
+    a.mode = 0;
+    a.actions = actions;
+    HIP_TRY(launch_env_step(a, (hipStream_t)stream));
+    return F110_OK;
+}
+
+extern "C" int f110_get_state(f110_ctx *ctx, double *state, double *steer_buf, int32_t *steer_cnt, void *stream) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_get_state: null context");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    const size_t EA = (size_t)ctx->cfg.n_envs * ctx->cfg.n_agents;
+    hipStream_t s = (hipStream_t)stream;
+    if (state) HIP_TRY(hipMemcpyAsync(state, ctx->st, 7 * EA * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (steer_buf) HIP_TRY(hipMemcpyAsync(steer_buf, ctx->sb, 2 * EA * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (steer_cnt) HIP_TRY(hipMemcpyAsync(steer_cnt, ctx->scnt, EA * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    return F110_OK;
+}
+
+extern "C" int f110_set_state(f110_ctx *ctx, const double *state, const double *steer_buf, const int32_t *steer_cnt,
+                              void *stream) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_set_state: null context");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    const size_t EA = (size_t)ctx->cfg.n_envs * ctx->cfg.n_agents;
+    hipStream_t s = (hipStream_t)stream;
+    if (state) HIP_TRY(hipMemcpyAsync(ctx->st, state, 7 * EA * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (steer_buf) HIP_TRY(hipMemcpyAsync(ctx->sb, steer_buf, 2 * EA * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (steer_cnt) HIP_TRY(hipMemcpyAsync(ctx->scnt, steer_cnt, EA * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    return F110_OK;
+}
+
+extern "C" int f110_scan_batch(f110_ctx *ctx, const double *poses, int64_t M, double *scans, int32_t *lookups,
+                               int32_t *hit_rc, void *stream) {
+    if (!ctx || !poses || !scans || M < 0) return fail(F110_E_INVALID, "f110_scan_batch: bad arguments");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    ScanArgs a{};
+    a.map = map_view(ctx);
+    a.sines = ctx->sines;
+    a.cosines = ctx->cosines;
+    a.B = ctx->cfg.n_beams;
+    a.theta_dis = ctx->cfg.theta_dis;
+    a.fov = ctx->cfg.fov;
+    a.eps = ctx->cfg.eps;
+    a.max_range = ctx->cfg.max_range;
+    a.inc = ctx->inc;
+    a.poses = poses;
+    a.M = M;
+    a.scans = scans;
+    a.lookups = lookups;
+    a.hit_rc = hit_rc;
+    a.ctr = ctx->ctr;
+    HIP_TRY(launch_scan_batch(a, (hipStream_t)stream));
+    return F110_OK;
+}
+
+extern "C" int f110_dynamics_batch(f110_ctx *ctx, const double *x, const double *u, double *f, int64_t M,
+                                   void *stream) {
+    if (!ctx || !x || !u || !f || M < 0) return fail(F110_E_INVALID, "f110_dynamics_batch: bad arguments");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    HIP_TRY(launch_dynamics_batch(x, u, f, M, ctx->p, (hipStream_t)stream));
+    return F110_OK;
+}
+
+extern "C" int f110_read_counters(f110_ctx *ctx, uint64_t *lookups, uint64_t *rays, void *stream) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_read_counters: null context");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    unsigned long long h[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(h, ctx->ctr, sizeof(h), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    if (lookups) *lookups = h[0];
+    if (rays) *rays = h[1];
+    return F110_OK;
+}
+
+extern "C" int f110_reset_counters(f110_ctx *ctx, void *stream) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_reset_counters: null context");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    HIP_TRY(hipMemsetAsync(ctx->ctr, 0, 2 * sizeof(unsigned long long), (hipStream_t)stream));
+    return F110_OK;
+}

@@ -1,0 +1,494 @@
+// f110_device.h — device (and host/device) building blocks of the gfx950 step.
+//
+// Semantics restate the reference hot path term by term (paths relative to
+// f110_gymnasium/gym/f110_gym/envs/ of ahoop004/f110_gymnasium_ros2_jazzy).
+// Compiled with -ffp-contract=off: every a*b+c below rounds twice, exactly as
+// the Python/Numba source does.  Where the reference's NumPy calls reach BLAS
+// (ndarray.dot, np.linalg.norm) the rounding pattern of the reference run is
+// reproduced with explicit fma() (see DESIGN.md "Rounding contract").
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/f110.h"
+
+#define F110_HD __host__ __device__ __forceinline__
+#define F110_D __device__ __forceinline__
+
+namespace f110 {
+
+constexpr double kPi = 3.141592653589793;      // np.pi
+constexpr double kTwoPi = 6.283185307179586;   // 2 * np.pi
+constexpr double kHalfPi = 1.5707963267948966; // np.pi / 2
+constexpr double kSlipCap = 1.0471975511965976; // np.deg2rad(60)  (base_classes.py:414)
+constexpr double kYawRateCap = 10.0;           // base_classes.py:410
+constexpr double kG = 9.81;                    // dynamic_models.py:146
+constexpr int kMaxAgents = 8;
+constexpr int kMaxSeg = 80;
+
+// ----------------------------------------------------------------- scalars --
+F110_HD double clip(double a, double lo, double hi) {  // np.clip (NaN propagates)
+    if (a != a) return a;
+    return a < lo ? lo : (a > hi ? hi : a);
+}
+
+// Python / NumPy float remainder (npy_divmod): result takes the divisor's sign.
+F110_HD double pymod(double a, double b) {
+    double mod = fmod(a, b);
+    if (mod != 0.0) {
+        if ((b < 0) != (mod < 0)) mod += b;
+    } else {
+        mod = copysign(0.0, b);
+    }
+    return mod;
+}
+
+// F110Env._wrap_angle / update_pose yaw wrap: ((a + pi) % 2pi) - pi.
+F110_HD double wrap_angle(double a) { return pymod(a + kPi, kTwoPi) - kPi; }
+
+// ------------------------------------------------------------- dynamics --
+// accl_constraints, dynamic_models.py:29-60
+F110_HD double accl_constraints(double vel, double accl, double v_switch, double a_max, double v_min,
+                                double v_max) {
+    double pos_limit = vel > v_switch ? a_max * v_switch / vel : a_max;
+    if ((vel <= v_min && accl <= 0) || (vel >= v_max && accl >= 0))
+        accl = 0.;
+    else if (accl <= -a_max)
+        accl = -a_max;
+    else if (accl >= pos_limit)
+        accl = pos_limit;
+    return accl;
+}
+
+// steering_constraint, dynamic_models.py:62-87
+F110_HD double steering_constraint(double sa, double sv, double s_min, double s_max, double sv_min,
+                                   double sv_max) {
+    if ((sa <= s_min && sv <= 0) || (sa >= s_max && sv >= 0))
+        sv = 0.;
+    else if (sv <= sv_min)
+        sv = sv_min;
+    else if (sv >= sv_max)
+        sv = sv_max;
+    return sv;
+}
+
+// vehicle_dynamics_st, dynamic_models.py:123-176 (KS branch :152-160 via
+// vehicle_dynamics_ks :90-121).  Python's left-to-right order kept.
+F110_HD void vehicle_dynamics_st(const double x[7], double u0_in, double u1_in, const f110_params &p,
+                                 double f[7]) {
+    const double mu = p.mu, C_Sf = p.C_Sf, C_Sr = p.C_Sr, lf = p.lf, lr = p.lr, h = p.h, m = p.m, I = p.I;
+    double u0 = steering_constraint(x[2], u0_in, p.s_min, p.s_max, p.sv_min, p.sv_max);
+    double u1 = accl_constraints(x[3], u1_in, p.v_switch, p.a_max, p.v_min, p.v_max);
+    if (fabs(x[3]) < 0.5) {
+        double lwb = lf + lr;
+        // vehicle_dynamics_ks re-applies the (idempotent) constraints to u
+        double k0 = steering_constraint(x[2], u0, p.s_min, p.s_max, p.sv_min, p.sv_max);
+        double k1 = accl_constraints(x[3], u1, p.v_switch, p.a_max, p.v_min, p.v_max);
+        double tn = tan(x[2]);
+        double c2 = cos(x[2]);
+        f[0] = x[3] * cos(x[4]);
+        f[1] = x[3] * sin(x[4]);
+        f[2] = k0;
+        f[3] = k1;
+        f[4] = x[3] / lwb * tn;
+        f[5] = u1 / lwb * tn + x[3] / (lwb * (c2 * c2)) * u0;
+        f[6] = 0.0;
+    } else {
+        const double glr_m = kG * lr - u1 * h;
+        const double glf_p = kG * lf + u1 * h;
+        const double lrlf = lr + lf;
+        const double a = x[6] + x[4];
+        f[0] = x[3] * cos(a);
+        f[1] = x[3] * sin(a);
+        f[2] = u0;
+        f[3] = u1;
+        f[4] = x[5];
+        double t1 = -mu * m / (x[3] * I * lrlf) * (lf * lf * C_Sf * glr_m + lr * lr * C_Sr * glf_p) * x[5];
+        double t2 = mu * m / (I * lrlf) * (lr * C_Sr * glf_p - lf * C_Sf * glr_m) * x[6];
+        double t3 = mu * m / (I * lrlf) * lf * C_Sf * glr_m * x[2];
+        f[5] = t1 + t2 + t3;
+        double s1 = (mu / (x[3] * x[3] * lrlf) * (C_Sr * glf_p * lr - C_Sf * glr_m * lf) - 1) * x[5];
+        double s2 = mu / (x[3] * lrlf) * (C_Sr * glf_p + C_Sf * glr_m) * x[6];
+        double s3 = mu / (x[3] * lrlf) * (C_Sf * glr_m) * x[2];
+        f[6] = s1 - s2 + s3;
+    }
+}
+
+// pid, dynamic_models.py:178-221 (v_min = 1e-8 braking quirk included).
+F110_HD void pid(double speed, double steer, double cur_speed, double cur_steer, double max_sv, double max_a,
+                 double max_v, double min_v, double &accl, double &sv) {
+    double steer_diff = steer - cur_steer;
+    sv = fabs(steer_diff) > 1e-4 ? (steer_diff / fabs(steer_diff)) * max_sv : 0.0;
+    double vel_diff = speed - cur_speed;
+    double kp;
+    if (cur_speed > 0.)
+        kp = vel_diff > 0 ? 10.0 * max_a / max_v : 10.0 * max_a / (-min_v);
+    else
+        kp = vel_diff > 0 ? 2.0 * max_a / max_v : 2.0 * max_a / (-min_v);
+    accl = kp * vel_diff;
+}
+
+// RaceCar.update_pose without the scan, base_classes.py:256-417.
+// s[7] in/out; b0 = newest buffered steer, b1 = older; cnt = buffer fill.
+F110_HD void update_pose(double s[7], double &b0, double &b1, int &cnt, double raw_steer, double vel,
+                         const f110_params &p, double dt, int integrator) {
+    double steer;
+    if (cnt < 2) {  // :272-274
+        steer = 0.0;
+        b1 = b0;
+        b0 = raw_steer;
+        cnt += 1;
+    } else {        // :275-278
+        steer = b1;
+        b1 = b0;
+        b0 = raw_steer;
+    }
+    double accl, sv;
+    pid(vel, steer, s[3], s[2], p.sv_max, p.a_max, p.v_max, p.v_min, accl, sv);
+    sv = clip(sv, p.sv_min, p.sv_max);
+    accl = clip(accl, -p.a_max, p.a_max);
+    double ns[7];
+    if (integrator == F110_INTEGRATOR_RK4) {  // :285-374
+        double k1[7], k2[7], k3[7], k4[7], xs[7];
+        vehicle_dynamics_st(s, sv, accl, p, k1);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) xs[i] = s[i] + dt * (k1[i] / 2);
+        vehicle_dynamics_st(xs, sv, accl, p, k2);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) xs[i] = s[i] + dt * (k2[i] / 2);
+        vehicle_dynamics_st(xs, sv, accl, p, k3);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) xs[i] = s[i] + dt * k3[i];
+        vehicle_dynamics_st(xs, sv, accl, p, k4);
+        const double w = dt * (1.0 / 6.0);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) ns[i] = s[i] + w * (k1[i] + 2 * k2[i] + 2 * k3[i] + k4[i]);
+    } else {                                  // :376-396
+        double fe[7];
+        vehicle_dynamics_st(s, sv, accl, p, fe);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) ns[i] = s[i] + dt * fe[i];
+    }
+    ns[2] = clip(ns[2], p.s_min, p.s_max);   // :400-401
+    ns[3] = clip(ns[3], p.v_min, p.v_max);
+    ns[4] = wrap_angle(ns[4]);               // :408
+    double yr = ns[5];                       // :410-412
+    if (yr != yr) yr = 0.0;
+    else if (isinf(yr)) yr = yr > 0 ? kYawRateCap : -kYawRateCap;
+    ns[5] = clip(yr, -kYawRateCap, kYawRateCap);
+    double sl = ns[6];                       // :414-417
+    if (sl != sl) sl = 0.0;
+    ns[6] = clip(sl, -kSlipCap, kSlipCap);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) s[i] = ns[i];
+}
+
+// -------------------------------------------------------------- the map --
+struct MapView {
+    const double *dt;  // [H*W] metres (res * EDT), row-major
+    int32_t H, W;
+    int64_t n;         // H*W
+    double res, ox, oy, oc, os;
+    double wres, hres; // width*resolution, height*resolution (laser_models.py:79)
+};
+
+// xy_2_rc + distance_transform, laser_models.py:55-104: the linear EDT index
+// a lookup at (x, y) reads.  Out-of-map (r,c) = (-1,-1) reads dt[-1,-1].
+F110_HD int64_t cell_index(const MapView &m, double x, double y) {
+    double xt = x - m.ox;
+    double yt = y - m.oy;
+    double xr = xt * m.oc + yt * m.os;
+    double yr = -xt * m.os + yt * m.oc;
+    if (xr < 0 || xr >= m.wres || yr < 0 || yr >= m.hres || xr != xr || yr != yr) return m.n - 1;
+    int c = (int)(xr / m.res);
+    int r = (int)(yr / m.res);
+    int64_t lin = (int64_t)r * m.W + c;
+    return lin < m.n ? lin : m.n - 1;
+}
+
+// ------------------------------------------------------ beam index runs --
+// get_scan's beam index (laser_models.py:167-184) is a SEQUENTIAL float
+// accumulation t_{i+1} = wrap(fl(t_i + inc)).  Inside one binade [2^(e-1), 2^e)
+// every t_i is a multiple of u = ulp and fl(t_i + inc) = t_i + RN_u(inc), so the
+// sequence is an exact arithmetic progression until it leaves the binade or
+// wraps.  A run {start, count, t0, delta} holds t_{start+k} = t0 + k*delta
+// (exact in fp64).  Ties (inc exactly half-way on the u grid) round to even:
+// once t/u is even the increment is constant again, so an odd start is one
+// single step.  Bound for fov < 2*pi (one wrap): < 80 runs.
+struct BeamRun {
+    int32_t start, count;
+    double t0, delta;
+};
+
+F110_HD double first_theta_index(double yaw, double fov, int theta_dis) {
+    const double td = (double)theta_dis;
+    double t = td * (yaw - fov / 2.) / (2. * kPi);  // :167
+    t = fmod(t, td);                                // :170
+    while (t < 0) t += td;                          // :171-172
+    return t;
+}
+
+// Returns the number of runs written, or -1 if max_runs is too small.
+F110_HD int build_beam_runs(double t, double inc, int theta_dis, int B, BeamRun *runs, int max_runs) {
+    const double td = (double)theta_dis;
+    int i = 0, n = 0;
+    while (i < B) {
+        if (n >= max_runs) return -1;
+        int run = 1;
+        double delta = 0.0;
+        if (t >= 1.0 && t < td) {
+            int e;
+            frexp(t, &e);  // t in [2^(e-1), 2^e)
+            double lim = ldexp(1.0, e);
+            if (lim > td) lim = td;
+            double v = t + inc;
+            if (v < lim) {
+                delta = v - t;               // exact (same binade)
+                double rem = inc - delta;    // exact (|rem| <= u/2, u >= 2^-52)
+                double half_u = ldexp(1.0, e - 54);
+                bool tie = fabs(rem) == half_u;
+                bool even = fmod(ldexp(t, 52 - e), 1.0) == 0.0;  // t/u even
+                if (!tie || even) {
+                    int64_t span_u = (int64_t)ldexp(lim - t, 53 - e);
+                    int64_t d_u = (int64_t)ldexp(delta, 53 - e);
+                    int64_t kmax = (span_u - 1) / d_u;
+                    int64_t left = (int64_t)(B - i - 1);
+                    run = 1 + (int)(kmax < left ? kmax : left);
+                }
+            }
+        }
+        runs[n].start = i;
+        runs[n].count = run;
+        runs[n].t0 = t;
+        runs[n].delta = delta;
+        ++n;
+        double last = t + (double)(run - 1) * delta;
+        i += run;
+        t = last + inc;               // :180
+        while (t >= td) t -= td;      // :183-184
+    }
+    return n;
+}
+
+// theta index (as get_scan would have it) of beam b, given its runs.
+F110_HD double beam_theta_index(const BeamRun *runs, int n, int b) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {  // last run with start <= b
+        int mid = (lo + hi + 1) >> 1;
+        if (runs[mid].start <= b) lo = mid; else hi = mid - 1;
+    }
+    return runs[lo].t0 + (double)(b - runs[lo].start) * runs[lo].delta;
+}
+
+// ------------------------------------------------------------- geometry --
+F110_HD double dot2(double a0, double a1, double b0, double b1) {  // ndarray.dot of 2-vectors (BLAS)
+    return fma(a1, b1, a0 * b0);
+}
+
+// get_trmtx + get_vertices, collision_models.py:218-260 -> [rl, rr, fr, fl].
+F110_HD void get_vertices(double x, double y, double th, double length, double width, double v[8]) {
+    double c = cos(th), s = sin(th);
+    const double px[4] = {-length / 2, -length / 2, length / 2, length / 2};
+    const double py[4] = {width / 2, -width / 2, -width / 2, width / 2};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[2 * k] = c * px[k] + ((-s) * py[k] + x);
+        v[2 * k + 1] = s * px[k] + (c * py[k] + y);
+    }
+}
+
+// indexOfFurthestPoint + support, collision_models.py:81-110
+F110_HD void gjk_support(const double *v1, const double *v2, double d0, double d1, double &o0, double &o1) {
+    int i = 0, j = 0;
+    double b1 = 0, b2 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        double p1 = fma(v1[2 * k], d0, v1[2 * k + 1] * d1);
+        double p2 = fma(v2[2 * k], -d0, v2[2 * k + 1] * -d1);
+        if (k == 0 || p1 > b1) { b1 = p1; i = k; }
+        if (k == 0 || p2 > b2) { b2 = p2; j = k; }
+    }
+    o0 = v1[2 * i] - v2[2 * j];
+    o1 = v1[2 * i + 1] - v2[2 * j + 1];
+}
+
+F110_HD void triple(double a0, double a1, double b0, double b1, double c0, double c1, double &o0, double &o1) {
+    double ac = dot2(a0, a1, c0, c1), bc = dot2(b0, b1, c0, c1);  // tripleProduct :52-64
+    o0 = b0 * ac - a0 * bc;
+    o1 = b1 * ac - a1 * bc;
+}
+
+// collision (2-D GJK), collision_models.py:113-182
+F110_HD bool gjk_collision(const double *v1, const double *v2) {
+    double sx[3], sy[3];
+    int index = 0;
+    double p10 = (((v1[0] + v1[2]) + v1[4]) + v1[6]) / 4, p11 = (((v1[1] + v1[3]) + v1[5]) + v1[7]) / 4;
+    double p20 = (((v2[0] + v2[2]) + v2[4]) + v2[6]) / 4, p21 = (((v2[1] + v2[3]) + v2[5]) + v2[7]) / 4;
+    double d0 = p10 - p20, d1 = p11 - p21;
+    if (d0 == 0 && d1 == 0) d0 = 1.0;
+    double a0, a1;
+    gjk_support(v1, v2, d0, d1, a0, a1);
+    sx[0] = a0;
+    sy[0] = a1;
+    if (dot2(d0, d1, a0, a1) <= 0) return false;
+    d0 = -a0;
+    d1 = -a1;
+    int iter = 0;
+    while (iter < 1000) {
+        gjk_support(v1, v2, d0, d1, a0, a1);
+        ++index;
+        sx[index] = a0;
+        sy[index] = a1;
+        if (dot2(d0, d1, a0, a1) <= 0) return false;
+        double ao0 = -a0, ao1 = -a1;
+        if (index < 2) {
+            double ab0 = sx[0] - a0, ab1 = sy[0] - a1;
+            triple(ab0, ab1, ao0, ao1, ab0, ab1, d0, d1);
+            if (sqrt(fma(d1, d1, d0 * d0)) < 1e-10) {  // perpendicular(ab)
+                d0 = ab1;
+                d1 = -1 * ab0;
+            }
+            continue;
+        }
+        double ab0 = sx[1] - a0, ab1 = sy[1] - a1;
+        double ac0 = sx[0] - a0, ac1 = sy[0] - a1;
+        double q0, q1;
+        triple(ab0, ab1, ac0, ac1, ac0, ac1, q0, q1);  // acperp
+        if (dot2(q0, q1, ao0, ao1) >= 0) {
+            d0 = q0;
+            d1 = q1;
+        } else {
+            triple(ac0, ac1, ab0, ab1, ab0, ab1, q0, q1);  // abperp
+            if (dot2(q0, q1, ao0, ao1) < 0) return true;
+            sx[0] = sx[1];
+            sy[0] = sy[1];
+            d0 = q0;
+            d1 = q1;
+        }
+        sx[1] = sx[2];
+        sy[1] = sy[2];
+        --index;
+        ++iter;
+    }
+    return false;
+}
+
+// argmin_k |angles[k] - a| over the uniform beam grid angles[k] = -fov/2 + k*incr
+// (get_blocked_view_indices, laser_models.py:310-313).  The grid is strictly
+// increasing, so |angles[k]-a| is V-shaped: test the analytic guess +-2 with
+// NumPy's first-minimum tie break instead of a 1080-long scan.
+F110_HD int nearest_beam(const double *angles, int B, double fov, double incr, double a) {
+    if (a != a) return 0;  // np.argmin of an all-NaN array
+    double g = (a + fov / 2.0) / incr;
+    int k0 = g < 0 ? 0 : (g > (double)(B - 1) ? B - 1 : (int)(g + 0.5));
+    int lo = k0 - 2 < 0 ? 0 : k0 - 2;
+    int hi = k0 + 2 > B - 1 ? B - 1 : k0 + 2;
+    int best = lo;
+    double bd = fabs(angles[lo] - a);
+    for (int k = lo + 1; k <= hi; ++k) {
+        double d = fabs(angles[k] - a);
+        if (d < bd) { bd = d; best = k; }
+    }
+    return best;
+}
+
+// get_blocked_view_indices, laser_models.py:282-315
+F110_HD void blocked_range(double px, double py, double pth, const double v[8], const double *angles, int B,
+                           double fov, double incr, int &lo, int &hi) {
+    double ex = cos(pth), ey = sin(pth);
+    double ego = atan2(ey, ex);
+    int mn = 0, mx = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        double vx = v[2 * i] - px, vy = v[2 * i + 1] - py;
+        double nrm = sqrt(vx * vx + vy * vy);
+        double ux = vx / nrm, uy = vy / nrm;
+        double angle = ego - atan2(uy, ux);
+        if (angle > kPi) angle = angle - 2 * kPi;
+        else if (angle < -kPi) angle = angle + 2 * kPi;
+        int k = nearest_beam(angles, B, fov, incr, -angle);
+        if (i == 0 || k < mn) mn = k;
+        if (i == 0 || k > mx) mx = k;
+    }
+    lo = mn;
+    hi = mx;
+}
+
+// get_range, laser_models.py:249-280, with the beam's (cos, sin)(theta + pi/2)
+// hoisted out of the 4-edge loop (same values each call).
+F110_HD double get_range(double ox, double oy, double v30, double v31, double va0, double va1, double vb0,
+                         double vb1) {
+    double v10 = ox - va0, v11 = oy - va1;
+    double v20 = vb0 - va0, v21 = vb1 - va1;
+    double denom = dot2(v20, v21, v30, v31);
+    double distance = INFINITY;
+    if (fabs(denom) > 0.0) {
+        double d1 = (v20 * v11 - v21 * v10) / denom;
+        double d2 = dot2(v10, v11, v30, v31) / denom;
+        if (d1 >= 0.0 && d2 >= 0.0 && d2 <= 1.0) distance = d1;
+    } else {
+        double ba0 = va0 - ox, ba1 = va1 - oy;  // are_collinear(o, va, vb) :232-247
+        double ca0 = ox - vb0, ca1 = oy - vb1;
+        if (fabs(ba0 * ca1 - ba1 * ca0) < 1e-8) {
+            double e0 = va0 - ox, e1 = va1 - oy, f0 = vb0 - ox, f1 = vb1 - oy;
+            double da = sqrt(fma(e1, e1, e0 * e0));
+            double db = sqrt(fma(f1, f1, f0 * f0));
+            distance = da <= db ? da : db;
+        }
+    }
+    return distance;
+}
+
+// ----------------------------------------------------------------- noise --
+// Philox4x32-10 (Salmon et al., SC'11) keyed by (seed, global env id);
+// counter = (beam pair, steps since reset, stream tag).  Scan noise replaces
+// numpy default_rng(seed).normal(0, std, B) (laser_models.py:450-452): same
+// stream for every agent of an env and restarted at every reset
+// (base_classes.py:119,204), like the reference.
+struct U4 { uint32_t x, y, z, w; };
+
+F110_HD U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+        U4 n;
+        n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+        n.y = (uint32_t)p1;
+        n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+        n.w = (uint32_t)p0;
+        c = n;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+F110_HD double u01_open(uint32_t hi, uint32_t lo) {  // (0, 1], 53 bits
+    uint64_t v = ((uint64_t)(hi >> 5) << 26) | (uint64_t)(lo >> 6);
+    return ((double)v + 1.0) * (1.0 / 9007199254740992.0);
+}
+
+// N(0,1) for beam b of the env's stream at `step`: one Philox block per beam
+// pair, Box-Muller (cos branch for even beams, sin branch for odd beams).
+F110_HD double beam_normal(uint64_t seed, uint64_t env, uint64_t step, int b) {
+    U4 c = {(uint32_t)(b >> 1), (uint32_t)step, (uint32_t)(step >> 32), 0x5CA77u};
+    uint32_t k0 = (uint32_t)seed ^ (uint32_t)env;
+    uint32_t k1 = (uint32_t)(seed >> 32) ^ ((uint32_t)(env >> 32) * 0x85EBCA6Bu) ^ 0x3C6EF372u;
+    U4 r = philox(c, k0, k1);
+    double u1 = u01_open(r.x, r.y);
+    double u2 = u01_open(r.z, r.w);
+    double rad = sqrt(-2.0 * log(u1));
+    double ang = kTwoPi * u2;
+    return (b & 1) ? rad * sin(ang) : rad * cos(ang);
+}
+
+// uniform u32 for (seed, env, episode) — autoreset spawn choice.
+F110_HD uint32_t spawn_draw(uint64_t seed, uint64_t env, uint64_t episode) {
+    U4 c = {(uint32_t)episode, (uint32_t)(episode >> 32), 0x5BA3Eu, 0u};
+    U4 r = philox(c, (uint32_t)seed ^ (uint32_t)env, (uint32_t)(seed >> 32) ^ (uint32_t)(env >> 32) ^ 0xA5A5A5A5u);
+    return r.x;
+}
+
+}  // namespace f110

@@ -1,0 +1,188 @@
+/*
+ * f110.h — C ABI of libf110.so, the MI355X (gfx950) batched F1TENTH step.
+ *
+ * This is the drop-in boundary for the per-step hot path of f110_gym
+ * (ahoop004/f110_gymnasium_ros2_jazzy, paths below are relative to
+ * f110_gymnasium/gym/f110_gym/envs/).  The reference has no FFI: its hot path
+ * is a set of Numba @njit functions driven by the Python classes RaceCar /
+ * Simulator / F110Env.  Each entry point below names the reference interface
+ * it replaces.  INTEGRATION.md shows the ctypes binding the reference side
+ * would add.
+ *
+ * Conventions
+ *  - Plain C types only.  Every array argument of f110_reset / f110_step /
+ *    f110_*_batch is a DEVICE pointer owned by the caller (e.g. a
+ *    torch.Tensor's data_ptr()).  f110_edt_k and f110_create take HOST
+ *    pointers (cold path, once per map).
+ *  - Work is enqueued asynchronously on the hipStream_t passed as `stream`
+ *    (NULL = the default stream).  No call below synchronises the device or
+ *    allocates memory after f110_create.
+ *  - Return value: 0 on success, a negative F110_E* code on error;
+ *    f110_last_error() describes the last error of the calling thread.
+ *  - One context = one device, one map, one batch of n_envs x n_agents cars.
+ *    A context is not thread-safe; use one per host thread.  (The reference
+ *    shares a class-level ScanSimulator2D across every env in the process,
+ *    base_classes.py:64-67,118-120; contexts share nothing.)
+ *  - Layouts: agent index g = env * n_agents + agent.  State is kept on the
+ *    device as structure-of-arrays fp64: state[k * n_envs*n_agents + g],
+ *    k = 0..6 = [x, y, steer, v, yaw, yaw_rate, slip] (base_classes.py:97).
+ */
+#ifndef F110_H
+#define F110_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define F110_API __attribute__((visibility("default")))
+#else
+#define F110_API
+#endif
+
+#define F110_ABI_VERSION 1
+
+#define F110_OK 0
+#define F110_E_INVALID (-1)  /* bad argument / shape */
+#define F110_E_HIP (-2)      /* HIP runtime error */
+#define F110_E_NOMAP (-3)    /* ScanSimulator2D.scan without a map (laser_models.py:445-446) */
+#define F110_E_NODEVICE (-4) /* no gfx950 device */
+#define F110_E_ALLOC (-5)
+
+#define F110_INTEGRATOR_RK4 1   /* base_classes.py:40-42 */
+#define F110_INTEGRATOR_EULER 2
+
+/* Vehicle parameters: F110Env default params dict (f110_env.py:132-156). */
+typedef struct f110_params {
+    double mu, C_Sf, C_Sr, lf, lr, h, m, I;
+    double s_min, s_max, sv_min, sv_max, v_switch, a_max, v_min, v_max;
+    double width, length, lidar_max;
+} f110_params;
+
+/* Simulator / sensor configuration (F110Env.__init__ kwargs f110_env.py:104-186,
+ * RaceCar.__init__ base_classes.py:69-115, ScanSimulator2D.__init__
+ * laser_models.py:360-381). */
+typedef struct f110_config {
+    int32_t n_envs;      /* environments in this context (this rank's shard) */
+    int32_t n_agents;    /* cars per environment, 1..8 */
+    int32_t n_beams;     /* 1080 */
+    int32_t theta_dis;   /* 2000 */
+    int32_t integrator;  /* F110_INTEGRATOR_RK4 (F110Env default) */
+    int32_t ego_idx;     /* 0 */
+    int32_t autoreset;   /* 1: a terminated env is reset (spawn table) at its next f110_step */
+    int32_t _pad;
+    double fov;          /* 4.7 */
+    double eps;          /* 1e-4 */
+    double max_range;    /* 30.0 */
+    double time_step;    /* 0.01 */
+    double lidar_dist;   /* 0.0 */
+    double ttc_thresh;   /* 0.005 (base_classes.py:115) */
+    double noise_std;    /* 0.01 (laser_models.py:429); 0 disables scan noise */
+    int64_t env_offset;  /* global id of env 0 of this context (RNG keying across ranks) */
+    uint64_t seed;       /* scan-noise / autoreset seed (F110Env 'seed' kwarg) */
+} f110_config;
+
+/* Per-step outputs (all optional except where noted; NULL = not written). */
+typedef struct f110_outputs {
+    float *obs;          /* [n_envs][n_beams + 4*n_agents]: F110Env._pack_flat_obs
+                            (f110_env.py:552-584) generalised to A agents; A=2 -> 1088 */
+    float *scans;        /* [n_envs][n_agents][n_beams] f32 ranges (info["scans"], :599) */
+    double *scans_f64;   /* [n_envs][n_agents][n_beams] fp64 ranges (Simulator.step obs['scans']) */
+    uint8_t *collisions; /* [n_envs][n_agents] 0/1 (Simulator.collisions) */
+    uint8_t *terminated; /* [n_envs] F110Env._check_done (f110_env.py:310-352) */
+    uint8_t *was_reset;  /* [n_envs] 1 where this call reset the env (autoreset / f110_reset) */
+    float *lap_times;    /* [n_envs][n_agents] */
+    float *lap_counts;   /* [n_envs][n_agents] */
+    double *sim_time;    /* [n_envs] F110Env.current_time */
+} f110_outputs;
+
+typedef struct f110_ctx f110_ctx;
+
+/* ---- library ---------------------------------------------------------- */
+F110_API int f110_abi_version(void);
+F110_API const char *f110_last_error(void);
+/* Fills the F110Env defaults (f110_env.py:132-156, :159-186). */
+F110_API void f110_default_params(f110_params *p);
+F110_API void f110_default_config(f110_config *c);
+
+/* ---- map (cold path, host memory) -------------------------------------- */
+/* Exact squared EDT of an occupancy grid: k[r*W+c] = squared distance (in
+ * cells) from (r,c) to the nearest occupied cell (free_mask == 0).
+ * Replaces get_dt / scipy.ndimage.distance_transform_edt
+ * (laser_models.py:40-53, :425): dt = resolution * sqrt((double)k), bit-for-bit.
+ * free_mask is the image after ScanSimulator2D.set_map's flip + threshold
+ * (laser_models.py:397-404). */
+F110_API int f110_edt_k(const uint8_t *free_mask, int32_t H, int32_t W, uint32_t *k_out);
+
+/* ---- context ------------------------------------------------------------
+ * Replaces Simulator.__init__ + set_map (base_classes.py:478-524) and
+ * ScanSimulator2D.__init__/set_map (laser_models.py:360-427).  edt_k: HOST
+ * [H*W] from f110_edt_k.  origin = map yaml 'origin' (x, y, yaw).
+ * spawn_poses: optional HOST [n_spawn][n_agents][3] table used by autoreset. */
+F110_API int f110_create(f110_ctx **out, int32_t device, const f110_config *cfg, const f110_params *params,
+                const uint32_t *edt_k, int32_t H, int32_t W, double resolution, const double origin[3],
+                const double *spawn_poses, int32_t n_spawn);
+F110_API int f110_destroy(f110_ctx *ctx);
+
+/* ---- per step (device pointers, async on stream) ----------------------- */
+/* Replaces F110Env.reset (f110_env.py:425-472) = Simulator.reset
+ * (base_classes.py:627-643) + RaceCar.reset (:183-204) + the zero-action
+ * step the reference performs inside reset (f110_env.py:457-458).
+ * poses: [n_envs][n_agents][3] f64.  env_mask: [n_envs] u8, NULL = all envs.
+ * Only masked envs are touched; their outputs are written. */
+F110_API int f110_reset(f110_ctx *ctx, const double *poses, const uint8_t *env_mask, const f110_outputs *out,
+               void *stream);
+
+/* Replaces F110Env.step (f110_env.py:371-421) = Simulator.step
+ * (base_classes.py:566-625): per agent update_pose (steer delay, pid, RK4 of
+ * vehicle_dynamics_st, clamps) + ScanSimulator2D.scan (+ noise), GJK
+ * collision_multiple, TTC (check_ttc_jit), agent ray_cast, obs packing,
+ * _check_done.  actions: [n_envs][n_agents][2] f32 (steer, velocity). */
+F110_API int f110_step(f110_ctx *ctx, const float *actions, const f110_outputs *out, void *stream);
+
+/* ---- state access ------------------------------------------------------- */
+/* state: device [7][n_envs*n_agents] f64 (SoA, see header comment).
+ * steer_buf: device [2][n_envs*n_agents] f64 ([newest, older]); steer_cnt:
+ * device [n_envs*n_agents] i32 — RaceCar.steer_buffer (base_classes.py:108-109). */
+F110_API int f110_get_state(f110_ctx *ctx, double *state, double *steer_buf, int32_t *steer_cnt, void *stream);
+F110_API int f110_set_state(f110_ctx *ctx, const double *state, const double *steer_buf, const int32_t *steer_cnt,
+                   void *stream);
+
+/* ---- building blocks (device pointers) ----------------------------------
+ * Replaces ScanSimulator2D.scan with rng=None (laser_models.py:429-454) =
+ * get_scan/trace_ray (:106-186): poses [M][3] (x, y, yaw) -> scans [M][n_beams]
+ * f64.  lookups [M][n_beams] i32 and hit_rc [M][n_beams][2] i32 (last EDT cell
+ * read by each ray) are optional probes. */
+F110_API int f110_scan_batch(f110_ctx *ctx, const double *poses, int64_t M, double *scans, int32_t *lookups,
+                    int32_t *hit_rc, void *stream);
+
+/* Replaces vehicle_dynamics_st (dynamic_models.py:123-176) on M states:
+ * x [M][7], u [M][2] (steer velocity, acceleration) -> f [M][7]. */
+F110_API int f110_dynamics_batch(f110_ctx *ctx, const double *x, const double *u, double *f, int64_t M, void *stream);
+
+/* ---- counters -------------------------------------------------------------
+ * EDT lookups and rays traced by f110_step/f110_reset/f110_scan_batch since
+ * the last reset of the counters (device-side accumulation; reading syncs
+ * `stream`).  Used for the measured mean lookups per ray (roofline). */
+F110_API int f110_read_counters(f110_ctx *ctx, uint64_t *lookups, uint64_t *rays, void *stream);
+F110_API int f110_reset_counters(f110_ctx *ctx, void *stream);
+
+/* ---- host-side test hooks (no device work) -------------------------------
+ * The lookup tables f110_create uploads: ScanSimulator2D sines/cosines
+ * (laser_models.py:379-381) and RaceCar's class-level beam tables
+ * (base_classes.py:122-158).  Any pointer may be NULL. */
+F110_API void f110_host_tables(int32_t theta_dis, int32_t n_beams, double fov, const f110_params *p,
+                               double *sines, double *cosines, double *angles, double *beam_cos, double *side);
+/* get_scan's sequentially accumulated beam index (laser_models.py:167-184)
+ * for every beam at yaw, evaluated through the run decomposition the kernels
+ * use.  Returns the number of runs (>0) or a negative error. */
+F110_API int f110_host_beam_indices(double yaw, double fov, int32_t theta_dis, int32_t n_beams,
+                                    double *theta_index_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* F110_H */
