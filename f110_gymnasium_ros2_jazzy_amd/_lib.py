@@ -37,6 +37,8 @@ class F110Outputs(ctypes.Structure):
                 ("was_reset", _P), ("lap_times", _P), ("lap_counts", _P), ("sim_time", _P)]
 
 
+F32 = 0
+F64 = 1
 INTEGRATOR_RK4 = 1
 INTEGRATOR_EULER = 2
 
@@ -87,7 +89,7 @@ def load(build_if_missing: bool = True):
                               _P, i32, i32, ctypes.c_double, _D, _P, i32]
     L.f110_destroy.argtypes = [_P]
     L.f110_reset.argtypes = [_P, _P, _P, ctypes.POINTER(F110Outputs), _P]
-    L.f110_step.argtypes = [_P, _P, ctypes.POINTER(F110Outputs), _P]
+    L.f110_step.argtypes = [_P, _P, i32, ctypes.POINTER(F110Outputs), _P]
     L.f110_get_state.argtypes = [_P, _P, _P, _P, _P]
     L.f110_set_state.argtypes = [_P, _P, _P, _P, _P]
     L.f110_scan_batch.argtypes = [_P, _P, i64, _P, _P, _P, _P]

@@ -44,9 +44,12 @@ struct f110_ctx {
     // device buffers
     double *dt = nullptr, *sines = nullptr, *cosines = nullptr, *angles = nullptr, *beam_cos = nullptr,
            *side = nullptr, *spawn = nullptr;
-    double *st = nullptr, *sb = nullptr, *start = nullptr, *sim_time = nullptr;
+    double *st = nullptr, *sb = nullptr, *start = nullptr, *sim_time = nullptr, *ray0 = nullptr, *scan = nullptr;
+    BeamRun *runs = nullptr;
+    int32_t *nruns = nullptr;
+    uint64_t *noise_step = nullptr;
     int32_t *scnt = nullptr, *toggles = nullptr;
-    uint8_t *near_start = nullptr, *pending = nullptr;
+    uint8_t *near_start = nullptr, *pending = nullptr, *reset_flag = nullptr;
     float *lap_times = nullptr, *lap_counts = nullptr;
     uint64_t *episode = nullptr, *nstep = nullptr;
     unsigned long long *ctr = nullptr;
@@ -265,6 +268,7 @@ static MapView map_view(const f110_ctx *c) {
     m.os = std::sin(c->origin[2]);
     m.wres = (double)c->W * c->res;
     m.hres = (double)c->H * c->res;
+    m.inv_res = 1.0 / c->res;
     return m;
 }
 
@@ -332,6 +336,12 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     ALLOC(c->st, 7 * EA);
     ALLOC(c->sb, 2 * EA);
     ALLOC(c->scnt, EA);
+    ALLOC(c->ray0, 3 * EA);
+    ALLOC(c->runs, (size_t)kMaxSeg * EA);
+    ALLOC(c->nruns, EA);
+    ALLOC(c->scan, EA * (size_t)C.n_beams);
+    ALLOC(c->reset_flag, (size_t)C.n_envs);
+    ALLOC(c->noise_step, (size_t)C.n_envs);
     ALLOC(c->start, 3 * EA);
     ALLOC(c->toggles, EA);
     ALLOC(c->near_start, EA);
@@ -341,7 +351,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     ALLOC(c->pending, (size_t)C.n_envs);
     ALLOC(c->episode, (size_t)C.n_envs);
     ALLOC(c->nstep, (size_t)C.n_envs);
-    ALLOC(c->ctr, 2);
+    ALLOC(c->ctr, (size_t)kCtrSlots * kCtrStride);
     if (spawn_poses && n_spawn > 0) ALLOC(c->spawn, (size_t)n_spawn * C.n_agents * 3);
 #undef ALLOC
 
@@ -417,6 +427,12 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.pending = c->pending;
     a.episode = c->episode;
     a.nstep = c->nstep;
+    a.ray0 = c->ray0;
+    a.runs = c->runs;
+    a.nruns = c->nruns;
+    a.scan = c->scan;
+    a.reset_flag = c->reset_flag;
+    a.noise_step = c->noise_step;
     a.spawn = c->spawn;
     a.n_spawn = c->n_spawn;
     if (out) a.out = *out;
@@ -436,12 +452,18 @@ extern "C" int f110_reset(f110_ctx *ctx, const double *poses, const uint8_t *env
     return F110_OK;
 }
 
-extern "C" int f110_step(f110_ctx *ctx, const float *actions, const f110_outputs *out, void *stream) {
+extern "C" int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dtype, const f110_outputs *out,
+                         void *stream) {
     if (!ctx || !actions) return fail(F110_E_INVALID, "f110_step: null argument");
+    if (actions_dtype != F110_F32 && actions_dtype != F110_F64)
+        return fail(F110_E_INVALID, "f110_step: actions_dtype must be F110_F32 or F110_F64");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     StepArgs a = make_step_args(ctx, out);
     a.mode = 0;
-    a.actions = actions;
+    if (actions_dtype == F110_F64)
+        a.actions_f64 = static_cast<const double *>(actions);
+    else
+        a.actions = static_cast<const float *>(actions);
     HIP_TRY(launch_env_step(a, (hipStream_t)stream));
     return F110_OK;
 }
@@ -489,6 +511,8 @@ extern "C" int f110_scan_batch(f110_ctx *ctx, const double *poses, int64_t M, do
     a.lookups = lookups;
     a.hit_rc = hit_rc;
     a.ctr = ctx->ctr;
+    const char *v = std::getenv("F110_SCAN_VARIANT");
+    a.variant = v ? std::atoi(v) : 0;
     HIP_TRY(launch_scan_batch(a, (hipStream_t)stream));
     return F110_OK;
 }
@@ -504,17 +528,24 @@ extern "C" int f110_dynamics_batch(f110_ctx *ctx, const double *x, const double 
 extern "C" int f110_read_counters(f110_ctx *ctx, uint64_t *lookups, uint64_t *rays, void *stream) {
     if (!ctx) return fail(F110_E_INVALID, "f110_read_counters: null context");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
-    unsigned long long h[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(h, ctx->ctr, sizeof(h), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    std::vector<unsigned long long> h((size_t)kCtrSlots * kCtrStride);
+    HIP_TRY(hipMemcpyAsync(h.data(), ctx->ctr, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           (hipStream_t)stream));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    if (lookups) *lookups = h[0];
-    if (rays) *rays = h[1];
+    unsigned long long lk = 0, ry = 0;
+    for (int i = 0; i < kCtrSlots; ++i) {
+        lk += h[(size_t)i * kCtrStride];
+        ry += h[(size_t)i * kCtrStride + 1];
+    }
+    if (lookups) *lookups = lk;
+    if (rays) *rays = ry;
     return F110_OK;
 }
 
 extern "C" int f110_reset_counters(f110_ctx *ctx, void *stream) {
     if (!ctx) return fail(F110_E_INVALID, "f110_reset_counters: null context");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
-    HIP_TRY(hipMemsetAsync(ctx->ctr, 0, 2 * sizeof(unsigned long long), (hipStream_t)stream));
+    HIP_TRY(hipMemsetAsync(ctx->ctr, 0, (size_t)kCtrSlots * kCtrStride * sizeof(unsigned long long),
+                           (hipStream_t)stream));
     return F110_OK;
 }

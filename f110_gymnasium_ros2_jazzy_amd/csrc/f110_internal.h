@@ -9,6 +9,12 @@
 
 namespace f110 {
 
+// Lookup/ray counters are spread over kCtrSlots 128-B lines: ~10^5 waves
+// adding into ONE address serialise at the memory side (measured: 2.7 ms of
+// a 3.4 ms scan at 8192 envs); 256 slots make the adds contention-free.
+constexpr int kCtrSlots = 256;
+constexpr int kCtrStride = 16;  // u64 per slot (128 B)
+
 // Everything one launch of the fused env-step kernel needs, passed by value.
 struct StepArgs {
     MapView map;
@@ -32,14 +38,22 @@ struct StepArgs {
     uint8_t *pending;    // [E] autoreset pending
     uint64_t *episode;   // [E]
     uint64_t *nstep;     // [E] steps since reset (noise counter)
+    // k_agents -> k_rays -> k_post hand-off buffers (context scratch)
+    double *ray0;        // [3][E*A] scan pose x, y and first EDT lookup d0
+    BeamRun *runs;       // [E*A][kMaxSeg] beam-index runs
+    int32_t *nruns;      // [E*A]
+    double *scan;        // [E*A][B] ranges (noise added) before the collision stage
+    uint8_t *reset_flag; // [E] this call reset the env
+    uint64_t *noise_step;// [E] noise counter used by this step
     const double *spawn; // [n_spawn][A][3]
     int32_t n_spawn;
     // inputs
-    const float *actions;       // [E][A][2]
+    const float *actions;       // [E][A][2] f32, or
+    const double *actions_f64;  // [E][A][2] f64
     const double *reset_poses;  // [E][A][3]
     const uint8_t *reset_mask;  // [E] or null
     f110_outputs out;
-    unsigned long long *ctr;    // [2] lookups, rays
+    unsigned long long *ctr;    // [kCtrSlots][16]: [0] lookups, [1] rays (see count_rays)
 };
 
 struct ScanArgs {
@@ -53,6 +67,7 @@ struct ScanArgs {
     int32_t *lookups;     // [M][B] or null
     int32_t *hit_rc;      // [M][B][2] or null
     unsigned long long *ctr;
+    int32_t variant;      // A/B experiments (F110_SCAN_VARIANT): 0 default
 };
 
 size_t step_lds_bytes(int A, int B);

@@ -1,17 +1,22 @@
 // f110_kernels.hip — gfx950 kernels of the batched F1TENTH step.
 //
-//  k_env_step     one 256-thread workgroup (4 waves) per environment; the
-//                 whole Simulator.step + F110Env.step of that env in one
-//                 launch: dynamics -> 1080*A sphere-traced rays (scan held in
-//                 LDS) -> GJK -> TTC -> agent ray_cast -> obs pack / done.
-//  k_scan_batch   ScanSimulator2D.scan (rng=None) for M arbitrary poses.
-//  k_dynamics     vehicle_dynamics_st on M (x, u) pairs.
+// One f110_step = three launches on the caller's stream:
 //
-// The ray loop is latency bound (dependent gathers into the EDT, ~7 per ray):
-// each wave owns a contiguous pool of rays and every lane that finishes a ray
-// immediately takes the next one from the pool (ballot + popcount, no
-// atomics), so lanes stay busy until the pool drains instead of idling
-// behind the longest ray of a fixed 64-ray group.
+//  k_agents    one thread per car: reset/autoreset, RaceCar.update_pose
+//              (steer delay, pid, RK4 of vehicle_dynamics_st, clamps), scan
+//              pose, first EDT lookup, and the car's beam-index runs.
+//  k_rays      one thread per lidar ray (E*A*B threads): the EDT
+//              sphere-trace of ScanSimulator2D (trace_ray), + scan noise.
+//              This is the hot kernel: ~7 dependent fp64 gathers per ray.
+//              Kept minimal so it runs at the full 8 waves/SIMD; the
+//              hardware's wave scheduler does the load balancing of the
+//              ragged ray lengths (one ray per lane beat a per-wave ray pool
+//              with lane refill by 1.35x at 8192 envs).
+//  k_post      one 256-thread workgroup per env: scan -> LDS, TTC, GJK,
+//              agent ray_cast, obs packing, _check_done.
+//
+//  k_scan_batch / k_dynamics: the C-ABI building blocks (f110_scan_batch,
+//  f110_dynamics_batch).
 #include <hip/hip_runtime.h>
 
 #include "f110_internal.h"
@@ -19,31 +24,8 @@
 namespace f110 {
 
 constexpr int kBlock = 256;
-constexpr int kWaves = kBlock / 64;
 
-struct EnvShared {
-    double stl[kMaxAgents][7];   // state after update_pose (TTC may zero 3..6)
-    double spose[kMaxAgents][2]; // scan pose x, y (lidar offset applied)
-    double apose[kMaxAgents][3]; // agent_poses (x, y, yaw) before TTC (base_classes.py:587)
-    double verts[kMaxAgents][8]; // get_vertices(agent_poses)
-    double d0[kMaxAgents];       // EDT at the scan pose (first lookup of every ray)
-    int32_t nruns[kMaxAgents];
-    int32_t hit[kMaxAgents];     // TTC hit
-    int32_t col[kMaxAgents];     // collisions (GJK | TTC)
-    int32_t blo[kMaxAgents * kMaxAgents], bhi[kMaxAgents * kMaxAgents];
-    int32_t do_reset;
-    int32_t pad_;
-    uint64_t noise_step;
-};
-
-static_assert(sizeof(EnvShared) % 16 == 0, "LDS carve alignment");
 static_assert(sizeof(BeamRun) == 24, "BeamRun layout");
-
-size_t step_lds_bytes(int A, int B) {
-    size_t runs = sizeof(BeamRun) * (size_t)A * kMaxSeg;
-    runs = (runs + 15) & ~(size_t)15;
-    return sizeof(EnvShared) + runs + sizeof(double) * (size_t)A * B;
-}
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
@@ -51,79 +33,45 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-// Ray pool of one wave.  Ray id -> (agent a = id / B, beam b = id % B).
-// Fin(id, range, lookups) consumes each finished ray (range already clamped).
-template <class Fin>
-__device__ __forceinline__ uint32_t trace_pool(const MapView &m, const double *__restrict__ sines,
-                                               const double *__restrict__ cosines, int theta_dis, double eps,
-                                               double max_range, int B, int begin, int end,
-                                               const double (*spose)[2], const double *d0,
-                                               const BeamRun *runs, const int32_t *nruns, Fin fin) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    uint32_t look_total = 0;
-    int next = begin + 64;
-    int my = begin + lane;
-    bool act = my < end;
-    double x = 0, y = 0, c = 0, s = 0, d = 0, tot = 0;
-    uint32_t n = 0;
-    auto init = [&](int id) {
-        int a = id / B;
-        int b = id - a * B;
-        double t = beam_theta_index(runs + a * kMaxSeg, nruns[a], b);
-        int ti = (int)t;                 // int(theta_index), laser_models.py:124
-        if (ti >= theta_dis) ti = 0;
-        s = sines[ti];
-        c = cosines[ti];
-        x = spose[a][0];
-        y = spose[a][1];
-        d = d0[a];                       // :129
-        tot = d;                         // :130
-        n = 1;
-    };
-    if (act) init(my);
-    while (true) {
-        bool done = act && !(d > eps && tot <= max_range);   // :133
-        uint64_t dm = __ballot(done);
-        while (dm) {
-            if (done) {
-                look_total += n;
-                fin(my, tot > max_range ? max_range : tot, n);  // :143-144
-                my = next + __popcll(dm & lt);
-                act = my < end;
-                if (act) init(my);
-            }
-            next += __popcll(dm);
-            done = act && !(d > eps && tot <= max_range);
-            dm = __ballot(done);
-        }
-        if (!__ballot(act)) break;
-        if (act) {                        // :135-141
-            x += d * c;
-            y += d * s;
-            d = m.dt[cell_index(m, x, y)];
-            tot += d;
-            ++n;
-        }
+// One (lookups, rays) atomic pair per wave into a per-block slot.
+__device__ __forceinline__ void count_rays(unsigned long long *ctr, uint32_t n) {
+    uint32_t tot = wave_sum(n);
+    uint32_t cnt = wave_sum(n ? 1u : 0u);
+    if ((threadIdx.x & 63) == 0 && cnt) {
+        unsigned long long *slot = ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+        atomicAdd(slot, (unsigned long long)tot);
+        atomicAdd(slot + 1, (unsigned long long)cnt);
     }
-    return look_total;
+}
+
+// trace_ray, laser_models.py:106-146, from the shared first lookup d0 at the
+// scan pose.  Returns the clamped range; n = EDT lookups made.
+__device__ __forceinline__ double trace(const MapView &m, double x, double y, double c, double s, double d0,
+                                        double eps, double max_range, uint32_t &n) {
+    double d = d0;       // :129
+    double tot = d;      // :130
+    uint32_t k = 1;
+    while (d > eps && tot <= max_range) {  // :133
+        x += d * c;                        // :135
+        y += d * s;                        // :136
+        d = m.dt[cell_index_fast(m, x, y)];
+        tot += d;                          // :141
+        ++k;
+    }
+    n = k;
+    return tot > max_range ? max_range : tot;  // :143-144
 }
 
 // ------------------------------------------------------------------------
-__global__ void __launch_bounds__(kBlock) k_env_step(StepArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    EnvShared &sh = *reinterpret_cast<EnvShared *>(smem);
-    size_t runs_bytes = (sizeof(BeamRun) * (size_t)a.A * kMaxSeg + 15) & ~(size_t)15;
-    BeamRun *runs = reinterpret_cast<BeamRun *>(smem + sizeof(EnvShared));
-    double *scan = reinterpret_cast<double *>(smem + sizeof(EnvShared) + runs_bytes);
-
-    const int e = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int A = a.A, B = a.B;
-    const int EA = a.E * A;
+// k_agents: one thread per car.
+__global__ void __launch_bounds__(kBlock) k_agents(StepArgs a) {
+    const int g = blockIdx.x * kBlock + threadIdx.x;
+    const int EA = a.E * a.A;
+    if (g >= EA) return;
+    const int A = a.A;
+    const int e = g / A;
+    const int ag = g - e * A;
     const uint64_t genv = (uint64_t)(a.env_offset + e);
-
-    // ---- which envs run, and do they reset? (uniform per block) ----------
     int do_reset;
     if (a.mode == 1) {
         if (a.reset_mask && !a.reset_mask[e]) return;
@@ -131,110 +79,133 @@ __global__ void __launch_bounds__(kBlock) k_env_step(StepArgs a) {
     } else {
         do_reset = (a.autoreset && a.pending[e]) ? 1 : 0;
     }
-
-    // ---- phase A: one lane per agent: reset, update_pose, scan setup --------
-    if (tid < A) {
-        const int ag = tid;
-        const int g = e * A + ag;
-        double s[7];
-        double b0, b1;
-        int cnt;
-        double raw_steer, vel;
-        if (do_reset) {
-            // RaceCar.reset (base_classes.py:183-204) then F110Env.reset's zero step (f110_env.py:457)
-            const double *pz;
-            if (a.mode == 1) {
-                pz = a.reset_poses + ((size_t)e * A + ag) * 3;
-            } else {
-                uint64_t ep = a.episode[e];
-                uint32_t k = spawn_draw(a.seed, genv, ep) % (uint32_t)a.n_spawn;
-                pz = a.spawn + ((size_t)k * A + ag) * 3;
-            }
-#pragma unroll
-            for (int k = 0; k < 7; ++k) s[k] = 0.0;
-            s[0] = pz[0];
-            s[1] = pz[1];
-            s[4] = pz[2];
-            b0 = b1 = 0.0;
-            cnt = 0;
-            raw_steer = 0.0;
-            vel = 0.0;
-            a.start[g] = pz[0];
-            a.start[EA + g] = pz[1];
-            a.start[2 * EA + g] = pz[2];
-            a.toggles[g] = 0;
-            a.near_start[g] = 1;
-            a.lap_times[g] = 0.0f;
-            a.lap_counts[g] = 0.0f;
+    double s[7];
+    double b0, b1;
+    int cnt;
+    double raw_steer, vel;
+    if (do_reset) {
+        // RaceCar.reset (base_classes.py:183-204), then F110Env.reset's zero-action step (f110_env.py:457)
+        const double *pz;
+        if (a.mode == 1) {
+            pz = a.reset_poses + (size_t)g * 3;
         } else {
+            uint32_t k = spawn_draw(a.seed, genv, a.episode[e]) % (uint32_t)a.n_spawn;
+            pz = a.spawn + ((size_t)k * A + ag) * 3;
+        }
 #pragma unroll
-            for (int k = 0; k < 7; ++k) s[k] = a.st[(size_t)k * EA + g];
-            b0 = a.sb[g];
-            b1 = a.sb[EA + g];
-            cnt = a.scnt[g];
+        for (int k = 0; k < 7; ++k) s[k] = 0.0;
+        s[0] = pz[0];
+        s[1] = pz[1];
+        s[4] = pz[2];
+        b0 = b1 = 0.0;
+        cnt = 0;
+        raw_steer = 0.0;
+        vel = 0.0;
+        a.start[g] = pz[0];
+        a.start[EA + g] = pz[1];
+        a.start[2 * EA + g] = pz[2];
+        a.toggles[g] = 0;
+        a.near_start[g] = 1;
+        a.lap_times[g] = 0.0f;
+        a.lap_counts[g] = 0.0f;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) s[k] = a.st[(size_t)k * EA + g];
+        b0 = a.sb[g];
+        b1 = a.sb[EA + g];
+        cnt = a.scnt[g];
+        if (a.actions_f64) {
+            raw_steer = a.actions_f64[(size_t)g * 2];
+            vel = a.actions_f64[(size_t)g * 2 + 1];
+        } else {
             raw_steer = (double)a.actions[(size_t)g * 2];
             vel = (double)a.actions[(size_t)g * 2 + 1];
         }
-        update_pose(s, b0, b1, cnt, raw_steer, vel, a.p, a.dt, a.integrator);
+    }
+    update_pose(s, b0, b1, cnt, raw_steer, vel, a.p, a.dt, a.integrator);
 #pragma unroll
-        for (int k = 0; k < 7; ++k) {
-            a.st[(size_t)k * EA + g] = s[k];
-            sh.stl[ag][k] = s[k];
-        }
-        a.sb[g] = b0;
-        a.sb[EA + g] = b1;
-        a.scnt[g] = cnt;
-        double sx = s[0] + a.lidar_dist * cos(s[4]);  // base_classes.py:420-422
-        double sy = s[1] + a.lidar_dist * sin(s[4]);
-        sh.spose[ag][0] = sx;
-        sh.spose[ag][1] = sy;
-        sh.apose[ag][0] = s[0];
-        sh.apose[ag][1] = s[1];
-        sh.apose[ag][2] = s[4];
-        sh.d0[ag] = a.map.dt[cell_index(a.map, sx, sy)];
-        double t0 = first_theta_index(s[4], a.fov, a.theta_dis);
-        sh.nruns[ag] = build_beam_runs(t0, a.inc, a.theta_dis, B, runs + ag * kMaxSeg, kMaxSeg);
-        sh.hit[ag] = 0;
-        sh.col[ag] = 0;
+    for (int k = 0; k < 7; ++k) a.st[(size_t)k * EA + g] = s[k];
+    a.sb[g] = b0;
+    a.sb[EA + g] = b1;
+    a.scnt[g] = cnt;
+    // scan pose (base_classes.py:420-422) and everything every ray of this car shares
+    const double sx = s[0] + a.lidar_dist * cos(s[4]);
+    const double sy = s[1] + a.lidar_dist * sin(s[4]);
+    a.ray0[g] = sx;
+    a.ray0[EA + g] = sy;
+    a.ray0[2 * EA + g] = a.map.dt[cell_index(a.map, sx, sy)];  // first lookup (laser_models.py:129)
+    double t0 = first_theta_index(s[4], a.fov, a.theta_dis);
+    a.nruns[g] = build_beam_runs(t0, a.inc, a.theta_dis, a.B, a.runs + (size_t)g * kMaxSeg, kMaxSeg);
+    if (ag == 0) {
+        a.reset_flag[e] = (uint8_t)do_reset;
+        a.noise_step[e] = do_reset ? 0ull : a.nstep[e];
     }
-    if (tid == 0) {
-        sh.do_reset = do_reset;
-        sh.noise_step = do_reset ? 0ull : a.nstep[e];
-    }
-    __syncthreads();
+}
 
-    // ---- phase B: A*B rays, per-wave pools with lane refill ----------------
-    {
-        const int R = A * B;
-        const int wave = tid >> 6;
-        const int chunk = (R + kWaves - 1) / kWaves;
-        const int begin = wave * chunk;
-        const int end = min(R, begin + chunk);
-        const double nstd = a.noise_std;
-        const uint64_t nstep = sh.noise_step;
-        const uint64_t seed = a.seed;
-        uint32_t looks = trace_pool(
-            a.map, a.sines, a.cosines, a.theta_dis, a.eps, a.max_range, B, begin, end, sh.spose, sh.d0, runs,
-            sh.nruns, [&](int id, double range, uint32_t) {
-                if (nstd > 0.0) {  // ScanSimulator2D.scan noise, added after the clamp (laser_models.py:450-452)
-                    int b = id % B;
-                    range += nstd * beam_normal(seed, genv, nstep, b);
-                }
-                scan[id] = range;
-            });
-        uint32_t tot = wave_sum(looks);
-        if ((tid & 63) == 0 && a.ctr) {
-            atomicAdd(a.ctr, (unsigned long long)tot);
-            atomicAdd(a.ctr + 1, (unsigned long long)(end > begin ? end - begin : 0));
+// ------------------------------------------------------------------------
+// k_rays: one thread per ray; ray r -> car g = r / B, beam b = r % B.
+__global__ void __launch_bounds__(kBlock) k_rays(StepArgs a) {
+    const int EA = a.E * a.A;
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int B = a.B;
+    uint32_t n = 0;
+    if (r < (int64_t)EA * B) {
+        const int g = (int)(r / B);
+        const int b = (int)(r - (int64_t)g * B);
+        const int e = g / a.A;
+        if (!(a.mode == 1 && a.reset_mask && !a.reset_mask[e])) {
+            double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
+            int ti = (int)t;  // int(theta_index), laser_models.py:124
+            if (ti >= a.theta_dis) ti = 0;
+            double range = trace(a.map, a.ray0[g], a.ray0[EA + g], a.cosines[ti], a.sines[ti], a.ray0[2 * EA + g],
+                                 a.eps, a.max_range, n);
+            if (a.noise_std > 0.0)  // ScanSimulator2D.scan: noise after the clamp (laser_models.py:450-452)
+                range += a.noise_std * (double)beam_normal(a.seed, (uint64_t)(a.env_offset + e), a.noise_step[e], b);
+            a.scan[r] = range;
         }
     }
-    __syncthreads();
+    if (a.ctr) count_rays(a.ctr, n);
+}
 
-    // ---- phase C1: GJK between agents (check_collision, base_classes.py:549-563) --
+// ------------------------------------------------------------------------
+struct PostShared {
+    double stl[kMaxAgents][7];   // state after update_pose (TTC may zero 3..6)
+    double verts[kMaxAgents][8]; // get_vertices(agent_poses) (base_classes.py:562, :223)
+    int32_t hit[kMaxAgents];     // TTC hit
+    int32_t col[kMaxAgents];     // collisions (GJK | TTC)
+    int32_t blo[kMaxAgents * kMaxAgents], bhi[kMaxAgents * kMaxAgents];
+    int32_t do_reset, pad_[3];
+};
+static_assert(sizeof(PostShared) % 16 == 0, "LDS carve alignment");
+
+size_t post_lds_bytes(int A, int B) { return sizeof(PostShared) + sizeof(double) * (size_t)A * B; }
+
+// k_post: one workgroup per env: Simulator.step's collision stage + F110Env's epilogue.
+__global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    PostShared &sh = *reinterpret_cast<PostShared *>(smem);
+    double *scan = reinterpret_cast<double *>(smem + sizeof(PostShared));
+    const int e = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int A = a.A, B = a.B;
+    const int EA = a.E * A;
+    if (a.mode == 1 && a.reset_mask && !a.reset_mask[e]) return;  // uniform per block
+
+    const double *gscan = a.scan + (size_t)e * A * B;
+    for (int id = tid; id < A * B; id += kBlock) scan[id] = gscan[id];
     if (tid < A) {
-        get_vertices(sh.apose[tid][0], sh.apose[tid][1], sh.apose[tid][2], a.p.length, a.p.width, sh.verts[tid]);
+        const int g = e * A + tid;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) sh.stl[tid][k] = a.st[(size_t)k * EA + g];
+        // agent_poses (x, y, yaw) are taken before the TTC response (base_classes.py:587)
+        get_vertices(sh.stl[tid][0], sh.stl[tid][1], sh.stl[tid][4], a.p.length, a.p.width, sh.verts[tid]);
+        sh.hit[tid] = 0;
+        sh.col[tid] = 0;
     }
-    // ---- phase C2: TTC against the environment (check_ttc_jit, laser_models.py:188-217)
+    if (tid == 0) sh.do_reset = a.reset_flag[e];
+    __syncthreads();
+
+    // TTC against the environment (check_ttc_jit, laser_models.py:188-217) on the noisy scan
     for (int id = tid; id < A * B; id += kBlock) {
         int ag = id / B;
         int b = id - ag * B;
@@ -245,9 +216,8 @@ __global__ void __launch_bounds__(kBlock) k_env_step(StepArgs a) {
             if (ttc < a.ttc_thresh && ttc >= 0.0) sh.hit[ag] = 1;
         }
     }
-    __syncthreads();
-    if (tid == 0) {
-        for (int i = 0; i < A - 1; ++i)  // collision_multiple, collision_models.py:184-212
+    if (tid == 0) {  // collision_multiple (collision_models.py:184-212) on pre-TTC poses
+        for (int i = 0; i < A - 1; ++i)
             for (int j = i + 1; j < A; ++j)
                 if (gjk_collision(sh.verts[i], sh.verts[j])) {
                     sh.col[i] = 1;
@@ -255,20 +225,17 @@ __global__ void __launch_bounds__(kBlock) k_env_step(StepArgs a) {
                 }
     }
     __syncthreads();
-    // ---- phase C3: collision response, blocked beam ranges -------------------
-    if (tid < A) {
+    if (tid < A && sh.hit[tid]) {  // RaceCar.check_ttc (base_classes.py:246-249): state[3:] = 0
         const int g = e * A + tid;
-        if (sh.hit[tid]) {  // RaceCar.check_ttc, base_classes.py:246-249: state[3:] = 0
 #pragma unroll
-            for (int k = 3; k < 7; ++k) {
-                sh.stl[tid][k] = 0.0;
-                a.st[(size_t)k * EA + g] = 0.0;
-            }
-            sh.col[tid] = 1;  // Simulator.step :601-602
+        for (int k = 3; k < 7; ++k) {
+            sh.stl[tid][k] = 0.0;
+            a.st[(size_t)k * EA + g] = 0.0;
         }
+        sh.col[tid] = 1;  // Simulator.step :601-602
     }
     __syncthreads();
-    if (tid < A * (A - 1)) {  // pair (i, jj-th opponent) -> get_blocked_view_indices
+    if (tid < A * (A - 1)) {  // pair (i, jj-th opponent) -> get_blocked_view_indices on i's post-TTC pose
         int i = tid / (A - 1);
         int jj = tid - i * (A - 1);
         int j = jj < i ? jj : jj + 1;
@@ -279,7 +246,7 @@ __global__ void __launch_bounds__(kBlock) k_env_step(StepArgs a) {
         sh.bhi[tid] = hi;
     }
     __syncthreads();
-    // ---- phase C4: agent ray_cast (RaceCar.ray_cast_agents, base_classes.py:206-227)
+    // agent ray_cast (RaceCar.ray_cast_agents, base_classes.py:206-227; ray_cast, laser_models.py:318-346)
     for (int jj = 0; jj < A - 1; ++jj) {
         for (int i = 0; i < A; ++i) {
             int j = jj < i ? jj : jj + 1;
@@ -294,8 +261,8 @@ __global__ void __launch_bounds__(kBlock) k_env_step(StepArgs a) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     int q1 = (q + 1) & 3;
-                    double r = get_range(ox, oy, v30, v31, v[2 * q], v[2 * q + 1], v[2 * q1], v[2 * q1 + 1]);
-                    if (r < cur) cur = r;
+                    double rr = get_range(ox, oy, v30, v31, v[2 * q], v[2 * q + 1], v[2 * q1], v[2 * q1 + 1]);
+                    if (rr < cur) cur = rr;
                 }
                 scan[i * B + b] = cur;
             }
@@ -303,9 +270,9 @@ __global__ void __launch_bounds__(kBlock) k_env_step(StepArgs a) {
         __syncthreads();
     }
 
-    // ---- phase D: outputs ---------------------------------------------------
+    // ---- outputs --------------------------------------------------------
     const int obs_len = B + 4 * A;
-    if (a.out.obs) {  // F110Env._pack_flat_obs, f110_env.py:552-584 (scan of agent 0)
+    if (a.out.obs) {  // F110Env._pack_flat_obs, f110_env.py:552-584 (scan of agent 0, e = 0)
         float *o = a.out.obs + (size_t)e * obs_len;
         const float lmax = (float)a.p.lidar_max;
         for (int b = tid; b < B; b += kBlock) {
@@ -330,6 +297,7 @@ __global__ void __launch_bounds__(kBlock) k_env_step(StepArgs a) {
         double *o = a.out.scans_f64 + (size_t)e * A * B;
         for (int id = tid; id < A * B; id += kBlock) o[id] = scan[id];
     }
+    if (a.out.collisions && tid < A) a.out.collisions[(size_t)e * A + tid] = (uint8_t)sh.col[tid];
     if (tid == 0) {
         // F110Env.step time + _check_done (f110_env.py:404-406, :310-352)
         double tnow = (sh.do_reset ? 0.0 : a.sim_time[e]) + a.dt;
@@ -368,115 +336,86 @@ __global__ void __launch_bounds__(kBlock) k_env_step(StepArgs a) {
         if (a.out.sim_time) a.out.sim_time[e] = tnow;
         a.pending[e] = (a.autoreset && term) ? 1 : 0;
         if (sh.do_reset && a.mode == 0) a.episode[e] += 1;
-        a.nstep[e] = sh.noise_step + 1;
+        a.nstep[e] = a.noise_step[e] + 1;
     }
-    if (a.out.collisions && tid < A) a.out.collisions[(size_t)e * A + tid] = (uint8_t)sh.col[tid];
 }
 
 hipError_t prepare_env_step(size_t lds_bytes) {
     if (lds_bytes <= 64 * 1024) return hipSuccess;
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(&k_env_step),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(&k_post), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds_bytes);
 }
 
+size_t step_lds_bytes(int A, int B) { return post_lds_bytes(A, B); }
+
 hipError_t launch_env_step(const StepArgs &a, hipStream_t s) {
-    size_t lds = step_lds_bytes(a.A, a.B);
-    hipLaunchKernelGGL(k_env_step, dim3(a.E), dim3(kBlock), lds, s, a);
+    const int EA = a.E * a.A;
+    hipLaunchKernelGGL(k_agents, dim3((EA + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int64_t R = (int64_t)EA * a.B;
+    hipLaunchKernelGGL(k_rays, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_post, dim3(a.E), dim3(kBlock), post_lds_bytes(a.A, a.B), s, a);
     return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------
-struct ScanShared {
-    double spose[1][2];
-    double d0[1];
-    int32_t nruns[1];
-    int32_t pad_;
-};
-
+// ScanSimulator2D.scan with rng=None for M poses: one thread per ray, beam
+// runs rebuilt per thread (cheap: < 20 runs), optional probes.
+template <int V>
 __global__ void __launch_bounds__(kBlock) k_scan_batch(ScanArgs a) {
-    __shared__ ScanShared sh;
-    __shared__ BeamRun runs[kMaxSeg];
-    const int64_t m = blockIdx.x;
-    const int tid = threadIdx.x;
-    const double *pose = a.poses + 3 * m;
-    if (tid == 0) {
-        sh.spose[0][0] = pose[0];
-        sh.spose[0][1] = pose[1];
-        sh.d0[0] = a.map.dt[cell_index(a.map, pose[0], pose[1])];
-        double t0 = first_theta_index(pose[2], a.fov, a.theta_dis);
-        sh.nruns[0] = build_beam_runs(t0, a.inc, a.theta_dis, a.B, runs, kMaxSeg);
-    }
-    __syncthreads();
-    const int B = a.B;
-    const int wave = tid >> 6;
-    const int chunk = (B + kWaves - 1) / kWaves;
-    const int begin = wave * chunk;
-    const int end = min(B, begin + chunk);
-    double *out = a.scans + m * B;
-    int32_t *lk = a.lookups ? a.lookups + m * B : nullptr;
-    uint32_t looks = trace_pool(a.map, a.sines, a.cosines, a.theta_dis, a.eps, a.max_range, B, begin, end, sh.spose,
-                                sh.d0, runs, sh.nruns, [&](int id, double range, uint32_t n) {
-                                    out[id] = range;
-                                    if (lk) lk[id] = (int32_t)n;
-                                });
-    uint32_t tot = wave_sum(looks);
-    if ((tid & 63) == 0 && a.ctr) {
-        atomicAdd(a.ctr, (unsigned long long)tot);
-        atomicAdd(a.ctr + 1, (unsigned long long)(end > begin ? end - begin : 0));
-    }
-}
-
-// Probe variant for hit cells: one thread per ray, plain loop (tests only).
-__global__ void __launch_bounds__(kBlock) k_scan_probe(ScanArgs a) {
     const int64_t gid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (gid >= a.M * a.B) return;
-    const int64_t m = gid / a.B;
-    const int b = (int)(gid - m * a.B);
-    const double *pose = a.poses + 3 * m;
-    BeamRun runs[kMaxSeg];
-    double t0 = first_theta_index(pose[2], a.fov, a.theta_dis);
-    int nr = build_beam_runs(t0, a.inc, a.theta_dis, a.B, runs, kMaxSeg);
-    double t = beam_theta_index(runs, nr, b);
-    int ti = (int)t;
-    if (ti >= a.theta_dis) ti = 0;
-    double s = a.sines[ti], c = a.cosines[ti];
-    double x = pose[0], y = pose[1];
-    int64_t cell = cell_index(a.map, x, y);
-    double d = a.map.dt[cell];
-    double tot = d;
-    int n = 1;
-    while (d > a.eps && tot <= a.max_range) {
-        x += d * c;
-        y += d * s;
-        cell = cell_index(a.map, x, y);
-        d = a.map.dt[cell];
-        tot += d;
-        ++n;
+    uint32_t n = 0;
+    if (gid < a.M * a.B) {
+        const int64_t m = gid / a.B;
+        const int b = (int)(gid - m * a.B);
+        const double *pose = a.poses + 3 * m;
+        BeamRun runs[kMaxSeg];
+        double t0 = first_theta_index(pose[2], a.fov, a.theta_dis);
+        int nr = build_beam_runs(t0, a.inc, a.theta_dis, a.B, runs, kMaxSeg);
+        double t = beam_theta_index(runs, nr, b);
+        int ti = (int)t;
+        if (ti >= a.theta_dis) ti = 0;
+        double s = a.sines[ti], c = a.cosines[ti];
+        double x = pose[0], y = pose[1];
+        double d = a.map.dt[cell_index(a.map, x, y)];
+        double tot = d;
+        n = 1;
+        while (d > a.eps && tot <= a.max_range) {
+            x += d * c;
+            y += d * s;
+            d = a.map.dt[V == 1 ? cell_index(a.map, x, y) : cell_index_fast(a.map, x, y)];
+            tot += d;
+            ++n;
+        }
+        if (tot > a.max_range) tot = a.max_range;
+        a.scans[gid] = tot;
+        if (a.lookups) a.lookups[gid] = (int32_t)n;
+        if (a.hit_rc) {  // (r, c) of the last lookup; out-of-map reads report (-1, -1)
+            double xt = x - a.map.ox, yt = y - a.map.oy;
+            double xr = xt * a.map.oc + yt * a.map.os;
+            double yr = -xt * a.map.os + yt * a.map.oc;
+            int rr = -1, cc = -1;
+            if (!(xr < 0 || xr >= a.map.wres || yr < 0 || yr >= a.map.hres || xr != xr || yr != yr)) {
+                cc = (int)(xr / a.map.res);
+                rr = (int)(yr / a.map.res);
+            }
+            a.hit_rc[2 * gid] = rr;
+            a.hit_rc[2 * gid + 1] = cc;
+        }
     }
-    if (tot > a.max_range) tot = a.max_range;
-    if (a.scans) a.scans[gid] = tot;
-    if (a.lookups) a.lookups[gid] = n;
-    // recover (r, c) of the last lookup; out-of-map reads report (-1, -1)
-    double xt = x - a.map.ox, yt = y - a.map.oy;
-    double xr = xt * a.map.oc + yt * a.map.os;
-    double yr = -xt * a.map.os + yt * a.map.oc;
-    int r = -1, cc = -1;
-    if (!(xr < 0 || xr >= a.map.wres || yr < 0 || yr >= a.map.hres || xr != xr || yr != yr)) {
-        cc = (int)(xr / a.map.res);
-        r = (int)(yr / a.map.res);
-    }
-    a.hit_rc[2 * gid] = r;
-    a.hit_rc[2 * gid + 1] = cc;
+    if (a.ctr) count_rays(a.ctr, n);
 }
 
 hipError_t launch_scan_batch(const ScanArgs &a, hipStream_t s) {
     if (a.M <= 0) return hipSuccess;
-    if (a.hit_rc) {
-        int64_t n = a.M * a.B;
-        hipLaunchKernelGGL(k_scan_probe, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
-    } else {
-        hipLaunchKernelGGL(k_scan_batch, dim3((unsigned)a.M), dim3(kBlock), 0, s, a);
-    }
+    int64_t n = a.M * a.B;
+    if (a.variant == 1)
+        hipLaunchKernelGGL(k_scan_batch<1>, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_scan_batch<0>, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 

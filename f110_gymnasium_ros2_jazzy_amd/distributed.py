@@ -1,0 +1,81 @@
+"""Env-batch sharding across GPUs.
+
+Environments are independent: a global batch of envs is split into
+contiguous per-rank blocks and every rank steps its block on its own GPU.
+There is no data-path collective; ranks only meet for barriers and the
+max-over-ranks timing reduction.  RNG streams (scan noise, autoreset spawns)
+are keyed by *global* env id (f110_config.env_offset), so an env's
+trajectory does not depend on how many GPUs share the batch.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass(frozen=True)
+class Shard:
+    rank: int
+    world: int
+    offset: int   # global id of this rank's first env
+    count: int    # envs on this rank
+
+
+def shard_range(total: int, world: int, rank: int) -> Shard:
+    """Contiguous near-equal blocks: the first total % world ranks get one more."""
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError("bad world/rank")
+    base, extra = divmod(int(total), int(world))
+    count = base + (1 if rank < extra else 0)
+    offset = rank * base + min(rank, extra)
+    return Shard(rank, world, offset, count)
+
+
+def env_rank_world():
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
+
+
+def init(backend: str | None = None) -> tuple[int, int, int]:
+    """Initialise torch.distributed from torchrun's env (no-op for world 1)."""
+    rank, world, local = env_rank_world()
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {}
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            kw["device_id"] = torch.device(f"cuda:{local}")
+        dist.init_process_group(backend=backend, **kw)
+    return rank, world, local
+
+
+def barrier():
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+
+
+def max_over_ranks(x: float) -> float:
+    if not (dist.is_available() and dist.is_initialized()):
+        return float(x)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: float) -> float:
+    if not (dist.is_available() and dist.is_initialized()):
+        return float(x)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def shutdown():
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()

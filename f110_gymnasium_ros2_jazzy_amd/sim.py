@@ -135,8 +135,11 @@ class BatchSim:
         return self.out
 
     def step(self, actions, minimal_outputs: bool = False) -> StepOut:
-        """actions: [E, A, 2] (steer, velocity) f32 device tensor (or array)."""
-        a = torch.as_tensor(actions, dtype=torch.float32, device=self.device)
+        """actions: [E, A, 2] (steer, velocity); float32 or float64 tensor/array
+        (float64 keeps Simulator.step's full-precision control inputs)."""
+        a = torch.as_tensor(actions, device=self.device)
+        if a.dtype not in (torch.float32, torch.float64):
+            a = a.to(torch.float32)
         if a.dim() == 2 and self.E == 1:
             a = a.unsqueeze(0)
         if tuple(a.shape) != (self.E, self.A, 2):
@@ -144,7 +147,8 @@ class BatchSim:
         a = a.contiguous()
         self._keep_a = a
         outs = self._outs_min if minimal_outputs else self._outs
-        _lib.check(self.L.f110_step(self.ctx, _ptr(a), ctypes.byref(outs), self._stream()), "f110_step")
+        dt = _lib.F64 if a.dtype == torch.float64 else _lib.F32
+        _lib.check(self.L.f110_step(self.ctx, _ptr(a), dt, ctypes.byref(outs), self._stream()), "f110_step")
         return self.out
 
     def get_state(self):

@@ -52,6 +52,9 @@ extern "C" {
 #define F110_E_NODEVICE (-4) /* no gfx950 device */
 #define F110_E_ALLOC (-5)
 
+#define F110_F32 0  /* action dtypes for f110_step */
+#define F110_F64 1
+
 #define F110_INTEGRATOR_RK4 1   /* base_classes.py:40-42 */
 #define F110_INTEGRATOR_EULER 2
 
@@ -140,8 +143,12 @@ F110_API int f110_reset(f110_ctx *ctx, const double *poses, const uint8_t *env_m
  * (base_classes.py:566-625): per agent update_pose (steer delay, pid, RK4 of
  * vehicle_dynamics_st, clamps) + ScanSimulator2D.scan (+ noise), GJK
  * collision_multiple, TTC (check_ttc_jit), agent ray_cast, obs packing,
- * _check_done.  actions: [n_envs][n_agents][2] f32 (steer, velocity). */
-F110_API int f110_step(f110_ctx *ctx, const float *actions, const f110_outputs *out, void *stream);
+ * _check_done.  actions: [n_envs][n_agents][2] (steer, velocity), f32
+ * (F110Env's action_space dtype, f110_env.py:238-242) or f64 (Simulator.step
+ * takes whatever control_inputs dtype it is given): actions_dtype = F110_F32 /
+ * F110_F64. */
+F110_API int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dtype, const f110_outputs *out,
+                       void *stream);
 
 /* ---- state access ------------------------------------------------------- */
 /* state: device [7][n_envs*n_agents] f64 (SoA, see header comment).
