@@ -54,6 +54,22 @@ struct f110_ctx {
     uint64_t *episode = nullptr, *nstep = nullptr;
     unsigned long long *ctr = nullptr;
     std::vector<void *> allocs;
+    // f110_profile_begin/end
+    std::vector<hipEvent_t> prof_ev;  // 4 per recorded step
+    int prof_max = 0, prof_n = 0;
+    int rays_per_thread = 1;  // k_rays ILP; F110_RAYS_PER_THREAD overrides (A/B experiments)
+    int pool = 0;             // F110_RAY_POOL: rays per lane of k_rays_pool (0 = k_rays)
+    int refill_min = 16;      // F110_REFILL_MIN
+
+    hipEvent_t *next_prof_events() {
+        if (prof_n >= prof_max) return nullptr;
+        return &prof_ev[(size_t)4 * prof_n++];
+    }
+    void free_prof() {
+        for (hipEvent_t e : prof_ev) (void)hipEventDestroy(e);
+        prof_ev.clear();
+        prof_max = prof_n = 0;
+    }
 
     template <class T>
     hipError_t alloc(T **p, size_t n) {
@@ -313,6 +329,12 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     c->inc = (double)C.theta_dis * (C.fov / (double)(C.n_beams - 1)) / (2. * kPi);  // laser_models.py:367-368
     c->beam_incr = C.fov / (double)(C.n_beams - 1);
     c->n_spawn = n_spawn;
+    if (const char *v = std::getenv("F110_RAY_POOL")) c->pool = std::atoi(v);
+    if (const char *v = std::getenv("F110_REFILL_MIN")) c->refill_min = std::atoi(v);
+    if (const char *v = std::getenv("F110_RAYS_PER_THREAD")) {
+        int k = std::atoi(v);
+        c->rays_per_thread = (k == 1 || k == 2 || k == 4) ? k : c->rays_per_thread;
+    }
     const size_t EA = (size_t)C.n_envs * C.n_agents;
 
     auto cleanup = [&](int code, const std::string &msg) {
@@ -383,6 +405,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
 extern "C" int f110_destroy(f110_ctx *ctx) {
     if (!ctx) return F110_OK;
     (void)hipSetDevice(ctx->device);
+    ctx->free_prof();
     for (void *q : ctx->allocs) (void)hipFree(q);
     delete ctx;
     return F110_OK;
@@ -415,6 +438,9 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.beam_incr = c->beam_incr;
     a.seed = c->cfg.seed;
     a.env_offset = c->cfg.env_offset;
+    a.rays_per_thread = c->rays_per_thread;
+    a.pool = c->pool;
+    a.refill_min = c->refill_min;
     a.st = c->st;
     a.sb = c->sb;
     a.scnt = c->scnt;
@@ -448,7 +474,7 @@ extern "C" int f110_reset(f110_ctx *ctx, const double *poses, const uint8_t *env
     a.mode = 1;
     a.reset_poses = poses;
     a.reset_mask = env_mask;
-    HIP_TRY(launch_env_step(a, (hipStream_t)stream));
+    HIP_TRY(launch_env_step(a, (hipStream_t)stream, ctx->next_prof_events()));
     return F110_OK;
 }
 
@@ -464,7 +490,7 @@ extern "C" int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dty
         a.actions_f64 = static_cast<const double *>(actions);
     else
         a.actions = static_cast<const float *>(actions);
-    HIP_TRY(launch_env_step(a, (hipStream_t)stream));
+    HIP_TRY(launch_env_step(a, (hipStream_t)stream, ctx->next_prof_events()));
     return F110_OK;
 }
 
@@ -547,5 +573,43 @@ extern "C" int f110_reset_counters(f110_ctx *ctx, void *stream) {
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     HIP_TRY(hipMemsetAsync(ctx->ctr, 0, (size_t)kCtrSlots * kCtrStride * sizeof(unsigned long long),
                            (hipStream_t)stream));
+    return F110_OK;
+}
+
+extern "C" int f110_profile_begin(f110_ctx *ctx, int32_t max_steps) {
+    if (!ctx || max_steps < 0) return fail(F110_E_INVALID, "f110_profile_begin: bad arguments");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    ctx->free_prof();
+    ctx->prof_ev.resize((size_t)4 * max_steps);
+    for (size_t i = 0; i < ctx->prof_ev.size(); ++i) {
+        hipError_t e = hipEventCreate(&ctx->prof_ev[i]);
+        if (e != hipSuccess) {
+            ctx->prof_ev.resize(i);
+            ctx->free_prof();
+            return fail(F110_E_HIP, std::string("hipEventCreate: ") + hipGetErrorString(e));
+        }
+    }
+    ctx->prof_max = max_steps;
+    ctx->prof_n = 0;
+    return F110_OK;
+}
+
+extern "C" int f110_profile_end(f110_ctx *ctx, double ms_out[3], int32_t *steps_out) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_profile_end: null context");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    double acc[3] = {0, 0, 0};
+    for (int i = 0; i < ctx->prof_n; ++i) {
+        hipEvent_t *ev = &ctx->prof_ev[(size_t)4 * i];
+        HIP_TRY(hipEventSynchronize(ev[3]));
+        for (int k = 0; k < 3; ++k) {
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+            acc[k] += ms;
+        }
+    }
+    if (ms_out)
+        for (int k = 0; k < 3; ++k) ms_out[k] = acc[k];
+    if (steps_out) *steps_out = ctx->prof_n;
+    ctx->free_prof();
     return F110_OK;
 }

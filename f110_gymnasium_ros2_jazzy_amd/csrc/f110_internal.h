@@ -22,6 +22,9 @@ struct StepArgs {
     const double *angles, *beam_cos, *side;   // [B] RaceCar class-level beam tables
     f110_params p;
     int32_t E, A, B, theta_dis, integrator, ego, autoreset, mode;  // mode 0 step, 1 reset
+    int32_t rays_per_thread;  // k_rays ILP (1, 2 or 4)
+    int32_t pool;             // >0: k_rays_pool with this many rays per lane (4, 8, 16)
+    int32_t refill_min;       // k_rays_pool: parked lanes that trigger a refill
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
     uint64_t seed;
     int64_t env_offset;
@@ -72,7 +75,7 @@ struct ScanArgs {
 
 size_t step_lds_bytes(int A, int B);
 hipError_t prepare_env_step(size_t lds_bytes);
-hipError_t launch_env_step(const StepArgs &a, hipStream_t s);
+hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev = nullptr);  // ev: 4 events or null
 hipError_t launch_scan_batch(const ScanArgs &a, hipStream_t s);
 hipError_t launch_dynamics_batch(const double *x, const double *u, double *f, int64_t M, const f110_params &p,
                                  hipStream_t s);

@@ -33,10 +33,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-// One (lookups, rays) atomic pair per wave into a per-block slot.
-__device__ __forceinline__ void count_rays(unsigned long long *ctr, uint32_t n) {
+// One (lookups, rays) atomic pair per wave into a per-block slot.  n = lookups
+// of this lane's rays (0 for a lane without rays), rays = rays per busy lane.
+__device__ __forceinline__ void count_rays(unsigned long long *ctr, uint32_t n, uint32_t rays = 1) {
     uint32_t tot = wave_sum(n);
-    uint32_t cnt = wave_sum(n ? 1u : 0u);
+    uint32_t cnt = wave_sum(n ? rays : 0u);
     if ((threadIdx.x & 63) == 0 && cnt) {
         unsigned long long *slot = ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
         atomicAdd(slot, (unsigned long long)tot);
@@ -64,8 +65,8 @@ __device__ __forceinline__ double trace(const MapView &m, double x, double y, do
 
 // ------------------------------------------------------------------------
 // k_agents: one thread per car.
-__global__ void __launch_bounds__(kBlock) k_agents(StepArgs a) {
-    const int g = blockIdx.x * kBlock + threadIdx.x;
+__global__ void __launch_bounds__(64) k_agents(StepArgs a) {
+    const int g = blockIdx.x * 64 + threadIdx.x;
     const int EA = a.E * a.A;
     if (g >= EA) return;
     const int A = a.A;
@@ -143,28 +144,176 @@ __global__ void __launch_bounds__(kBlock) k_agents(StepArgs a) {
 }
 
 // ------------------------------------------------------------------------
-// k_rays: one thread per ray; ray r -> car g = r / B, beam b = r % B.
+// k_rays: thread t traces the K consecutive rays r = K*t .. K*t+K-1
+// (ray r -> car g = r / B, beam b = r % B).  The K sphere traces are
+// interleaved step by step, so a lane keeps K independent EDT gathers in
+// flight (memory-level parallelism) while neighbouring beams, whose traces
+// have near-equal lengths, keep the lane's iterations in lock-step.
+template <int K>
 __global__ void __launch_bounds__(kBlock) k_rays(StepArgs a) {
     const int EA = a.E * a.A;
-    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int B = a.B;
-    uint32_t n = 0;
-    if (r < (int64_t)EA * B) {
+    const int64_t R = (int64_t)EA * B;
+    const int64_t r0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * K;
+    const MapView &m = a.map;
+    double x[K], y[K], c[K], s[K], d[K], tot[K];
+    uint32_t n[K];
+    bool act[K], valid[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int64_t r = r0 + k;
+        valid[k] = false;
+        act[k] = false;
+        n[k] = 0;
+        x[k] = y[k] = c[k] = s[k] = d[k] = tot[k] = 0.0;
+        if (r < R) {
+            const int g = (int)(r / B);
+            const int b = (int)(r - (int64_t)g * B);
+            const int e = g / a.A;
+            if (!(a.mode == 1 && a.reset_mask && !a.reset_mask[e])) {
+                double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
+                int ti = (int)t;  // int(theta_index), laser_models.py:124
+                if (ti >= a.theta_dis) ti = 0;
+                c[k] = a.cosines[ti];
+                s[k] = a.sines[ti];
+                x[k] = a.ray0[g];
+                y[k] = a.ray0[EA + g];
+                d[k] = a.ray0[2 * EA + g];  // :129
+                tot[k] = d[k];              // :130
+                n[k] = 1;
+                valid[k] = true;
+                act[k] = d[k] > a.eps && tot[k] <= a.max_range;  // :133
+            }
+        }
+    }
+    while (true) {
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (act[k]) {
+                x[k] += d[k] * c[k];  // :135
+                y[k] += d[k] * s[k];  // :136
+                d[k] = m.dt[cell_index_fast(m, x[k], y[k])];
+                tot[k] += d[k];       // :141
+                ++n[k];
+                act[k] = d[k] > a.eps && tot[k] <= a.max_range;
+            }
+            any = any || act[k];
+        }
+        if (!any) break;
+    }
+    uint32_t nsum = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if (!valid[k]) continue;
+        const int64_t r = r0 + k;
         const int g = (int)(r / B);
         const int b = (int)(r - (int64_t)g * B);
         const int e = g / a.A;
-        if (!(a.mode == 1 && a.reset_mask && !a.reset_mask[e])) {
-            double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
-            int ti = (int)t;  // int(theta_index), laser_models.py:124
-            if (ti >= a.theta_dis) ti = 0;
-            double range = trace(a.map, a.ray0[g], a.ray0[EA + g], a.cosines[ti], a.sines[ti], a.ray0[2 * EA + g],
-                                 a.eps, a.max_range, n);
-            if (a.noise_std > 0.0)  // ScanSimulator2D.scan: noise after the clamp (laser_models.py:450-452)
-                range += a.noise_std * (double)beam_normal(a.seed, (uint64_t)(a.env_offset + e), a.noise_step[e], b);
-            a.scan[r] = range;
+        double range = tot[k] > a.max_range ? a.max_range : tot[k];  // :143-144
+        if (a.noise_std > 0.0)  // ScanSimulator2D.scan: noise after the clamp (laser_models.py:450-452)
+            range += a.noise_std * (double)beam_normal(a.seed, (uint64_t)(a.env_offset + e), a.noise_step[e], b);
+        a.scan[r] = range;
+        nsum += n[k];
+    }
+    if (a.ctr) count_rays(a.ctr, nsum, K);
+}
+
+// ------------------------------------------------------------------------
+// k_rays_pool: every wave owns a pool of P*64 consecutive rays.  Lanes whose
+// ray finished park (result in registers); once at least `refill` lanes are
+// parked, they are finalised (noise, store) and re-armed with the next rays
+// of the pool in ONE divergent phase, so the ~40-instruction ray set-up is
+// paid once per group instead of once per iteration.  Lanes stay busy until
+// the pool drains: the wave no longer waits for its longest ray.
+__device__ __forceinline__ void ray_init(const StepArgs &a, int64_t r, int EA, double &x, double &y, double &c,
+                                         double &s, double &d, double &tot) {
+    const int B = a.B;
+    const int g = (int)(r / B);
+    const int b = (int)(r - (int64_t)g * B);
+    double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
+    int ti = (int)t;  // int(theta_index), laser_models.py:124
+    if (ti >= a.theta_dis) ti = 0;
+    c = a.cosines[ti];
+    s = a.sines[ti];
+    x = a.ray0[g];
+    y = a.ray0[EA + g];
+    d = a.ray0[2 * EA + g];  // :129
+    tot = d;                 // :130
+}
+
+__device__ __forceinline__ void ray_finish(const StepArgs &a, int64_t r, double tot) {
+    const int B = a.B;
+    const int g = (int)(r / B);
+    const int b = (int)(r - (int64_t)g * B);
+    const int e = g / a.A;
+    double range = tot > a.max_range ? a.max_range : tot;  // :143-144
+    if (a.noise_std > 0.0)  // ScanSimulator2D.scan: noise after the clamp (laser_models.py:450-452)
+        range += a.noise_std * (double)beam_normal(a.seed, (uint64_t)(a.env_offset + e), a.noise_step[e], b);
+    a.scan[r] = range;
+}
+
+template <int P>
+__global__ void __launch_bounds__(kBlock) k_rays_pool(StepArgs a) {
+    const int EA = a.E * a.A;
+    const int64_t R = (int64_t)EA * a.B;
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t begin = wave * (64 * P);
+    const int64_t end = begin + 64 * P < R ? begin + 64 * P : R;
+    const MapView &m = a.map;
+    const int refill = a.refill_min;
+    int64_t next = begin + 64;  // wave-uniform
+    int64_t my = begin + lane;
+    bool have = my < end;       // lane holds a ray (running or parked)
+    double x = 0, y = 0, c = 0, s = 0, d = 0, tot = 0;
+    uint32_t n = 0, looks = 0;
+    if (have) {
+        ray_init(a, my, EA, x, y, c, s, d, tot);
+        n = 1;
+    }
+    bool act = have && d > a.eps && tot <= a.max_range;  // :133
+    while (true) {
+        const uint64_t parked = __ballot(have && !act);
+        const uint64_t running = __ballot(act);
+        const int np = __popcll(parked);
+        // refill when enough lanes are parked, or when nothing runs any more
+        if (np && (np >= refill || !running || next >= end)) {
+            if (have && !act) {
+                ray_finish(a, my, tot);
+                looks += n;
+                my = next + __popcll(parked & lt);
+                have = my < end;
+                if (have) {
+                    ray_init(a, my, EA, x, y, c, s, d, tot);
+                    n = 1;
+                    act = d > a.eps && tot <= a.max_range;
+                }
+            }
+            next += np;
+            continue;  // fresh rays may already be finished (d0 <= eps)
+        }
+        if (!running) break;
+        if (act) {
+            x += d * c;  // :135
+            y += d * s;  // :136
+            d = m.dt[cell_index_fast(m, x, y)];
+            tot += d;    // :141
+            ++n;
+            act = d > a.eps && tot <= a.max_range;
         }
     }
-    if (a.ctr) count_rays(a.ctr, n);
+    if (a.ctr) {
+        // rays traced by this lane are counted through their lookups; the ray
+        // count of the wave is its pool size
+        uint32_t tot_l = wave_sum(looks);
+        if (lane == 0 && end > begin) {
+            unsigned long long *slot = a.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+            atomicAdd(slot, (unsigned long long)tot_l);
+            atomicAdd(slot + 1, (unsigned long long)(end - begin));
+        }
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -348,17 +497,39 @@ hipError_t prepare_env_step(size_t lds_bytes) {
 
 size_t step_lds_bytes(int A, int B) { return post_lds_bytes(A, B); }
 
-hipError_t launch_env_step(const StepArgs &a, hipStream_t s) {
+hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     const int EA = a.E * a.A;
-    hipLaunchKernelGGL(k_agents, dim3((EA + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    hipError_t e;
+    if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
+    // 64-thread blocks: a few thousand cars must still spread over all CUs
+    hipLaunchKernelGGL(k_agents, dim3((EA + 63) / 64), dim3(64), 0, s, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
     const int64_t R = (int64_t)EA * a.B;
-    hipLaunchKernelGGL(k_rays, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    const int K = a.rays_per_thread;
+    const int64_t T = (R + K - 1) / K;
+    const dim3 grid((unsigned)((T + kBlock - 1) / kBlock));
+    if (a.pool > 0) {
+        const int64_t per_block = (int64_t)kBlock * a.pool;  // 4 waves x 64 lanes x P rays
+        const dim3 pg((unsigned)((R + per_block - 1) / per_block));
+        if (a.pool == 8)
+            hipLaunchKernelGGL(k_rays_pool<8>, pg, dim3(kBlock), 0, s, a);
+        else if (a.pool == 16)
+            hipLaunchKernelGGL(k_rays_pool<16>, pg, dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_rays_pool<4>, pg, dim3(kBlock), 0, s, a);
+    } else if (K == 4)
+        hipLaunchKernelGGL(k_rays<4>, grid, dim3(kBlock), 0, s, a);
+    else if (K == 2)
+        hipLaunchKernelGGL(k_rays<2>, grid, dim3(kBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_rays<1>, grid, dim3(kBlock), 0, s, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_post, dim3(a.E), dim3(kBlock), post_lds_bytes(a.A, a.B), s, a);
-    return hipGetLastError();
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (ev && (e = hipEventRecord(ev[3], s)) != hipSuccess) return e;
+    return hipSuccess;
 }
 
 // ------------------------------------------------------------------------

@@ -1,0 +1,282 @@
+"""F110Env: drop-in for f110_gym.envs.F110Env (f110_env.py:55-602) on MI355X.
+
+Same constructor kwargs and defaults (f110_env.py:104-186), same
+``reset(seed, options=poses) -> (obs, info)`` and
+``step(action) -> (obs, reward, terminated, truncated, info)`` contract, the
+same 1088-float flat observation, the same ``info`` keys, ``timestep``
+attribute and ``close()``, so rl_training/train_ddpg.py runs unchanged.
+
+The physics + lidar + collision step runs on the GPU (one env of a
+BatchSim).  The reference's lap bookkeeping (_check_done, f110_env.py:310-352)
+is evaluated here on the host with NumPy exactly as the reference writes it
+(including its dtype behaviour when ``options`` are float32), because it is
+a handful of scalar operations on two cars.
+
+Differences, by design:
+  * scan noise comes from a counter-based Philox stream (device) instead of
+    NumPy's PCG64; it has the same N(0, 0.01) law, is added after the clamp,
+    is shared by every agent and restarts at every reset, like the reference
+    (laser_models.py:450-452, base_classes.py:119,204).  ``noise_std=0``
+    (extension kwarg) turns it off for bit-level comparisons.
+  * render() is not provided (visualisation is out of scope; the DDPG
+    script never calls it).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+try:  # gymnasium is optional: the env works without it (no registry)
+    import gymnasium as _gym
+    from gymnasium import spaces as _spaces
+    _EnvBase = _gym.Env
+except Exception:  # pragma: no cover - exercised where gymnasium is absent
+    _gym = None
+    _spaces = None
+    _EnvBase = object
+
+from . import _lib
+
+DEFAULT_PARAMS = {'mu': 1.0489, 'C_Sf': 4.718, 'C_Sr': 5.4562, 'lf': 0.15875, 'lr': 0.17145, 'h': 0.074,
+                  'm': 3.74, 'I': 0.04712, 's_min': -0.4189, 's_max': 0.4189, 'sv_min': -3.2, 'sv_max': 3.2,
+                  'v_switch': 7.319, 'a_max': 9.51, 'v_min': 0.00000001, 'v_max': 20.0, 'width': 0.31,
+                  'length': 0.58, 'lidar_max': 30.0}
+
+
+class Integrator:
+    """Mirror of base_classes.Integrator (base_classes.py:40-42)."""
+    RK4 = _lib.INTEGRATOR_RK4
+    Euler = _lib.INTEGRATOR_EULER
+
+
+class _Box:
+    """Minimal stand-in for gymnasium.spaces.Box when gymnasium is absent."""
+
+    def __init__(self, low, high, dtype=np.float32):
+        self.low = np.asarray(low, dtype)
+        self.high = np.asarray(high, dtype)
+        self.shape = self.low.shape
+        self.dtype = np.dtype(dtype)
+
+    def sample(self, rng=None):
+        rng = rng or np.random.default_rng()
+        return rng.uniform(self.low, self.high).astype(self.dtype)
+
+    def contains(self, x):
+        x = np.asarray(x)
+        return x.shape == self.shape and bool(np.all(x >= self.low) and np.all(x <= self.high))
+
+
+def _box(low, high):
+    if _spaces is not None:
+        return _spaces.Box(low=low, high=high, dtype=np.float32)
+    return _Box(low, high, np.float32)
+
+
+def _integrator_code(v):
+    if isinstance(v, (int, np.integer)):
+        return int(v)
+    name = getattr(v, "name", str(v))
+    if "RK4" in name:
+        return _lib.INTEGRATOR_RK4
+    if "Euler" in name:
+        return _lib.INTEGRATOR_EULER
+    raise SyntaxError(f"Invalid Integrator Specified. Provided {name}. Please choose RK4 or Euler")
+
+
+class F110Env(_EnvBase):
+    metadata = {'render_modes': ['human', 'human_fast'], 'render_fps': 30}
+
+    def __init__(self, **kwargs):
+        from .maps import load_map
+        from .sim import BatchSim
+
+        self.conf = kwargs.get('conf')
+        self.seed = kwargs.get('seed', 42)
+        if 'map_dir' in kwargs and 'map' in kwargs:
+            self.map_dir = kwargs['map_dir']
+            self.map_name = kwargs['map']
+            self.map_path = self.map_dir + self.map_name + '.yaml'
+        else:
+            # the reference falls back to a bundled 'vegas' map; ours bundles Spielberg
+            self.map_dir = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'maps') + os.sep
+            self.map_name = kwargs.get('map', 'Spielberg_map')
+            self.map_path = self.map_dir + self.map_name + '.yaml'
+        self.map_ext = kwargs.get('map_ext', '.png')
+        self.params = dict(kwargs.get('params', DEFAULT_PARAMS))
+        self.num_agents = kwargs.get('num_agents', 2)
+        self.timestep = kwargs.get('timestep', 0.01)
+        self.ego_idx = kwargs.get('ego_idx', 0)
+        self.integrator = kwargs.get('integrator', Integrator.RK4)
+        self.lidar_dist = kwargs.get('lidar_dist', 0.0)
+        self.render_mode = kwargs.get('render_mode')
+        noise_std = kwargs.get('noise_std', 0.01)
+        device = kwargs.get('device', 0)
+
+        self.start_thresh = 0.1
+        self.poses_x, self.poses_y, self.poses_theta = [], [], []
+        self.collisions = np.zeros((self.num_agents,))
+        self.lidar_max = self.params["lidar_max"]
+        self.near_start = True
+        self.num_toggles = 0
+        self.lap_times = np.zeros((self.num_agents,))
+        self.lap_counts = np.zeros((self.num_agents,))
+        self.current_time = 0.0
+        self.near_starts = np.array([True] * self.num_agents)
+        self.toggle_list = np.zeros((self.num_agents,))
+        self.start_xs = np.zeros((self.num_agents,))
+        self.start_ys = np.zeros((self.num_agents,))
+        self.start_thetas = np.zeros((self.num_agents,))
+        self.start_rot = np.eye(2)
+
+        self.track = load_map(self.map_path, self.map_ext)
+        self.sim = BatchSim(self.track, n_envs=1, n_agents=self.num_agents, params=self.params, device=device,
+                            seed=self.seed, timestep=self.timestep, integrator=_integrator_code(self.integrator),
+                            ego_idx=self.ego_idx, lidar_dist=self.lidar_dist, noise_std=noise_std,
+                            keep_f64_scans=True)
+
+        self.resolution = self.track.resolution
+        self.x0, self.y0 = self.track.origin[0], self.track.origin[1]
+        self.x_min, self.x_max, self.y_min, self.y_max = self.track.bounds
+        low = np.array([self.params['s_min'], self.params['v_min']], dtype=np.float32)
+        high = np.array([self.params['s_max'], self.params['v_max']], dtype=np.float32)
+        self.action_space = _box(np.tile(low, (self.num_agents, 1)), np.tile(high, (self.num_agents, 1)))
+        B = self.sim.B
+        olow = np.array([0.0] * B + [self.x_min, self.y_min, -np.pi, 0.0] * self.num_agents, dtype=np.float32)
+        ohigh = np.array([1.0] * B + [self.x_max, self.y_max, np.pi, 1.0] * self.num_agents, dtype=np.float32)
+        self.observation_space = _box(olow, ohigh)
+        self.render_obs = None
+
+    # ------------------------------------------------------------------
+    def _check_done(self):
+        """Lap toggles + ego collision (f110_env.py:310-352), NumPy on the host."""
+        left_t, right_t = 2, 2
+        dx = np.array(self.poses_x) - self.start_xs
+        dy = np.array(self.poses_y) - self.start_ys
+        delta_pt = np.dot(self.start_rot, np.stack((dx, dy), axis=0))
+        temp_y = delta_pt[1, :]
+        beyond_left = temp_y > left_t
+        beyond_right = temp_y < -right_t
+        temp_y[beyond_left] -= left_t
+        temp_y[beyond_right] = -right_t - temp_y[beyond_right]
+        temp_y[np.invert(np.logical_or(beyond_left, beyond_right))] = 0
+        closes = (delta_pt[0, :] ** 2 + temp_y ** 2) <= 0.1
+        for i in range(self.num_agents):
+            if closes[i] and not self.near_starts[i]:
+                self.near_starts[i] = True
+                self.toggle_list[i] += 1
+            elif not closes[i] and self.near_starts[i]:
+                self.near_starts[i] = False
+                self.toggle_list[i] += 1
+            self.lap_counts[i] = self.toggle_list[i] // 2
+            if self.toggle_list[i] < 4:
+                self.lap_times[i] = self.current_time
+        done = (self.collisions[self.ego_idx]) or np.all(self.toggle_list >= 4)
+        return bool(done), self.toggle_list >= 4
+
+    def _obs_dict(self, out):
+        """Simulator.step's observation dict (base_classes.py:607-625) from device outputs."""
+        st = self.sim.agent_states()[0].cpu().numpy()          # [A, 7] f64
+        scans64 = out.scans_f64[0].cpu().numpy()               # [A, B] f64
+        cols = out.collisions[0].cpu().numpy().astype(np.float64)
+        return {
+            'ego_idx': self.ego_idx,
+            'scans': [scans64[i] for i in range(self.num_agents)],
+            'poses_x': [st[i, 0] for i in range(self.num_agents)],
+            'poses_y': [st[i, 1] for i in range(self.num_agents)],
+            'poses_theta': [st[i, 4] for i in range(self.num_agents)],
+            'linear_vels_x': [st[i, 3] for i in range(self.num_agents)],
+            'linear_vels_y': [0. for _ in range(self.num_agents)],
+            'ang_vels_z': [st[i, 5] for i in range(self.num_agents)],
+            'collisions': cols,
+        }, out.obs[0].cpu().numpy()
+
+    def _finish_step(self, out):
+        obs_dict, flat = self._obs_dict(out)
+        obs_dict['lap_times'] = self.lap_times.astype(np.float32)
+        obs_dict['lap_counts'] = self.lap_counts.astype(np.float32)
+        F110Env.current_obs = obs_dict
+        self.render_obs = {k: obs_dict[k] for k in ('ego_idx', 'poses_x', 'poses_y', 'poses_theta', 'lap_times',
+                                                    'lap_counts', 'scans')}
+        reward = self.timestep
+        self.current_time = self.current_time + self.timestep
+        self.poses_x = obs_dict['poses_x']
+        self.poses_y = obs_dict['poses_y']
+        self.poses_theta = obs_dict['poses_theta']
+        self.collisions = obs_dict['collisions']
+        terminated, toggle_list = self._check_done()
+        info = self._build_info(obs_dict)
+        info["checkpoint_done"] = toggle_list
+        return flat, reward, terminated, False, info
+
+    def _build_info(self, obs_dict):
+        return {
+            "ego_idx": int(obs_dict["ego_idx"]),
+            "poses_x": np.asarray(obs_dict["poses_x"], dtype=np.float32),
+            "poses_y": np.asarray(obs_dict["poses_y"], dtype=np.float32),
+            "poses_theta": np.asarray(obs_dict["poses_theta"], dtype=np.float32),
+            "linear_vels_x": np.asarray(obs_dict["linear_vels_x"], dtype=np.float32),
+            "linear_vels_y": np.asarray(obs_dict["linear_vels_y"], dtype=np.float32),
+            "ang_vels_z": np.asarray(obs_dict["ang_vels_z"], dtype=np.float32),
+            "collisions": np.asarray(obs_dict["collisions"], dtype=np.int8),
+            "lap_times": self.lap_times.astype(np.float32),
+            "lap_counts": self.lap_counts.astype(np.float32),
+            "scans": [np.asarray(s, dtype=np.float32) for s in obs_dict["scans"]],
+            "checkpoint_done": getattr(self, "toggle_list", None),
+            "time": float(self.current_time),
+        }
+
+    # ------------------------------------------------------------------
+    def step(self, action):
+        """F110Env.step (f110_env.py:371-421); action [num_agents, 2] (steer, velocity)."""
+        a = np.asarray(action)
+        if a.dtype not in (np.float32, np.float64):
+            a = a.astype(np.float32)
+        out = self.sim.step(a.reshape(1, self.num_agents, 2))
+        return self._finish_step(out)
+
+    def reset(self, seed=None, options=None):
+        """F110Env.reset (f110_env.py:425-472): options = poses [num_agents, 3]."""
+        poses = options
+        if poses is None:
+            raise ValueError("reset(options=poses) requires the start poses [num_agents, 3]")
+        poses = np.asarray(poses)
+        if poses.shape[0] != self.num_agents:
+            raise ValueError('Number of poses for reset does not match number of agents.')
+        self.current_time = 0.0
+        self.collisions = np.zeros((self.num_agents,))
+        self.num_toggles = 0
+        self.near_start = True
+        self.near_starts = np.array([True] * self.num_agents)
+        self.toggle_list = np.zeros((self.num_agents,))
+        self.start_xs = poses[:, 0]
+        self.start_ys = poses[:, 1]
+        self.start_thetas = poses[:, 2]
+        th = self.start_thetas[self.ego_idx]
+        self.start_rot = np.array([[np.cos(-th), -np.sin(-th)], [np.sin(-th), np.cos(-th)]])
+        # device: RaceCar.reset for every car + the reference's zero-action step (f110_env.py:457)
+        out = self.sim.reset(np.asarray(poses, dtype=np.float64).reshape(1, self.num_agents, 3))
+        obs_flat, _, _, _, info = self._finish_step(out)
+        return obs_flat, info
+
+    def update_map(self, map_path, map_ext):
+        raise NotImplementedError("update_map: create a new env (the EDT is built once per context)")
+
+    def update_params(self, params, index=-1):
+        raise NotImplementedError("update_params: pass params= at construction")
+
+    def add_render_callback(self, callback_func):
+        pass
+
+    def render(self, mode='human'):
+        raise NotImplementedError("rendering is out of scope of the MI355X simulator")
+
+    def close(self):
+        if getattr(self, "sim", None) is not None:
+            self.sim.close()
+            self.sim = None
+
+    @property
+    def unwrapped(self):
+        return self

@@ -201,6 +201,17 @@ class BatchSim:
     def reset_counters(self):
         _lib.check(self.L.f110_reset_counters(self.ctx, self._stream()), "f110_reset_counters")
 
+    def profile_begin(self, max_steps: int):
+        """Time each kernel of the next max_steps step/reset calls (HIP events)."""
+        _lib.check(self.L.f110_profile_begin(self.ctx, int(max_steps)), "f110_profile_begin")
+
+    def profile_end(self) -> dict:
+        ms = (ctypes.c_double * 3)()
+        n = ctypes.c_int32()
+        _lib.check(self.L.f110_profile_end(self.ctx, ms, ctypes.byref(n)), "f110_profile_end")
+        k = max(n.value, 1)
+        return {"steps": n.value, "k_agents_ms": ms[0] / k, "k_rays_ms": ms[1] / k, "k_post_ms": ms[2] / k}
+
     def close(self):
         if getattr(self, "ctx", None):
             torch.cuda.synchronize(self.device)

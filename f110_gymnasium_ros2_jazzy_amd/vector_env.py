@@ -1,0 +1,103 @@
+"""F110VectorEnv: N F1TENTH envs stepped as one batch on one GPU.
+
+Gymnasium-1.x vector surface (``reset(seed, options) -> (obs, infos)``,
+``step(actions) -> (obs, rewards, terminations, truncations, infos)``,
+``num_envs``, ``single_observation_space``, ``single_action_space``) with
+observations and infos kept as device tensors (``as_numpy=True`` converts).
+
+Per env the semantics are F110Env's (f110_env.py:371-472): reward = timestep,
+terminated = ego collision or 4 lap toggles, truncated = False, flat obs =
+[agent-0 scan / lidar_max, (x, y, yaw, collision) per agent].  Autoreset is
+the gymnasium NEXT_STEP mode and runs on the device: the step after an env
+terminates resets it to a pose drawn from ``spawn_poses`` (and performs the
+reference's zero-action reset step); that step's reward is 0.
+
+Multi-GPU: give each rank its block of envs (distributed.shard_range) and
+``env_offset`` = the block's first global id; RNG streams are keyed by global
+env id, so results do not depend on the GPU count.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .f110_env import DEFAULT_PARAMS, _box
+from .maps import centerline_spawns, load_map
+from .sim import BatchSim
+
+
+class F110VectorEnv:
+    metadata = {"autoreset_mode": "NextStep", "render_modes": []}
+
+    def __init__(self, num_envs: int, map: str = "Spielberg_map", map_ext: str = ".png", num_agents: int = 1,
+                 params: dict | None = None, seed: int = 42, timestep: float = 0.01, device=0,
+                 spawn_poses: np.ndarray | None = None, noise_std: float = 0.01, env_offset: int = 0,
+                 ego_idx: int = 0, as_numpy: bool = False, autoreset: bool = True, **kwargs):
+        self.num_envs = int(num_envs)
+        self.num_agents = int(num_agents)
+        self.params = dict(params or DEFAULT_PARAMS)
+        self.timestep = timestep
+        self.as_numpy = as_numpy
+        self.track = load_map(map, map_ext)
+        if spawn_poses is None:
+            spawn_poses = centerline_spawns(map.replace("_map", ""), self.num_agents)
+        self.spawn_poses = np.ascontiguousarray(spawn_poses, dtype=np.float64)
+        self.sim = BatchSim(self.track, n_envs=self.num_envs, n_agents=self.num_agents, params=self.params,
+                            device=device, seed=seed, timestep=timestep, ego_idx=ego_idx, noise_std=noise_std,
+                            autoreset=autoreset, spawn_poses=self.spawn_poses, env_offset=env_offset, **kwargs)
+        self.device = self.sim.device
+        B, A = self.sim.B, self.num_agents
+        x_min, x_max, y_min, y_max = self.track.bounds
+        self.single_observation_space = _box(
+            np.array([0.0] * B + [x_min, y_min, -np.pi, 0.0] * A, np.float32),
+            np.array([1.0] * B + [x_max, y_max, np.pi, 1.0] * A, np.float32))
+        low = np.array([self.params["s_min"], self.params["v_min"]], np.float32)
+        high = np.array([self.params["s_max"], self.params["v_max"]], np.float32)
+        self.single_action_space = _box(np.tile(low, (A, 1)), np.tile(high, (A, 1)))
+        self._rng = np.random.default_rng(seed)
+
+    # ------------------------------------------------------------------
+    def _infos(self, out):
+        st = self.sim.agent_states()  # [E, A, 7]
+        infos = {
+            "poses_x": st[..., 0].float(), "poses_y": st[..., 1].float(), "poses_theta": st[..., 4].float(),
+            "linear_vels_x": st[..., 3].float(), "ang_vels_z": st[..., 5].float(),
+            "collisions": out.collisions.to(torch.int8), "lap_times": out.lap_times.clone(),
+            "lap_counts": out.lap_counts.clone(), "scans": out.scans.clone(), "time": out.sim_time.clone(),
+            "reset": out.was_reset.bool(),
+        }
+        if self.as_numpy:
+            infos = {k: v.cpu().numpy() for k, v in infos.items()}
+        return infos
+
+    def reset(self, seed=None, options=None):
+        """options: poses [N, A, 3] (or [A, 3] for every env); default: spawn table draws."""
+        if seed is not None:
+            self._rng = np.random.default_rng(seed)
+        if options is None:
+            idx = self._rng.integers(0, self.spawn_poses.shape[0], self.num_envs)
+            options = self.spawn_poses[idx]
+        out = self.sim.reset(options)
+        obs = out.obs.clone()
+        return (obs.cpu().numpy() if self.as_numpy else obs), self._infos(out)
+
+    def step(self, actions):
+        a = torch.as_tensor(actions, device=self.device)
+        if a.dim() == 2 and self.num_agents == 1:
+            a = a.unsqueeze(1)
+        out = self.sim.step(a)
+        reset = out.was_reset.bool()
+        rewards = torch.where(reset, torch.zeros((), device=self.device),
+                              torch.full((), self.timestep, device=self.device)).float()
+        term = out.terminated.bool()
+        trunc = torch.zeros_like(term)
+        obs = out.obs.clone()
+        if self.as_numpy:
+            return (obs.cpu().numpy(), rewards.cpu().numpy(), term.cpu().numpy(), trunc.cpu().numpy(),
+                    self._infos(out))
+        return obs, rewards, term, trunc, self._infos(out)
+
+    def close(self):
+        if getattr(self, "sim", None) is not None:
+            self.sim.close()
+            self.sim = None

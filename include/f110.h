@@ -177,6 +177,15 @@ F110_API int f110_dynamics_batch(f110_ctx *ctx, const double *x, const double *u
 F110_API int f110_read_counters(f110_ctx *ctx, uint64_t *lookups, uint64_t *rays, void *stream);
 F110_API int f110_reset_counters(f110_ctx *ctx, void *stream);
 
+/* ---- per-kernel timing ----------------------------------------------------
+ * Records HIP events around each of the three launches of the next
+ * max_steps f110_step/f110_reset calls (k_agents, k_rays, k_post).
+ * f110_profile_end waits for them and returns the summed milliseconds per
+ * kernel and the number of steps recorded.  Used by bench.py for the
+ * roofline of the dominant kernel (k_rays). */
+F110_API int f110_profile_begin(f110_ctx *ctx, int32_t max_steps);
+F110_API int f110_profile_end(f110_ctx *ctx, double ms_out[3], int32_t *steps_out);
+
 /* ---- host-side test hooks (no device work) -------------------------------
  * The lookup tables f110_create uploads: ScanSimulator2D sines/cosines
  * (laser_models.py:379-381) and RaceCar's class-level beam tables

@@ -20,7 +20,16 @@ sp = centerline_spawns("Spielberg", 1)
 rng = np.random.default_rng(0)
 poses = sp[rng.integers(0, sp.shape[0], E), 0]
 poses = poses + np.stack([rng.normal(0, .2, E), rng.normal(0, .2, E), rng.normal(0, .2, E)], 1)
-sim = BatchSim(tm, n_envs=E, n_agents=1, noise_std=0.01, autoreset=True, spawn_poses=sp)
+sims = {}
+variants = {"K1": {}, "P4r16": {"F110_RAY_POOL": "4", "F110_REFILL_MIN": "16"},
+            "P8r16": {"F110_RAY_POOL": "8", "F110_REFILL_MIN": "16"}, "P8r32": {"F110_RAY_POOL": "8", "F110_REFILL_MIN": "32"},
+            "P16r24": {"F110_RAY_POOL": "16", "F110_REFILL_MIN": "24"}, "P8r8": {"F110_RAY_POOL": "8", "F110_REFILL_MIN": "8"}}
+for K, envs in variants.items():
+    for k in ("F110_RAY_POOL", "F110_REFILL_MIN", "F110_RAYS_PER_THREAD"):
+        os.environ.pop(k, None)
+    os.environ.update(envs)
+    sims[K] = BatchSim(tm, n_envs=E, n_agents=1, noise_std=0.01, autoreset=True, spawn_poses=sp, keep_f64_scans=True)
+sim = sims["K1"]
 pt = torch.as_tensor(poses, device="cuda")
 scans = torch.empty(E, 1080, dtype=torch.float64, device="cuda")
 res = {}
@@ -35,8 +44,22 @@ os.environ["F110_SCAN_VARIANT"] = "1"
 res["scan_batch_div_ms"] = timeit(lambda: sim.scan_batch(pt))
 os.environ["F110_SCAN_VARIANT"] = "0"
 res["scan_batch_ms_again"] = timeit(lambda: sim.scan_batch(pt))
-sim.reset(sp[rng.integers(0, sp.shape[0], E)])
 acts = torch.rand(E, 1, 2, device="cuda"); acts[..., 0] = acts[..., 0] * 0.8378 - 0.4189; acts[..., 1] *= 20
-for _ in range(50): sim.step(acts, minimal_outputs=True)
-res["step_ms"] = timeit(lambda: sim.step(acts, minimal_outputs=True), n=50)
+p0 = sp[rng.integers(0, sp.shape[0], E)]
+for rnd in range(3):  # interleaved rounds (A/B in one process)
+    for K, sm in sims.items():
+        sm.reset(p0)
+        for _ in range(30): sm.step(acts, minimal_outputs=True)
+        sm.profile_begin(100)
+        t = timeit(lambda: sm.step(acts, minimal_outputs=True), n=100, warm=0)
+        pk = sm.profile_end()
+        res.setdefault(f"step_ms_{K}", []).append(round(t, 4))
+        res.setdefault(f"rays_ms_{K}", []).append(round(pk["k_rays_ms"], 4))
+# parity of the variants: same inputs -> identical scans
+outs = {}
+for K, sm in sims.items():
+    sm.reset(p0); o = sm.step(acts)
+    outs[K] = o.scans_f64.clone()
+res["variants_identical"] = all(bool(torch.equal(outs["K1"], v)) for v in outs.values())
+res["agents_ms"] = round(pk["k_agents_ms"], 4); res["post_ms"] = round(pk["k_post_ms"], 4)
 print(json.dumps(res))

@@ -1,0 +1,82 @@
+"""Collect the rocprofv3 evidence for one round (run on the GPU box).
+
+  python scripts/profile_round.py r01
+
+1. kernel trace + stats of `bench.py` (same command as the headline, fewer
+   steps, no cpu leg) -> profiles/<tag>_kernel_stats.csv (+ summary json)
+2. PMC passes, one counter group per run (FETCH_SIZE, WRITE_SIZE,
+   TCC_HIT/TCC_MISS): per-launch HBM-side bytes of k_rays -> profiles/pmc_traffic.json
+   FETCH_SIZE/WRITE_SIZE are in KiB per dispatch (rocprofv3 derived counters).
+The parent process never touches the GPU; rocprofv3 launches python itself.
+"""
+import csv, glob, json, os, shutil, subprocess, sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+OUT = os.path.join(REPO, "gpurun_out", f"prof_{tag}")
+PROF = os.path.join(REPO, "profiles")
+os.makedirs(PROF, exist_ok=True)
+BENCH = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "300", "--warmup", "50", "--no-cpu-baseline"]
+env = dict(os.environ, TMPDIR="/tmp")
+
+
+def run(name, extra, timeout=400):
+    d = os.path.join(OUT, name)
+    shutil.rmtree(d, ignore_errors=True)
+    cmd = ["rocprofv3"] + extra + ["--output-format", "csv", "-d", d, "-o", "run", "--"] + BENCH
+    print(" ".join(cmd), flush=True)
+    with open(os.path.join(OUT, f"{name}.log"), "w") as log:
+        subprocess.run(["timeout", "-k", "10", str(timeout)] + cmd, cwd="/tmp", env=env, stdout=log,
+                       stderr=subprocess.STDOUT, check=True)
+    return d
+
+
+def find(d, suffix):
+    hits = glob.glob(os.path.join(d, "**", f"*{suffix}"), recursive=True)
+    if not hits:
+        raise FileNotFoundError(f"{suffix} under {d}")
+    return hits[0]
+
+
+def counters(d, kernel="k_rays"):
+    path = find(d, "counter_collection.csv")
+    vals = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel in row.get("Kernel_Name", ""):
+                vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}, path
+
+
+os.makedirs(OUT, exist_ok=True)
+d = run("trace", ["--kernel-trace", "--stats"])
+stats = find(d, "kernel_stats.csv")
+shutil.copy(stats, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+summary = {}
+with open(stats) as f:
+    for row in csv.DictReader(f):
+        summary[row["Name"][:80]] = {k: row[k] for k in ("Calls", "TotalDurationNs", "AverageNs", "Percentage")
+                                     if k in row}
+json.dump(summary, open(os.path.join(PROF, f"{tag}_kernel_stats.json"), "w"), indent=1)
+
+res = {"kernel": "k_rays", "envs": 8192, "agents": 1}
+for grp in (["FETCH_SIZE"], ["WRITE_SIZE"], ["TCC_HIT_sum", "TCC_MISS_sum"]):
+    name = "pmc_" + "_".join(g.lower() for g in grp)
+    try:
+        dd = run(name, ["--pmc"] + grp)
+        v, path = counters(dd)
+        res.update(v)
+        shutil.copy(path, os.path.join(PROF, f"{tag}_{name}.csv"))
+    except Exception as exc:  # record, do not hide
+        res[name + "_error"] = repr(exc)
+if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
+    res["fetch_bytes"] = res["FETCH_SIZE"] * 1024.0
+    res["write_bytes"] = res["WRITE_SIZE"] * 1024.0
+    res["bytes_per_launch"] = res["fetch_bytes"] + res["write_bytes"]
+    res["note"] = ("FETCH_SIZE/WRITE_SIZE (KiB) per k_rays dispatch; gather widths are uncalibrated on gfx950 "
+                   "(MI355X_MICROARCH.md HBM section: 16-B streaming reads report 1/2); Infinity-Cache hits are "
+                   "counted by these TCC_EA counters")
+if "TCC_HIT_sum" in res:
+    res["l2_hit_rate"] = res["TCC_HIT_sum"] / max(1.0, res["TCC_HIT_sum"] + res["TCC_MISS_sum"])
+json.dump(res, open(os.path.join(PROF, "pmc_traffic.json"), "w"), indent=1)
+print(json.dumps(res))
