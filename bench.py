@@ -116,8 +116,9 @@ def main():
     rank, world, local = D.init()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device(f"cuda:{local}")
+    dev_index = D.local_device_index(local)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device(f"cuda:{dev_index}")
     E, A = args.envs_per_gpu, args.agents
     shard = D.shard_range(E * world, world, rank)
 

@@ -42,6 +42,9 @@ struct f110_ctx {
     double inc = 0, beam_incr = 0;
     int n_spawn = 0;
     // device buffers
+    double *dt_tiled = nullptr;
+    int32_t wt = 0, tiles_h = 0;
+    int ray_kernel = 1;  // F110_RAY_KERNEL=0 selects the row-major k_rays (A/B)
     double *dt = nullptr, *sines = nullptr, *cosines = nullptr, *angles = nullptr, *beam_cos = nullptr,
            *side = nullptr, *spawn = nullptr;
     double *st = nullptr, *sb = nullptr, *start = nullptr, *sim_time = nullptr, *ray0 = nullptr, *scan = nullptr;
@@ -330,6 +333,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     c->beam_incr = C.fov / (double)(C.n_beams - 1);
     c->n_spawn = n_spawn;
     if (const char *v = std::getenv("F110_RAY_POOL")) c->pool = std::atoi(v);
+    if (const char *v = std::getenv("F110_RAY_KERNEL")) c->ray_kernel = std::atoi(v);
     if (const char *v = std::getenv("F110_REFILL_MIN")) c->refill_min = std::atoi(v);
     if (const char *v = std::getenv("F110_RAYS_PER_THREAD")) {
         int k = std::atoi(v);
@@ -350,6 +354,9 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
 
     const size_t N = (size_t)H * W;
     ALLOC(c->dt, N);
+    c->wt = (W + 3) / 4;
+    c->tiles_h = (H + 3) / 4;
+    ALLOC(c->dt_tiled, (size_t)c->wt * c->tiles_h * 16);
     ALLOC(c->sines, (size_t)C.theta_dis);
     ALLOC(c->cosines, (size_t)C.theta_dis);
     ALLOC(c->angles, (size_t)C.n_beams);
@@ -380,10 +387,15 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     // dt = res * EDT (get_dt, laser_models.py:52) — bit-exact from the integer k.
     std::vector<double> dt(N);
     for (size_t i = 0; i < N; ++i) dt[i] = resolution * std::sqrt((double)edt_k[i]);
+    std::vector<double> dtt((size_t)c->wt * c->tiles_h * 16, 0.0);  // padding cells are never read
+    for (int r = 0; r < H; ++r)
+        for (int q = 0; q < W; ++q) dtt[(size_t)tiled_index(c->wt, r, q)] = dt[(size_t)r * W + q];
     std::vector<double> s(C.theta_dis), co(C.theta_dis), an(C.n_beams), bc(C.n_beams), sd(C.n_beams);
     f110_host_tables(C.theta_dis, C.n_beams, C.fov, params, s.data(), co.data(), an.data(), bc.data(), sd.data());
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipMemcpy(c->dt, dt.data(), N * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(c->dt_tiled, dtt.data(), dtt.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->sines, s.data(), s.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->cosines, co.data(), co.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->angles, an.data(), an.size() * sizeof(double), hipMemcpyHostToDevice);
@@ -411,9 +423,30 @@ extern "C" int f110_destroy(f110_ctx *ctx) {
     return F110_OK;
 }
 
+static TiledMapView tiled_view(const f110_ctx *c) {
+    const MapView m = map_view(c);
+    TiledMapView t;
+    t.dt = c->dt_tiled;
+    t.H = c->H;
+    t.W = c->W;
+    t.wt = c->wt;
+    t.oob = tiled_index(c->wt, c->H - 1, c->W - 1);
+    t.res = m.res;
+    t.inv_res = m.inv_res;
+    t.ox = m.ox;
+    t.oy = m.oy;
+    t.oc = m.oc;
+    t.os = m.os;
+    t.wres = m.wres;
+    t.hres = m.hres;
+    return t;
+}
+
 static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     StepArgs a{};
     a.map = map_view(c);
+    a.tmap = tiled_view(c);
+    a.ray_kernel = c->ray_kernel;
     a.sines = c->sines;
     a.cosines = c->cosines;
     a.angles = c->angles;

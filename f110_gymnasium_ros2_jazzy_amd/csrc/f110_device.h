@@ -234,6 +234,58 @@ F110_HD int64_t cell_index_fast(const MapView &m, double x, double y) {
     return lin < m.n ? lin : m.n - 1;
 }
 
+// The EDT in 4x4-cell tiles (16 f64 = one 128-B cache line): the 64 lanes of
+// a wave trace 64 neighbouring beams whose samples form a short arc of cells
+// in ANY direction; square tiles bound the cache lines that arc touches,
+// where row-major lines are 16 x 1 cells and an arc along a column touches
+// one line per cell.
+struct TiledMapView {
+    const double *dt;  // [(Hp/4)*(Wp/4)][16], Hp/Wp = H/W rounded up to 4
+    int32_t H, W, wt;  // wt = Wp / 4 tiles per tile-row
+    int32_t oob;       // tiled index of dt[H-1][W-1] (the reference's dt[-1,-1])
+    double res, inv_res, ox, oy, oc, os, wres, hres;
+};
+
+F110_HD int32_t tiled_index(int32_t wt, int32_t r, int32_t c) {
+    return (((r >> 2) * wt + (c >> 2)) << 4) + ((r & 3) << 2) + (c & 3);
+}
+
+// xy_2_rc + distance_transform (laser_models.py:55-104) on the tiled EDT.
+// ROT = false when the map's origin yaw is exactly 0 (cos = 1, sin = 0): then
+// x_rot = x_trans*1 + y_trans*0 == x_trans for every finite input (a NaN or
+// inf input still lands off-map), so the rotation is skipped bit-exactly.
+template <bool ROT>
+F110_HD int32_t tiled_cell(const TiledMapView &m, double x, double y) {
+    double xr = x - m.ox;
+    double yr = y - m.oy;
+    if (ROT) {
+        const double xt = xr, yt = yr;
+        xr = xt * m.oc + yt * m.os;
+        yr = -xt * m.os + yt * m.oc;
+    }
+    const bool inb = (xr >= 0) & (xr < m.wres) & (yr >= 0) & (yr < m.hres);  // false for NaN
+    const double qx = xr * m.inv_res, qy = yr * m.inv_res;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double fx = __builtin_amdgcn_fract(qx), fy = __builtin_amdgcn_fract(qy);
+#else
+    const double fx = qx - floor(qx), fy = qy - floor(qy);
+#endif
+    int32_t c = (int32_t)qx, r = (int32_t)qy;
+    // guard band (see trunc_div): near an integer the IEEE quotient decides
+    const double band = fmax(fabs(fx - 0.5), fabs(fy - 0.5));
+    if (inb && band > 0.5 - 1e-9) {
+        c = (int32_t)(xr / m.res);
+        r = (int32_t)(yr / m.res);
+        if (c >= m.W) {  // int(x_rot/res) == W: the reference reads dt[r, W] = dt[r+1, 0] (row-major, no bounds check)
+            int64_t lin = (int64_t)r * m.W + c;
+            if (lin >= (int64_t)m.H * m.W) return m.oob;
+            r = (int32_t)(lin / m.W);
+            c = (int32_t)(lin - (int64_t)r * m.W);
+        }
+    }
+    return inb ? tiled_index(m.wt, r, c) : m.oob;
+}
+
 // ------------------------------------------------------ beam index runs --
 // get_scan's beam index (laser_models.py:167-184) is a SEQUENTIAL float
 // accumulation t_{i+1} = wrap(fl(t_i + inc)).  Inside one binade [2^(e-1), 2^e)

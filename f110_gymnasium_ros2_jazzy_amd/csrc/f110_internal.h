@@ -18,6 +18,7 @@ constexpr int kCtrStride = 16;  // u64 per slot (128 B)
 // Everything one launch of the fused env-step kernel needs, passed by value.
 struct StepArgs {
     MapView map;
+    TiledMapView tmap;
     const double *sines, *cosines;            // [theta_dis]  ScanSimulator2D tables
     const double *angles, *beam_cos, *side;   // [B] RaceCar class-level beam tables
     f110_params p;
@@ -25,6 +26,7 @@ struct StepArgs {
     int32_t rays_per_thread;  // k_rays ILP (1, 2 or 4)
     int32_t pool;             // >0: k_rays_pool with this many rays per lane (4, 8, 16)
     int32_t refill_min;       // k_rays_pool: parked lanes that trigger a refill
+    int32_t ray_kernel;       // 0: k_rays<1> on the row-major EDT; 1: k_rays_tiled (default)
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
     uint64_t seed;
     int64_t env_offset;

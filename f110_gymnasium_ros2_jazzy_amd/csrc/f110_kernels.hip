@@ -220,6 +220,47 @@ __global__ void __launch_bounds__(kBlock) k_rays(StepArgs a) {
 }
 
 // ------------------------------------------------------------------------
+// k_rays_tiled: one thread per ray on the 4x4-tiled EDT, with the rotation
+// compiled out for axis-aligned maps.  Same results as k_rays, bit for bit.
+template <bool ROT>
+__global__ void __launch_bounds__(kBlock) k_rays_tiled(StepArgs a) {
+    const int EA = a.E * a.A;
+    const int B = a.B;
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    uint32_t n = 0;
+    if (r < (int64_t)EA * B) {
+        const int g = (int)(r / B);
+        const int b = (int)(r - (int64_t)g * B);
+        const int e = g / a.A;
+        if (!(a.mode == 1 && a.reset_mask && !a.reset_mask[e])) {
+            double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
+            int ti = (int)t;  // int(theta_index), laser_models.py:124
+            if (ti >= a.theta_dis) ti = 0;
+            const double c = a.cosines[ti], s = a.sines[ti];
+            double x = a.ray0[g], y = a.ray0[EA + g];
+            double d = a.ray0[2 * EA + g];  // :129
+            double tot = d;                 // :130
+            uint32_t k = 1;
+            const TiledMapView &m = a.tmap;
+            const double eps = a.eps, mr = a.max_range;
+            while (d > eps && tot <= mr) {  // :133
+                x += d * c;                 // :135
+                y += d * s;                 // :136
+                d = m.dt[tiled_cell<ROT>(m, x, y)];
+                tot += d;                   // :141
+                ++k;
+            }
+            n = k;
+            double range = tot > mr ? mr : tot;  // :143-144
+            if (a.noise_std > 0.0)  // ScanSimulator2D.scan: noise after the clamp (laser_models.py:450-452)
+                range += a.noise_std * (double)beam_normal(a.seed, (uint64_t)(a.env_offset + e), a.noise_step[e], b);
+            a.scan[r] = range;
+        }
+    }
+    if (a.ctr) count_rays(a.ctr, n);
+}
+
+// ------------------------------------------------------------------------
 // k_rays_pool: every wave owns a pool of P*64 consecutive rays.  Lanes whose
 // ray finished park (result in registers); once at least `refill` lanes are
 // parked, they are finalised (noise, store) and re-armed with the next rays
@@ -509,7 +550,13 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     const int K = a.rays_per_thread;
     const int64_t T = (R + K - 1) / K;
     const dim3 grid((unsigned)((T + kBlock - 1) / kBlock));
-    if (a.pool > 0) {
+    if (a.ray_kernel == 1 && a.pool == 0 && K == 1) {
+        const dim3 g1((unsigned)((R + kBlock - 1) / kBlock));
+        if (a.tmap.os == 0.0 && a.tmap.oc == 1.0)
+            hipLaunchKernelGGL(k_rays_tiled<false>, g1, dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_rays_tiled<true>, g1, dim3(kBlock), 0, s, a);
+    } else if (a.pool > 0) {
         const int64_t per_block = (int64_t)kBlock * a.pool;  // 4 waves x 64 lanes x P rays
         const dim3 pg((unsigned)((R + per_block - 1) / per_block));
         if (a.pool == 8)

@@ -38,17 +38,24 @@ def env_rank_world():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
 
 
+def local_device_index(local_rank: int) -> int:
+    """GPU of this rank: LOCAL_RANK (one process per GPU).  F110_SAME_DEVICE=1
+    maps every rank to GPU 0 (rehearsing the multi-rank path on a 1-GPU box)."""
+    return 0 if os.environ.get("F110_SAME_DEVICE") == "1" else local_rank
+
+
 def init(backend: str | None = None) -> tuple[int, int, int]:
     """Initialise torch.distributed from torchrun's env (no-op for world 1)."""
     rank, world, local = env_rank_world()
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = backend or os.environ.get("F110_DIST_BACKEND")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         kw = {}
         if backend == "nccl":
-            torch.cuda.set_device(local)
-            kw["device_id"] = torch.device(f"cuda:{local}")
+            torch.cuda.set_device(local_device_index(local))
+            kw["device_id"] = torch.device(f"cuda:{local_device_index(local)}")
         dist.init_process_group(backend=backend, **kw)
     return rank, world, local
 

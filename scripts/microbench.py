@@ -21,11 +21,9 @@ rng = np.random.default_rng(0)
 poses = sp[rng.integers(0, sp.shape[0], E), 0]
 poses = poses + np.stack([rng.normal(0, .2, E), rng.normal(0, .2, E), rng.normal(0, .2, E)], 1)
 sims = {}
-variants = {"K1": {}, "P4r16": {"F110_RAY_POOL": "4", "F110_REFILL_MIN": "16"},
-            "P8r16": {"F110_RAY_POOL": "8", "F110_REFILL_MIN": "16"}, "P8r32": {"F110_RAY_POOL": "8", "F110_REFILL_MIN": "32"},
-            "P16r24": {"F110_RAY_POOL": "16", "F110_REFILL_MIN": "24"}, "P8r8": {"F110_RAY_POOL": "8", "F110_REFILL_MIN": "8"}}
+variants = {"K1": {"F110_RAY_KERNEL": "0"}, "tiled": {"F110_RAY_KERNEL": "1"}}
 for K, envs in variants.items():
-    for k in ("F110_RAY_POOL", "F110_REFILL_MIN", "F110_RAYS_PER_THREAD"):
+    for k in ("F110_RAY_POOL", "F110_REFILL_MIN", "F110_RAYS_PER_THREAD", "F110_RAY_KERNEL"):
         os.environ.pop(k, None)
     os.environ.update(envs)
     sims[K] = BatchSim(tm, n_envs=E, n_agents=1, noise_std=0.01, autoreset=True, spawn_poses=sp, keep_f64_scans=True)

@@ -1,6 +1,8 @@
 """Collect the rocprofv3 evidence for one round (run on the GPU box).
 
-  python scripts/profile_round.py r01
+  python scripts/profile_round.py r01            # on the GPU box (via gpurun)
+  python scripts/profile_round.py r01 --collect  # here: raw csvs merged back under
+                                                 # gpurun_out/prof_r01 -> profiles/
 
 1. kernel trace + stats of `bench.py` (same command as the headline, fewer
    steps, no cpu leg) -> profiles/<tag>_kernel_stats.csv (+ summary json)
@@ -14,14 +16,17 @@ import csv, glob, json, os, shutil, subprocess, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 OUT = os.path.join(REPO, "gpurun_out", f"prof_{tag}")
-PROF = os.path.join(REPO, "profiles")
-os.makedirs(PROF, exist_ok=True)
+COLLECT = "--collect" in sys.argv
+# only gpurun_out/ comes back from the box: write there, copy into profiles/ locally
+PROF = os.path.join(REPO, "profiles") if COLLECT else os.path.join(OUT, "summary")
 BENCH = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "300", "--warmup", "50", "--no-cpu-baseline"]
 env = dict(os.environ, TMPDIR="/tmp")
 
 
 def run(name, extra, timeout=400):
     d = os.path.join(OUT, name)
+    if COLLECT:
+        return d
     shutil.rmtree(d, ignore_errors=True)
     cmd = ["rocprofv3"] + extra + ["--output-format", "csv", "-d", d, "-o", "run", "--"] + BENCH
     print(" ".join(cmd), flush=True)
@@ -38,17 +43,23 @@ def find(d, suffix):
     return hits[0]
 
 
-def counters(d, kernel="k_rays"):
+def counters(d, dst, kernel="k_rays"):
+    """Mean per-dispatch counter values for `kernel`; its rows are copied to dst."""
     path = find(d, "counter_collection.csv")
     vals = {}
-    with open(path) as f:
-        for row in csv.DictReader(f):
+    with open(path) as f, open(dst, "w", newline="") as g:
+        rd = csv.DictReader(f)
+        wr = csv.DictWriter(g, fieldnames=rd.fieldnames)
+        wr.writeheader()
+        for row in rd:
             if kernel in row.get("Kernel_Name", ""):
+                wr.writerow(row)
                 vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}, path
+    return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
 os.makedirs(OUT, exist_ok=True)
+os.makedirs(PROF, exist_ok=True)
 d = run("trace", ["--kernel-trace", "--stats"])
 stats = find(d, "kernel_stats.csv")
 shutil.copy(stats, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
@@ -64,9 +75,7 @@ for grp in (["FETCH_SIZE"], ["WRITE_SIZE"], ["TCC_HIT_sum", "TCC_MISS_sum"]):
     name = "pmc_" + "_".join(g.lower() for g in grp)
     try:
         dd = run(name, ["--pmc"] + grp)
-        v, path = counters(dd)
-        res.update(v)
-        shutil.copy(path, os.path.join(PROF, f"{tag}_{name}.csv"))
+        res.update(counters(dd, os.path.join(PROF, f"{tag}_{name}.csv")))
     except Exception as exc:  # record, do not hide
         res[name + "_error"] = repr(exc)
 if "FETCH_SIZE" in res and "WRITE_SIZE" in res:

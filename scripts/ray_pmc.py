@@ -1,0 +1,19 @@
+"""Counter-collection target: 100 f110_step launches at 8192 envs (bench
+workload), nothing else on the GPU.  Used with rocprofv3 --pmc."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np, torch
+from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
+from f110_gymnasium_ros2_jazzy_amd.maps import load_map, centerline_spawns
+E = int(os.environ.get("MB_ENVS", 8192))
+sp = centerline_spawns("Spielberg", 1)
+sim = BatchSim(load_map("Spielberg_map"), n_envs=E, n_agents=1, autoreset=True, spawn_poses=sp)
+rng = np.random.default_rng(0)
+sim.reset(sp[rng.integers(0, sp.shape[0], E)])
+g = torch.Generator(device="cuda"); g.manual_seed(0)
+acts = torch.rand(100, E, 1, 2, device="cuda", generator=g)
+acts[..., 0] = acts[..., 0] * 0.8378 - 0.4189; acts[..., 1] *= 20
+for k in range(100):
+    sim.step(acts[k], minimal_outputs=True)
+torch.cuda.synchronize()
+print("done")
