@@ -47,6 +47,7 @@ EXPORTS = [
     "f110_create", "f110_destroy", "f110_reset", "f110_step", "f110_get_state", "f110_set_state",
     "f110_scan_batch", "f110_dynamics_batch", "f110_read_counters", "f110_reset_counters",
     "f110_profile_begin", "f110_profile_end", "f110_host_tables", "f110_host_beam_indices",
+    "f110_set_scan_noise", "f110_set_params", "f110_host_cell_index",
 ]
 
 _lib = None
@@ -96,6 +97,9 @@ def load(build_if_missing: bool = True):
     L.f110_dynamics_batch.argtypes = [_P, _P, _P, _P, i64, _P]
     L.f110_read_counters.argtypes = [_P, ctypes.POINTER(u64), ctypes.POINTER(u64), _P]
     L.f110_reset_counters.argtypes = [_P, _P]
+    L.f110_set_scan_noise.argtypes = [_P, _P]
+    L.f110_host_cell_index.argtypes = [i32, i32, ctypes.c_double, _D, _P, i64, _P]
+    L.f110_set_params.argtypes = [_P, ctypes.POINTER(F110Params), i32, _P]
     L.f110_profile_begin.argtypes = [_P, i32]
     L.f110_profile_end.argtypes = [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
     L.f110_host_tables.argtypes = [i32, i32, ctypes.c_double, ctypes.POINTER(F110Params), _P, _P, _P, _P, _P]

@@ -36,7 +36,9 @@ int fail(int code, const std::string &msg) {
 struct f110_ctx {
     int device = 0;
     f110_config cfg{};
-    f110_params p{};
+    f110_params p{};                 // Simulator-level params (fixed at create)
+    std::vector<f110_params> agent_p;  // RaceCar params per agent (f110_set_params)
+    f110_params *pa = nullptr;       // device copy of agent_p
     int H = 0, W = 0;
     double res = 0, origin[3] = {0, 0, 0};
     double inc = 0, beam_incr = 0;
@@ -60,9 +62,7 @@ struct f110_ctx {
     // f110_profile_begin/end
     std::vector<hipEvent_t> prof_ev;  // 4 per recorded step
     int prof_max = 0, prof_n = 0;
-    int rays_per_thread = 1;  // k_rays ILP; F110_RAYS_PER_THREAD overrides (A/B experiments)
-    int pool = 0;             // F110_RAY_POOL: rays per lane of k_rays_pool (0 = k_rays)
-    int refill_min = 16;      // F110_REFILL_MIN
+    const double *noise_ext = nullptr;  // f110_set_scan_noise (caller-owned)
 
     hipEvent_t *next_prof_events() {
         if (prof_n >= prof_max) return nullptr;
@@ -274,22 +274,42 @@ static bool is_gfx950(int dev) {
     return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
 }
 
-static MapView map_view(const f110_ctx *c) {
+static MapView make_map_view(const double *dt, int32_t H, int32_t W, double res, const double origin[3]) {
     MapView m;
-    m.dt = c->dt;
-    m.H = c->H;
-    m.W = c->W;
-    m.n = (int64_t)c->H * c->W;
-    m.res = c->res;
-    m.ox = c->origin[0];
-    m.oy = c->origin[1];
-    m.oc = std::cos(c->origin[2]);  // laser_models.py:421-422 (np.sin/np.cos of the yaml yaw)
-    m.os = std::sin(c->origin[2]);
-    m.wres = (double)c->W * c->res;
-    m.hres = (double)c->H * c->res;
-    m.inv_res = 1.0 / c->res;
+    m.dt = dt;
+    m.H = H;
+    m.W = W;
+    m.n = (int64_t)H * W;
+    m.res = res;
+    m.ox = origin[0];
+    m.oy = origin[1];
+    m.oc = std::cos(origin[2]);  // laser_models.py:421-422 (np.sin/np.cos of the yaml yaw)
+    m.os = std::sin(origin[2]);
+    m.wres = (double)W * res;
+    m.hres = (double)H * res;
+    m.inv_res = 1.0 / res;
     return m;
 }
+
+static TiledMapView make_tiled_view(const MapView &m, const double *dt_tiled) {
+    TiledMapView t;
+    t.dt = dt_tiled;
+    t.H = m.H;
+    t.W = m.W;
+    t.wt = (m.W + 3) / 4;
+    t.oob = tiled_index(t.wt, m.H - 1, m.W - 1);
+    t.res = m.res;
+    t.inv_res = m.inv_res;
+    t.ox = m.ox;
+    t.oy = m.oy;
+    t.oc = m.oc;
+    t.os = m.os;
+    t.wres = m.wres;
+    t.hres = m.hres;
+    return t;
+}
+
+static MapView map_view(const f110_ctx *c) { return make_map_view(c->dt, c->H, c->W, c->res, c->origin); }
 
 static int use_device(const f110_ctx *c) {
     int cur = -1;
@@ -332,13 +352,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     c->inc = (double)C.theta_dis * (C.fov / (double)(C.n_beams - 1)) / (2. * kPi);  // laser_models.py:367-368
     c->beam_incr = C.fov / (double)(C.n_beams - 1);
     c->n_spawn = n_spawn;
-    if (const char *v = std::getenv("F110_RAY_POOL")) c->pool = std::atoi(v);
-    if (const char *v = std::getenv("F110_RAY_KERNEL")) c->ray_kernel = std::atoi(v);
-    if (const char *v = std::getenv("F110_REFILL_MIN")) c->refill_min = std::atoi(v);
-    if (const char *v = std::getenv("F110_RAYS_PER_THREAD")) {
-        int k = std::atoi(v);
-        c->rays_per_thread = (k == 1 || k == 2 || k == 4) ? k : c->rays_per_thread;
-    }
+    if (const char *v = std::getenv("F110_RAY_KERNEL")) c->ray_kernel = std::atoi(v) == 0 ? 0 : 1;
     const size_t EA = (size_t)C.n_envs * C.n_agents;
 
     auto cleanup = [&](int code, const std::string &msg) {
@@ -381,6 +395,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     ALLOC(c->episode, (size_t)C.n_envs);
     ALLOC(c->nstep, (size_t)C.n_envs);
     ALLOC(c->ctr, (size_t)kCtrSlots * kCtrStride);
+    ALLOC(c->pa, (size_t)C.n_agents);
     if (spawn_poses && n_spawn > 0) ALLOC(c->spawn, (size_t)n_spawn * C.n_agents * 3);
 #undef ALLOC
 
@@ -401,6 +416,9 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (e == hipSuccess) e = hipMemcpy(c->angles, an.data(), an.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->beam_cos, bc.data(), bc.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->side, sd.data(), sd.size() * sizeof(double), hipMemcpyHostToDevice);
+    c->agent_p.assign((size_t)C.n_agents, *params);
+    if (e == hipSuccess)
+        e = hipMemcpy(c->pa, c->agent_p.data(), c->agent_p.size() * sizeof(f110_params), hipMemcpyHostToDevice);
     if (e == hipSuccess && c->spawn)
         e = hipMemcpy(c->spawn, spawn_poses, (size_t)n_spawn * C.n_agents * 3 * sizeof(double),
                       hipMemcpyHostToDevice);
@@ -423,24 +441,7 @@ extern "C" int f110_destroy(f110_ctx *ctx) {
     return F110_OK;
 }
 
-static TiledMapView tiled_view(const f110_ctx *c) {
-    const MapView m = map_view(c);
-    TiledMapView t;
-    t.dt = c->dt_tiled;
-    t.H = c->H;
-    t.W = c->W;
-    t.wt = c->wt;
-    t.oob = tiled_index(c->wt, c->H - 1, c->W - 1);
-    t.res = m.res;
-    t.inv_res = m.inv_res;
-    t.ox = m.ox;
-    t.oy = m.oy;
-    t.oc = m.oc;
-    t.os = m.os;
-    t.wres = m.wres;
-    t.hres = m.hres;
-    return t;
-}
+static TiledMapView tiled_view(const f110_ctx *c) { return make_tiled_view(map_view(c), c->dt_tiled); }
 
 static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     StepArgs a{};
@@ -471,9 +472,6 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.beam_incr = c->beam_incr;
     a.seed = c->cfg.seed;
     a.env_offset = c->cfg.env_offset;
-    a.rays_per_thread = c->rays_per_thread;
-    a.pool = c->pool;
-    a.refill_min = c->refill_min;
     a.st = c->st;
     a.sb = c->sb;
     a.scnt = c->scnt;
@@ -492,6 +490,8 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.scan = c->scan;
     a.reset_flag = c->reset_flag;
     a.noise_step = c->noise_step;
+    a.noise_ext = c->noise_ext;
+    a.pa = c->pa;
     a.spawn = c->spawn;
     a.n_spawn = c->n_spawn;
     if (out) a.out = *out;
@@ -601,6 +601,26 @@ extern "C" int f110_read_counters(f110_ctx *ctx, uint64_t *lookups, uint64_t *ra
     return F110_OK;
 }
 
+extern "C" int f110_set_params(f110_ctx *ctx, const f110_params *params, int32_t agent_idx, void *stream) {
+    if (!ctx || !params) return fail(F110_E_INVALID, "f110_set_params: null argument");
+    if (agent_idx >= ctx->cfg.n_agents)  // Simulator.update_params raises IndexError (base_classes.py:544-546)
+        return fail(F110_E_INVALID, "f110_set_params: Index given is out of bounds for list of agents.");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    for (int i = 0; i < ctx->cfg.n_agents; ++i)
+        if (agent_idx < 0 || i == agent_idx) ctx->agent_p[(size_t)i] = *params;
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemcpyAsync(ctx->pa, ctx->agent_p.data(), ctx->agent_p.size() * sizeof(f110_params),
+                           hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));  // agent_p may change again before an async copy would have read it
+    return F110_OK;
+}
+
+extern "C" int f110_set_scan_noise(f110_ctx *ctx, const double *noise) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_set_scan_noise: null context");
+    ctx->noise_ext = noise;
+    return F110_OK;
+}
+
 extern "C" int f110_reset_counters(f110_ctx *ctx, void *stream) {
     if (!ctx) return fail(F110_E_INVALID, "f110_reset_counters: null context");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
@@ -644,5 +664,25 @@ extern "C" int f110_profile_end(f110_ctx *ctx, double ms_out[3], int32_t *steps_
         for (int k = 0; k < 3; ++k) ms_out[k] = acc[k];
     if (steps_out) *steps_out = ctx->prof_n;
     ctx->free_prof();
+    return F110_OK;
+}
+
+extern "C" int f110_host_cell_index(int32_t H, int32_t W, double resolution, const double origin[3],
+                                    const double *xy, int64_t n, int64_t *lin_out) {
+    if (H <= 0 || W <= 0 || !(resolution > 0) || !origin || (n > 0 && (!xy || !lin_out)))
+        return fail(F110_E_INVALID, "f110_host_cell_index: bad arguments");
+    const MapView m = make_map_view(nullptr, H, W, resolution, origin);
+    const TiledMapView t = make_tiled_view(m, nullptr);
+    const bool rot = !(t.os == 0.0 && t.oc == 1.0);
+    for (int64_t i = 0; i < n; ++i) {
+        const double x = xy[2 * i], y = xy[2 * i + 1];
+        lin_out[3 * i] = cell_index(m, x, y);
+        lin_out[3 * i + 1] = cell_index_fast(m, x, y);
+        const int32_t q = rot ? tiled_cell<true>(t, x, y) : tiled_cell<false>(t, x, y);
+        const int32_t tile = q >> 4, within = q & 15;
+        const int64_t r = (int64_t)(tile / t.wt) * 4 + (within >> 2);
+        const int64_t c = (int64_t)(tile % t.wt) * 4 + (within & 3);
+        lin_out[3 * i + 2] = r * W + c;
+    }
     return F110_OK;
 }

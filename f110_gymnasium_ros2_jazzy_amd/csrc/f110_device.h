@@ -276,12 +276,14 @@ F110_HD int32_t tiled_cell(const TiledMapView &m, double x, double y) {
     if (inb && band > 0.5 - 1e-9) {
         c = (int32_t)(xr / m.res);
         r = (int32_t)(yr / m.res);
-        if (c >= m.W) {  // int(x_rot/res) == W: the reference reads dt[r, W] = dt[r+1, 0] (row-major, no bounds check)
-            int64_t lin = (int64_t)r * m.W + c;
-            if (lin >= (int64_t)m.H * m.W) return m.oob;
-            r = (int32_t)(lin / m.W);
-            c = (int32_t)(lin - (int64_t)r * m.W);
+        // x_rot < W*res and y_rot < H*res, yet the rounded quotient can reach W
+        // (or H) exactly.  Same cell as cell_index's flat row-major read:
+        // dt[r, W] is dt[r+1, 0]; anything past the last cell is dt[-1, -1].
+        if (c >= m.W) {
+            c = 0;
+            ++r;
         }
+        if (r >= m.H) return m.oob;
     }
     return inb ? tiled_index(m.wt, r, c) : m.oob;
 }

@@ -21,12 +21,10 @@ struct StepArgs {
     TiledMapView tmap;
     const double *sines, *cosines;            // [theta_dis]  ScanSimulator2D tables
     const double *angles, *beam_cos, *side;   // [B] RaceCar class-level beam tables
-    f110_params p;
+    f110_params p;                            // Simulator / F110Env params (GJK boxes, lidar_max)
+    const f110_params *pa;                    // [A] RaceCar params (update_pose, ray_cast boxes)
     int32_t E, A, B, theta_dis, integrator, ego, autoreset, mode;  // mode 0 step, 1 reset
-    int32_t rays_per_thread;  // k_rays ILP (1, 2 or 4)
-    int32_t pool;             // >0: k_rays_pool with this many rays per lane (4, 8, 16)
-    int32_t refill_min;       // k_rays_pool: parked lanes that trigger a refill
-    int32_t ray_kernel;       // 0: k_rays<1> on the row-major EDT; 1: k_rays_tiled (default)
+    int32_t ray_kernel;       // 0: k_rays on the row-major EDT; 1: k_rays_tiled (default)
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
     uint64_t seed;
     int64_t env_offset;
@@ -50,6 +48,7 @@ struct StepArgs {
     double *scan;        // [E*A][B] ranges (noise added) before the collision stage
     uint8_t *reset_flag; // [E] this call reset the env
     uint64_t *noise_step;// [E] noise counter used by this step
+    const double *noise_ext;  // [E][B] caller-supplied scan noise (f110_set_scan_noise) or null
     const double *spawn; // [n_spawn][A][3]
     int32_t n_spawn;
     // inputs
@@ -59,6 +58,25 @@ struct StepArgs {
     const uint8_t *reset_mask;  // [E] or null
     f110_outputs out;
     unsigned long long *ctr;    // [kCtrSlots][16]: [0] lookups, [1] rays (see count_rays)
+};
+
+// k_rays_tiled's own argument block: only what the ray loop and its epilogue
+// read (the full StepArgs kept 90 SGPRs live: 7 instead of 8 blocks per CU).
+struct RayArgs {
+    TiledMapView m;
+    const double *sines, *cosines;
+    const double *ray0;        // [3][EA]
+    const BeamRun *runs;       // [EA][kMaxSeg]
+    const int32_t *nruns;      // [EA]
+    const uint8_t *reset_mask; // [E]: f110_reset with an env mask, else null
+    double *scan;              // [EA][B]
+    const double *noise_ext;   // [E][B] or null
+    const uint64_t *noise_step;// [E]
+    unsigned long long *ctr;
+    double eps, max_range, noise_std;
+    uint64_t seed;
+    int64_t env_offset;
+    int32_t EA, A, B, theta_dis;
 };
 
 struct ScanArgs {

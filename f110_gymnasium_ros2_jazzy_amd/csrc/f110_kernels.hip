@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
             vel = (double)a.actions[(size_t)g * 2 + 1];
         }
     }
-    update_pose(s, b0, b1, cnt, raw_steer, vel, a.p, a.dt, a.integrator);
+    update_pose(s, b0, b1, cnt, raw_steer, vel, a.pa[ag], a.dt, a.integrator);  // RaceCar.params (per agent)
 #pragma unroll
     for (int k = 0; k < 7; ++k) a.st[(size_t)k * EA + g] = s[k];
     a.sb[g] = b0;
@@ -144,86 +144,24 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
 }
 
 // ------------------------------------------------------------------------
-// k_rays: thread t traces the K consecutive rays r = K*t .. K*t+K-1
-// (ray r -> car g = r / B, beam b = r % B).  The K sphere traces are
-// interleaved step by step, so a lane keeps K independent EDT gathers in
-// flight (memory-level parallelism) while neighbouring beams, whose traces
-// have near-equal lengths, keep the lane's iterations in lock-step.
-template <int K>
-__global__ void __launch_bounds__(kBlock) k_rays(StepArgs a) {
-    const int EA = a.E * a.A;
-    const int B = a.B;
-    const int64_t R = (int64_t)EA * B;
-    const int64_t r0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * K;
-    const MapView &m = a.map;
-    double x[K], y[K], c[K], s[K], d[K], tot[K];
-    uint32_t n[K];
-    bool act[K], valid[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const int64_t r = r0 + k;
-        valid[k] = false;
-        act[k] = false;
-        n[k] = 0;
-        x[k] = y[k] = c[k] = s[k] = d[k] = tot[k] = 0.0;
-        if (r < R) {
-            const int g = (int)(r / B);
-            const int b = (int)(r - (int64_t)g * B);
-            const int e = g / a.A;
-            if (!(a.mode == 1 && a.reset_mask && !a.reset_mask[e])) {
-                double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
-                int ti = (int)t;  // int(theta_index), laser_models.py:124
-                if (ti >= a.theta_dis) ti = 0;
-                c[k] = a.cosines[ti];
-                s[k] = a.sines[ti];
-                x[k] = a.ray0[g];
-                y[k] = a.ray0[EA + g];
-                d[k] = a.ray0[2 * EA + g];  // :129
-                tot[k] = d[k];              // :130
-                n[k] = 1;
-                valid[k] = true;
-                act[k] = d[k] > a.eps && tot[k] <= a.max_range;  // :133
-            }
-        }
-    }
-    while (true) {
-        bool any = false;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (act[k]) {
-                x[k] += d[k] * c[k];  // :135
-                y[k] += d[k] * s[k];  // :136
-                d[k] = m.dt[cell_index_fast(m, x[k], y[k])];
-                tot[k] += d[k];       // :141
-                ++n[k];
-                act[k] = d[k] > a.eps && tot[k] <= a.max_range;
-            }
-            any = any || act[k];
-        }
-        if (!any) break;
-    }
-    uint32_t nsum = 0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        if (!valid[k]) continue;
-        const int64_t r = r0 + k;
-        const int g = (int)(r / B);
-        const int b = (int)(r - (int64_t)g * B);
-        const int e = g / a.A;
-        double range = tot[k] > a.max_range ? a.max_range : tot[k];  // :143-144
-        if (a.noise_std > 0.0)  // ScanSimulator2D.scan: noise after the clamp (laser_models.py:450-452)
-            range += a.noise_std * (double)beam_normal(a.seed, (uint64_t)(a.env_offset + e), a.noise_step[e], b);
-        a.scan[r] = range;
-        nsum += n[k];
-    }
-    if (a.ctr) count_rays(a.ctr, nsum, K);
+// Ray epilogue shared by the ray kernels: clamp, noise, store.
+// ScanSimulator2D.scan adds the noise after the clamp (laser_models.py:450-452).
+// Caller-supplied noise (f110_set_scan_noise: [E][B], shared by the env's
+// agents like the reference's equal-seeded per-car generators,
+// base_classes.py:119,204) wins over the device Philox stream.
+__device__ __forceinline__ void store_ray(const StepArgs &a, int64_t r, int e, int b, double tot) {
+    double range = tot > a.max_range ? a.max_range : tot;  // :143-144
+    if (a.noise_ext)
+        range += a.noise_ext[(size_t)e * a.B + b];
+    else if (a.noise_std > 0.0)
+        range += a.noise_std * (double)beam_normal(a.seed, (uint64_t)(a.env_offset + e), a.noise_step[e], b);
+    a.scan[r] = range;
 }
 
-// ------------------------------------------------------------------------
-// k_rays_tiled: one thread per ray on the 4x4-tiled EDT, with the rotation
-// compiled out for axis-aligned maps.  Same results as k_rays, bit for bit.
-template <bool ROT>
-__global__ void __launch_bounds__(kBlock) k_rays_tiled(StepArgs a) {
+// k_rays: one thread per ray (ray r -> car g = r / B, beam b = r % B) on the
+// row-major EDT.  Kept as the A/B baseline of k_rays_tiled (F110_RAY_KERNEL=0);
+// the two produce identical results.
+__global__ void __launch_bounds__(kBlock) k_rays(StepArgs a) {
     const int EA = a.E * a.A;
     const int B = a.B;
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -236,131 +174,66 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(StepArgs a) {
             double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
             int ti = (int)t;  // int(theta_index), laser_models.py:124
             if (ti >= a.theta_dis) ti = 0;
-            const double c = a.cosines[ti], s = a.sines[ti];
-            double x = a.ray0[g], y = a.ray0[EA + g];
-            double d = a.ray0[2 * EA + g];  // :129
-            double tot = d;                 // :130
-            uint32_t k = 1;
-            const TiledMapView &m = a.tmap;
-            const double eps = a.eps, mr = a.max_range;
-            while (d > eps && tot <= mr) {  // :133
-                x += d * c;                 // :135
-                y += d * s;                 // :136
-                d = m.dt[tiled_cell<ROT>(m, x, y)];
-                tot += d;                   // :141
-                ++k;
-            }
-            n = k;
-            double range = tot > mr ? mr : tot;  // :143-144
-            if (a.noise_std > 0.0)  // ScanSimulator2D.scan: noise after the clamp (laser_models.py:450-452)
-                range += a.noise_std * (double)beam_normal(a.seed, (uint64_t)(a.env_offset + e), a.noise_step[e], b);
-            a.scan[r] = range;
+            double tot = trace(a.map, a.ray0[g], a.ray0[EA + g], a.cosines[ti], a.sines[ti], a.ray0[2 * EA + g],
+                               a.eps, a.max_range, n);
+            store_ray(a, r, e, b, tot);
         }
     }
     if (a.ctr) count_rays(a.ctr, n);
 }
 
 // ------------------------------------------------------------------------
-// k_rays_pool: every wave owns a pool of P*64 consecutive rays.  Lanes whose
-// ray finished park (result in registers); once at least `refill` lanes are
-// parked, they are finalised (noise, store) and re-armed with the next rays
-// of the pool in ONE divergent phase, so the ~40-instruction ray set-up is
-// paid once per group instead of once per iteration.  Lanes stay busy until
-// the pool drains: the wave no longer waits for its longest ray.
-__device__ __forceinline__ void ray_init(const StepArgs &a, int64_t r, int EA, double &x, double &y, double &c,
-                                         double &s, double &d, double &tot) {
+// k_rays_tiled: one thread per ray on the 4x4-tiled EDT, with the rotation
+// compiled out for axis-aligned maps.  Same results as k_rays, bit for bit.
+//
+// One ray per lane, 8 waves per SIMD, no lane refill: the hardware wave
+// scheduler absorbs the ragged ray lengths.  Measured alternatives that lost
+// (DESIGN.md §3): 2 and 4 interleaved rays per lane (1.4x / 2x slower), a
+// per-wave ray pool with lane refill (1.35x slower).
+template <bool ROT, bool MASK>
+__global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
     const int B = a.B;
-    const int g = (int)(r / B);
-    const int b = (int)(r - (int64_t)g * B);
-    double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
-    int ti = (int)t;  // int(theta_index), laser_models.py:124
-    if (ti >= a.theta_dis) ti = 0;
-    c = a.cosines[ti];
-    s = a.sines[ti];
-    x = a.ray0[g];
-    y = a.ray0[EA + g];
-    d = a.ray0[2 * EA + g];  // :129
-    tot = d;                 // :130
-}
-
-__device__ __forceinline__ void ray_finish(const StepArgs &a, int64_t r, double tot) {
-    const int B = a.B;
-    const int g = (int)(r / B);
-    const int b = (int)(r - (int64_t)g * B);
-    const int e = g / a.A;
-    double range = tot > a.max_range ? a.max_range : tot;  // :143-144
-    if (a.noise_std > 0.0)  // ScanSimulator2D.scan: noise after the clamp (laser_models.py:450-452)
-        range += a.noise_std * (double)beam_normal(a.seed, (uint64_t)(a.env_offset + e), a.noise_step[e], b);
-    a.scan[r] = range;
-}
-
-template <int P>
-__global__ void __launch_bounds__(kBlock) k_rays_pool(StepArgs a) {
-    const int EA = a.E * a.A;
-    const int64_t R = (int64_t)EA * a.B;
-    const int lane = threadIdx.x & 63;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int64_t begin = wave * (64 * P);
-    const int64_t end = begin + 64 * P < R ? begin + 64 * P : R;
-    const MapView &m = a.map;
-    const int refill = a.refill_min;
-    int64_t next = begin + 64;  // wave-uniform
-    int64_t my = begin + lane;
-    bool have = my < end;       // lane holds a ray (running or parked)
-    double x = 0, y = 0, c = 0, s = 0, d = 0, tot = 0;
-    uint32_t n = 0, looks = 0;
-    if (have) {
-        ray_init(a, my, EA, x, y, c, s, d, tot);
-        n = 1;
-    }
-    bool act = have && d > a.eps && tot <= a.max_range;  // :133
-    while (true) {
-        const uint64_t parked = __ballot(have && !act);
-        const uint64_t running = __ballot(act);
-        const int np = __popcll(parked);
-        // refill when enough lanes are parked, or when nothing runs any more
-        if (np && (np >= refill || !running || next >= end)) {
-            if (have && !act) {
-                ray_finish(a, my, tot);
-                looks += n;
-                my = next + __popcll(parked & lt);
-                have = my < end;
-                if (have) {
-                    ray_init(a, my, EA, x, y, c, s, d, tot);
-                    n = 1;
-                    act = d > a.eps && tot <= a.max_range;
-                }
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    uint32_t n = 0;
+    if (r < (int64_t)a.EA * B) {
+        const int g = (int)(r / B);
+        const int b = (int)(r - (int64_t)g * B);
+        const int e = g / a.A;
+        if (!MASK || a.reset_mask[e]) {
+            double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
+            int ti = (int)t;  // int(theta_index), laser_models.py:124
+            if (ti >= a.theta_dis) ti = 0;
+            const double c = a.cosines[ti], s = a.sines[ti];
+            double x = a.ray0[g], y = a.ray0[a.EA + g];
+            double d = a.ray0[2 * a.EA + g];  // :129
+            double tot = d;                   // :130
+            uint32_t k = 1;
+            const double eps = a.eps, mr = a.max_range;
+            while (d > eps && tot <= mr) {  // :133
+                x += d * c;                 // :135
+                y += d * s;                 // :136
+                d = a.m.dt[tiled_cell<ROT>(a.m, x, y)];
+                tot += d;                   // :141
+                ++k;
             }
-            next += np;
-            continue;  // fresh rays may already be finished (d0 <= eps)
-        }
-        if (!running) break;
-        if (act) {
-            x += d * c;  // :135
-            y += d * s;  // :136
-            d = m.dt[cell_index_fast(m, x, y)];
-            tot += d;    // :141
-            ++n;
-            act = d > a.eps && tot <= a.max_range;
+            n = k;
+            double range = tot > mr ? mr : tot;  // :143-144
+            if (a.noise_ext)  // see store_ray
+                range += a.noise_ext[(size_t)e * B + b];
+            else if (a.noise_std > 0.0)
+                range += a.noise_std * (double)beam_normal(a.seed, (uint64_t)(a.env_offset + e), a.noise_step[e], b);
+            a.scan[r] = range;
         }
     }
-    if (a.ctr) {
-        // rays traced by this lane are counted through their lookups; the ray
-        // count of the wave is its pool size
-        uint32_t tot_l = wave_sum(looks);
-        if (lane == 0 && end > begin) {
-            unsigned long long *slot = a.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
-            atomicAdd(slot, (unsigned long long)tot_l);
-            atomicAdd(slot + 1, (unsigned long long)(end - begin));
-        }
-    }
+    count_rays(a.ctr, n);
 }
 
 // ------------------------------------------------------------------------
 struct PostShared {
     double stl[kMaxAgents][7];   // state after update_pose (TTC may zero 3..6)
-    double verts[kMaxAgents][8]; // get_vertices(agent_poses) (base_classes.py:562, :223)
+    double pose0[kMaxAgents][3]; // agent_poses: (x, y, yaw) before the TTC response (base_classes.py:587)
+    double verts[kMaxAgents][8]; // Simulator.check_collision's get_vertices (Simulator.params, :562)
+    double rv[kMaxAgents * (kMaxAgents - 1)][8];  // opponent j seen by agent i: RaceCar i's params (:223)
     int32_t hit[kMaxAgents];     // TTC hit
     int32_t col[kMaxAgents];     // collisions (GJK | TTC)
     int32_t blo[kMaxAgents * kMaxAgents], bhi[kMaxAgents * kMaxAgents];
@@ -388,6 +261,9 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
 #pragma unroll
         for (int k = 0; k < 7; ++k) sh.stl[tid][k] = a.st[(size_t)k * EA + g];
         // agent_poses (x, y, yaw) are taken before the TTC response (base_classes.py:587)
+        sh.pose0[tid][0] = sh.stl[tid][0];
+        sh.pose0[tid][1] = sh.stl[tid][1];
+        sh.pose0[tid][2] = sh.stl[tid][4];
         get_vertices(sh.stl[tid][0], sh.stl[tid][1], sh.stl[tid][4], a.p.length, a.p.width, sh.verts[tid]);
         sh.hit[tid] = 0;
         sh.col[tid] = 0;
@@ -429,9 +305,12 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
         int i = tid / (A - 1);
         int jj = tid - i * (A - 1);
         int j = jj < i ? jj : jj + 1;
+        // RaceCar.ray_cast_agents: get_vertices(opp_pose, self.params['length'], self.params['width'])
+        double *v = sh.rv[tid];
+        const f110_params &pi = a.pa[i];
+        get_vertices(sh.pose0[j][0], sh.pose0[j][1], sh.pose0[j][2], pi.length, pi.width, v);
         int lo, hi;
-        blocked_range(sh.stl[i][0], sh.stl[i][1], sh.stl[i][4], sh.verts[j], a.angles, B, a.fov, a.beam_incr, lo,
-                      hi);
+        blocked_range(sh.stl[i][0], sh.stl[i][1], sh.stl[i][4], v, a.angles, B, a.fov, a.beam_incr, lo, hi);
         sh.blo[tid] = lo;
         sh.bhi[tid] = hi;
     }
@@ -439,11 +318,10 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
     // agent ray_cast (RaceCar.ray_cast_agents, base_classes.py:206-227; ray_cast, laser_models.py:318-346)
     for (int jj = 0; jj < A - 1; ++jj) {
         for (int i = 0; i < A; ++i) {
-            int j = jj < i ? jj : jj + 1;
             int pr = i * (A - 1) + jj;
             int lo = sh.blo[pr], hi = sh.bhi[pr];
             const double ox = sh.stl[i][0], oy = sh.stl[i][1], oth = sh.stl[i][4];
-            const double *v = sh.verts[j];
+            const double *v = sh.rv[pr];
             for (int b = lo + tid; b <= hi; b += kBlock) {
                 double bt = oth + a.angles[b] + kPi / 2.;
                 double v30 = cos(bt), v31 = sin(bt);
@@ -547,30 +425,42 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
     const int64_t R = (int64_t)EA * a.B;
-    const int K = a.rays_per_thread;
-    const int64_t T = (R + K - 1) / K;
-    const dim3 grid((unsigned)((T + kBlock - 1) / kBlock));
-    if (a.ray_kernel == 1 && a.pool == 0 && K == 1) {
-        const dim3 g1((unsigned)((R + kBlock - 1) / kBlock));
-        if (a.tmap.os == 0.0 && a.tmap.oc == 1.0)
-            hipLaunchKernelGGL(k_rays_tiled<false>, g1, dim3(kBlock), 0, s, a);
+    const dim3 grid((unsigned)((R + kBlock - 1) / kBlock));
+    if (a.ray_kernel == 0) {
+        hipLaunchKernelGGL(k_rays, grid, dim3(kBlock), 0, s, a);
+    } else {
+        RayArgs ra;
+        ra.m = a.tmap;
+        ra.sines = a.sines;
+        ra.cosines = a.cosines;
+        ra.ray0 = a.ray0;
+        ra.runs = a.runs;
+        ra.nruns = a.nruns;
+        ra.reset_mask = a.mode == 1 ? a.reset_mask : nullptr;
+        ra.scan = a.scan;
+        ra.noise_ext = a.noise_ext;
+        ra.noise_step = a.noise_step;
+        ra.ctr = a.ctr;
+        ra.eps = a.eps;
+        ra.max_range = a.max_range;
+        ra.noise_std = a.noise_std;
+        ra.seed = a.seed;
+        ra.env_offset = a.env_offset;
+        ra.EA = EA;
+        ra.A = a.A;
+        ra.B = a.B;
+        ra.theta_dis = a.theta_dis;
+        const bool rot = !(a.tmap.os == 0.0 && a.tmap.oc == 1.0);
+        const bool mask = ra.reset_mask != nullptr;
+        if (!rot && !mask)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rays_tiled<false, false>), grid, dim3(kBlock), 0, s, ra);
+        else if (!rot)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rays_tiled<false, true>), grid, dim3(kBlock), 0, s, ra);
+        else if (!mask)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rays_tiled<true, false>), grid, dim3(kBlock), 0, s, ra);
         else
-            hipLaunchKernelGGL(k_rays_tiled<true>, g1, dim3(kBlock), 0, s, a);
-    } else if (a.pool > 0) {
-        const int64_t per_block = (int64_t)kBlock * a.pool;  // 4 waves x 64 lanes x P rays
-        const dim3 pg((unsigned)((R + per_block - 1) / per_block));
-        if (a.pool == 8)
-            hipLaunchKernelGGL(k_rays_pool<8>, pg, dim3(kBlock), 0, s, a);
-        else if (a.pool == 16)
-            hipLaunchKernelGGL(k_rays_pool<16>, pg, dim3(kBlock), 0, s, a);
-        else
-            hipLaunchKernelGGL(k_rays_pool<4>, pg, dim3(kBlock), 0, s, a);
-    } else if (K == 4)
-        hipLaunchKernelGGL(k_rays<4>, grid, dim3(kBlock), 0, s, a);
-    else if (K == 2)
-        hipLaunchKernelGGL(k_rays<2>, grid, dim3(kBlock), 0, s, a);
-    else
-        hipLaunchKernelGGL(k_rays<1>, grid, dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rays_tiled<true, true>), grid, dim3(kBlock), 0, s, ra);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_post, dim3(a.E), dim3(kBlock), post_lds_bytes(a.A, a.B), s, a);

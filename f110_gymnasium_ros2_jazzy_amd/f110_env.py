@@ -12,12 +12,16 @@ is evaluated here on the host with NumPy exactly as the reference writes it
 (including its dtype behaviour when ``options`` are float32), because it is
 a handful of scalar operations on two cars.
 
+Scan noise is the reference's own stream: every RaceCar re-creates
+``np.random.default_rng(seed)`` at reset and ScanSimulator2D.scan adds
+``rng.normal(0, 0.01, num_beams)`` after the clamp (base_classes.py:119,204,
+laser_models.py:450-452).  All cars share the seed, so they draw the same
+vector; the facade draws it once per step on the host and hands it to the
+device (f110_set_scan_noise), so noisy trajectories match the reference.
+``noise_std`` (extension kwarg) scales it; 0 turns it off.  The batched
+F110VectorEnv uses the device Philox stream instead (same law).
+
 Differences, by design:
-  * scan noise comes from a counter-based Philox stream (device) instead of
-    NumPy's PCG64; it has the same N(0, 0.01) law, is added after the clamp,
-    is shared by every agent and restarts at every reset, like the reference
-    (laser_models.py:450-452, base_classes.py:119,204).  ``noise_std=0``
-    (extension kwarg) turns it off for bit-level comparisons.
   * render() is not provided (visualisation is out of scope; the DDPG
     script never calls it).
 """
@@ -111,7 +115,7 @@ class F110Env(_EnvBase):
         self.integrator = kwargs.get('integrator', Integrator.RK4)
         self.lidar_dist = kwargs.get('lidar_dist', 0.0)
         self.render_mode = kwargs.get('render_mode')
-        noise_std = kwargs.get('noise_std', 0.01)
+        self.noise_std = float(kwargs.get('noise_std', 0.01))
         device = kwargs.get('device', 0)
 
         self.start_thresh = 0.1
@@ -133,8 +137,15 @@ class F110Env(_EnvBase):
         self.track = load_map(self.map_path, self.map_ext)
         self.sim = BatchSim(self.track, n_envs=1, n_agents=self.num_agents, params=self.params, device=device,
                             seed=self.seed, timestep=self.timestep, integrator=_integrator_code(self.integrator),
-                            ego_idx=self.ego_idx, lidar_dist=self.lidar_dist, noise_std=noise_std,
+                            ego_idx=self.ego_idx, lidar_dist=self.lidar_dist, noise_std=self.noise_std,
                             keep_f64_scans=True)
+        self._scan_rng = None
+        self._agent_params = [None] * self.num_agents
+        self._noise = None
+        if self.noise_std > 0.0:
+            import torch
+            self._noise = torch.zeros(1, self.sim.B, dtype=torch.float64, device=self.sim.device)
+            self.sim.set_scan_noise(self._noise)
 
         self.resolution = self.track.resolution
         self.x0, self.y0 = self.track.origin[0], self.track.origin[1]
@@ -227,12 +238,22 @@ class F110Env(_EnvBase):
             "time": float(self.current_time),
         }
 
+    def _draw_noise(self):
+        """This step's ScanSimulator2D.scan noise (laser_models.py:450-452)."""
+        if self._noise is not None:
+            import torch
+            n = self._scan_rng.normal(0., self.noise_std, size=self.sim.B)
+            self._noise.copy_(torch.from_numpy(n).view(1, -1))
+
     # ------------------------------------------------------------------
     def step(self, action):
         """F110Env.step (f110_env.py:371-421); action [num_agents, 2] (steer, velocity)."""
+        if self._noise is not None and self._scan_rng is None:
+            raise RuntimeError("call reset() before step()")  # the reference's cars lack scan_rng too
         a = np.asarray(action)
         if a.dtype not in (np.float32, np.float64):
             a = a.astype(np.float32)
+        self._draw_noise()
         out = self.sim.step(a.reshape(1, self.num_agents, 2))
         return self._finish_step(out)
 
@@ -256,15 +277,46 @@ class F110Env(_EnvBase):
         th = self.start_thetas[self.ego_idx]
         self.start_rot = np.array([[np.cos(-th), -np.sin(-th)], [np.sin(-th), np.cos(-th)]])
         # device: RaceCar.reset for every car + the reference's zero-action step (f110_env.py:457)
+        self._scan_rng = np.random.default_rng(seed=self.seed)  # RaceCar.reset, base_classes.py:204
+        self._draw_noise()
         out = self.sim.reset(np.asarray(poses, dtype=np.float64).reshape(1, self.num_agents, 3))
         obs_flat, _, _, _, info = self._finish_step(out)
         return obs_flat, info
 
     def update_map(self, map_path, map_ext):
-        raise NotImplementedError("update_map: create a new env (the EDT is built once per context)")
+        """F110Env.update_map (f110_env.py:474-485): new map, cars keep their state.
+        The device context is rebuilt for the new EDT; state and steer buffers
+        are carried over (the reference's RaceCars keep theirs too)."""
+        from .maps import load_map
+        from .sim import BatchSim
+        track = load_map(map_path, map_ext)
+        state = self.sim.get_state()
+        old = self.sim
+        self.sim = BatchSim(track, n_envs=1, n_agents=self.num_agents, params=self.params, device=old.device,
+                            seed=self.seed, timestep=self.timestep, integrator=_integrator_code(self.integrator),
+                            ego_idx=self.ego_idx, lidar_dist=self.lidar_dist, noise_std=self.noise_std,
+                            keep_f64_scans=True)
+        for i, p in enumerate(self._agent_params):
+            if p is not None:
+                self.sim.update_params(p, agent_idx=i)
+        self.sim.set_state(*state)
+        if self._noise is not None:
+            self.sim.set_scan_noise(self._noise)
+        old.close()
+        self.track = track
+        self.map_path = map_path
 
     def update_params(self, params, index=-1):
-        raise NotImplementedError("update_params: pass params= at construction")
+        """F110Env.update_params (f110_env.py:487-498) -> Simulator.update_params:
+        the car's dynamics and its agent ray_cast box use the new params; GJK,
+        TTC side distances and the obs lidar_max keep the construction params,
+        as in the reference (base_classes.py:223, :562, :122-158)."""
+        if not (index < self.num_agents):
+            raise IndexError('Index given is out of bounds for list of agents.')
+        self.sim.update_params(params, agent_idx=index)
+        for i in range(self.num_agents):
+            if index < 0 or i == index:
+                self._agent_params[i] = dict(params)
 
     def add_render_callback(self, callback_func):
         pass

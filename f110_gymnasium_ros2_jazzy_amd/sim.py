@@ -151,6 +151,30 @@ class BatchSim:
         _lib.check(self.L.f110_step(self.ctx, _ptr(a), dt, ctypes.byref(outs), self._stream()), "f110_step")
         return self.out
 
+    def update_params(self, params: dict, agent_idx: int = -1):
+        """Simulator.update_params (base_classes.py:527-546) for every env."""
+        p = _lib.F110Params()
+        ctypes.pointer(p)[0] = self.params
+        for k, _ in p._fields_:
+            if k in params:
+                setattr(p, k, float(params[k]))
+        _lib.check(self.L.f110_set_params(self.ctx, ctypes.byref(p), int(agent_idx), self._stream()),
+                   "f110_set_params")
+
+    def set_scan_noise(self, noise):
+        """Caller-supplied scan noise for the following step/reset calls
+        (f110_set_scan_noise): a device f64 tensor [E, B] that the caller
+        refills before each call; ``None`` returns to the device stream."""
+        if noise is None:
+            self._noise = None
+            _lib.check(self.L.f110_set_scan_noise(self.ctx, None), "f110_set_scan_noise")
+            return
+        if not (isinstance(noise, torch.Tensor) and noise.device == self.device and noise.dtype == torch.float64
+                and tuple(noise.shape) == (self.E, self.B) and noise.is_contiguous()):
+            raise ValueError(f"noise must be a contiguous float64 [{self.E}, {self.B}] tensor on {self.device}")
+        self._noise = noise
+        _lib.check(self.L.f110_set_scan_noise(self.ctx, _ptr(noise)), "f110_set_scan_noise")
+
     def get_state(self):
         """(state [7, E*A] f64, steer_buf [2, E*A] f64, steer_cnt [E*A] i32) — SoA."""
         EA = self.E * self.A

@@ -150,6 +150,29 @@ F110_API int f110_reset(f110_ctx *ctx, const double *poses, const uint8_t *env_m
 F110_API int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dtype, const f110_outputs *out,
                        void *stream);
 
+/* Replaces F110Env.update_params / Simulator.update_params
+ * (f110_env.py:487-498, base_classes.py:527-546): agent_idx < 0 updates every
+ * car, otherwise one car (out of range -> F110_E_INVALID, the reference's
+ * IndexError).  Like RaceCar.params, the update reaches the car's dynamics
+ * (update_pose) and the opponent boxes of its agent ray_cast
+ * (base_classes.py:223); the GJK boxes (Simulator.params, :562), the TTC
+ * side distances (class-level, :122-158) and the obs lidar_max keep the
+ * params given to f110_create, as in the reference.  params is a host
+ * pointer; the call is ordered on `stream` and returns when it is applied. */
+F110_API int f110_set_params(f110_ctx *ctx, const f110_params *params, int32_t agent_idx, void *stream);
+
+/* Scan-noise source of the following f110_step / f110_reset calls.
+ * noise: device [n_envs][n_beams] f64, or NULL for the built-in stream.
+ * The reference draws the noise as rng.normal(0, std_dev, num_beams) from a
+ * numpy Generator that every car re-creates with the same seed at reset
+ * (laser_models.py:450-452, base_classes.py:119,204), so the agents of one
+ * env see the same vector.  With a buffer set, each ray adds
+ * noise[env][beam] to its clamped range instead of the device Philox draw
+ * (noise_std is then unused).  The caller refills the buffer before each
+ * call, ordered on the same stream; it must outlive the calls that read it.
+ * The F110Env facade uses it to replay the reference's generator exactly. */
+F110_API int f110_set_scan_noise(f110_ctx *ctx, const double *noise);
+
 /* ---- state access ------------------------------------------------------- */
 /* state: device [7][n_envs*n_agents] f64 (SoA, see header comment).
  * steer_buf: device [2][n_envs*n_agents] f64 ([newest, older]); steer_cnt:
@@ -197,6 +220,16 @@ F110_API void f110_host_tables(int32_t theta_dis, int32_t n_beams, double fov, c
  * use.  Returns the number of runs (>0) or a negative error. */
 F110_API int f110_host_beam_indices(double yaw, double fov, int32_t theta_dis, int32_t n_beams,
                                     double *theta_index_out);
+
+/* xy_2_rc's cell (laser_models.py:55-104) for n points xy [n][2] on an H x W
+ * map, through the three device mappings: lin_out[n][3] = row-major index
+ * with the IEEE divide (cell_index), with the guarded fast quotient
+ * (cell_index_fast), and the 4x4-tiled mapping of the ray kernel translated
+ * back to row-major.  Out-of-map points give H*W-1 (the reference's
+ * dt[-1, -1]).  Host only; the CPU tests check the three agree on boundary
+ * points. */
+F110_API int f110_host_cell_index(int32_t H, int32_t W, double resolution, const double origin[3], const double *xy,
+                                  int64_t n, int64_t *lin_out);
 
 #ifdef __cplusplus
 }

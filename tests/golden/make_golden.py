@@ -421,6 +421,84 @@ def gen_env(rng, cl):
         bc.RaceCar.reset = orig_reset
 
 
+def _record_env(env, segments):
+    """Run F110Env through segments [(reset_poses, actions[T, A, 2]), ...] and
+    return the per-call obs / reward / flags / info arrays (reset calls
+    included, in call order; `is_reset` marks them)."""
+    obs, rew, term, trunc, infos, is_reset, acts = [], [], [], [], [], [], []
+    A = segments[0][0].shape[0]
+    for poses, seg_acts in segments:
+        o, inf = env.reset(options=poses)
+        obs.append(o); infos.append(inf); rew.append(0.0); term.append(False); trunc.append(False)
+        is_reset.append(True); acts.append(np.zeros((A, 2), np.float32))
+        for a in seg_acts:
+            o, r, te, tr, inf = env.step(a)
+            obs.append(o); infos.append(inf); rew.append(r); term.append(te); trunc.append(tr)
+            is_reset.append(False); acts.append(a)
+    keys = {}
+    for key in ["poses_x", "poses_y", "poses_theta", "linear_vels_x", "linear_vels_y",
+                "ang_vels_z", "collisions", "lap_times", "lap_counts", "checkpoint_done"]:
+        keys["info_" + key] = np.asarray([np.asarray(inf[key]) for inf in infos])
+    keys["info_time"] = np.asarray([inf["time"] for inf in infos])
+    keys["info_scans"] = np.asarray([np.stack(inf["scans"]) for inf in infos]).astype(np.float32)
+    return dict(actions=np.asarray(acts), is_reset=np.asarray(is_reset), obs=np.asarray(obs),
+                reward=np.asarray(rew), terminated=np.asarray(term), truncated=np.asarray(trunc), **keys)
+
+
+def _track_poses(cl, i, gap):
+    j = (i + 3) % cl.shape[0]
+    th = float(np.arctan2(cl[j, 1] - cl[i, 1], cl[j, 0] - cl[i, 0]))
+    k = (i + gap) % cl.shape[0]
+    return np.array([[cl[i, 0], cl[i, 1], th], [cl[k, 0], cl[k, 1], th]], np.float32)
+
+
+def gen_env_noise(cl):
+    """F110Env (2 agents) with the reference's own scan noise: every RaceCar
+    re-creates default_rng(seed) at reset (base_classes.py:204) and scan adds
+    rng.normal(0, 0.01, 1080) (laser_models.py:450-452).  Two episodes: the
+    second reset must restart the generators."""
+    rng = np.random.default_rng(777)
+    f110_env = _refload.load_env()
+    bc.RaceCar.scan_simulator = None
+    env = f110_env.F110Env(map_dir=MAPS + "/", map="Spielberg_map", map_ext=".png", num_agents=2, seed=1234)
+    poses = _track_poses(cl, 900, 12)
+    segs = []
+    for T in (40, 20):
+        segs.append((poses, np.stack([np.stack([rng.uniform(-0.4189, 0.4189, 2), rng.uniform(0, 20, 2)], 1)
+                                      for _ in range(T)]).astype(np.float32)))
+    rec = _record_env(env, segs)
+    save("env_2agent_noise.npz", reset_poses=poses, seed=np.int64(1234), **rec)
+
+
+def gen_env_params(cl):
+    """F110Env.update_params(params, index=0) (f110_env.py:487-498): agent 0 (behind)
+    gets its own mass/geometry and sees agent 1 through its own box size; noise off (scan_rng=None after reset).  The
+    cars start 8 centerline points apart so each sees the other (agent
+    ray_cast uses the observer's length/width, base_classes.py:223)."""
+    rng = np.random.default_rng(778)
+    f110_env = _refload.load_env()
+    bc.RaceCar.scan_simulator = None
+    orig_reset = bc.RaceCar.reset
+
+    def reset_no_noise(self, pose):
+        orig_reset(self, pose)
+        self.scan_rng = None
+
+    bc.RaceCar.reset = reset_no_noise
+    try:
+        env = f110_env.F110Env(map_dir=MAPS + "/", map="Spielberg_map", map_ext=".png", num_agents=2)
+        p1 = dict(DEFAULT_PARAMS, m=4.5, I=0.06, length=0.75, width=0.42, mu=0.9, v_max=15.0)
+        env.update_params(p1, index=0)
+        poses = _track_poses(cl, 1500, 14)
+        acts = np.stack([np.stack([rng.uniform(-0.2, 0.2, 2), rng.uniform(2, 12, 2)], 1)
+                         for _ in range(50)]).astype(np.float32)
+        rec = _record_env(env, [(poses, acts)])
+        save("env_2agent_params.npz", reset_poses=poses, params1=np.array([p1[k] for k in sorted(p1)]),
+             params1_keys=np.array(sorted(p1)), **rec)
+    finally:
+        bc.RaceCar.reset = orig_reset
+
+
 def gen_noise():
     """Noise semantics of ScanSimulator2D.scan (laser_models.py:450-452) with the
     per-agent default_rng(seed) re-seeded at reset (base_classes.py:119,204):
@@ -470,7 +548,14 @@ def main():
             action_fn=lambda t, A: np.tile([[0.05, 12.0]], (A, 1)))
     gen_env(rng, cl)
     gen_noise()
+    gen_env_noise(cl)
+    gen_env_params(cl)
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:  # regenerate selected fixtures only, e.g. `make_golden.py env_noise env_params`
+        _cl = centerline()
+        for name in sys.argv[1:]:
+            {"env_noise": gen_env_noise, "env_params": gen_env_params}[name](_cl)
+    else:
+        main()

@@ -78,3 +78,68 @@ def test_vector_env_numpy_two_agents(gpu):
     obs, rew, term, trunc, info = venv.step(a)
     assert rew.shape == (8,) and term.dtype == bool and info["scans"].shape == (8, 2, 1080)
     venv.close()
+
+
+def _replay(env, d, obs_exact=0.99):
+    """Drive the facade through a recorded reference run (resets marked by
+    is_reset) and compare every call's outputs."""
+    for t in range(d["obs"].shape[0]):
+        if d["is_reset"][t]:
+            obs, info = env.reset(options=d["reset_poses"])
+        else:
+            obs, r, term, trunc, info = env.step(d["actions"][t])
+            assert r == d["reward"][t] and term == d["terminated"][t] and trunc == d["truncated"][t]
+        np.testing.assert_allclose(obs, d["obs"][t], rtol=1e-5, atol=1e-5)
+        assert np.mean(obs == d["obs"][t]) >= obs_exact, t
+        for k in ("poses_x", "poses_y", "poses_theta", "linear_vels_x", "ang_vels_z"):
+            np.testing.assert_allclose(info[k], d["info_" + k][t], rtol=1e-5, atol=1e-5)
+        assert np.array_equal(info["collisions"], d["info_collisions"][t])
+        assert np.array_equal(info["lap_counts"], d["info_lap_counts"][t])
+        np.testing.assert_allclose(np.stack(info["scans"]), d["info_scans"][t], rtol=1e-5, atol=1e-5)
+
+
+def test_f110env_reference_noise_stream(gpu):
+    """Noise on (the reference default): the facade replays the reference's
+    per-car default_rng(seed) draws, so noisy scans match the reference run,
+    including the generator restart at the second reset."""
+    from f110_gym.envs import F110Env
+    d = golden("env_2agent_noise.npz")
+    env = F110Env(map_dir=MAPS + os.sep, map="Spielberg_map", map_ext=".png", num_agents=2, seed=int(d["seed"]))
+    try:
+        _replay(env, d)
+    finally:
+        env.close()
+
+
+def test_f110env_update_params_per_agent(gpu):
+    """update_params(p, index=0) before reset: agent 0's dynamics and the box
+    it ray-casts agent 1 with use p; GJK keeps the construction params."""
+    from f110_gym.envs import F110Env
+    d = golden("env_2agent_params.npz")
+    p1 = {str(k): float(v) for k, v in zip(d["params1_keys"], d["params1"])}
+    env = F110Env(map_dir=MAPS + os.sep, map="Spielberg_map", map_ext=".png", num_agents=2, noise_std=0.0)
+    try:
+        with pytest.raises(IndexError):
+            env.update_params(p1, index=2)
+        env.update_params(p1, index=0)
+        _replay(env, d)
+    finally:
+        env.close()
+
+
+def test_f110env_update_map_keeps_state(gpu):
+    """update_map swaps the EDT; the cars keep their state (f110_env.py:474-485)."""
+    from f110_gym.envs import F110Env
+    env = F110Env(map_dir=MAPS + os.sep, map="Spielberg_map", map_ext=".png", num_agents=1, noise_std=0.0)
+    try:
+        d = golden("env_2agent.npz")
+        env.reset(options=d["reset_poses"][:1])
+        for _ in range(5):
+            obs, *_ , info = env.step(np.array([[0.0, 5.0]], np.float32))
+        before = env.sim.agent_states().cpu().numpy()
+        env.update_map(os.path.join(MAPS, "straight_corridor.yaml"), ".png")
+        assert np.array_equal(env.sim.agent_states().cpu().numpy(), before)
+        obs2, *_ = env.step(np.array([[0.0, 5.0]], np.float32))
+        assert not np.array_equal(obs2[:1080], obs[:1080])   # new walls
+    finally:
+        env.close()

@@ -155,3 +155,65 @@ def test_batchsim_refuses_cpu():
         pytest.skip("GPU present")
     with pytest.raises(F110Error):
         BatchSim("Spielberg_map", n_envs=1, n_agents=1)
+
+
+def _boundary_points(H, W, res, origin, rng):
+    """Points whose map-frame coordinates sit on / next to cell boundaries
+    (including x_rot/res rounding up to W or H), off-map and non-finite ones,
+    mapped back to the world frame through the origin pose."""
+    xs = []
+    for n, lim in ((W, W), (H, H)):
+        k = np.arange(0, lim + 1, dtype=np.float64) * res
+        v = np.concatenate([k, np.nextafter(k, -np.inf), np.nextafter(k, np.inf),
+                            np.nextafter(np.nextafter(k, -np.inf), -np.inf), rng.uniform(-res, lim * res + res, 64)])
+        xs.append(v)
+    xr = rng.choice(xs[0], 4000)
+    yr = rng.choice(xs[1], 4000)
+    # also pair every x boundary with a y boundary row near the top / bottom
+    xr = np.concatenate([xr, xs[0], xs[0], [np.nan, np.inf, -np.inf, 0.0]])
+    yr = np.concatenate([yr, np.full(xs[0].size, np.nextafter(H * res, 0)), np.zeros(xs[0].size),
+                         [0.0, 0.0, 0.0, np.nan]])
+    c, s = np.cos(origin[2]), np.sin(origin[2])
+    # world = origin + R(yaw) [xr, yr]  (inverse of xy_2_rc's rotation; exactness is not needed:
+    # the three mappings are compared with each other on the same world points)
+    with np.errstate(invalid="ignore"):
+        x = origin[0] + c * xr - s * yr
+        y = origin[1] + s * xr + c * yr
+    if origin[2] == 0.0:
+        x, y = origin[0] + xr, origin[1] + yr
+    return np.ascontiguousarray(np.stack([x, y], 1))
+
+
+@pytest.mark.parametrize("H,W,res,origin,roundup", [
+    (2000, 2000, 0.05, (-78.21853769831466, -44.37590462453829, 0.0), False),   # Spielberg
+    (13, 7, 0.05, (-0.3, -0.2, 0.0), False),                                      # H, W not multiples of 4
+    (8, 12, 0.1, (0.0, 0.0, 0.0), False),                                         # multiples of 4 (tile edge)
+    (64, 40, 0.05, (-1.0, -1.0, 0.3), False),                                     # rotated origin
+    (33, 17, 0.07, (2.0, -3.0, -1.2), False),
+    # fl(v/res) == W (or H) for v = nextafter(W*res, 0): 17, 34, 39, 68 at res 0.05 / 0.1,
+    # 9 and 13 at 0.07; H = 68 is a multiple of 4 (the row past the last tile row)
+    (68, 17, 0.05, (0.0, 0.0, 0.0), True),
+    (39, 34, 0.1, (0.0, 0.0, 0.0), True),
+    (13, 9, 0.07, (0.0, 0.0, 0.0), True),
+])
+def test_cell_mappings_agree_on_boundaries(H, W, res, origin, roundup):
+    """The ray kernel's tiled, fast-quotient cell mapping equals xy_2_rc's
+    IEEE int(x_rot/res) row-major read (laser_models.py:55-104), including
+    quotients that round up to W or H and off-map / NaN points."""
+    import ctypes
+    from f110_gymnasium_ros2_jazzy_amd import _lib
+    L = _lib.load(build_if_missing=False)
+    rng = np.random.default_rng(H * 1000 + W)
+    xy = _boundary_points(H, W, res, origin, rng)
+    out = np.empty((xy.shape[0], 3), np.int64)
+    org = (ctypes.c_double * 3)(*origin)
+    assert L.f110_host_cell_index(H, W, res, org, xy.ctypes.data, xy.shape[0], out.ctypes.data) == 0
+    assert np.array_equal(out[:, 0], out[:, 1])
+    assert np.array_equal(out[:, 0], out[:, 2])
+    assert out.min() >= 0 and out.max() <= H * W - 1
+    assert (out[:, 0] == H * W - 1).any() and (out[:, 0] < H * W - 1).sum() > 1000
+    if roundup:  # map frame == world frame: the round-up case must be present
+        x, y = xy[:, 0], xy[:, 1]
+        with np.errstate(invalid="ignore"):
+            up = ((x < W * res) & (x >= 0) & (np.floor(x / res) == W)) | ((y < H * res) & (y >= 0) & (np.floor(y / res) == H))
+        assert up.any()
