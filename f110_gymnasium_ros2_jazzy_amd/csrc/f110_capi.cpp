@@ -686,3 +686,24 @@ extern "C" int f110_host_cell_index(int32_t H, int32_t W, double resolution, con
     }
     return F110_OK;
 }
+
+extern "C" int f110_gap_follow(const float *scans, int64_t n_scans, int64_t scan_stride, int32_t n_beams,
+                               double angle_min, double angle_increment, float *actions, int64_t action_stride,
+                               int32_t *gaps, void *stream) {
+    if (n_scans < 0 || n_beams <= 0 || (n_scans > 0 && (!scans || !actions)) || scan_stride < n_beams ||
+        action_stride < 2)
+        return fail(F110_E_INVALID, "f110_gap_follow: bad arguments");
+    if (gap_follow_lds_bytes(n_beams) > 160 * 1024) return fail(F110_E_INVALID, "f110_gap_follow: n_beams too large");
+    GapFollowArgs a;
+    a.scans = scans;
+    a.M = n_scans;
+    a.scan_stride = scan_stride;
+    a.action_stride = action_stride;
+    a.actions = actions;
+    a.gaps = gaps;
+    a.angle_min = angle_min;
+    a.angle_increment = angle_increment;
+    a.B = n_beams;
+    HIP_TRY(launch_gap_follow(a, (hipStream_t)stream));
+    return F110_OK;
+}

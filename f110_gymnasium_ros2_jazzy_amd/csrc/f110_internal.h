@@ -93,10 +93,22 @@ struct ScanArgs {
     int32_t variant;      // A/B experiments (F110_SCAN_VARIANT): 0 default
 };
 
+// gap_follow_action over M float32 scans (f110_gap_follow).
+struct GapFollowArgs {
+    const float *scans;   // scan m at scans + m * scan_stride
+    int64_t M, scan_stride, action_stride;
+    float *actions;       // (steer, speed) of scan m at actions + m * action_stride
+    int32_t *gaps;        // [M][2] chosen (start, end) or null
+    double angle_min, angle_increment;
+    int32_t B;
+};
+
 size_t step_lds_bytes(int A, int B);
 hipError_t prepare_env_step(size_t lds_bytes);
 hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev = nullptr);  // ev: 4 events or null
 hipError_t launch_scan_batch(const ScanArgs &a, hipStream_t s);
+hipError_t launch_gap_follow(const GapFollowArgs &a, hipStream_t s);
+size_t gap_follow_lds_bytes(int B);
 hipError_t launch_dynamics_batch(const double *x, const double *u, double *f, int64_t M, const f110_params &p,
                                  hipStream_t s);
 

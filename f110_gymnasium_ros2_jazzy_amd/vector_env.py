@@ -12,6 +12,13 @@ the gymnasium NEXT_STEP mode and runs on the device: the step after an env
 terminates resets it to a pose drawn from ``spawn_poses`` (and performs the
 reference's zero-action reset step); that step's reward is 0.
 
+``opponent="gap_follow"`` drives agent ``opponent_idx`` with the reference's
+rule-based opponent (gap_follow.py) on the device, as train_ddpg.py:168 does
+on the host: its action for step t comes from its own float32 scan of step
+t-1 (or of the reset).  ``step`` then takes the other agents' actions
+([N, 2] for two agents) and ``infos["opponent_actions"]`` shows the
+opponent's.
+
 Multi-GPU: give each rank its block of envs (distributed.shard_range) and
 ``env_offset`` = the block's first global id; RNG streams are keyed by global
 env id, so results do not depend on the GPU count.
@@ -32,7 +39,8 @@ class F110VectorEnv:
     def __init__(self, num_envs: int, map: str = "Spielberg_map", map_ext: str = ".png", num_agents: int = 1,
                  params: dict | None = None, seed: int = 42, timestep: float = 0.01, device=0,
                  spawn_poses: np.ndarray | None = None, noise_std: float = 0.01, env_offset: int = 0,
-                 ego_idx: int = 0, as_numpy: bool = False, autoreset: bool = True, **kwargs):
+                 ego_idx: int = 0, as_numpy: bool = False, autoreset: bool = True, opponent: str | None = None,
+                 opponent_idx: int = 1, **kwargs):
         self.num_envs = int(num_envs)
         self.num_agents = int(num_agents)
         self.params = dict(params or DEFAULT_PARAMS)
@@ -55,6 +63,21 @@ class F110VectorEnv:
         high = np.array([self.params["s_max"], self.params["v_max"]], np.float32)
         self.single_action_space = _box(np.tile(low, (A, 1)), np.tile(high, (A, 1)))
         self._rng = np.random.default_rng(seed)
+        self.opponent = opponent
+        self.opponent_idx = int(opponent_idx)
+        if opponent is not None:
+            if opponent != "gap_follow":
+                raise ValueError(f"unknown opponent policy {opponent!r} (supported: 'gap_follow')")
+            if not (0 <= self.opponent_idx < A) or A < 2:
+                raise ValueError("opponent needs num_agents >= 2 and 0 <= opponent_idx < num_agents")
+            self._act = torch.zeros(self.num_envs, A, 2, dtype=torch.float32, device=self.device)
+            self._others = [i for i in range(A) if i != self.opponent_idx]
+
+    def _opponent_next(self, out):
+        """Next step's opponent action from this step's scans (train_ddpg.py:168)."""
+        if self.opponent is not None:
+            from .opponent import gap_follow
+            gap_follow(out.scans[:, self.opponent_idx], out=self._act[:, self.opponent_idx])
 
     # ------------------------------------------------------------------
     def _infos(self, out):
@@ -66,6 +89,8 @@ class F110VectorEnv:
             "lap_counts": out.lap_counts.clone(), "scans": out.scans.clone(), "time": out.sim_time.clone(),
             "reset": out.was_reset.bool(),
         }
+        if self.opponent is not None:
+            infos["opponent_actions"] = self._act[:, self.opponent_idx].clone()
         if self.as_numpy:
             infos = {k: v.cpu().numpy() for k, v in infos.items()}
         return infos
@@ -78,14 +103,23 @@ class F110VectorEnv:
             idx = self._rng.integers(0, self.spawn_poses.shape[0], self.num_envs)
             options = self.spawn_poses[idx]
         out = self.sim.reset(options)
+        self._opponent_next(out)
         obs = out.obs.clone()
         return (obs.cpu().numpy() if self.as_numpy else obs), self._infos(out)
 
     def step(self, actions):
         a = torch.as_tensor(actions, device=self.device)
-        if a.dim() == 2 and self.num_agents == 1:
+        if self.opponent is not None:
+            if a.dim() == 2:
+                a = a.reshape(self.num_envs, len(self._others), 2)
+            if a.shape[1] == self.num_agents:
+                a = a[:, self._others]
+            self._act[:, self._others] = a.to(torch.float32)
+            a = self._act
+        elif a.dim() == 2 and self.num_agents == 1:
             a = a.unsqueeze(1)
         out = self.sim.step(a)
+        self._opponent_next(out)
         reset = out.was_reset.bool()
         rewards = torch.where(reset, torch.zeros((), device=self.device),
                               torch.full((), self.timestep, device=self.device)).float()

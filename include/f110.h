@@ -209,6 +209,21 @@ F110_API int f110_reset_counters(f110_ctx *ctx, void *stream);
 F110_API int f110_profile_begin(f110_ctx *ctx, int32_t max_steps);
 F110_API int f110_profile_end(f110_ctx *ctx, double ms_out[3], int32_t *steps_out);
 
+/* ---- opponent policy -------------------------------------------------------
+ * Replaces gap_follow_action (rl_training/utils/gap_follow.py:3-58), the
+ * rule-based opponent train_ddpg.py:168 computes on the host each step from
+ * the float32 info["scans"][1].  Device pointers: scan m is the n_beams
+ * float32 values at scans + m*scan_stride (e.g. agent 1 of env m in
+ * f110_outputs.scans: scans + B, stride A*B); its (steer, speed) goes to
+ * actions[m*action_stride + 0/1] as float32 (e.g. agent 1's slot of the next
+ * f110_step's action array: stride 2*A).  gaps [n_scans][2] (optional) gets
+ * the chosen gap (start, end).  Bit-exact with the reference's NumPy
+ * float32 arithmetic; angle_min / angle_increment are the reference
+ * defaults -pi/2 and pi/1080 unless overridden.  Async on stream. */
+F110_API int f110_gap_follow(const float *scans, int64_t n_scans, int64_t scan_stride, int32_t n_beams,
+                             double angle_min, double angle_increment, float *actions, int64_t action_stride,
+                             int32_t *gaps, void *stream);
+
 /* ---- host-side test hooks (no device work) -------------------------------
  * The lookup tables f110_create uploads: ScanSimulator2D sines/cosines
  * (laser_models.py:379-381) and RaceCar's class-level beam tables

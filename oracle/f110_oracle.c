@@ -668,3 +668,61 @@ OR_API void or_sim_reset(int64_t n, double *state, double *buf, int32_t *cnt, co
         cnt[i] = 0;
     }
 }
+
+/* ---------------------------------------------------------------------------
+ * Opponent policy of the training loop: gap_follow_action
+ * (rl_training/utils/gap_follow.py:3-58, called by train_ddpg.py:168 on the
+ * float32 info["scans"][1]).  float32 stages follow NumPy:
+ *   preprocess_lidar  :3-12  window [max(0,i-2), min(N-1,i+2)] of
+ *                     clip(r, 0, 3.0) (float32); np.mean = left-to-right
+ *                     float32 sum / count in float32 (measured: identical on
+ *                     200k windows of length 3..5)
+ *   create_bubble     :14-19 argmin (first minimum; a NaN wins, first NaN),
+ *                     zero [cp-30, cp+30] clipped to the scan
+ *   find_max_gap      :21-39 runs of value > 0.5; the first run of maximal
+ *                     end-start wins (Python max); none -> (0, N-1)
+ *   best point        :41-42 (start+end)//2
+ *   action            :44-58 steer = angle_min + best*angle_increment (f64),
+ *                     speed 2.5 / 2 / 1.5 by |steer| < radians(10) / (20)
+ * gap_out (optional) = the chosen (start, end). */
+OR_API void or_gap_follow(const float *r, int32_t n, double angle_min, double angle_increment, double *action,
+                          int32_t *gap_out) {
+    float *p = (float *)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+    for (int32_t i = 0; i < n; ++i) {
+        int32_t s = i - 2 > 0 ? i - 2 : 0;
+        int32_t e = i + 2 < n - 1 ? i + 2 : n - 1;
+        float sum = 0.0f;
+        for (int32_t j = s; j <= e; ++j) {
+            float v = r[j];
+            v = v < 0.0f ? 0.0f : v;   /* np.clip(x, 0, 3.0): NaN propagates */
+            v = v > 3.0f ? 3.0f : v;
+            sum = sum + v;
+        }
+        p[i] = sum / (float)(e - s + 1);
+    }
+    int32_t cp = 0;
+    for (int32_t i = 0; i < n; ++i) {  /* np.argmin */
+        if (p[i] != p[i]) { cp = i; break; }
+        if (p[i] < p[cp]) cp = i;
+    }
+    int32_t bs = cp - 30 > 0 ? cp - 30 : 0;
+    int32_t be = cp + 30 < n - 1 ? cp + 30 : n - 1;
+    for (int32_t i = bs; i <= be; ++i) p[i] = 0.0f;
+    int32_t g0 = 0, g1 = n - 1, best_len = -1, start = -1;
+    for (int32_t i = 0; i <= n; ++i) {
+        int m = i < n && p[i] > 0.5f;
+        if (m && start < 0) start = i;
+        else if (!m && start >= 0) {
+            if (i - 1 - start > best_len) { best_len = i - 1 - start; g0 = start; g1 = i - 1; }
+            start = -1;
+        }
+    }
+    free(p);
+    int32_t best = (g0 + g1) / 2;
+    double steer = angle_min + (double)best * angle_increment;
+    double a = fabs(steer);
+    double speed = a < 10.0 * (M_PI / 180.0) ? 2.5 : (a < 20.0 * (M_PI / 180.0) ? 2.0 : 1.5);
+    action[0] = steer;
+    action[1] = speed;
+    if (gap_out) { gap_out[0] = g0; gap_out[1] = g1; }
+}

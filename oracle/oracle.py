@@ -84,6 +84,8 @@ def lib():
         L.or_ray_cast.argtypes = [_D, _D, _D, ctypes.c_int, _D]
         L.or_sim_step.argtypes = [ctypes.POINTER(Sim), ctypes.c_int64, _D, _D, _I32, _D, _D, _D, ctypes.c_int]
         L.or_sim_reset.argtypes = [ctypes.c_int64, _D, _D, _I32, _D]
+        L.or_gap_follow.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_int32, ctypes.c_double,
+                                    ctypes.c_double, _D, _I32]
         _lib = L
     return _lib
 
@@ -250,6 +252,16 @@ class OracleSim:
 
 
 # ------------------------------------------------------------------ map ----
+def gap_follow_action(scan, angle_min=-np.pi / 2, angle_increment=np.pi / 1080):
+    """gap_follow.py:44-58 on one float32 scan -> (action f64 [2], gap (start, end))."""
+    s = np.ascontiguousarray(scan, dtype=np.float32)
+    act = np.empty(2)
+    gap = np.empty(2, np.int32)
+    lib().or_gap_follow(s.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), s.shape[0], angle_min, angle_increment,
+                        _p(act), _p(gap, _I32))
+    return act, gap
+
+
 def load_map(yaml_path, map_ext=".png"):
     """ScanSimulator2D.set_map (laser_models.py:383-427) restated:
     PIL load -> FLIP_TOP_BOTTOM -> (<=128 -> occupied) ; returns

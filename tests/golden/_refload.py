@@ -111,3 +111,15 @@ def load_all():
 def load_env():
     load_all()
     return load("f110_env")
+
+
+def load_path(modname: str, relpath: str) -> types.ModuleType:
+    """Load a plain-NumPy reference module outside f110_gym by file path,
+    e.g. load_path("gap_follow", "rl_training/utils/gap_follow.py")."""
+    if modname in _loaded:
+        return _loaded[modname]
+    spec = importlib.util.spec_from_file_location("_ref_" + modname, os.path.join(REF_ROOT, relpath))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    _loaded[modname] = mod
+    return mod

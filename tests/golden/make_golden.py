@@ -499,6 +499,83 @@ def gen_env_params(cl):
         bc.RaceCar.reset = orig_reset
 
 
+def gen_gap_follow():
+    """rl_training/utils/gap_follow.py:gap_follow_action on float32 scans, as
+    train_ddpg.py:168 calls it on info["scans"][1]: recorded F110Env scans
+    (noise-free and noisy) plus edge cases (no gap, ties, bubble at either
+    end, values on the 0.5 / 3.0 thresholds)."""
+    gf = _refload.load_path("gap_follow", "rl_training/utils/gap_follow.py")
+    rng = np.random.default_rng(779)
+    scans = []
+    for f in ("env_2agent.npz", "env_2agent_noise.npz", "env_2agent_params.npz"):
+        d = np.load(os.path.join(HERE, f))
+        scans += list(d["info_scans"][::3, 1]) + list(d["info_scans"][::15, 0])
+    B = 1080
+    z = np.zeros(B, np.float32)
+    scans.append(z)                                            # no gap -> (0, B-1)
+    scans.append(np.full(B, 10.0, np.float32))                 # all beyond max_distance
+    scans.append(np.full(B, 0.5, np.float32))                  # exactly on the gap threshold
+    two = np.full(B, 2.0, np.float32); two[300:310] = 0.1; two[700:710] = 0.1
+    scans.append(two)                                          # equal gaps -> first maximal wins
+    e0 = np.full(B, 4.0, np.float32); e0[0] = 0.05
+    scans.append(e0)                                           # closest point at beam 0
+    e1 = np.full(B, 4.0, np.float32); e1[-1] = 0.05
+    scans.append(e1)                                           # closest point at the last beam
+    tie = np.full(B, 4.0, np.float32); tie[100] = 0.2; tie[900] = 0.2
+    scans.append(tie)                                          # argmin tie -> first index
+    for _ in range(40):
+        s = rng.uniform(0.0, 5.0, B).astype(np.float32)
+        k = rng.integers(1, 6)
+        for _ in range(k):
+            a = rng.integers(0, B)
+            s[a:a + rng.integers(1, 120)] = rng.uniform(0.0, 0.6)
+        scans.append(s)
+    for _ in range(10):                                        # values near 3.0 and 0.5 in f32
+        s = rng.choice(np.array([0.5, 0.49999997, 0.50000006, 3.0, 2.9999998, 3.0000002, 1.0], np.float32), B)
+        scans.append(s.astype(np.float32))
+    scans = np.stack(scans).astype(np.float32)
+    acts, gaps, proc = [], [], []
+    for s in scans:
+        acts.append(gf.gap_follow_action(s))
+        p = gf.create_bubble(gf.preprocess_lidar(s))
+        proc.append(p)
+        gaps.append(gf.find_max_gap(p))
+    save("gap_follow.npz", scans=scans, actions=np.asarray(acts), gaps=np.asarray(gaps, np.int64),
+         processed16=np.asarray(proc[:16]))
+
+
+def gen_env_gapfollow(cl):
+    """train_ddpg.py's loop (:150-174) with noise off: agent 1 is driven by
+    gap_follow_action(info["scans"][1]) of the previous call, agent 0 by
+    recorded random actions (float32)."""
+    gf = _refload.load_path("gap_follow", "rl_training/utils/gap_follow.py")
+    rng = np.random.default_rng(780)
+    f110_env = _refload.load_env()
+    bc.RaceCar.scan_simulator = None
+    orig_reset = bc.RaceCar.reset
+
+    def reset_no_noise(self, pose):
+        orig_reset(self, pose)
+        self.scan_rng = None
+
+    bc.RaceCar.reset = reset_no_noise
+    try:
+        env = f110_env.F110Env(map_dir=MAPS + "/", map="Spielberg_map", map_ext=".png", num_agents=2)
+        poses = _track_poses(cl, 2100, 25)
+        obs, info = env.reset(options=poses)
+        T = 80
+        ego = np.stack([np.stack([rng.uniform(-0.3, 0.3), rng.uniform(3, 9)]) for _ in range(T)]).astype(np.float32)
+        obs_l, opp_l, term_l, scans_l = [obs], [], [], [np.stack(info["scans"])]
+        for t in range(T):
+            opp = gf.gap_follow_action(info["scans"][1]).astype(np.float32)
+            obs, r, term, trunc, info = env.step(np.stack([ego[t], opp], axis=0).astype(np.float32))
+            obs_l.append(obs); opp_l.append(opp); term_l.append(term); scans_l.append(np.stack(info["scans"]))
+        save("env_gapfollow.npz", reset_poses=poses, ego_actions=ego, opp_actions=np.asarray(opp_l),
+             obs=np.asarray(obs_l), terminated=np.asarray(term_l), info_scans=np.asarray(scans_l))
+    finally:
+        bc.RaceCar.reset = orig_reset
+
+
 def gen_noise():
     """Noise semantics of ScanSimulator2D.scan (laser_models.py:450-452) with the
     per-agent default_rng(seed) re-seeded at reset (base_classes.py:119,204):
@@ -550,12 +627,15 @@ def main():
     gen_noise()
     gen_env_noise(cl)
     gen_env_params(cl)
+    gen_gap_follow()
+    gen_env_gapfollow(cl)
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 1:  # regenerate selected fixtures only, e.g. `make_golden.py env_noise env_params`
         _cl = centerline()
         for name in sys.argv[1:]:
-            {"env_noise": gen_env_noise, "env_params": gen_env_params}[name](_cl)
+            {"env_noise": lambda c: gen_env_noise(c), "env_params": lambda c: gen_env_params(c),
+             "gap_follow": lambda c: gen_gap_follow(), "env_gapfollow": gen_env_gapfollow}[name](_cl)
     else:
         main()

@@ -140,3 +140,13 @@ def test_noise_fixture_properties():
     # every agent's rng is default_rng(seed) -> identical streams (base_classes.py:119,204)
     assert np.array_equal(n["agent0"], n["agent1"])
     assert abs(n["agent0"].mean()) < 1e-3 and abs(n["agent0"].std() - 0.01) < 5e-4
+
+
+def test_gap_follow(oracle_mod):
+    """gap_follow_action (rl_training/utils/gap_follow.py:44-58) restated in C:
+    action and chosen gap bit-exact on every recorded case."""
+    d = golden("gap_follow.npz")
+    for i, (s, a, g) in enumerate(zip(d["scans"], d["actions"], d["gaps"])):
+        act, gap = oracle_mod.gap_follow_action(s)
+        assert np.array_equal(act, a), i
+        assert np.array_equal(gap, g), i
