@@ -54,7 +54,7 @@ struct f110_ctx {
     int32_t *nruns = nullptr;
     uint64_t *noise_step = nullptr;
     int32_t *scnt = nullptr, *toggles = nullptr;
-    uint8_t *near_start = nullptr, *pending = nullptr, *reset_flag = nullptr;
+    uint8_t *near_start = nullptr, *pending = nullptr, *reset_flag = nullptr, *ttc_hit = nullptr;
     float *lap_times = nullptr, *lap_counts = nullptr;
     uint64_t *episode = nullptr, *nstep = nullptr;
     unsigned long long *ctr = nullptr;
@@ -384,6 +384,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     ALLOC(c->nruns, EA);
     ALLOC(c->scan, EA * (size_t)C.n_beams);
     ALLOC(c->reset_flag, (size_t)C.n_envs);
+    ALLOC(c->ttc_hit, EA);
     ALLOC(c->noise_step, (size_t)C.n_envs);
     ALLOC(c->start, 3 * EA);
     ALLOC(c->toggles, EA);
@@ -489,6 +490,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.nruns = c->nruns;
     a.scan = c->scan;
     a.reset_flag = c->reset_flag;
+    a.ttc_hit = c->ttc_hit;
     a.noise_step = c->noise_step;
     a.noise_ext = c->noise_ext;
     a.pa = c->pa;

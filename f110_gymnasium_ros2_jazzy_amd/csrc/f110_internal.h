@@ -47,6 +47,7 @@ struct StepArgs {
     int32_t *nruns;      // [E*A]
     double *scan;        // [E*A][B] ranges (noise added) before the collision stage
     uint8_t *reset_flag; // [E] this call reset the env
+    uint8_t *ttc_hit;    // [E*A] TTC fired in the fused single-agent ray pass
     uint64_t *noise_step;// [E] noise counter used by this step
     const double *noise_ext;  // [E][B] caller-supplied scan noise (f110_set_scan_noise) or null
     const double *spawn; // [n_spawn][A][3]
@@ -77,6 +78,16 @@ struct RayArgs {
     uint64_t seed;
     int64_t env_offset;
     int32_t EA, A, B, theta_dis;
+    // FUSED single-agent epilogue (k_rays_tiled<.., .., true>)
+    const double *vel;         // state[3][EA]
+    const double *beam_cos, *side;
+    double ttc_thresh;
+    uint8_t *ttc_hit;          // [EA]
+    float *obs;                // [E][obs_len] or null
+    float *scans_f32;          // [EA][B] or null
+    double *scans_f64;         // [EA][B] or null
+    int32_t obs_len;
+    float lidar_max;
 };
 
 struct ScanArgs {

@@ -45,6 +45,29 @@ __device__ __forceinline__ void count_rays(unsigned long long *ctr, uint32_t n, 
     }
 }
 
+// F110Env._pack_flat_obs's scan entry (f110_env.py:557-560): f32, NaN ->
+// lidar_max, +-inf -> lidar_max / 0, clip, / lidar_max in f32.
+__device__ __forceinline__ float obs_scan_value(double r, float lmax) {
+    float v = (float)r;
+    if (v != v) v = lmax;
+    else if (isinf(v)) v = v > 0 ? lmax : 0.0f;
+    v = v < 0.0f ? 0.0f : (v > lmax ? lmax : v);
+    return v / lmax;
+}
+
+// check_ttc_jit's per-beam test (laser_models.py:188-217):
+//   ttc = (range - side) / proj_vel;  hit = ttc < thresh && ttc >= 0.
+// The f64 divide only runs for beams that can fire: with num = range - side
+// > 0 and num >= fl(1.2 * thresh * |proj_vel|), |num / proj_vel| >= 1.2 *
+// thresh * (1 - 2^-53) > thresh, so the reference's test is false whatever
+// the quotient rounds to.  Every other beam takes the exact divide.
+__device__ __forceinline__ bool ttc_fires(double range, double side, double proj_vel, double thresh) {
+    const double num = range - side;
+    if (num > 0.0 && num >= (1.2 * thresh) * fabs(proj_vel)) return false;
+    const double ttc = num / proj_vel;
+    return ttc < thresh && ttc >= 0.0;
+}
+
 // trace_ray, laser_models.py:106-146, from the shared first lookup d0 at the
 // scan pose.  Returns the clamped range; n = EDT lookups made.
 __device__ __forceinline__ double trace(const MapView &m, double x, double y, double c, double s, double d0,
@@ -137,6 +160,7 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
     a.ray0[2 * EA + g] = a.map.dt[cell_index(a.map, sx, sy)];  // first lookup (laser_models.py:129)
     double t0 = first_theta_index(s[4], a.fov, a.theta_dis);
     a.nruns[g] = build_beam_runs(t0, a.inc, a.theta_dis, a.B, a.runs + (size_t)g * kMaxSeg, kMaxSeg);
+    a.ttc_hit[g] = 0;
     if (ag == 0) {
         a.reset_flag[e] = (uint8_t)do_reset;
         a.noise_step[e] = do_reset ? 0ull : a.nstep[e];
@@ -182,6 +206,15 @@ __global__ void __launch_bounds__(kBlock) k_rays(StepArgs a) {
     if (a.ctr) count_rays(a.ctr, n);
 }
 
+// The RayArgs block in the kernarg segment (k_rays_tiled's only argument).
+__device__ __forceinline__ const RayArgs *kernarg_rays() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return reinterpret_cast<const RayArgs *>(__builtin_amdgcn_kernarg_segment_ptr());
+#else
+    return nullptr;
+#endif
+}
+
 // ------------------------------------------------------------------------
 // k_rays_tiled: one thread per ray on the 4x4-tiled EDT, with the rotation
 // compiled out for axis-aligned maps.  Same results as k_rays, bit for bit.
@@ -190,7 +223,13 @@ __global__ void __launch_bounds__(kBlock) k_rays(StepArgs a) {
 // scheduler absorbs the ragged ray lengths.  Measured alternatives that lost
 // (DESIGN.md §3): 2 and 4 interleaved rays per lane (1.4x / 2x slower), a
 // per-wave ray pool with lane refill (1.35x slower).
-template <bool ROT, bool MASK>
+//
+// FUSED (single-agent envs): nothing rewrites a scan after it is traced
+// (there is no agent ray_cast), so the ray also runs its TTC test
+// (check_ttc_jit, laser_models.py:188-217) and writes the observation /
+// scan outputs itself; k_post_single then only resolves the per-env state.
+// The f64 scan hand-off to k_post (8 B per ray written and read back) is gone.
+template <bool ROT, bool MASK, bool FUSED>
 __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
     const int B = a.B;
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -217,15 +256,75 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
                 ++k;
             }
             n = k;
+            // Epilogue fields are read through the kernarg pointer HERE, after
+            // the loop: argument loads would otherwise sit at kernel entry and
+            // stay live in SGPRs across the loop (84 instead of 68 SGPRs:
+            // 7 instead of 8 blocks per CU).
+            const RayArgs &K = *kernarg_rays();
             double range = tot > mr ? mr : tot;  // :143-144
-            if (a.noise_ext)  // see store_ray
-                range += a.noise_ext[(size_t)e * B + b];
-            else if (a.noise_std > 0.0)
-                range += a.noise_std * (double)beam_normal(a.seed, (uint64_t)(a.env_offset + e), a.noise_step[e], b);
-            a.scan[r] = range;
+            if (K.noise_ext)  // see store_ray
+                range += K.noise_ext[(size_t)e * B + b];
+            else if (K.noise_std > 0.0)
+                range += K.noise_std * (double)beam_normal(K.seed, (uint64_t)(K.env_offset + e), K.noise_step[e], b);
+            if (FUSED) {
+                const double v = K.vel[g];  // state[3] after update_pose
+                if (v != 0.0 && ttc_fires(range, K.side[b], v * K.beam_cos[b], K.ttc_thresh)) K.ttc_hit[g] = 1;
+                if (K.obs) K.obs[(size_t)e * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
+                if (K.scans_f32) K.scans_f32[r] = (float)range;
+                if (K.scans_f64) K.scans_f64[r] = range;
+            } else {
+                K.scan[r] = range;
+            }
         }
     }
-    count_rays(a.ctr, n);
+    count_rays(kernarg_rays()->ctr, n);
+}
+
+// F110Env.step's time + _check_done (f110_env.py:404-406, :310-352) and the
+// env's autoreset / episode / noise bookkeeping, for env e.  stl: post-TTC
+// state rows of its A agents (x at [i*stride], y at [i*stride + 1]); col:
+// collision flags.
+__device__ void env_epilogue(const StepArgs &a, int e, const double *stl, int stride, const int32_t *col,
+                             int do_reset) {
+    const int A = a.A;
+    const int EA = a.E * A;
+    double tnow = (do_reset ? 0.0 : a.sim_time[e]) + a.dt;
+    a.sim_time[e] = tnow;
+    const double th = a.start[2 * EA + e * A + a.ego];
+    const double r00 = cos(-th), r01 = -sin(-th), r10 = sin(-th), r11 = cos(-th);
+    bool all4 = true;
+    for (int i = 0; i < A; ++i) {
+        const int g = e * A + i;
+        double px = stl[i * stride] - a.start[g];
+        double py = stl[i * stride + 1] - a.start[EA + g];
+        double dx = r00 * px + r01 * py;
+        double dy = r10 * px + r11 * py;
+        double ty;
+        if (dy > 2.0) ty = dy - 2.0;
+        else if (dy < -2.0) ty = -2.0 - dy;
+        else ty = 0.0;
+        bool close = dx * dx + ty * ty <= 0.1;
+        int tg = a.toggles[g];
+        uint8_t ns = a.near_start[g];
+        if (close && !ns) { ns = 1; ++tg; }
+        else if (!close && ns) { ns = 0; ++tg; }
+        a.toggles[g] = tg;
+        a.near_start[g] = ns;
+        float lc = (float)(tg / 2);
+        float lt = tg < 4 ? (float)tnow : a.lap_times[g];
+        a.lap_counts[g] = lc;
+        a.lap_times[g] = lt;
+        if (a.out.lap_counts) a.out.lap_counts[g] = lc;
+        if (a.out.lap_times) a.out.lap_times[g] = lt;
+        all4 = all4 && tg >= 4;
+    }
+    bool term = col[a.ego] || all4;
+    if (a.out.terminated) a.out.terminated[e] = term ? 1 : 0;
+    if (a.out.was_reset) a.out.was_reset[e] = (uint8_t)do_reset;
+    if (a.out.sim_time) a.out.sim_time[e] = tnow;
+    a.pending[e] = (a.autoreset && term) ? 1 : 0;
+    if (do_reset && a.mode == 0) a.episode[e] += 1;
+    a.nstep[e] = a.noise_step[e] + 1;
 }
 
 // ------------------------------------------------------------------------
@@ -276,11 +375,7 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
         int ag = id / B;
         int b = id - ag * B;
         double v = sh.stl[ag][3];
-        if (v != 0.0) {
-            double proj_vel = v * a.beam_cos[b];
-            double ttc = (scan[id] - a.side[b]) / proj_vel;
-            if (ttc < a.ttc_thresh && ttc >= 0.0) sh.hit[ag] = 1;
-        }
+        if (v != 0.0 && ttc_fires(scan[id], a.side[b], v * a.beam_cos[b], a.ttc_thresh)) sh.hit[ag] = 1;
     }
     if (tid == 0) {  // collision_multiple (collision_models.py:184-212) on pre-TTC poses
         for (int i = 0; i < A - 1; ++i)
@@ -343,13 +438,7 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
     if (a.out.obs) {  // F110Env._pack_flat_obs, f110_env.py:552-584 (scan of agent 0, e = 0)
         float *o = a.out.obs + (size_t)e * obs_len;
         const float lmax = (float)a.p.lidar_max;
-        for (int b = tid; b < B; b += kBlock) {
-            float v = (float)scan[b];
-            if (v != v) v = lmax;
-            else if (isinf(v)) v = v > 0 ? lmax : 0.0f;
-            v = v < 0.0f ? 0.0f : (v > lmax ? lmax : v);
-            o[b] = v / lmax;
-        }
+        for (int b = tid; b < B; b += kBlock) o[b] = obs_scan_value(scan[b], lmax);
         if (tid < A) {
             o[B + 4 * tid + 0] = (float)sh.stl[tid][0];
             o[B + 4 * tid + 1] = (float)sh.stl[tid][1];
@@ -366,46 +455,34 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
         for (int id = tid; id < A * B; id += kBlock) o[id] = scan[id];
     }
     if (a.out.collisions && tid < A) a.out.collisions[(size_t)e * A + tid] = (uint8_t)sh.col[tid];
-    if (tid == 0) {
-        // F110Env.step time + _check_done (f110_env.py:404-406, :310-352)
-        double tnow = (sh.do_reset ? 0.0 : a.sim_time[e]) + a.dt;
-        a.sim_time[e] = tnow;
-        const double th = a.start[2 * EA + e * A + a.ego];
-        const double r00 = cos(-th), r01 = -sin(-th), r10 = sin(-th), r11 = cos(-th);
-        bool all4 = true;
-        for (int i = 0; i < A; ++i) {
-            const int g = e * A + i;
-            double px = sh.stl[i][0] - a.start[g];
-            double py = sh.stl[i][1] - a.start[EA + g];
-            double dx = r00 * px + r01 * py;
-            double dy = r10 * px + r11 * py;
-            double ty;
-            if (dy > 2.0) ty = dy - 2.0;
-            else if (dy < -2.0) ty = -2.0 - dy;
-            else ty = 0.0;
-            bool close = dx * dx + ty * ty <= 0.1;
-            int tg = a.toggles[g];
-            uint8_t ns = a.near_start[g];
-            if (close && !ns) { ns = 1; ++tg; }
-            else if (!close && ns) { ns = 0; ++tg; }
-            a.toggles[g] = tg;
-            a.near_start[g] = ns;
-            float lc = (float)(tg / 2);
-            float lt = tg < 4 ? (float)tnow : a.lap_times[g];
-            a.lap_counts[g] = lc;
-            a.lap_times[g] = lt;
-            if (a.out.lap_counts) a.out.lap_counts[g] = lc;
-            if (a.out.lap_times) a.out.lap_times[g] = lt;
-            all4 = all4 && tg >= 4;
-        }
-        bool term = sh.col[a.ego] || all4;
-        if (a.out.terminated) a.out.terminated[e] = term ? 1 : 0;
-        if (a.out.was_reset) a.out.was_reset[e] = (uint8_t)sh.do_reset;
-        if (a.out.sim_time) a.out.sim_time[e] = tnow;
-        a.pending[e] = (a.autoreset && term) ? 1 : 0;
-        if (sh.do_reset && a.mode == 0) a.episode[e] += 1;
-        a.nstep[e] = a.noise_step[e] + 1;
+    if (tid == 0) env_epilogue(a, e, &sh.stl[0][0], 7, sh.col, sh.do_reset);
+}
+
+// k_post_single: single-agent envs after the FUSED ray kernel, one thread per
+// env: the TTC response (RaceCar.check_ttc, base_classes.py:246-249), the
+// pose part of the observation, collisions and the env epilogue.
+__global__ void __launch_bounds__(64) k_post_single(StepArgs a) {
+    const int e = blockIdx.x * 64 + threadIdx.x;
+    if (e >= a.E) return;
+    if (a.mode == 1 && a.reset_mask && !a.reset_mask[e]) return;
+    const int EA = a.E;  // A == 1: car g == env e
+    double stl[2] = {a.st[e], a.st[EA + e]};
+    double yaw = a.st[(size_t)4 * EA + e];
+    int32_t col = a.ttc_hit[e];
+    if (col) {  // state[3:] = 0 (yaw included)
+#pragma unroll
+        for (int k = 3; k < 7; ++k) a.st[(size_t)k * EA + e] = 0.0;
+        yaw = 0.0;
     }
+    if (a.out.obs) {
+        float *o = a.out.obs + (size_t)e * (a.B + 4) + a.B;
+        o[0] = (float)stl[0];
+        o[1] = (float)stl[1];
+        o[2] = (float)wrap_angle(yaw);
+        o[3] = col ? 1.0f : 0.0f;
+    }
+    if (a.out.collisions) a.out.collisions[e] = (uint8_t)col;
+    env_epilogue(a, e, stl, 2, &col, a.reset_flag[e]);
 }
 
 hipError_t prepare_env_step(size_t lds_bytes) {
@@ -426,10 +503,12 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
     const int64_t R = (int64_t)EA * a.B;
     const dim3 grid((unsigned)((R + kBlock - 1) / kBlock));
+    // single-agent envs on the tiled kernel: TTC + outputs fused into the ray pass
+    const bool fused = a.A == 1 && a.ray_kernel != 0;
     if (a.ray_kernel == 0) {
         hipLaunchKernelGGL(k_rays, grid, dim3(kBlock), 0, s, a);
     } else {
-        RayArgs ra;
+        RayArgs ra{};
         ra.m = a.tmap;
         ra.sines = a.sines;
         ra.cosines = a.cosines;
@@ -450,20 +529,37 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         ra.A = a.A;
         ra.B = a.B;
         ra.theta_dis = a.theta_dis;
+        ra.vel = a.st + (size_t)3 * EA;
+        ra.beam_cos = a.beam_cos;
+        ra.side = a.side;
+        ra.ttc_thresh = a.ttc_thresh;
+        ra.ttc_hit = a.ttc_hit;
+        ra.obs = a.out.obs;
+        ra.obs_len = a.B + 4 * a.A;
+        ra.lidar_max = (float)a.p.lidar_max;
+        ra.scans_f32 = a.out.scans;
+        ra.scans_f64 = a.out.scans_f64;
         const bool rot = !(a.tmap.os == 0.0 && a.tmap.oc == 1.0);
         const bool mask = ra.reset_mask != nullptr;
-        if (!rot && !mask)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rays_tiled<false, false>), grid, dim3(kBlock), 0, s, ra);
-        else if (!rot)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rays_tiled<false, true>), grid, dim3(kBlock), 0, s, ra);
-        else if (!mask)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rays_tiled<true, false>), grid, dim3(kBlock), 0, s, ra);
-        else
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rays_tiled<true, true>), grid, dim3(kBlock), 0, s, ra);
+        const int v = (rot ? 4 : 0) + (mask ? 2 : 0) + (fused ? 1 : 0);
+        const void *fn[8] = {
+            reinterpret_cast<const void *>(&k_rays_tiled<false, false, false>),
+            reinterpret_cast<const void *>(&k_rays_tiled<false, false, true>),
+            reinterpret_cast<const void *>(&k_rays_tiled<false, true, false>),
+            reinterpret_cast<const void *>(&k_rays_tiled<false, true, true>),
+            reinterpret_cast<const void *>(&k_rays_tiled<true, false, false>),
+            reinterpret_cast<const void *>(&k_rays_tiled<true, false, true>),
+            reinterpret_cast<const void *>(&k_rays_tiled<true, true, false>),
+            reinterpret_cast<const void *>(&k_rays_tiled<true, true, true>)};
+        void *args[] = {&ra};
+        if ((e = hipLaunchKernel(fn[v], grid, dim3(kBlock), args, 0, s)) != hipSuccess) return e;
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_post, dim3(a.E), dim3(kBlock), post_lds_bytes(a.A, a.B), s, a);
+    if (fused)
+        hipLaunchKernelGGL(k_post_single, dim3((a.E + 63) / 64), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_post, dim3(a.E), dim3(kBlock), post_lds_bytes(a.A, a.B), s, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[3], s)) != hipSuccess) return e;
     return hipSuccess;
