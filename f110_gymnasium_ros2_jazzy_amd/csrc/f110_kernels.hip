@@ -246,6 +246,24 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
             double x = a.ray0[g], y = a.ray0[a.EA + g];
             double d = a.ray0[2 * a.EA + g];  // :129
             double tot = d;                   // :130
+            // FUSED: the TTC operands are loaded before the loop, which hides
+            // their latency (the epilogue would otherwise wait on them)
+            double v = 0.0, bcos = 0.0, side = 0.0;
+            if (FUSED) {
+                v = a.vel[g];
+                bcos = a.beam_cos[b];
+                side = a.side[b];
+            }
+            // the ray's scan noise does not depend on the trace: drawn (or
+            // loaded) here, it overlaps the set-up loads above
+            double noise = 0.0;
+            {
+                const RayArgs &K = *kernarg_rays();
+                if (K.noise_ext)
+                    noise = K.noise_ext[(size_t)e * B + b];
+                else if (K.noise_std > 0.0)
+                    noise = K.noise_std * (double)beam_normal(K.seed, (uint64_t)(K.env_offset + e), K.noise_step[e], b);
+            }
             uint32_t k = 1;
             const double eps = a.eps, mr = a.max_range;
             while (d > eps && tot <= mr) {  // :133
@@ -262,13 +280,10 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
             // 7 instead of 8 blocks per CU).
             const RayArgs &K = *kernarg_rays();
             double range = tot > mr ? mr : tot;  // :143-144
-            if (K.noise_ext)  // see store_ray
-                range += K.noise_ext[(size_t)e * B + b];
-            else if (K.noise_std > 0.0)
-                range += K.noise_std * (double)beam_normal(K.seed, (uint64_t)(K.env_offset + e), K.noise_step[e], b);
+            if (K.noise_ext || K.noise_std > 0.0) range += noise;  // noise after the clamp (see store_ray)
             if (FUSED) {
-                const double v = K.vel[g];  // state[3] after update_pose
-                if (v != 0.0 && ttc_fires(range, K.side[b], v * K.beam_cos[b], K.ttc_thresh)) K.ttc_hit[g] = 1;
+                // state[3] after update_pose; check_ttc_jit on the noisy scan
+                if (v != 0.0 && ttc_fires(range, side, v * bcos, K.ttc_thresh)) K.ttc_hit[g] = 1;
                 if (K.obs) K.obs[(size_t)e * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
                 if (K.scans_f32) K.scans_f32[r] = (float)range;
                 if (K.scans_f64) K.scans_f64[r] = range;
