@@ -49,6 +49,7 @@ struct f110_ctx {
     int ray_kernel = 1;  // F110_RAY_KERNEL=0 selects the row-major k_rays (A/B)
     double *dt = nullptr, *sines = nullptr, *cosines = nullptr, *angles = nullptr, *beam_cos = nullptr,
            *side = nullptr, *spawn = nullptr;
+    double *start_rot = nullptr;
     double *st = nullptr, *sb = nullptr, *start = nullptr, *sim_time = nullptr, *ray0 = nullptr, *scan = nullptr;
     BeamRun *runs = nullptr;
     int32_t *nruns = nullptr;
@@ -387,6 +388,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     ALLOC(c->ttc_hit, EA);
     ALLOC(c->noise_step, (size_t)C.n_envs);
     ALLOC(c->start, 3 * EA);
+    ALLOC(c->start_rot, 2 * (size_t)C.n_envs);
     ALLOC(c->toggles, EA);
     ALLOC(c->near_start, EA);
     ALLOC(c->lap_times, EA);
@@ -477,6 +479,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.sb = c->sb;
     a.scnt = c->scnt;
     a.start = c->start;
+    a.start_rot = c->start_rot;
     a.toggles = c->toggles;
     a.near_start = c->near_start;
     a.lap_times = c->lap_times;

@@ -33,6 +33,7 @@ struct StepArgs {
     double *sb;          // [2][E*A] steer buffer (newest, older)
     int32_t *scnt;       // [E*A]
     double *start;       // [3][E*A] reset poses (lap logic)
+    double *start_rot;   // [2][E] cos(-th), sin(-th) of the ego's reset yaw
     int32_t *toggles;    // [E*A]
     uint8_t *near_start; // [E*A]
     float *lap_times;    // [E*A]

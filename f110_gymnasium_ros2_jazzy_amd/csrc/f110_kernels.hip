@@ -128,6 +128,10 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
         a.start[g] = pz[0];
         a.start[EA + g] = pz[1];
         a.start[2 * EA + g] = pz[2];
+        if (ag == a.ego) {  // F110Env.reset's start_rot (f110_env.py:450-451), once per episode
+            a.start_rot[e] = cos(-pz[2]);
+            a.start_rot[a.E + e] = sin(-pz[2]);
+        }
         a.toggles[g] = 0;
         a.near_start[g] = 1;
         a.lap_times[g] = 0.0f;
@@ -153,8 +157,12 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
     a.sb[EA + g] = b1;
     a.scnt[g] = cnt;
     // scan pose (base_classes.py:420-422) and everything every ray of this car shares
-    const double sx = s[0] + a.lidar_dist * cos(s[4]);
-    const double sy = s[1] + a.lidar_dist * sin(s[4]);
+    // base_classes.py:420-422; with lidar_dist == 0 the offset is +-0 for any
+    // finite yaw, so the transcendentals are skipped (a non-finite yaw keeps
+    // the reference's NaN)
+    const bool no_offset = a.lidar_dist == 0.0 && isfinite(s[4]);
+    const double sx = no_offset ? s[0] + 0.0 : s[0] + a.lidar_dist * cos(s[4]);
+    const double sy = no_offset ? s[1] + 0.0 : s[1] + a.lidar_dist * sin(s[4]);
     a.ray0[g] = sx;
     a.ray0[EA + g] = sy;
     a.ray0[2 * EA + g] = a.map.dt[cell_index(a.map, sx, sy)];  // first lookup (laser_models.py:129)
@@ -305,8 +313,8 @@ __device__ void env_epilogue(const StepArgs &a, int e, const double *stl, int st
     const int EA = a.E * A;
     double tnow = (do_reset ? 0.0 : a.sim_time[e]) + a.dt;
     a.sim_time[e] = tnow;
-    const double th = a.start[2 * EA + e * A + a.ego];
-    const double r00 = cos(-th), r01 = -sin(-th), r10 = sin(-th), r11 = cos(-th);
+    const double ct = a.start_rot[e], st = a.start_rot[a.E + e];  // cos(-th), sin(-th) of the ego start yaw
+    const double r00 = ct, r01 = -st, r10 = st, r11 = ct;
     bool all4 = true;
     for (int i = 0; i < A; ++i) {
         const int g = e * A + i;
