@@ -496,6 +496,56 @@ F110_HD void blocked_range(double px, double py, double pth, const double v[8], 
     hi = mx;
 }
 
+// Which beams of a ray_cast can reach an opponent's box at all.  From scan
+// origin o outside the (convex) box, a ray at world angle theta meets an
+// edge only if theta lies in the angular interval the box subtends at o.
+// Beams more than kBeamMargin outside it miss every edge by a relative
+// margin (>= 1e-9 of the edge parameter for o at least kBoxClearance away),
+// far above f64 rounding, so the reference's get_range returns inf for all
+// four edges and the beam can be skipped.  The filter is off (half = inf)
+// when o is within kBoxClearance of a vertex or of an edge's line (which
+// includes are_collinear's 1e-8 test: get_range's denom == 0 branch ignores
+// the beam direction there), or inside the box.
+constexpr double kBeamMargin = 1e-5;
+constexpr double kBoxClearance = 1e-3;
+
+F110_HD double wrap_pm_pi(double a) { return a - 2.0 * kPi * rint(a / (2.0 * kPi)); }
+
+F110_HD void box_beam_window(double ox, double oy, const double v[8], double &center, double &half) {
+    center = 0.0;
+    half = INFINITY;
+    double phi[4];
+    int inside_pos = 0, inside_neg = 0;
+    for (int q = 0; q < 4; ++q) {
+        const double ax = v[2 * q], ay = v[2 * q + 1];
+        const double bx = v[2 * ((q + 1) & 3)], by = v[2 * ((q + 1) & 3) + 1];
+        const double dx = ax - ox, dy = ay - oy;
+        if (dx * dx + dy * dy < kBoxClearance * kBoxClearance) return;
+        // |cross(va - o, o - vb)| = |edge| * distance(o, edge line): no filter
+        // within kBoxClearance of any edge line (this also covers
+        // are_collinear's 1e-8 test and keeps d1's sign robust for rays whose
+        // backward half crosses an edge)
+        const double c = dx * (oy - by) - dy * (ox - bx);
+        const double ex = bx - ax, ey = by - ay;
+        if (fabs(c) < 1e-8 || c * c < kBoxClearance * kBoxClearance * (ex * ex + ey * ey)) return;
+        // side of o relative to edge a->b (all one sign: o inside the box)
+        const double side = (bx - ax) * (oy - ay) - (by - ay) * (ox - ax);
+        inside_pos += side > 0.0;
+        inside_neg += side < 0.0;
+        phi[q] = atan2(dy, dx);
+    }
+    if (inside_pos == 4 || inside_neg == 4) return;
+    double lo = 0.0, hi = 0.0;
+    for (int q = 1; q < 4; ++q) {
+        const double d = wrap_pm_pi(phi[q] - phi[0]);
+        lo = d < lo ? d : lo;
+        hi = d > hi ? d : hi;
+    }
+    if (hi - lo > kPi - 1e-3) return;  // o very close to the box: no filter
+    center = phi[0] + 0.5 * (lo + hi);
+    half = 0.5 * (hi - lo) + kBeamMargin;
+}
+
 // get_range, laser_models.py:249-280, with the beam's (cos, sin)(theta + pi/2)
 // hoisted out of the 4-edge loop (same values each call).
 F110_HD double get_range(double ox, double oy, double v30, double v31, double va0, double va1, double vb0,

@@ -232,12 +232,14 @@ __device__ __forceinline__ const RayArgs *kernarg_rays() {
 // (DESIGN.md §3): 2 and 4 interleaved rays per lane (1.4x / 2x slower), a
 // per-wave ray pool with lane refill (1.35x slower).
 //
-// FUSED (single-agent envs): nothing rewrites a scan after it is traced
-// (there is no agent ray_cast), so the ray also runs its TTC test
-// (check_ttc_jit, laser_models.py:188-217) and writes the observation /
-// scan outputs itself; k_post_single then only resolves the per-env state.
-// The f64 scan hand-off to k_post (8 B per ray written and read back) is gone.
-template <bool ROT, bool MASK, bool FUSED>
+// Every ray also runs its TTC test (check_ttc_jit, laser_models.py:188-217,
+// on the noisy pre-ray_cast scan) and raises its car's flag.  SINGLE
+// (single-agent envs): nothing rewrites a scan after it is traced (there is
+// no agent ray_cast), so the ray writes the observation / scan outputs itself
+// and k_post_single only resolves the per-env state; the f64 scan hand-off
+// (8 B per ray written and read back) is gone.  Multi-agent envs hand the f64
+// scan to k_post_multi, whose agent ray_cast edits it.
+template <bool ROT, bool MASK, bool SINGLE>
 __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
     const int B = a.B;
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -254,14 +256,9 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
             double x = a.ray0[g], y = a.ray0[a.EA + g];
             double d = a.ray0[2 * a.EA + g];  // :129
             double tot = d;                   // :130
-            // FUSED: the TTC operands are loaded before the loop, which hides
-            // their latency (the epilogue would otherwise wait on them)
-            double v = 0.0, bcos = 0.0, side = 0.0;
-            if (FUSED) {
-                v = a.vel[g];
-                bcos = a.beam_cos[b];
-                side = a.side[b];
-            }
+            // the TTC operands are loaded before the loop, which hides their
+            // latency (the epilogue would otherwise wait on them)
+            const double v = a.vel[g], bcos = a.beam_cos[b], side = a.side[b];
             // the ray's scan noise does not depend on the trace: drawn (or
             // loaded) here, it overlaps the set-up loads above
             double noise = 0.0;
@@ -289,9 +286,10 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
             const RayArgs &K = *kernarg_rays();
             double range = tot > mr ? mr : tot;  // :143-144
             if (K.noise_ext || K.noise_std > 0.0) range += noise;  // noise after the clamp (see store_ray)
-            if (FUSED) {
-                // state[3] after update_pose; check_ttc_jit on the noisy scan
-                if (v != 0.0 && ttc_fires(range, side, v * bcos, K.ttc_thresh)) K.ttc_hit[g] = 1;
+            // state[3] after update_pose; check_ttc_jit on the noisy scan,
+            // before the agent ray_cast (base_classes.py:597-599)
+            if (v != 0.0 && ttc_fires(range, side, v * bcos, K.ttc_thresh)) K.ttc_hit[g] = 1;
+            if (SINGLE) {
                 if (K.obs) K.obs[(size_t)e * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
                 if (K.scans_f32) K.scans_f32[r] = (float)range;
                 if (K.scans_f64) K.scans_f64[r] = range;
@@ -358,6 +356,7 @@ struct PostShared {
     double rv[kMaxAgents * (kMaxAgents - 1)][8];  // opponent j seen by agent i: RaceCar i's params (:223)
     int32_t hit[kMaxAgents];     // TTC hit
     int32_t col[kMaxAgents];     // collisions (GJK | TTC)
+    double wcen[kMaxAgents * (kMaxAgents - 1)], whalf[kMaxAgents * (kMaxAgents - 1)];  // box_beam_window
     int32_t blo[kMaxAgents * kMaxAgents], bhi[kMaxAgents * kMaxAgents];
     int32_t do_reset, pad_[3];
 };
@@ -429,6 +428,7 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
         get_vertices(sh.pose0[j][0], sh.pose0[j][1], sh.pose0[j][2], pi.length, pi.width, v);
         int lo, hi;
         blocked_range(sh.stl[i][0], sh.stl[i][1], sh.stl[i][4], v, a.angles, B, a.fov, a.beam_incr, lo, hi);
+        box_beam_window(sh.stl[i][0], sh.stl[i][1], v, sh.wcen[tid], sh.whalf[tid]);
         sh.blo[tid] = lo;
         sh.bhi[tid] = hi;
     }
@@ -440,7 +440,12 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
             int lo = sh.blo[pr], hi = sh.bhi[pr];
             const double ox = sh.stl[i][0], oy = sh.stl[i][1], oth = sh.stl[i][4];
             const double *v = sh.rv[pr];
+            const double wc = sh.wcen[pr], wh = sh.whalf[pr];
             for (int b = lo + tid; b <= hi; b += kBlock) {
+                // beams that cannot reach the box keep their range (see box_beam_window);
+                // get_blocked_view_indices' min..max spans most of the scan for an
+                // opponent behind the car, the filter keeps ~the box's own beams
+                if (!(fabs(wrap_pm_pi(oth + a.angles[b] - wc)) <= wh)) continue;
                 double bt = oth + a.angles[b] + kPi / 2.;
                 double v30 = cos(bt), v31 = sin(bt);
                 double cur = scan[i * B + b];
@@ -508,6 +513,128 @@ __global__ void __launch_bounds__(64) k_post_single(StepArgs a) {
     env_epilogue(a, e, stl, 2, &col, a.reset_flag[e]);
 }
 
+// k_post_multi: multi-agent envs after the tiled ray kernel (TTC flags are
+// already set).  Two waves per env and no LDS copy of the scans: the agent
+// ray_cast edits the f64 hand-off in place, so many envs stay resident per CU
+// and their serial phases overlap.  Wave 0 runs GJK (collision_multiple on
+// the pre-TTC poses) while wave 1 builds each (car, opponent) pair's box,
+// blocked beam range and beam window (on the post-TTC pose).
+constexpr int kMultiBlock = 128;
+
+struct MultiShared {
+    double stl[kMaxAgents][7];   // state after the TTC response
+    double pose0[kMaxAgents][3]; // agent_poses: before the TTC response (base_classes.py:587)
+    double verts[kMaxAgents][8]; // Simulator.check_collision's boxes (Simulator.params)
+    double rv[kMaxAgents * (kMaxAgents - 1)][8];  // opponent j seen by car i (RaceCar i's params)
+    double wcen[kMaxAgents * (kMaxAgents - 1)], whalf[kMaxAgents * (kMaxAgents - 1)];
+    int32_t blo[kMaxAgents * (kMaxAgents - 1)], bhi[kMaxAgents * (kMaxAgents - 1)];
+    int32_t col[kMaxAgents];
+    int32_t do_reset;
+};
+
+__global__ void __launch_bounds__(kMultiBlock) k_post_multi(StepArgs a) {
+    __shared__ MultiShared sh;
+    const int e = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int A = a.A, B = a.B;
+    const int EA = a.E * A;
+    if (a.mode == 1 && a.reset_mask && !a.reset_mask[e]) return;  // uniform per block
+    double *scan = a.scan + (size_t)e * A * B;
+    if (tid < A) {
+        const int g = e * A + tid;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) sh.stl[tid][k] = a.st[(size_t)k * EA + g];
+        sh.pose0[tid][0] = sh.stl[tid][0];
+        sh.pose0[tid][1] = sh.stl[tid][1];
+        sh.pose0[tid][2] = sh.stl[tid][4];
+        get_vertices(sh.stl[tid][0], sh.stl[tid][1], sh.stl[tid][4], a.p.length, a.p.width, sh.verts[tid]);
+        const int hit = a.ttc_hit[g];
+        sh.col[tid] = hit;  // Simulator.step :601-602
+        if (hit) {          // RaceCar.check_ttc (base_classes.py:246-249): state[3:] = 0
+#pragma unroll
+            for (int k = 3; k < 7; ++k) {
+                sh.stl[tid][k] = 0.0;
+                a.st[(size_t)k * EA + g] = 0.0;
+            }
+        }
+    }
+    if (tid == 0) sh.do_reset = a.reset_flag[e];
+    __syncthreads();
+    if (tid == 0) {  // collision_multiple (collision_models.py:184-212)
+        for (int i = 0; i < A - 1; ++i)
+            for (int j = i + 1; j < A; ++j)
+                if (gjk_collision(sh.verts[i], sh.verts[j])) {
+                    sh.col[i] = 1;
+                    sh.col[j] = 1;
+                }
+    } else if (tid >= 64 && tid - 64 < A * (A - 1)) {
+        const int pr = tid - 64;
+        const int i = pr / (A - 1);
+        const int jj = pr - i * (A - 1);
+        const int j = jj < i ? jj : jj + 1;
+        // RaceCar.ray_cast_agents: get_vertices(opp_pose, self.params['length'], self.params['width'])
+        double *v = sh.rv[pr];
+        const f110_params &pi = a.pa[i];
+        get_vertices(sh.pose0[j][0], sh.pose0[j][1], sh.pose0[j][2], pi.length, pi.width, v);
+        int lo, hi;
+        blocked_range(sh.stl[i][0], sh.stl[i][1], sh.stl[i][4], v, a.angles, B, a.fov, a.beam_incr, lo, hi);
+        sh.blo[pr] = lo;
+        sh.bhi[pr] = hi;
+        box_beam_window(sh.stl[i][0], sh.stl[i][1], v, sh.wcen[pr], sh.whalf[pr]);
+    }
+    __syncthreads();
+    // agent ray_cast (base_classes.py:206-227; laser_models.py:318-346), one
+    // opponent at a time per car (each pass min-updates the same beams)
+    for (int jj = 0; jj < A - 1; ++jj) {
+        for (int i = 0; i < A; ++i) {
+            const int pr = i * (A - 1) + jj;
+            const int lo = sh.blo[pr], hi = sh.bhi[pr];
+            const double ox = sh.stl[i][0], oy = sh.stl[i][1], oth = sh.stl[i][4];
+            const double *v = sh.rv[pr];
+            const double wc = sh.wcen[pr], wh = sh.whalf[pr];
+            for (int b = lo + tid; b <= hi; b += kMultiBlock) {
+                if (!(fabs(wrap_pm_pi(oth + a.angles[b] - wc)) <= wh)) continue;  // box_beam_window
+                const double bt = oth + a.angles[b] + kPi / 2.;
+                const double v30 = cos(bt), v31 = sin(bt);
+                double cur = scan[i * B + b];
+                const double cur0 = cur;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int q1 = (q + 1) & 3;
+                    const double rr = get_range(ox, oy, v30, v31, v[2 * q], v[2 * q + 1], v[2 * q1], v[2 * q1 + 1]);
+                    if (rr < cur) cur = rr;
+                }
+                if (cur != cur0) scan[i * B + b] = cur;
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- outputs --------------------------------------------------------
+    const int obs_len = B + 4 * A;
+    if (a.out.obs) {  // F110Env._pack_flat_obs, f110_env.py:552-584 (scan of agent 0)
+        float *o = a.out.obs + (size_t)e * obs_len;
+        const float lmax = (float)a.p.lidar_max;
+        for (int b = tid; b < B; b += kMultiBlock) o[b] = obs_scan_value(scan[b], lmax);
+        if (tid < A) {
+            o[B + 4 * tid + 0] = (float)sh.stl[tid][0];
+            o[B + 4 * tid + 1] = (float)sh.stl[tid][1];
+            o[B + 4 * tid + 2] = (float)wrap_angle(sh.stl[tid][4]);
+            o[B + 4 * tid + 3] = sh.col[tid] ? 1.0f : 0.0f;
+        }
+    }
+    if (a.out.scans) {
+        float *o = a.out.scans + (size_t)e * A * B;
+        for (int id = tid; id < A * B; id += kMultiBlock) o[id] = (float)scan[id];
+    }
+    if (a.out.scans_f64) {
+        double *o = a.out.scans_f64 + (size_t)e * A * B;
+        for (int id = tid; id < A * B; id += kMultiBlock) o[id] = scan[id];
+    }
+    if (a.out.collisions && tid < A) a.out.collisions[(size_t)e * A + tid] = (uint8_t)sh.col[tid];
+    if (tid == 0) env_epilogue(a, e, &sh.stl[0][0], 7, sh.col, sh.do_reset);
+}
+
 hipError_t prepare_env_step(size_t lds_bytes) {
     if (lds_bytes <= 64 * 1024) return hipSuccess;
     return hipFuncSetAttribute(reinterpret_cast<const void *>(&k_post), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -526,8 +653,10 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
     const int64_t R = (int64_t)EA * a.B;
     const dim3 grid((unsigned)((R + kBlock - 1) / kBlock));
-    // single-agent envs on the tiled kernel: TTC + outputs fused into the ray pass
-    const bool fused = a.A == 1 && a.ray_kernel != 0;
+    // tiled kernel: TTC in the ray pass; single-agent envs also write their
+    // outputs there (k_post_single), multi-agent envs go through k_post_multi
+    const bool tiled = a.ray_kernel != 0;
+    const bool single = a.A == 1 && tiled;
     if (a.ray_kernel == 0) {
         hipLaunchKernelGGL(k_rays, grid, dim3(kBlock), 0, s, a);
     } else {
@@ -564,7 +693,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         ra.scans_f64 = a.out.scans_f64;
         const bool rot = !(a.tmap.os == 0.0 && a.tmap.oc == 1.0);
         const bool mask = ra.reset_mask != nullptr;
-        const int v = (rot ? 4 : 0) + (mask ? 2 : 0) + (fused ? 1 : 0);
+        const int v = (rot ? 4 : 0) + (mask ? 2 : 0) + (single ? 1 : 0);
         const void *fn[8] = {
             reinterpret_cast<const void *>(&k_rays_tiled<false, false, false>),
             reinterpret_cast<const void *>(&k_rays_tiled<false, false, true>),
@@ -579,8 +708,10 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;
-    if (fused)
+    if (single)
         hipLaunchKernelGGL(k_post_single, dim3((a.E + 63) / 64), dim3(64), 0, s, a);
+    else if (tiled)
+        hipLaunchKernelGGL(k_post_multi, dim3(a.E), dim3(kMultiBlock), 0, s, a);
     else
         hipLaunchKernelGGL(k_post, dim3(a.E), dim3(kBlock), post_lds_bytes(a.A, a.B), s, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;

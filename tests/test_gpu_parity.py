@@ -173,3 +173,57 @@ def test_obs_packing(sims):
         assert np.array_equal(obs[:, 1080 + 4 * a + 1], st[:, a, 1].astype(np.float32))
         assert np.array_equal(obs[:, 1080 + 4 * a + 2], np.array([wrap(float(v)) for v in st[:, a, 4]], np.float32))
         assert np.array_equal(obs[:, 1080 + 4 * a + 3], out.collisions.cpu().numpy()[:, a].astype(np.float32))
+
+
+def _adversarial_poses(rng, E, A, sp):
+    """Per env: agent 0 on the centerline; the others behind it (where
+    get_blocked_view_indices spans most of the scan), beside it, touching or
+    overlapping it, or exactly on the extension of one of its edge lines."""
+    W, L = 0.31, 0.58
+    out = np.zeros((E, A, 3))
+    for e in range(E):
+        x, y, th = sp[rng.integers(0, sp.shape[0]), 0]
+        out[e, 0] = (x, y, th)
+        c, s = np.cos(th), np.sin(th)
+        for a in range(1, A):
+            kind = rng.integers(0, 6)
+            if kind == 0:    # behind, 0.5 - 3 m
+                dx, dy, dth = -rng.uniform(0.5, 3.0), rng.uniform(-0.5, 0.5), rng.normal(0, 0.3)
+            elif kind == 1:  # beside
+                dx, dy, dth = rng.uniform(-0.5, 0.5), rng.choice([-1, 1]) * rng.uniform(0.35, 1.5), rng.normal(0, 0.5)
+            elif kind == 2:  # touching / overlapping
+                dx, dy, dth = rng.uniform(-0.7, 0.7), rng.uniform(-0.35, 0.35), rng.uniform(-np.pi, np.pi)
+            elif kind == 3:  # agent 0's scan origin on the line of the other car's side edge
+                dx, dy, dth = rng.uniform(0.8, 3.0), W / 2, 0.0
+            elif kind == 4:  # ... or of its rear edge (car rotated 90 degrees)
+                dx, dy, dth = rng.uniform(0.8, 3.0), L / 2, np.pi / 2
+            else:            # ahead
+                dx, dy, dth = rng.uniform(0.6, 4.0), rng.uniform(-0.6, 0.6), rng.normal(0, 0.3)
+            out[e, a] = (x + c * dx - s * dy, y + s * dx + c * dy, th + dth)
+    return out
+
+
+@pytest.mark.parametrize("A", [2, 3])
+def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A):
+    """Agent ray_cast (base_classes.py:206-227, laser_models.py:318-346) with
+    opponents behind / beside / touching / on edge-line extensions: the device
+    beam-window filter must not change a single range."""
+    from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns
+    import oracle as O
+    E = 256
+    rng = np.random.default_rng(100 + A)
+    poses = _adversarial_poses(rng, E, A, centerline_spawns("Spielberg", 1))
+    sim = sims("Spielberg_map", E, A)
+    ref = O.OracleSim(oracle_scanners("Spielberg_map"), E, A)
+    sim.reset(poses)
+    ref.reset(poses)
+    rs, rc = ref.step(np.zeros((E, A, 2)))
+    for t in range(4):
+        g = sim.out.scans_f64.cpu().numpy()
+        np.testing.assert_allclose(g, rs, rtol=1e-9, atol=1e-9)
+        assert np.mean(g == rs) > 0.99, t
+        np.testing.assert_array_equal(sim.out.collisions.cpu().numpy(), rc.astype(np.uint8))
+        act = np.stack([rng.uniform(-0.2, 0.2, (E, A)), rng.uniform(0, 3, (E, A))], -1)
+        ref.state[:] = sim.agent_states().cpu().numpy().reshape(E * A, 7)
+        sim.step(act)
+        rs, rc = ref.step(act)
