@@ -48,6 +48,7 @@ EXPORTS = [
     "f110_scan_batch", "f110_dynamics_batch", "f110_read_counters", "f110_reset_counters",
     "f110_profile_begin", "f110_profile_end", "f110_host_tables", "f110_host_beam_indices",
     "f110_set_scan_noise", "f110_set_params", "f110_host_cell_index", "f110_gap_follow",
+    "f110_host_window_ranges",
 ]
 
 _lib = None
@@ -98,6 +99,9 @@ def load(build_if_missing: bool = True):
     L.f110_read_counters.argtypes = [_P, ctypes.POINTER(u64), ctypes.POINTER(u64), _P]
     L.f110_reset_counters.argtypes = [_P, _P]
     L.f110_set_scan_noise.argtypes = [_P, _P]
+    L.f110_host_window_ranges.argtypes = [ctypes.c_double, ctypes.c_double, i32, ctypes.c_double, ctypes.c_double,
+                                          _P]
+    L.f110_host_window_ranges.restype = None
     L.f110_gap_follow.argtypes = [_P, i64, i64, i32, ctypes.c_double, ctypes.c_double, _P, i64, _P, _P]
     L.f110_host_cell_index.argtypes = [i32, i32, ctypes.c_double, _D, _P, i64, _P]
     L.f110_set_params.argtypes = [_P, ctypes.POINTER(F110Params), i32, _P]
@@ -108,7 +112,7 @@ def load(build_if_missing: bool = True):
     L.f110_host_beam_indices.restype = ctypes.c_int
     for name in EXPORTS:
         if name not in ("f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config",
-                        "f110_host_tables"):
+                        "f110_host_tables", "f110_host_window_ranges"):
             getattr(L, name).restype = ctypes.c_int
     if L.f110_abi_version() != 1:
         raise F110Error("libf110.so ABI version mismatch")

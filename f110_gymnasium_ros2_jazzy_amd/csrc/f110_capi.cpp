@@ -712,3 +712,13 @@ extern "C" int f110_gap_follow(const float *scans, int64_t n_scans, int64_t scan
     HIP_TRY(launch_gap_follow(a, (hipStream_t)stream));
     return F110_OK;
 }
+
+extern "C" void f110_host_window_ranges(double yaw, double fov, int32_t n_beams, double center, double half,
+                                        int32_t ranges_out[4]) {
+    int r0a, r0b, r1a, r1b;
+    window_beam_ranges(yaw, fov, fov / (double)(n_beams - 1), n_beams, center, half, r0a, r0b, r1a, r1b);
+    ranges_out[0] = r0a;
+    ranges_out[1] = r0b;
+    ranges_out[2] = r1a;
+    ranges_out[3] = r1b;
+}

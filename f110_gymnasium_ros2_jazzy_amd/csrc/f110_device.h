@@ -474,6 +474,21 @@ F110_HD int nearest_beam(const double *angles, int B, double fov, double incr, d
     return best;
 }
 
+// One vertex of get_blocked_view_indices (laser_models.py:282-315): the beam
+// nearest to the vertex bearing, relative to ego = atan2(sin(yaw), cos(yaw)).
+// phi receives the vertex bearing atan2(uy, ux) (used by box_beam_window).
+F110_HD int blocked_vertex_beam(double px, double py, double ego, double vx0, double vy0, const double *angles, int B,
+                                double fov, double incr, double &phi) {
+    double vx = vx0 - px, vy = vy0 - py;
+    double nrm = sqrt(vx * vx + vy * vy);
+    double ux = vx / nrm, uy = vy / nrm;
+    phi = atan2(uy, ux);
+    double angle = ego - phi;
+    if (angle > kPi) angle = angle - 2 * kPi;
+    else if (angle < -kPi) angle = angle + 2 * kPi;
+    return nearest_beam(angles, B, fov, incr, -angle);
+}
+
 // get_blocked_view_indices, laser_models.py:282-315
 F110_HD void blocked_range(double px, double py, double pth, const double v[8], const double *angles, int B,
                            double fov, double incr, int &lo, int &hi) {
@@ -509,9 +524,40 @@ F110_HD void blocked_range(double px, double py, double pth, const double v[8], 
 constexpr double kBeamMargin = 1e-5;
 constexpr double kBoxClearance = 1e-3;
 
-F110_HD double wrap_pm_pi(double a) { return a - 2.0 * kPi * rint(a / (2.0 * kPi)); }
+F110_HD double wrap_pm_pi(double a) { return a - 2.0 * kPi * rint(a * (0.5 / kPi)); }  // approximate
 
-F110_HD void box_beam_window(double ox, double oy, const double v[8], double &center, double &half) {
+// The beam-index ranges [r0a, r0b] and [r1a, r1b] (either may be empty) that
+// can hold beams of the window (center, half) for a car at yaw oth:
+// angle(b) = oth + angles[b] with angles[b] ~ -fov/2 + b*incr.  Padded by 2
+// beams; callers still apply the exact per-beam window test.
+F110_HD void window_beam_ranges(double oth, double fov, double incr, int B, double center, double half, int &r0a,
+                                int &r0b, int &r1a, int &r1b) {
+    r0a = 0;
+    r0b = B - 1;
+    r1a = 1;
+    r1b = 0;
+    if (!(half < kPi)) return;  // no filter: every beam
+    // u(b) = angle(b) - (center - half), taken mod 2pi into [0, 2pi)
+    double c0 = oth - fov / 2.0 - (center - half);
+    c0 = c0 - 2.0 * kPi * floor(c0 * (0.5 / kPi));
+    // in the window iff (c0 + b*incr) mod 2pi <= 2*half
+    const double w = 2.0 * half;
+    r0a = 0;
+    r0b = c0 <= w ? (int)floor((w - c0) / incr) + 2 : -1;
+    r1a = (int)ceil((2.0 * kPi - c0) / incr) - 2;
+    r1b = (int)floor((2.0 * kPi - c0 + w) / incr) + 2;
+    if (r0b > B - 1) r0b = B - 1;
+    if (r1a < 0) r1a = 0;
+    if (r1b > B - 1) r1b = B - 1;
+    if (r1a <= r1b && r0a <= r0b && r1a <= r0b + 1) {  // overlapping: one range
+        r0b = r1b > r0b ? r1b : r0b;
+        r1a = 1;
+        r1b = 0;
+    }
+}
+
+F110_HD void box_beam_window(double ox, double oy, const double v[8], const double phi_in[4], double &center,
+                             double &half) {
     center = 0.0;
     half = INFINITY;
     double phi[4];
@@ -532,7 +578,9 @@ F110_HD void box_beam_window(double ox, double oy, const double v[8], double &ce
         const double side = (bx - ax) * (oy - ay) - (by - ay) * (ox - ax);
         inside_pos += side > 0.0;
         inside_neg += side < 0.0;
-        phi[q] = atan2(dy, dx);
+        // bearing of the vertex from o (any approximation is fine: the margin
+        // is 1e-5 rad); phi_in = the blocked-range bearings when available
+        phi[q] = phi_in ? phi_in[q] : atan2(dy, dx);
     }
     if (inside_pos == 4 || inside_neg == 4) return;
     double lo = 0.0, hi = 0.0;

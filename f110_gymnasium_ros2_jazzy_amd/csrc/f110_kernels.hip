@@ -233,13 +233,12 @@ __device__ __forceinline__ const RayArgs *kernarg_rays() {
 // per-wave ray pool with lane refill (1.35x slower).
 //
 // Every ray also runs its TTC test (check_ttc_jit, laser_models.py:188-217,
-// on the noisy pre-ray_cast scan) and raises its car's flag.  SINGLE
-// (single-agent envs): nothing rewrites a scan after it is traced (there is
-// no agent ray_cast), so the ray writes the observation / scan outputs itself
-// and k_post_single only resolves the per-env state; the f64 scan hand-off
-// (8 B per ray written and read back) is gone.  Multi-agent envs hand the f64
-// scan to k_post_multi, whose agent ray_cast edits it.
-template <bool ROT, bool MASK, bool SINGLE>
+// on the noisy pre-ray_cast scan) and raises its car's flag, and writes its
+// observation / scan output entries.  Single-agent envs are then finished
+// (k_post_single resolves the per-env state; no f64 scan hand-off at all).
+// With other cars in the env (HANDOFF) the f64 range also goes to
+// k_post_multi, whose agent ray_cast re-writes the entries it shortens.
+template <bool ROT, bool MASK, bool HANDOFF>
 __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
     const int B = a.B;
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -289,13 +288,12 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
             // state[3] after update_pose; check_ttc_jit on the noisy scan,
             // before the agent ray_cast (base_classes.py:597-599)
             if (v != 0.0 && ttc_fires(range, side, v * bcos, K.ttc_thresh)) K.ttc_hit[g] = 1;
-            if (SINGLE) {
-                if (K.obs) K.obs[(size_t)e * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
-                if (K.scans_f32) K.scans_f32[r] = (float)range;
-                if (K.scans_f64) K.scans_f64[r] = range;
-            } else {
-                K.scan[r] = range;
-            }
+            // outputs straight from the ray; with other cars in the env
+            // (HANDOFF) k_post_multi patches the beams its ray_cast shortens
+            if (K.obs && g == e * a.A) K.obs[(size_t)e * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
+            if (K.scans_f32) K.scans_f32[r] = (float)range;
+            if (K.scans_f64) K.scans_f64[r] = range;
+            if (HANDOFF) K.scan[r] = range;
         }
     }
     count_rays(kernarg_rays()->ctr, n);
@@ -428,7 +426,7 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
         get_vertices(sh.pose0[j][0], sh.pose0[j][1], sh.pose0[j][2], pi.length, pi.width, v);
         int lo, hi;
         blocked_range(sh.stl[i][0], sh.stl[i][1], sh.stl[i][4], v, a.angles, B, a.fov, a.beam_incr, lo, hi);
-        box_beam_window(sh.stl[i][0], sh.stl[i][1], v, sh.wcen[tid], sh.whalf[tid]);
+        box_beam_window(sh.stl[i][0], sh.stl[i][1], v, nullptr, sh.wcen[tid], sh.whalf[tid]);
         sh.blo[tid] = lo;
         sh.bhi[tid] = hi;
     }
@@ -527,10 +525,21 @@ struct MultiShared {
     double verts[kMaxAgents][8]; // Simulator.check_collision's boxes (Simulator.params)
     double rv[kMaxAgents * (kMaxAgents - 1)][8];  // opponent j seen by car i (RaceCar i's params)
     double wcen[kMaxAgents * (kMaxAgents - 1)], whalf[kMaxAgents * (kMaxAgents - 1)];
+    double phi[kMaxAgents * (kMaxAgents - 1)][4];  // vertex bearings of each pair's box
+    double ego[kMaxAgents];                        // atan2(sin(yaw), cos(yaw)), post-TTC
+    int32_t kq[kMaxAgents * (kMaxAgents - 1)][4];  // nearest beam of each vertex
     int32_t blo[kMaxAgents * (kMaxAgents - 1)], bhi[kMaxAgents * (kMaxAgents - 1)];
+    int32_t rng[kMaxAgents * (kMaxAgents - 1)][4]; // window_beam_ranges, clipped to [blo, bhi]
     int32_t col[kMaxAgents];
     int32_t do_reset;
 };
+
+// LDS hand-off between the lanes of ONE wave (no workgroup barrier).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __global__ void __launch_bounds__(kMultiBlock) k_post_multi(StepArgs a) {
     __shared__ MultiShared sh;
@@ -567,32 +576,65 @@ __global__ void __launch_bounds__(kMultiBlock) k_post_multi(StepArgs a) {
                     sh.col[i] = 1;
                     sh.col[j] = 1;
                 }
-    } else if (tid >= 64 && tid - 64 < A * (A - 1)) {
-        const int pr = tid - 64;
-        const int i = pr / (A - 1);
-        const int jj = pr - i * (A - 1);
-        const int j = jj < i ? jj : jj + 1;
-        // RaceCar.ray_cast_agents: get_vertices(opp_pose, self.params['length'], self.params['width'])
-        double *v = sh.rv[pr];
-        const f110_params &pi = a.pa[i];
-        get_vertices(sh.pose0[j][0], sh.pose0[j][1], sh.pose0[j][2], pi.length, pi.width, v);
-        int lo, hi;
-        blocked_range(sh.stl[i][0], sh.stl[i][1], sh.stl[i][4], v, a.angles, B, a.fov, a.beam_incr, lo, hi);
-        sh.blo[pr] = lo;
-        sh.bhi[pr] = hi;
-        box_beam_window(sh.stl[i][0], sh.stl[i][1], v, sh.wcen[pr], sh.whalf[pr]);
+    } else if (tid >= 64) {
+        // per-pair geometry on wave 1, spread over lanes: boxes and ego
+        // headings, then one (pair, vertex) per lane, then per-pair reductions
+        const int lane = tid - 64;
+        const int NP = A * (A - 1);
+        for (int pr = lane; pr < NP; pr += 64) {
+            const int i = pr / (A - 1);
+            const int jj = pr - i * (A - 1);
+            const int j = jj < i ? jj : jj + 1;
+            // RaceCar.ray_cast_agents: get_vertices(opp_pose, self.params['length'], self.params['width'])
+            const f110_params &pi = a.pa[i];
+            get_vertices(sh.pose0[j][0], sh.pose0[j][1], sh.pose0[j][2], pi.length, pi.width, sh.rv[pr]);
+        }
+        if (lane < A) sh.ego[lane] = atan2(sin(sh.stl[lane][4]), cos(sh.stl[lane][4]));  // post-TTC yaw
+        wave_sync();
+        for (int w = lane; w < 4 * NP; w += 64) {  // get_blocked_view_indices, one vertex per lane
+            const int pr = w >> 2, q = w & 3;
+            const int i = pr / (A - 1);
+            sh.kq[pr][q] = blocked_vertex_beam(sh.stl[i][0], sh.stl[i][1], sh.ego[i], sh.rv[pr][2 * q],
+                                               sh.rv[pr][2 * q + 1], a.angles, B, a.fov, a.beam_incr, sh.phi[pr][q]);
+        }
+        wave_sync();
+        for (int pr = lane; pr < NP; pr += 64) {
+            const int i = pr / (A - 1);
+            int lo = sh.kq[pr][0], hi = sh.kq[pr][0];
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+                lo = sh.kq[pr][q] < lo ? sh.kq[pr][q] : lo;
+                hi = sh.kq[pr][q] > hi ? sh.kq[pr][q] : hi;
+            }
+            sh.blo[pr] = lo;
+            sh.bhi[pr] = hi;
+            double wc, wh;
+            box_beam_window(sh.stl[i][0], sh.stl[i][1], sh.rv[pr], sh.phi[pr], wc, wh);
+            sh.wcen[pr] = wc;
+            sh.whalf[pr] = wh;
+            int r0a, r0b, r1a, r1b;
+            window_beam_ranges(sh.stl[i][4], a.fov, a.beam_incr, B, wc, wh, r0a, r0b, r1a, r1b);
+            sh.rng[pr][0] = r0a > lo ? r0a : lo;  // beams lo..hi of ray_cast's loop that the window can hold
+            sh.rng[pr][1] = r0b < hi ? r0b : hi;
+            sh.rng[pr][2] = r1a > lo ? r1a : lo;
+            sh.rng[pr][3] = r1b < hi ? r1b : hi;
+        }
     }
     __syncthreads();
     // agent ray_cast (base_classes.py:206-227; laser_models.py:318-346), one
-    // opponent at a time per car (each pass min-updates the same beams)
+    // opponent at a time per car (each pass min-updates the same beams);
+    // only the beams of lo..hi that the box's window can hold are visited
     for (int jj = 0; jj < A - 1; ++jj) {
         for (int i = 0; i < A; ++i) {
             const int pr = i * (A - 1) + jj;
-            const int lo = sh.blo[pr], hi = sh.bhi[pr];
+            const int n0 = sh.rng[pr][1] - sh.rng[pr][0] + 1;
+            const int n1 = sh.rng[pr][3] - sh.rng[pr][2] + 1;
+            const int nb = (n0 > 0 ? n0 : 0) + (n1 > 0 ? n1 : 0);
             const double ox = sh.stl[i][0], oy = sh.stl[i][1], oth = sh.stl[i][4];
             const double *v = sh.rv[pr];
             const double wc = sh.wcen[pr], wh = sh.whalf[pr];
-            for (int b = lo + tid; b <= hi; b += kMultiBlock) {
+            for (int k = tid; k < nb; k += kMultiBlock) {
+                const int b = k < (n0 > 0 ? n0 : 0) ? sh.rng[pr][0] + k : sh.rng[pr][2] + k - (n0 > 0 ? n0 : 0);
                 if (!(fabs(wrap_pm_pi(oth + a.angles[b] - wc)) <= wh)) continue;  // box_beam_window
                 const double bt = oth + a.angles[b] + kPi / 2.;
                 const double v30 = cos(bt), v31 = sin(bt);
@@ -604,32 +646,26 @@ __global__ void __launch_bounds__(kMultiBlock) k_post_multi(StepArgs a) {
                     const double rr = get_range(ox, oy, v30, v31, v[2 * q], v[2 * q + 1], v[2 * q1], v[2 * q1 + 1]);
                     if (rr < cur) cur = rr;
                 }
-                if (cur != cur0) scan[i * B + b] = cur;
+                if (cur != cur0) {  // patch the ray pass's outputs for this beam
+                    scan[i * B + b] = cur;
+                    const size_t o = ((size_t)e * A + i) * B + b;
+                    if (a.out.scans) a.out.scans[o] = (float)cur;
+                    if (a.out.scans_f64) a.out.scans_f64[o] = cur;
+                    if (i == 0 && a.out.obs) a.out.obs[(size_t)e * (B + 4 * A) + b] = obs_scan_value(cur, (float)a.p.lidar_max);
+                }
             }
         }
         __syncthreads();
     }
 
     // ---- outputs --------------------------------------------------------
-    const int obs_len = B + 4 * A;
-    if (a.out.obs) {  // F110Env._pack_flat_obs, f110_env.py:552-584 (scan of agent 0)
-        float *o = a.out.obs + (size_t)e * obs_len;
-        const float lmax = (float)a.p.lidar_max;
-        for (int b = tid; b < B; b += kMultiBlock) o[b] = obs_scan_value(scan[b], lmax);
-        if (tid < A) {
-            o[B + 4 * tid + 0] = (float)sh.stl[tid][0];
-            o[B + 4 * tid + 1] = (float)sh.stl[tid][1];
-            o[B + 4 * tid + 2] = (float)wrap_angle(sh.stl[tid][4]);
-            o[B + 4 * tid + 3] = sh.col[tid] ? 1.0f : 0.0f;
-        }
-    }
-    if (a.out.scans) {
-        float *o = a.out.scans + (size_t)e * A * B;
-        for (int id = tid; id < A * B; id += kMultiBlock) o[id] = (float)scan[id];
-    }
-    if (a.out.scans_f64) {
-        double *o = a.out.scans_f64 + (size_t)e * A * B;
-        for (int id = tid; id < A * B; id += kMultiBlock) o[id] = scan[id];
+    // the scan entries were written by the ray pass (and patched above)
+    if (a.out.obs && tid < A) {  // F110Env._pack_flat_obs, f110_env.py:552-584: pose entries
+        float *o = a.out.obs + (size_t)e * (B + 4 * A) + B + 4 * tid;
+        o[0] = (float)sh.stl[tid][0];
+        o[1] = (float)sh.stl[tid][1];
+        o[2] = (float)wrap_angle(sh.stl[tid][4]);
+        o[3] = sh.col[tid] ? 1.0f : 0.0f;
     }
     if (a.out.collisions && tid < A) a.out.collisions[(size_t)e * A + tid] = (uint8_t)sh.col[tid];
     if (tid == 0) env_epilogue(a, e, &sh.stl[0][0], 7, sh.col, sh.do_reset);
@@ -693,7 +729,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         ra.scans_f64 = a.out.scans_f64;
         const bool rot = !(a.tmap.os == 0.0 && a.tmap.oc == 1.0);
         const bool mask = ra.reset_mask != nullptr;
-        const int v = (rot ? 4 : 0) + (mask ? 2 : 0) + (single ? 1 : 0);
+        const int v = (rot ? 4 : 0) + (mask ? 2 : 0) + (single ? 0 : 1);  // HANDOFF for A >= 2
         const void *fn[8] = {
             reinterpret_cast<const void *>(&k_rays_tiled<false, false, false>),
             reinterpret_cast<const void *>(&k_rays_tiled<false, false, true>),

@@ -246,6 +246,13 @@ F110_API int f110_host_beam_indices(double yaw, double fov, int32_t theta_dis, i
 F110_API int f110_host_cell_index(int32_t H, int32_t W, double resolution, const double origin[3], const double *xy,
                                   int64_t n, int64_t *lin_out);
 
+/* The beam-index ranges (r0a..r0b, r1a..r1b; empty when a > b) the agent
+ * ray_cast visits for an opponent box whose angular window at the scan
+ * origin is center +- half (world frame), for a car at yaw.  Host only; the
+ * CPU tests check they contain every beam inside the window. */
+F110_API void f110_host_window_ranges(double yaw, double fov, int32_t n_beams, double center, double half,
+                                      int32_t ranges_out[4]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -217,3 +217,27 @@ def test_cell_mappings_agree_on_boundaries(H, W, res, origin, roundup):
         with np.errstate(invalid="ignore"):
             up = ((x < W * res) & (x >= 0) & (np.floor(x / res) == W)) | ((y < H * res) & (y >= 0) & (np.floor(y / res) == H))
         assert up.any()
+
+
+def test_window_ranges_contain_window_beams():
+    """k_post_multi visits only the beam ranges window_beam_ranges returns;
+    every beam whose angle lies in the box window must be inside them."""
+    import ctypes
+    from f110_gymnasium_ros2_jazzy_amd import _lib
+    L = _lib.load(build_if_missing=False)
+    rng = np.random.default_rng(7)
+    for fov, B in ((4.7, 1080), (2 * np.pi - 0.01, 720), (1.0, 64), (4.7, 541)):
+        ang = np.empty(B)
+        L.f110_host_tables(2000, B, fov, ctypes.byref(_lib.default_params()), None, None,
+                           ang.ctypes.data, None, None)
+        for _ in range(3000):
+            yaw = rng.uniform(-50, 50)
+            center = rng.uniform(-10, 10)
+            half = rng.choice([rng.uniform(1e-5, 0.05), rng.uniform(0.05, 1.5), rng.uniform(1.5, 3.14)])
+            out = np.empty(4, np.int32)
+            L.f110_host_window_ranges(yaw, fov, B, center, half, out.ctypes.data)
+            d = yaw + ang - center
+            d = d - 2 * np.pi * np.rint(d / (2 * np.pi))
+            inside = np.nonzero(np.abs(d) <= half)[0]
+            covered = ((inside >= out[0]) & (inside <= out[1])) | ((inside >= out[2]) & (inside <= out[3]))
+            assert covered.all(), (fov, B, yaw, center, half, out, inside[~covered])
