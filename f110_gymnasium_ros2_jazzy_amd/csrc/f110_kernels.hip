@@ -576,10 +576,12 @@ __global__ void __launch_bounds__(kMultiBlock) k_post_multi(StepArgs a) {
                     sh.col[i] = 1;
                     sh.col[j] = 1;
                 }
-    } else if (tid >= 64) {
-        // per-pair geometry on wave 1, spread over lanes: boxes and ego
-        // headings, then one (pair, vertex) per lane, then per-pair reductions
-        const int lane = tid - 64;
+    }
+    if (kMultiBlock == 64 || tid >= 64) {
+        // per-pair geometry (on wave 1 when there are two), spread over lanes:
+        // boxes and ego headings, then one (pair, vertex) per lane, then
+        // per-pair reductions
+        const int lane = tid & 63;
         const int NP = A * (A - 1);
         for (int pr = lane; pr < NP; pr += 64) {
             const int i = pr / (A - 1);

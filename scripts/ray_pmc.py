@@ -6,12 +6,13 @@ import numpy as np, torch
 from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
 from f110_gymnasium_ros2_jazzy_amd.maps import load_map, centerline_spawns
 E = int(os.environ.get("MB_ENVS", 8192))
-sp = centerline_spawns("Spielberg", 1)
-sim = BatchSim(load_map("Spielberg_map"), n_envs=E, n_agents=1, autoreset=True, spawn_poses=sp)
+A = int(os.environ.get("MB_AGENTS", 1))
+sp = centerline_spawns("Spielberg", A)
+sim = BatchSim(load_map("Spielberg_map"), n_envs=E, n_agents=A, autoreset=True, spawn_poses=sp)
 rng = np.random.default_rng(0)
 sim.reset(sp[rng.integers(0, sp.shape[0], E)])
 g = torch.Generator(device="cuda"); g.manual_seed(0)
-acts = torch.rand(100, E, 1, 2, device="cuda", generator=g)
+acts = torch.rand(100, E, A, 2, device="cuda", generator=g)
 acts[..., 0] = acts[..., 0] * 0.8378 - 0.4189; acts[..., 1] *= 20
 for k in range(100):
     sim.step(acts[k], minimal_outputs=True)
