@@ -37,6 +37,17 @@ class F110Outputs(ctypes.Structure):
                 ("was_reset", _P), ("lap_times", _P), ("lap_counts", _P), ("sim_time", _P)]
 
 
+class F110RewardParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in
+                ("dt", "w_prog", "forward_sign", "alive_bonus", "w_rel_lead", "lead_clip", "w_lat", "lat_cap",
+                 "default_half_width", "lidar_max", "near_wall_dist", "w_wall", "wall_quantile", "opp_safe_dist",
+                 "w_opp", "ego_crash_penalty", "opp_crash_bonus", "beta")] + \
+               [(n, ctypes.c_int32) for n in ("grace_steps_wall", "grace_steps_opp", "auto_flip_steps",
+                                             "use_progress")]
+
+
+REWARD_STATE_BYTES = 8 * 12 + 4 * 4   # f110_reward_state
+
 F32 = 0
 F64 = 1
 INTEGRATOR_RK4 = 1
@@ -48,7 +59,8 @@ EXPORTS = [
     "f110_scan_batch", "f110_dynamics_batch", "f110_read_counters", "f110_reset_counters",
     "f110_profile_begin", "f110_profile_end", "f110_host_tables", "f110_host_beam_indices",
     "f110_set_scan_noise", "f110_set_params", "f110_host_cell_index", "f110_gap_follow",
-    "f110_host_window_ranges",
+    "f110_host_window_ranges", "f110_track_create", "f110_track_destroy", "f110_track_arrays",
+    "f110_default_reward_params", "f110_reward",
 ]
 
 _lib = None
@@ -102,6 +114,13 @@ def load(build_if_missing: bool = True):
     L.f110_host_window_ranges.argtypes = [ctypes.c_double, ctypes.c_double, i32, ctypes.c_double, ctypes.c_double,
                                           _P]
     L.f110_host_window_ranges.restype = None
+    L.f110_track_create.argtypes = [ctypes.POINTER(_P), i32, _P, _P, _P, i32, i32]
+    L.f110_track_destroy.argtypes = [_P]
+    L.f110_track_arrays.argtypes = [_P, _P, _P, _P, _P]
+    L.f110_track_arrays.restype = ctypes.c_double
+    L.f110_default_reward_params.argtypes = [ctypes.POINTER(F110RewardParams)]
+    L.f110_default_reward_params.restype = None
+    L.f110_reward.argtypes = [_P, ctypes.POINTER(F110RewardParams), _P, i64, i32, i32, _P, _P, _P, _P]
     L.f110_gap_follow.argtypes = [_P, i64, i64, i32, ctypes.c_double, ctypes.c_double, _P, i64, _P, _P]
     L.f110_host_cell_index.argtypes = [i32, i32, ctypes.c_double, _D, _P, i64, _P]
     L.f110_set_params.argtypes = [_P, ctypes.POINTER(F110Params), i32, _P]
@@ -112,7 +131,8 @@ def load(build_if_missing: bool = True):
     L.f110_host_beam_indices.restype = ctypes.c_int
     for name in EXPORTS:
         if name not in ("f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config",
-                        "f110_host_tables", "f110_host_window_ranges"):
+                        "f110_host_tables", "f110_host_window_ranges", "f110_track_arrays",
+                        "f110_default_reward_params"):
             getattr(L, name).restype = ctypes.c_int
     if L.f110_abi_version() != 1:
         raise F110Error("libf110.so ABI version mismatch")

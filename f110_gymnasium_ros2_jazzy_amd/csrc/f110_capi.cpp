@@ -6,6 +6,7 @@
 // (k_env_step) on the caller's stream; no allocation, no synchronisation.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -721,4 +722,137 @@ extern "C" void f110_host_window_ranges(double yaw, double fov, int32_t n_beams,
     ranges_out[1] = r0b;
     ranges_out[2] = r1a;
     ranges_out[3] = r1b;
+}
+
+// ---- training reward (rewards.py / track_progress.py) -----------------------
+struct f110_track {
+    int device = 0;
+    TrackView v{};
+    std::vector<double> s, tan, nrm, mid;
+    std::vector<void *> allocs;
+};
+
+extern "C" int f110_track_create(f110_track **out, int32_t device, const double *xy, const double *w_right,
+                                 const double *w_left, int32_t n, int32_t closed) {
+    if (!out || !xy || n < 2 || ((w_right == nullptr) != (w_left == nullptr)))
+        return fail(F110_E_INVALID, "f110_track_create: bad arguments (need >= 2 centerline points)");
+    const bool host_only = device < 0;  // derived arrays only (f110_track_arrays), no device copy
+    if (!host_only && hipSetDevice(device) != hipSuccess)
+        return fail(F110_E_NODEVICE, "f110_track_create: no such HIP device");
+    auto *t = new f110_track();
+    t->device = device;
+    // track_progress.py:29-46: seg = diff(xy); seg_len = norm(seg, axis=1) =
+    // sqrt(dx*dx + dy*dy); s = [0, cumsum(seg_len)]; tan = seg / max(seg_len,
+    // 1e-12); nrm = (-tan_y, tan_x); mid = (xy[:-1] + xy[1:]) * 0.5
+    t->s.assign((size_t)n, 0.0);
+    t->tan.assign((size_t)2 * (n - 1), 0.0);
+    t->nrm.assign((size_t)2 * (n - 1), 0.0);
+    t->mid.assign((size_t)2 * (n - 1), 0.0);
+    double acc = 0.0;
+    for (int32_t i = 0; i + 1 < n; ++i) {
+        const double dx = xy[2 * i + 2] - xy[2 * i], dy = xy[2 * i + 3] - xy[2 * i + 1];
+        const double len = std::sqrt(dx * dx + dy * dy);
+        acc = acc + len;
+        t->s[(size_t)i + 1] = acc;
+        const double den = len > 1e-12 ? len : 1e-12;
+        t->tan[2 * (size_t)i] = dx / den;
+        t->tan[2 * (size_t)i + 1] = dy / den;
+        t->nrm[2 * (size_t)i] = -t->tan[2 * (size_t)i + 1];
+        t->nrm[2 * (size_t)i + 1] = t->tan[2 * (size_t)i];
+        t->mid[2 * (size_t)i] = (xy[2 * i] + xy[2 * i + 2]) * 0.5;
+        t->mid[2 * (size_t)i + 1] = (xy[2 * i + 1] + xy[2 * i + 3]) * 0.5;
+    }
+    auto up = [&](const double *src, size_t cnt, const double **dst) -> hipError_t {
+        if (host_only) return hipSuccess;
+        void *q = nullptr;
+        hipError_t e = hipMalloc(&q, cnt * sizeof(double));
+        if (e != hipSuccess) return e;
+        t->allocs.push_back(q);
+        *dst = static_cast<const double *>(q);
+        return hipMemcpy(q, src, cnt * sizeof(double), hipMemcpyHostToDevice);
+    };
+    hipError_t e = up(xy, 2 * (size_t)n, &t->v.xy);
+    if (e == hipSuccess) e = up(t->s.data(), t->s.size(), &t->v.s);
+    if (e == hipSuccess) e = up(t->tan.data(), t->tan.size(), &t->v.tan);
+    if (e == hipSuccess) e = up(t->nrm.data(), t->nrm.size(), &t->v.nrm);
+    if (e == hipSuccess) e = up(t->mid.data(), t->mid.size(), &t->v.mid);
+    if (e == hipSuccess && w_right) e = up(w_right, (size_t)n, &t->v.wR);
+    if (e == hipSuccess && w_left) e = up(w_left, (size_t)n, &t->v.wL);
+    if (e != hipSuccess) {
+        for (void *q : t->allocs) (void)hipFree(q);
+        delete t;
+        return fail(F110_E_HIP, std::string("f110_track_create: ") + hipGetErrorString(e));
+    }
+    t->v.n = n;
+    t->v.closed = closed ? 1 : 0;
+    t->v.L = t->s[(size_t)n - 1];
+    *out = t;
+    return F110_OK;
+}
+
+extern "C" int f110_track_destroy(f110_track *t) {
+    if (!t) return F110_OK;
+    if (!t->allocs.empty()) (void)hipSetDevice(t->device);
+    for (void *q : t->allocs) (void)hipFree(q);
+    delete t;
+    return F110_OK;
+}
+
+extern "C" double f110_track_arrays(const f110_track *t, double *s, double *tan, double *nrm, double *mid) {
+    if (!t) return 0.0;
+    if (s) std::copy(t->s.begin(), t->s.end(), s);
+    if (tan) std::copy(t->tan.begin(), t->tan.end(), tan);
+    if (nrm) std::copy(t->nrm.begin(), t->nrm.end(), nrm);
+    if (mid) std::copy(t->mid.begin(), t->mid.end(), mid);
+    return t->v.L;
+}
+
+extern "C" void f110_default_reward_params(f110_reward_params *p) {
+    if (!p) return;
+    *p = f110_reward_params{};
+    // CenterlineSafetyProgressReward.__init__ defaults (rewards.py:196-230)
+    p->dt = 0.01;
+    p->w_prog = 1.2;
+    p->forward_sign = 1.0;
+    p->alive_bonus = 0.02;
+    p->w_rel_lead = 0.0;
+    p->lead_clip = 5.0;
+    p->w_lat = 0.35;
+    p->lat_cap = 4.0;
+    p->default_half_width = 1.5;
+    p->lidar_max = 1.0;  // LIDAR_MAX (rewards.py:7)
+    p->near_wall_dist = 0.35 / 30.0;
+    p->w_wall = 1.0;
+    p->wall_quantile = 0.05;
+    p->opp_safe_dist = 0.7;
+    p->w_opp = 0.8;
+    p->ego_crash_penalty = 50.0;
+    p->opp_crash_bonus = 50.0;
+    p->beta = 0.8;
+    p->grace_steps_wall = 25;
+    p->grace_steps_opp = 25;
+    p->auto_flip_steps = 20;
+    p->use_progress = 1;
+}
+
+extern "C" int f110_reward(const f110_track *track, const f110_reward_params *params, const float *obs,
+                           int64_t n_envs, int32_t obs_len, int32_t n_beams, f110_reward_state *state,
+                           const uint8_t *reset_mask, double *rewards, void *stream) {
+    if (!params || n_envs < 0 || (n_envs > 0 && (!obs || !state || !rewards)) || n_beams < 0 || n_beams > 2048 ||
+        obs_len < n_beams + 8)
+        return fail(F110_E_INVALID, "f110_reward: bad arguments (obs rows need n_beams + 8 entries, n_beams <= 2048)");
+    if (params->use_progress && (!track || !track->v.mid))
+        return fail(F110_E_INVALID, "f110_reward: use_progress needs a device track");
+    RewardArgs a{};
+    if (track) a.track = track->v;
+    a.p = *params;
+    a.obs = obs;
+    a.E = n_envs;
+    a.obs_len = obs_len;
+    a.B = n_beams;
+    a.state = state;
+    a.reset_mask = reset_mask;
+    a.rewards = rewards;
+    HIP_TRY(launch_reward(a, (hipStream_t)stream));
+    return F110_OK;
 }

@@ -115,11 +115,35 @@ struct GapFollowArgs {
     int32_t B;
 };
 
+// CenterlineProgress arrays on the device (f110_track).
+struct TrackView {
+    const double *xy;   // [n][2]
+    const double *s;    // [n] arclength
+    const double *tan;  // [n-1][2]
+    const double *nrm;  // [n-1][2]
+    const double *mid;  // [n-1][2] segment midpoints
+    const double *wR, *wL;  // [n] lane widths or null
+    int32_t n, closed;
+    double L;
+};
+
+struct RewardArgs {
+    TrackView track;
+    f110_reward_params p;
+    const float *obs;
+    int64_t E;
+    int32_t obs_len, B;
+    f110_reward_state *state;
+    const uint8_t *reset_mask;
+    double *rewards;
+};
+
 size_t step_lds_bytes(int A, int B);
 hipError_t prepare_env_step(size_t lds_bytes);
 hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev = nullptr);  // ev: 4 events or null
 hipError_t launch_scan_batch(const ScanArgs &a, hipStream_t s);
 hipError_t launch_gap_follow(const GapFollowArgs &a, hipStream_t s);
+hipError_t launch_reward(const RewardArgs &a, hipStream_t s);
 size_t gap_follow_lds_bytes(int B);
 hipError_t launch_dynamics_batch(const double *x, const double *u, double *f, int64_t M, const f110_params &p,
                                  hipStream_t s);

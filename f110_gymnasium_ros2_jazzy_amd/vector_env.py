@@ -12,6 +12,10 @@ the gymnasium NEXT_STEP mode and runs on the device: the step after an env
 terminates resets it to a pose drawn from ``spawn_poses`` (and performs the
 reference's zero-action reset step); that step's reward is 0.
 
+``reward_fn`` (a reward.BatchedCenterlineReward) replaces the timestep
+reward with the training reward train_ddpg.py computes per step, evaluated on
+the device; autoreset steps reset its state and are rewarded 0.
+
 ``opponent="gap_follow"`` drives agent ``opponent_idx`` with the reference's
 rule-based opponent (gap_follow.py) on the device, as train_ddpg.py:168 does
 on the host: its action for step t comes from its own float32 scan of step
@@ -40,7 +44,7 @@ class F110VectorEnv:
                  params: dict | None = None, seed: int = 42, timestep: float = 0.01, device=0,
                  spawn_poses: np.ndarray | None = None, noise_std: float = 0.01, env_offset: int = 0,
                  ego_idx: int = 0, as_numpy: bool = False, autoreset: bool = True, opponent: str | None = None,
-                 opponent_idx: int = 1, **kwargs):
+                 opponent_idx: int = 1, reward_fn=None, **kwargs):
         self.num_envs = int(num_envs)
         self.num_agents = int(num_agents)
         self.params = dict(params or DEFAULT_PARAMS)
@@ -65,6 +69,11 @@ class F110VectorEnv:
         self._rng = np.random.default_rng(seed)
         self.opponent = opponent
         self.opponent_idx = int(opponent_idx)
+        # reward_fn: a BatchedCenterlineReward (reward.py) evaluated on the device
+        # from every step's observations, as train_ddpg.py:176 does per env
+        self.reward_fn = reward_fn
+        if reward_fn is not None and reward_fn.n_envs != self.num_envs:
+            raise ValueError("reward_fn must be built for num_envs envs")
         if opponent is not None:
             if opponent != "gap_follow":
                 raise ValueError(f"unknown opponent policy {opponent!r} (supported: 'gap_follow')")
@@ -104,6 +113,8 @@ class F110VectorEnv:
             options = self.spawn_poses[idx]
         out = self.sim.reset(options)
         self._opponent_next(out)
+        if self.reward_fn is not None:
+            self.reward_fn.reset()
         obs = out.obs.clone()
         return (obs.cpu().numpy() if self.as_numpy else obs), self._infos(out)
 
@@ -121,8 +132,11 @@ class F110VectorEnv:
         out = self.sim.step(a)
         self._opponent_next(out)
         reset = out.was_reset.bool()
-        rewards = torch.where(reset, torch.zeros((), device=self.device),
-                              torch.full((), self.timestep, device=self.device)).float()
+        if self.reward_fn is not None:  # reset envs: reward_fn.reset(), reward 0
+            rewards = self.reward_fn(out.obs, reset_mask=reset).clone()
+        else:
+            rewards = torch.where(reset, torch.zeros((), dtype=torch.float64, device=self.device),
+                                  torch.full((), self.timestep, dtype=torch.float64, device=self.device))
         term = out.terminated.bool()
         trunc = torch.zeros_like(term)
         obs = out.obs.clone()

@@ -253,6 +253,63 @@ F110_API int f110_host_cell_index(int32_t H, int32_t W, double resolution, const
 F110_API void f110_host_window_ranges(double yaw, double fov, int32_t n_beams, double center, double half,
                                       int32_t ranges_out[4]);
 
+/* ---- training reward ---------------------------------------------------------
+ * Replaces rl_training/utils/rewards.py:CenterlineSafetyProgressReward
+ * (:185-355) over utils/track_progress.py:CenterlineProgress (:5-110), the
+ * reward train_ddpg.py:125-176 computes on the host from every next_obs.
+ * Batched over envs on the device, one wave per env. */
+typedef struct f110_track f110_track;
+
+/* CenterlineProgress(csv, closed): xy [n][2] and the optional lane widths
+ * (w_tr_right_m / w_tr_left_m, NULL = none) as the CSV holds them; arclength,
+ * tangents, normals and segment midpoints are derived here exactly as the
+ * reference derives them (track_progress.py:29-46).  Host pointers.
+ * device < 0 builds the host arrays only (f110_track_arrays; no reward). */
+F110_API int f110_track_create(f110_track **out, int32_t device, const double *xy, const double *w_right,
+                               const double *w_left, int32_t n, int32_t closed);
+F110_API int f110_track_destroy(f110_track *track);
+/* The derived arrays (host copies; any pointer may be NULL): s [n],
+ * tan/nrm/mid [n-1][2]; returns L (the total arclength). */
+F110_API double f110_track_arrays(const f110_track *track, double *s, double *tan, double *nrm, double *mid);
+
+/* CenterlineSafetyProgressReward.__init__ kwargs (rewards.py:196-230). */
+typedef struct f110_reward_params {
+    double dt, w_prog, forward_sign, alive_bonus, w_rel_lead, lead_clip, w_lat, lat_cap, default_half_width;
+    double lidar_max, near_wall_dist, w_wall, wall_quantile, opp_safe_dist, w_opp, ego_crash_penalty;
+    double opp_crash_bonus, beta;  /* beta: _Prog / _ProgFallback EMA factor (0.8) */
+    int32_t grace_steps_wall, grace_steps_opp, auto_flip_steps; /* auto_flip_steps: _Prog (20) */
+    int32_t use_progress;          /* 1: centerline _Prog (a track is given), 0: _ProgFallback */
+} f110_reward_params;
+
+/* Per-env reward state in device memory; all-zero bytes = reward_fn.reset()
+ * (rewards.py:97-107 _Prog.reset, :256 reset). */
+typedef struct f110_reward_state {
+    double s_prev[2];  /* ego, opp: last arclength (_Prog._s_prev) */
+    double px[2], py[2];  /* last positions (_p_prev / _ProgFallback.prev) */
+    double cum[2];     /* _cum */
+    double ema;        /* _ema_abs_dego / ma_ego */
+    double t_last[2];  /* last lateral offsets */
+    double auto_sum;   /* running sum of _auto_buf */
+    int32_t steps;     /* _steps */
+    int32_t auto_n;    /* len(_auto_buf) */
+    int32_t flags;     /* bit0/1: s_prev ego/opp set, bit2/3: p_prev ego/opp set, bit4: _flip == -1 */
+    int32_t pad_;
+} f110_reward_state;
+
+F110_API void f110_default_reward_params(f110_reward_params *p);
+
+/* reward_fn(next_obs) for n_envs flat observations (device, float32
+ * [n_envs][obs_len], the F110Env layout: n_beams scaled ranges, then x, y,
+ * yaw, collision of ego and opponent; parse_flat_obs, rewards.py:11-41).
+ * state: device [n_envs]; reset_mask: device [n_envs] u8 or NULL -- a
+ * masked env's state is reset (reward_fn.reset()) and its reward is 0 (the
+ * reset observation of an autoresetting vector env is not rewarded).
+ * rewards: device [n_envs] f64.  track may be NULL when
+ * params->use_progress == 0.  Async on stream. */
+F110_API int f110_reward(const f110_track *track, const f110_reward_params *params, const float *obs, int64_t n_envs,
+                         int32_t obs_len, int32_t n_beams, f110_reward_state *state, const uint8_t *reset_mask,
+                         double *rewards, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

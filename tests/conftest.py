@@ -9,7 +9,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(REPO, "tests", "golden")
 MAPS = os.path.join(REPO, "f110_gymnasium_ros2_jazzy_amd", "maps")
-for p in (REPO, os.path.join(REPO, "oracle")):
+for p in (REPO, os.path.join(REPO, "oracle"), GOLDEN):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -576,6 +576,62 @@ def gen_env_gapfollow(cl):
         bc.RaceCar.reset = orig_reset
 
 
+from make_golden_configs import REWARD_CONFIGS  # noqa: E402
+
+
+def gen_reward(cl):
+    """CenterlineSafetyProgressReward (rl_training/utils/rewards.py:185-355) over
+    CenterlineProgress (track_progress.py:5-110) on the Spielberg centerline,
+    fed the F110Env observations of three episodes (noise off; both cars
+    driven by gap_follow_action, the ego's steering perturbed), as
+    train_ddpg.py:150-185 calls it: reward_fn.reset() before each episode,
+    reward_fn(next_obs) after every step."""
+    gf = _refload.load_path("gap_follow", "rl_training/utils/gap_follow.py")
+    tp = _refload.load_path("track_progress", "rl_training/utils/track_progress.py")
+    rw = _refload.load_path("rewards", "rl_training/utils/rewards.py")
+    csv = os.path.join(REF, "tools", "Raceline-Optimization", "inputs", "tracks", "Spielberg_map.csv")
+    P = tp.CenterlineProgress(csv, closed=True)
+    rng = np.random.default_rng(781)
+    f110_env = _refload.load_env()
+    bc.RaceCar.scan_simulator = None
+    orig_reset = bc.RaceCar.reset
+
+    def reset_no_noise(self, pose):
+        orig_reset(self, pose)
+        self.scan_rng = None
+
+    bc.RaceCar.reset = reset_no_noise
+    try:
+        env = f110_env.F110Env(map_dir=MAPS + "/", map="Spielberg_map", map_ext=".png", num_agents=2)
+        fns = {k: rw.CenterlineSafetyProgressReward(dt=0.01, progress=P, **v) for k, v in REWARD_CONFIGS.items()}
+        obs_l, ep_l, rew = [], [], {k: [] for k in fns}
+        starts = [(600, 30, 200), (2500, 20, 240), (4100, 45, 220)]
+        for ep, (i, gap, T) in enumerate(starts):
+            poses = _track_poses(cl, i, gap)
+            for f in fns.values():
+                f.reset()
+            obs, info = env.reset(options=poses)
+            for t in range(T):
+                ego = gf.gap_follow_action(info["scans"][0]).astype(np.float32)
+                ego[0] += np.float32(rng.normal(0, 0.08))
+                ego[1] = np.float32(ego[1] * 1.6)
+                opp = gf.gap_follow_action(info["scans"][1]).astype(np.float32)
+                obs, _, term, trunc, info = env.step(np.stack([ego, opp]).astype(np.float32))
+                obs_l.append(obs)
+                ep_l.append(ep)
+                for k, f in fns.items():
+                    rew[k].append(float(f(obs)))
+                if term:
+                    break
+        save("reward.npz", obs=np.asarray(obs_l, np.float32), episode=np.asarray(ep_l, np.int32),
+             **{"reward_" + k: np.asarray(v) for k, v in rew.items()},
+             config_names=np.array(list(REWARD_CONFIGS)),
+             track_xy=P.xy, track_s=P.s, track_tan=P.tan, track_nrm=P.nrm, track_mid=P.mid, track_wR=P.wR,
+             track_wL=P.wL, track_L=np.float64(P.L))
+    finally:
+        bc.RaceCar.reset = orig_reset
+
+
 def gen_noise():
     """Noise semantics of ScanSimulator2D.scan (laser_models.py:450-452) with the
     per-agent default_rng(seed) re-seeded at reset (base_classes.py:119,204):
@@ -629,6 +685,7 @@ def main():
     gen_env_params(cl)
     gen_gap_follow()
     gen_env_gapfollow(cl)
+    gen_reward(cl)
 
 
 if __name__ == "__main__":
@@ -636,6 +693,7 @@ if __name__ == "__main__":
         _cl = centerline()
         for name in sys.argv[1:]:
             {"env_noise": lambda c: gen_env_noise(c), "env_params": lambda c: gen_env_params(c),
-             "gap_follow": lambda c: gen_gap_follow(), "env_gapfollow": gen_env_gapfollow}[name](_cl)
+             "gap_follow": lambda c: gen_gap_follow(), "env_gapfollow": gen_env_gapfollow,
+             "reward": gen_reward}[name](_cl)
     else:
         main()

@@ -1,0 +1,117 @@
+"""Device training reward (f110_reward) vs the reference classes
+(tests/golden/reward.npz) and the CPU restatement (oracle/reward_oracle.py)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import MAPS, golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _kwargs(name):
+    import make_golden_configs as C
+    return C.REWARD_CONFIGS[name]
+
+
+@pytest.fixture(scope="module")
+def track(gpu):
+    from f110_gymnasium_ros2_jazzy_amd.reward import CenterlineTrack
+    c = np.load(os.path.join(MAPS, "Spielberg_centerline.npz"))
+    t = CenterlineTrack(c["xy"], c["w_right"], c["w_left"], device=0)
+    yield t
+    t.close()
+
+
+@pytest.mark.parametrize("name", ["train_ddpg", "all_terms"])
+def test_reward_matches_reference_episodes(track, name):
+    from f110_gymnasium_ros2_jazzy_amd.reward import BatchedCenterlineReward
+    d = golden("reward.npz")
+    f = BatchedCenterlineReward(1, dt=0.01, progress=track, **_kwargs(name))
+    got, prev = [], -1
+    for o, ep in zip(d["obs"], d["episode"]):
+        if ep != prev:
+            f.reset()
+            prev = ep
+        got.append(float(f(torch.as_tensor(o[None], device="cuda"))[0]))
+    ref = d["reward_" + name]
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-12)
+    assert np.mean(np.asarray(got) == ref) > 0.9
+
+
+def _random_obs(rng, xy, E, B=1080):
+    """Cars near the centerline (ego and opponent), random scans with zeros,
+    NaN and far values, rare collision flags."""
+    n = xy.shape[0]
+    i = rng.integers(0, n - 1, E)
+    j = (i + rng.integers(-60, 60, E)) % (n - 1)
+    o = np.empty((E, B + 8), np.float32)
+    o[:, :B] = rng.uniform(0.0, 0.5, (E, B))
+    o[:, :B][rng.random((E, B)) < 0.02] = 0.0
+    o[:, :B][rng.random((E, B)) < 0.002] = np.nan
+    o[:, :B][rng.random((E, B)) < 0.3] = rng.uniform(0.0, 0.02)
+    o[:, B:B + 2] = xy[i] + rng.normal(0, 0.5, (E, 2))
+    o[:, B + 2] = rng.uniform(-np.pi, np.pi, E)
+    o[:, B + 3] = rng.random(E) < 0.02
+    o[:, B + 4:B + 6] = xy[j] + rng.normal(0, 0.5, (E, 2))
+    o[:, B + 6] = rng.uniform(-4, 4, E)
+    o[:, B + 7] = rng.random(E) < 0.02
+    return o
+
+
+@pytest.mark.parametrize("name,progress", [("train_ddpg", True), ("all_terms", True), ("all_terms", False)])
+def test_reward_batch_vs_oracle(track, name, progress):
+    """256 envs x 30 steps of random-walk observations with random resets."""
+    import reward_oracle as R
+    from f110_gymnasium_ros2_jazzy_amd.reward import BatchedCenterlineReward
+    E = 256
+    rng = np.random.default_rng(hash(name) % 1000 + progress)
+    kw = dict(_kwargs(name))
+    f = BatchedCenterlineReward(E, dt=0.01, progress=track if progress else None, **kw)
+    T = R.TrackOracle(track.xy, track.wR, track.wL) if progress else None
+    refs = [R.RewardOracle(T, **kw) for _ in range(E)]
+    f.reset()
+    o = _random_obs(rng, track.xy, E)
+    for t in range(30):
+        step = o.copy()
+        step[:, 1080:1082] += rng.normal(0, 0.05, (E, 2)).astype(np.float32) * t
+        step[:, 1084:1086] += rng.normal(0, 0.05, (E, 2)).astype(np.float32) * t
+        reset = rng.random(E) < 0.05
+        got = f(torch.as_tensor(step, device="cuda"), reset_mask=torch.as_tensor(reset, device="cuda")).cpu().numpy()
+        exp = np.empty(E)
+        for e in range(E):
+            if reset[e]:
+                refs[e].reset()
+                exp[e] = 0.0
+            else:
+                exp[e] = refs[e](step[e])
+        np.testing.assert_allclose(got, exp, rtol=1e-9, atol=1e-12, err_msg=f"step {t}")
+
+
+def test_vector_env_reward_fn(track):
+    """F110VectorEnv(reward_fn=...) rewards = the reward of its own observations."""
+    from f110_gymnasium_ros2_jazzy_amd.reward import BatchedCenterlineReward
+    from f110_gymnasium_ros2_jazzy_amd.vector_env import F110VectorEnv
+    import reward_oracle as R
+    E = 16
+    rf = BatchedCenterlineReward(E, dt=0.01, progress=track, **_kwargs("all_terms"))
+    venv = F110VectorEnv(E, num_agents=2, noise_std=0.0, opponent="gap_follow", reward_fn=rf, seed=4)
+    T = R.TrackOracle(track.xy, track.wR, track.wL)
+    refs = [R.RewardOracle(T, **_kwargs("all_terms")) for _ in range(E)]
+    try:
+        venv.reset(seed=4)
+        for t in range(25):
+            ego = torch.stack([torch.full((E,), 0.05, device="cuda"), torch.full((E,), 4.0, device="cuda")], -1)
+            obs, rew, term, trunc, info = venv.step(ego)
+            o = obs.cpu().numpy()
+            reset = info["reset"].cpu().numpy()
+            for e in range(E):
+                if reset[e]:
+                    refs[e].reset()
+                    assert rew[e].item() == 0.0
+                else:
+                    assert rew[e].item() == pytest.approx(refs[e](o[e]), rel=1e-9, abs=1e-12)
+    finally:
+        venv.close()

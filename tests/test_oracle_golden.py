@@ -150,3 +150,42 @@ def test_gap_follow(oracle_mod):
         act, gap = oracle_mod.gap_follow_action(s)
         assert np.array_equal(act, a), i
         assert np.array_equal(gap, g), i
+
+
+def _reward_kwargs(name):
+    import make_golden_configs as C
+    return C.REWARD_CONFIGS[name]
+
+
+def test_reward_oracle_matches_reference():
+    """CenterlineSafetyProgressReward restated (oracle/reward_oracle.py) vs the
+    reference classes' rewards over three recorded episodes, two configs."""
+    import reward_oracle as R
+    d = golden("reward.npz")
+    T = R.TrackOracle(d["track_xy"], d["track_wR"], d["track_wL"], closed=True)
+    for arr in ("s", "tan", "nrm", "mid"):
+        assert np.array_equal(getattr(T, arr), d["track_" + arr]), arr
+    for name in d["config_names"]:
+        name = str(name)
+        f = R.RewardOracle(T, dt=0.01, **_reward_kwargs(name))
+        prev_ep = -1
+        for t, (o, ep) in enumerate(zip(d["obs"], d["episode"])):
+            if ep != prev_ep:
+                f.reset()
+                prev_ep = ep
+            assert f(o) == d["reward_" + name][t], (name, t)
+
+
+def test_track_arrays_match_reference():
+    """f110_track (host-only) derives CenterlineProgress's arrays bit for bit
+    from the bundled Spielberg centerline (== the reference CSV as pandas parses it)."""
+    from f110_gymnasium_ros2_jazzy_amd.reward import CenterlineTrack
+    from f110_gymnasium_ros2_jazzy_amd.maps import MAP_DIR
+    d = golden("reward.npz")
+    c = np.load(os.path.join(MAP_DIR, "Spielberg_centerline.npz"))
+    assert np.array_equal(c["xy"], d["track_xy"]) and np.array_equal(c["w_right"], d["track_wR"])
+    t = CenterlineTrack(c["xy"], c["w_right"], c["w_left"], device=None)
+    for arr in ("s", "tan", "nrm", "mid"):
+        assert np.array_equal(getattr(t, arr), d["track_" + arr]), arr
+    assert t.L == float(d["track_L"])
+    t.close()
