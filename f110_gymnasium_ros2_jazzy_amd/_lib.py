@@ -60,7 +60,8 @@ EXPORTS = [
     "f110_profile_begin", "f110_profile_end", "f110_host_tables", "f110_host_beam_indices",
     "f110_set_scan_noise", "f110_set_params", "f110_host_cell_index", "f110_gap_follow",
     "f110_host_window_ranges", "f110_track_create", "f110_track_destroy", "f110_track_arrays",
-    "f110_default_reward_params", "f110_reward",
+    "f110_default_reward_params", "f110_reward", "f110_replay_create", "f110_replay_destroy", "f110_replay_add",
+    "f110_replay_sample", "f110_replay_update_priorities", "f110_replay_length", "f110_replay_arrays",
 ]
 
 _lib = None
@@ -129,6 +130,14 @@ def load(build_if_missing: bool = True):
     L.f110_host_tables.argtypes = [i32, i32, ctypes.c_double, ctypes.POINTER(F110Params), _P, _P, _P, _P, _P]
     L.f110_host_beam_indices.argtypes = [ctypes.c_double, ctypes.c_double, i32, i32, _P]
     L.f110_host_beam_indices.restype = ctypes.c_int
+    L.f110_replay_create.argtypes = [ctypes.POINTER(_P), i32, i64, i32, i32, i32, i64, ctypes.c_double,
+                                     ctypes.c_double, u64]
+    L.f110_replay_destroy.argtypes = [_P]
+    L.f110_replay_add.argtypes = [_P, _P, i64, _P, i64, _P, _P, i64, _P, _P, _P, i64, _P]
+    L.f110_replay_sample.argtypes = [_P, i32, ctypes.c_double, _P, _P, _P, _P, _P, _P, _P, _P]
+    L.f110_replay_update_priorities.argtypes = [_P, _P, _P, i64, i32, ctypes.c_float, _P]
+    L.f110_replay_length.argtypes = [_P, ctypes.POINTER(i64), ctypes.POINTER(i64), _P]
+    L.f110_replay_arrays.argtypes = [_P] + [ctypes.POINTER(_P)] * 6
     for name in EXPORTS:
         if name not in ("f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config",
                         "f110_host_tables", "f110_host_window_ranges", "f110_track_arrays",

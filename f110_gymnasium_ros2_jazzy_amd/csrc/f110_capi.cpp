@@ -34,6 +34,9 @@ int fail(int code, const std::string &msg) {
 
 }  // namespace
 
+// shared with f110_replay_capi.cpp (one thread-local error string per library)
+int f110_set_error(int code, const std::string &msg) { return fail(code, msg); }
+
 struct f110_ctx {
     int device = 0;
     f110_config cfg{};

@@ -138,6 +138,64 @@ struct RewardArgs {
     double *rewards;
 };
 
+// ---- prioritized replay (f110_replay.hip) ---------------------------------
+constexpr int kTieCap = 4096;        // keys equal to the selection threshold kept for the tie break
+constexpr int kReplayMaxGrid = 1024; // blocks of the streaming replay kernels
+constexpr int kReplayMaxBatch = 8192;
+
+// Device header of a replay buffer (one per f110_replay).
+struct ReplayHdr {
+    int64_t length;     // PrioritizedExperienceReplayBuffer._length
+    int64_t next;       // _next_idx
+    uint64_t draws;     // sample() calls so far (Philox counter)
+    double den;         // sum of (p + eps)^alpha at the last sample
+    uint32_t maxbits;   // f32 bits of the max stored priority (add)
+    int32_t replace;    // the last sample drew with replacement
+    uint32_t prefix;    // radix select: threshold key so far
+    uint32_t kleft;     //   rank still to select below/at the prefix
+    uint32_t n_lt, n_tie;  // keys below / equal to the threshold (cleared per sample)
+    uint32_t overflow;  // samples whose tie list overflowed kTieCap
+    uint32_t pad_;
+};
+
+struct ReplayView {
+    ReplayHdr *hdr;
+    int64_t capacity;
+    int32_t obs_dim, act_dim;
+    float *obs, *next_obs, *act, *reward, *done, *prio;  // [cap][D], [cap][D], [cap][A], [cap] x3
+    uint32_t *keys;      // [cap] exponential-race keys
+    uint32_t *hist;      // [4][256]
+    double *den_part;    // [kReplayMaxGrid]
+    uint64_t *sel;       // [kReplayMaxBatch] (key << 32 | index) below the threshold
+    uint32_t *tie;       // [kTieCap]
+    int64_t *pos;        // [max rows per add] ring slot of each added row (-1: not stored)
+    double alpha;
+    float eps;           // the buffer's priority_epsilon (replay_buffer.py:24, 88)
+    uint64_t seed;
+};
+
+struct ReplayRows {      // one add(): n transitions (device, f32 rows with strides in floats)
+    const float *obs, *next_obs, *act, *reward;
+    const float *priority;  // [n] explicit priorities or null (= the max priority)
+    const uint8_t *done;
+    int64_t obs_stride, next_stride, act_stride;
+    int32_t vec4;        // rows 16-B aligned and obs_dim % 4 == 0
+};
+
+struct ReplayBatch {     // one sample(): the gathered batch (device, contiguous)
+    float *obs, *next_obs, *act, *reward, *done;
+    int32_t vec4;
+};
+
+hipError_t launch_replay_add(const ReplayView &v, const ReplayRows &in, const uint8_t *mask, int64_t n,
+                             hipStream_t s);
+hipError_t launch_replay_sample(const ReplayView &v, int32_t batch, double beta, int64_t *idx, float *w,
+                                const ReplayBatch &out, hipStream_t s);
+hipError_t launch_replay_update(const ReplayView &v, const int64_t *idx, const float *val, int64_t n, float add_eps,
+                                int32_t from_td, int32_t serial, hipStream_t s);
+hipError_t prepare_replay(int32_t max_batch);
+int replay_grid(int64_t capacity);
+
 size_t step_lds_bytes(int A, int B);
 hipError_t prepare_env_step(size_t lds_bytes);
 hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev = nullptr);  // ev: 4 events or null

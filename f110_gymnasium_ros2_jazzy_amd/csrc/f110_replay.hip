@@ -1,0 +1,507 @@
+// f110_replay.hip — prioritized experience replay in HBM.
+//
+// Replaces rl_training/DDPG/replay_buffer.py:PrioritizedExperienceReplayBuffer
+// (the DDPG agent's memory, agent.py:194, :223-237, :254, :337-338).  The
+// reference keeps one Python object per transition and samples with an O(N)
+// numpy rng.choice on the host every update.  Here the ring of transitions
+// lives on the device as flat arrays and every operation is a few kernels:
+//
+//   add     (replay_buffer.py:48-71)   k_prio_max (max priority over the
+//           buffer) -> k_add_scan (one workgroup: ring slots of the masked
+//           rows, their priority) -> k_add_copy (one block per row).
+//   sample  (replay_buffer.py:76-116)  Sampling WITHOUT replacement from
+//           p_i = (prio_i + eps)^alpha / sum_j (...) by the exponential race
+//           (Efraimidis-Spirakis): key_i = E_i / w_i with E_i ~ Exp(1); the B
+//           smallest keys in increasing order are distributed exactly like B
+//           successive draws without replacement -- the ordered sample that
+//           numpy's Generator.choice(replace=False, p=...) returns (it draws,
+//           drops repeats in draw order and redraws the rest from the
+//           renormalised p).  The B smallest 32-bit key patterns are found by
+//           a 4-pass radix select (8-bit digits, LDS histograms); ties at the
+//           threshold go to the lowest indices; one workgroup then sorts the B
+//           (key, index) pairs and computes the IS weights.  With fewer stored
+//           rows than B (replace=True, :97) one workgroup draws i.i.d. by
+//           inverse CDF.
+//   update  (replay_buffer.py:121-135) clip, NaN -> 1e-6, scatter.
+//
+// Everything is ordered on the caller's stream.  The device header holds the
+// length and ring pointer, so adds with a row mask (autoreset rows are not
+// stored) need no host round trip; kernels of the path not taken (with /
+// without replacement) exit at their first instruction.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "f110_internal.h"
+
+namespace f110 {
+
+namespace {
+
+constexpr int kRB = 256;         // threads per block of the streaming kernels
+constexpr int kOneBlock = 1024;  // single-workgroup kernels
+
+__device__ __forceinline__ uint32_t f32_bits(float v) { return __float_as_uint(v); }
+
+// numpy: ps + self._eps with ps float32 and a Python float -> float32
+// (NEP 50), then np.power(., alpha, dtype=float64) (replay_buffer.py:88).
+__device__ __forceinline__ double prio_weight(float p, float eps, double alpha) {
+    const float s = p + eps;
+    return pow((double)s, alpha);
+}
+
+// p0 of add() (replay_buffer.py:52-63) from the max priority.
+__device__ __forceinline__ float add_priority(const ReplayHdr *h) {
+    double p0 = 1.0;
+    if (h->length > 0) {
+        p0 = (double)__uint_as_float(h->maxbits);
+        if (!isfinite(p0) || p0 <= 0.0) p0 = 1.0;
+    }
+    p0 = p0 < 1e-8 ? 1e-8 : p0;
+    p0 = p0 > (double)FLT_MAX ? (double)FLT_MAX : p0;
+    return (float)p0;
+}
+
+// Deterministic block sum: fixed shuffle tree per wave, waves added in order.
+__device__ __forceinline__ double block_sum_f64(double v, double *sh) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nw = (int)((blockDim.x + 63) >> 6);
+    __syncthreads();
+    if (lane == 0) sh[wave] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < nw; ++w) t += sh[w];
+    return t;  // valid in thread 0
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- add ------
+// np.max(self._buffer["priority"][:self._length]) (replay_buffer.py:54).
+// Stored priorities are finite and positive (add and update clamp them), so
+// their u32 patterns order like the floats.
+__global__ void __launch_bounds__(kRB) k_prio_max(ReplayView v) {
+    const int64_t len = v.hdr->length;
+    uint32_t m = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kRB + threadIdx.x; i < len; i += (int64_t)gridDim.x * kRB)
+        m = max(m, f32_bits(v.prio[i]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(&v.hdr->maxbits, m);
+}
+
+// Ring slots of the rows to store (mask[i] != 0, or all) in row order, as the
+// reference's one add() per transition (agent.remember) would fill them.
+__global__ void __launch_bounds__(kOneBlock) k_add_scan(ReplayView v, const uint8_t *mask, const float *priority,
+                                                        int64_t n) {
+    __shared__ int64_t part[kOneBlock];
+    const int t = threadIdx.x;
+    const int64_t chunk = (n + kOneBlock - 1) / kOneBlock;
+    const int64_t r0 = min((int64_t)t * chunk, n), r1 = min(r0 + chunk, n);
+    int64_t cnt = 0;
+    for (int64_t i = r0; i < r1; ++i) cnt += (!mask || mask[i]) ? 1 : 0;
+    part[t] = cnt;
+    __syncthreads();
+    for (int o = 1; o < kOneBlock; o <<= 1) {  // inclusive scan
+        const int64_t add = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += add;
+        __syncthreads();
+    }
+    const int64_t total = part[kOneBlock - 1];
+    int64_t rank = part[t] - cnt;
+    const int64_t cap = v.capacity, next = v.hdr->next;
+    const float p0 = add_priority(v.hdr);
+    for (int64_t i = r0; i < r1; ++i) {
+        if (!mask || mask[i]) {
+            const int64_t slot = (next + rank) % cap;
+            v.pos[i] = slot;
+            float p = p0;
+            if (priority) {  // add(exp, priority): np.clip(p, 1e-8, f32 max).astype(f32) (:59-63)
+                const double q = (double)priority[i];
+                p = (float)(q < 1e-8 ? 1e-8 : (q > (double)FLT_MAX ? (double)FLT_MAX : q));
+            }
+            v.prio[slot] = p;  // replay_buffer.py:65
+            ++rank;
+        } else {
+            v.pos[i] = -1;
+        }
+    }
+    __syncthreads();
+    if (t == 0) {  // replay_buffer.py:69-71
+        const int64_t len = v.hdr->length + total;
+        v.hdr->length = len < cap ? len : cap;
+        v.hdr->next = (next + total) % cap;
+    }
+}
+
+// One block per row: the obs / next_obs rows, action, reward and done.
+__global__ void __launch_bounds__(kRB) k_add_copy(ReplayView v, ReplayRows in, int64_t n) {
+    const int64_t i = blockIdx.x;
+    if (i >= n) return;
+    const int64_t slot = v.pos[i];
+    if (slot < 0) return;
+    const int D = v.obs_dim;
+    const float *so = in.obs + i * in.obs_stride, *sn = in.next_obs + i * in.next_stride;
+    float *dobs = v.obs + slot * D, *dnext = v.next_obs + slot * D;
+    if (in.vec4) {
+        const int D4 = D >> 2;
+        for (int k = threadIdx.x; k < D4; k += kRB) {
+            reinterpret_cast<float4 *>(dobs)[k] = reinterpret_cast<const float4 *>(so)[k];
+            reinterpret_cast<float4 *>(dnext)[k] = reinterpret_cast<const float4 *>(sn)[k];
+        }
+    } else {
+        for (int k = threadIdx.x; k < D; k += kRB) {
+            dobs[k] = so[k];
+            dnext[k] = sn[k];
+        }
+    }
+    if (threadIdx.x < v.act_dim) v.act[slot * v.act_dim + threadIdx.x] = in.act[i * in.act_stride + threadIdx.x];
+    if (threadIdx.x == 0) {
+        v.reward[slot] = in.reward[i];
+        v.done[slot] = in.done ? (in.done[i] ? 1.0f : 0.0f) : 0.0f;
+    }
+}
+
+// ------------------------------------------------------------- sample ------
+// Pass 0: sampling weights w_i, per-block partial sums of w (den, :88-89),
+// exponential-race keys and the top-digit histogram.
+__global__ void __launch_bounds__(kRB) k_keys(ReplayView v, int32_t batch) {
+    __shared__ uint32_t hist[256];
+    __shared__ double sh[kRB / 64];
+    const int64_t len = v.hdr->length;
+    if (len < batch) return;  // block-uniform
+    const uint64_t draw = v.hdr->draws;
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kRB + threadIdx.x; i < len; i += (int64_t)gridDim.x * kRB) {
+        const double w = prio_weight(v.prio[i], v.eps, v.alpha);
+        acc += w;
+        U4 c = {(uint32_t)i, (uint32_t)((uint64_t)i >> 32), (uint32_t)draw, (uint32_t)(draw >> 32)};
+        U4 r = philox(c, (uint32_t)v.seed, (uint32_t)(v.seed >> 32) ^ 0x9E3779B9u);
+        const double e = -log(u01_open(r.x, r.y));  // Exp(1)
+        const uint32_t key = f32_bits((float)(e / w));
+        v.keys[i] = key;
+        atomicAdd(&hist[key >> 24], 1u);
+    }
+    const double bsum = block_sum_f64(acc, sh);
+    if (threadIdx.x == 0) v.den_part[blockIdx.x] = bsum;
+    __syncthreads();
+    if (hist[threadIdx.x]) atomicAdd(&v.hist[threadIdx.x], hist[threadIdx.x]);
+}
+
+// Passes 1..3: histogram of digit `pass` over the keys whose higher digits
+// equal the prefix selected so far.
+__global__ void __launch_bounds__(kRB) k_hist(ReplayView v, int32_t batch, int pass) {
+    __shared__ uint32_t hist[256];
+    const int64_t len = v.hdr->length;
+    if (len < batch) return;
+    const int shift = 24 - 8 * pass;
+    const uint32_t want = v.hdr->prefix >> (shift + 8);
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * kRB + threadIdx.x; i < len; i += (int64_t)gridDim.x * kRB) {
+        const uint32_t key = v.keys[i];
+        if ((key >> (shift + 8)) == want) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (hist[threadIdx.x]) atomicAdd(&v.hist[pass * 256 + threadIdx.x], hist[threadIdx.x]);
+}
+
+// The digit holding the batch-th smallest key (one workgroup).  Pass 0 also
+// adds the partial dens in a fixed order.
+__global__ void __launch_bounds__(256) k_select(ReplayView v, int32_t batch, int pass, int n_part) {
+    __shared__ uint32_t inc[256];
+    __shared__ double sh[4];
+    const int64_t len = v.hdr->length;
+    if (len < batch) return;
+    const int t = threadIdx.x;
+    const int shift = 24 - 8 * pass;
+    if (pass == 0) {
+        double acc = 0.0;
+        for (int k = t; k < n_part; k += 256) acc += v.den_part[k];
+        const double den = block_sum_f64(acc, sh);
+        if (t == 0) v.hdr->den = den;
+    }
+    const uint32_t kleft = pass == 0 ? (uint32_t)batch : v.hdr->kleft;
+    const uint32_t prefix = pass == 0 ? 0u : v.hdr->prefix;
+    inc[t] = v.hist[pass * 256 + t];
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+        const uint32_t add = t >= o ? inc[t - o] : 0u;
+        __syncthreads();
+        inc[t] += add;
+        __syncthreads();
+    }
+    const uint32_t below = t ? inc[t - 1] : 0u;
+    if (inc[t] >= kleft && below < kleft) {
+        v.hdr->prefix = prefix | ((uint32_t)t << shift);
+        v.hdr->kleft = kleft - below;
+    }
+}
+
+// Keys below the threshold key T go to the selection; keys equal to T to the
+// tie list, of which the kleft lowest indices are taken.
+__global__ void __launch_bounds__(kRB) k_collect(ReplayView v, int32_t batch) {
+    const int64_t len = v.hdr->length;
+    if (len < batch) return;
+    const uint32_t T = v.hdr->prefix;
+    for (int64_t i = (int64_t)blockIdx.x * kRB + threadIdx.x; i < len; i += (int64_t)gridDim.x * kRB) {
+        const uint32_t key = v.keys[i];
+        if (key < T) {
+            const uint32_t s = atomicAdd(&v.hdr->n_lt, 1u);
+            if (s < (uint32_t)batch) v.sel[s] = ((uint64_t)key << 32) | (uint64_t)i;
+        } else if (key == T) {
+            const uint32_t s = atomicAdd(&v.hdr->n_tie, 1u);
+            if (s < (uint32_t)kTieCap) v.tie[s] = (uint32_t)i;
+        }
+    }
+}
+
+__device__ void bitonic_sort_u64(uint64_t *a, int P) {
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += blockDim.x) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const uint64_t x = a[i], y = a[l];
+                    const bool up = (i & k) == 0;
+                    if ((x > y) == up) {
+                        a[i] = y;
+                        a[l] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+// IS weights (replay_buffer.py:103-113) of the selected rows.
+__device__ void write_weights(const ReplayView &v, const int64_t *idx, int32_t batch, int64_t len, double den,
+                              double beta, double *wsh, int64_t *idx_out, float *w_out) {
+    __shared__ double wm[kOneBlock / 64];
+    double m = -INFINITY;
+    for (int j = threadIdx.x; j < batch; j += blockDim.x) {
+        const double p = prio_weight(v.prio[idx[j]], v.eps, v.alpha) / den;
+        const double w = pow((double)len * p, -beta);
+        wsh[j] = w;
+        m = fmax(m, w);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    double mx = wm[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) mx = fmax(mx, wm[w]);
+    const bool ok = isfinite(mx) && mx > 0.0;  // :109-112
+    for (int j = threadIdx.x; j < batch; j += blockDim.x) {
+        idx_out[j] = idx[j];
+        w_out[j] = ok ? (float)(wsh[j] / mx) : 1.0f;
+    }
+}
+
+// Without replacement: resolve the ties, sort the batch by (key, index) --
+// the draw order -- and write indices and weights.
+__global__ void __launch_bounds__(kOneBlock) k_finish(ReplayView v, int32_t batch, double beta, int64_t *idx_out,
+                                                      float *w_out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int64_t len = v.hdr->length;
+    if (len < batch) return;
+    int P = 1;
+    while (P < batch) P <<= 1;
+    uint64_t *a = reinterpret_cast<uint64_t *>(smem);  // [P]
+    int64_t *idx = reinterpret_cast<int64_t *>(a + P);  // [batch]
+    double *wsh = reinterpret_cast<double *>(idx + batch);  // [batch]
+    const uint32_t T = v.hdr->prefix;
+    const uint32_t n_lt = min(v.hdr->n_lt, (uint32_t)batch);
+    const uint32_t n_tie = min(v.hdr->n_tie, (uint32_t)kTieCap);
+    const uint32_t need = (uint32_t)batch - n_lt;
+    for (int j = threadIdx.x; j < P; j += blockDim.x) a[j] = j < (int)n_lt ? v.sel[j] : ~0ull;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < n_tie; t += blockDim.x) {  // rank among the ties by index
+        const uint32_t mine = v.tie[t];
+        uint32_t rank = 0;
+        for (uint32_t u = 0; u < n_tie; ++u) rank += v.tie[u] < mine ? 1u : 0u;
+        if (rank < need) a[n_lt + rank] = ((uint64_t)T << 32) | (uint64_t)mine;
+    }
+    __syncthreads();
+    bitonic_sort_u64(a, P);
+    for (int j = threadIdx.x; j < batch; j += blockDim.x) idx[j] = (int64_t)(a[j] & 0xffffffffull);
+    __syncthreads();
+    write_weights(v, idx, batch, len, v.hdr->den, beta, wsh, idx_out, w_out);
+    if (threadIdx.x == 0) {
+        v.hdr->draws += 1;
+        v.hdr->replace = 0;
+        if (v.hdr->n_tie > (uint32_t)kTieCap) v.hdr->overflow += 1;
+    }
+}
+
+// With replacement (0 < len < batch, replay_buffer.py:97): i.i.d. draws by
+// inverse CDF (numpy: cdf = cumsum(p), searchsorted(cdf, u, 'right')).
+__global__ void __launch_bounds__(kOneBlock) k_sample_replace(ReplayView v, int32_t batch, double beta,
+                                                              int64_t *idx_out, float *w_out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int64_t len = v.hdr->length;
+    if (len >= batch || len <= 0) return;
+    double *cdf = reinterpret_cast<double *>(smem);  // [batch] (len < batch)
+    int64_t *idx = reinterpret_cast<int64_t *>(cdf + batch);
+    double *wsh = reinterpret_cast<double *>(idx + batch);
+    for (int64_t i = threadIdx.x; i < len; i += blockDim.x) cdf[i] = prio_weight(v.prio[i], v.eps, v.alpha);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double acc = 0.0;
+        for (int64_t i = 0; i < len; ++i) {
+            acc += cdf[i];
+            cdf[i] = acc;
+        }
+    }
+    __syncthreads();
+    const double den = cdf[len - 1];
+    const uint64_t draw = v.hdr->draws;
+    for (int j = threadIdx.x; j < batch; j += blockDim.x) {
+        U4 c = {(uint32_t)j, 0x7E11u, (uint32_t)draw, (uint32_t)(draw >> 32)};
+        U4 r = philox(c, (uint32_t)v.seed, (uint32_t)(v.seed >> 32) ^ 0x9E3779B9u);
+        const double u = (u01_open(r.x, r.y) - 0x1p-53) * den;  // [0, den)
+        int64_t lo = 0, hi = len - 1;  // first i with cdf[i] > u
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (cdf[mid] > u) hi = mid;
+            else lo = mid + 1;
+        }
+        idx[j] = lo;
+    }
+    __syncthreads();
+    write_weights(v, idx, batch, len, den, beta, wsh, idx_out, w_out);
+    if (threadIdx.x == 0) {
+        v.hdr->draws += 1;
+        v.hdr->replace = 1;
+    }
+}
+
+// One block per sampled row: the arrays agent.replay stacks (agent.py:257-270).
+__global__ void __launch_bounds__(kRB) k_gather(ReplayView v, int32_t batch, const int64_t *idx, ReplayBatch out) {
+    const int j = blockIdx.x;
+    if (j >= batch || v.hdr->length <= 0) return;
+    const int64_t i = idx[j];
+    const int D = v.obs_dim;
+    const float *so = v.obs + i * D, *sn = v.next_obs + i * D;
+    float *dobs = out.obs + (int64_t)j * D, *dnext = out.next_obs + (int64_t)j * D;
+    if (out.vec4) {
+        const int D4 = D >> 2;
+        for (int k = threadIdx.x; k < D4; k += kRB) {
+            reinterpret_cast<float4 *>(dobs)[k] = reinterpret_cast<const float4 *>(so)[k];
+            reinterpret_cast<float4 *>(dnext)[k] = reinterpret_cast<const float4 *>(sn)[k];
+        }
+    } else {
+        for (int k = threadIdx.x; k < D; k += kRB) {
+            dobs[k] = so[k];
+            dnext[k] = sn[k];
+        }
+    }
+    if (threadIdx.x < v.act_dim) out.act[(int64_t)j * v.act_dim + threadIdx.x] = v.act[i * v.act_dim + threadIdx.x];
+    if (threadIdx.x == 0) {
+        out.reward[j] = v.reward[i];
+        out.done[j] = v.done[i];
+    }
+}
+
+// ------------------------------------------------------------- update ------
+// update_priorities (replay_buffer.py:121-135).  from_td: the values are TD
+// errors and the priority is agent.replay's |td| + priority_epsilon in
+// float32 (agent.py:337); otherwise they are the priorities themselves.
+// Indices of a without-replacement sample are distinct and scatter in
+// parallel; after a with-replacement sample (or serial != 0) one thread
+// applies them in order, so a repeated index keeps its last value like
+// numpy's fancy assignment.
+__global__ void __launch_bounds__(kRB) k_update(ReplayView v, const int64_t *idx, const float *val, int64_t n,
+                                                float add_eps, int32_t from_td, int32_t serial) {
+    auto pr_of = [&](int64_t j) -> float {
+        float p = from_td ? fabsf(val[j]) + add_eps : val[j];
+        if (p < 1e-8f) p = 1e-8f;         // np.clip(pr, 1e-8, f32max): NaN passes
+        else if (p > FLT_MAX) p = FLT_MAX;
+        if (!isfinite(p)) p = 1e-6f;      // :131-133
+        return p;
+    };
+    if (serial || v.hdr->replace) {
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            for (int64_t j = 0; j < n; ++j) {
+                const int64_t i = idx[j];
+                if (i >= 0 && i < v.capacity) v.prio[i] = pr_of(j);
+            }
+        return;
+    }
+    for (int64_t j = (int64_t)blockIdx.x * kRB + threadIdx.x; j < n; j += (int64_t)gridDim.x * kRB) {
+        const int64_t i = idx[j];
+        if (i >= 0 && i < v.capacity) v.prio[i] = pr_of(j);
+    }
+}
+
+// ------------------------------------------------------------ launchers ----
+int replay_grid(int64_t capacity) {
+    const int64_t per = (int64_t)kRB * 4;  // ~4 items per thread
+    int64_t g = (capacity + per - 1) / per;
+    return (int)(g < 1 ? 1 : (g > kReplayMaxGrid ? kReplayMaxGrid : g));
+}
+
+size_t replay_finish_lds(int32_t batch) {
+    size_t P = 1;
+    while (P < (size_t)batch) P <<= 1;
+    return P * 8 + (size_t)batch * 16;
+}
+
+size_t replay_replace_lds(int32_t batch) { return (size_t)batch * 24; }
+
+hipError_t launch_replay_add(const ReplayView &v, const ReplayRows &in, const uint8_t *mask, int64_t n,
+                             hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(&v.hdr->maxbits, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_prio_max, dim3(replay_grid(v.capacity)), dim3(kRB), 0, s, v);
+    hipLaunchKernelGGL(k_add_scan, dim3(1), dim3(kOneBlock), 0, s, v, mask, in.priority, n);
+    hipLaunchKernelGGL(k_add_copy, dim3((unsigned)n), dim3(kRB), 0, s, v, in, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_replay_sample(const ReplayView &v, int32_t batch, double beta, int64_t *idx, float *w,
+                                const ReplayBatch &out, hipStream_t s) {
+    const int grid = replay_grid(v.capacity);
+    hipError_t e = hipMemsetAsync(v.hist, 0, 4 * 256 * sizeof(uint32_t), s);  // histograms
+    if (e == hipSuccess) e = hipMemsetAsync(&v.hdr->n_lt, 0, 2 * sizeof(uint32_t), s);  // n_lt, n_tie
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_keys, dim3(grid), dim3(kRB), 0, s, v, batch);
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(256), 0, s, v, batch, 0, grid);
+    for (int pass = 1; pass < 4; ++pass) {
+        hipLaunchKernelGGL(k_hist, dim3(grid), dim3(kRB), 0, s, v, batch, pass);
+        hipLaunchKernelGGL(k_select, dim3(1), dim3(256), 0, s, v, batch, pass, grid);
+    }
+    hipLaunchKernelGGL(k_collect, dim3(grid), dim3(kRB), 0, s, v, batch);
+    hipLaunchKernelGGL(k_finish, dim3(1), dim3(kOneBlock), replay_finish_lds(batch), s, v, batch, beta, idx, w);
+    hipLaunchKernelGGL(k_sample_replace, dim3(1), dim3(kOneBlock), replay_replace_lds(batch), s, v, batch, beta,
+                       idx, w);
+    if (out.obs) hipLaunchKernelGGL(k_gather, dim3((unsigned)batch), dim3(kRB), 0, s, v, batch, idx, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_replay_update(const ReplayView &v, const int64_t *idx, const float *val, int64_t n, float add_eps,
+                                int32_t from_td, int32_t serial, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int64_t g = (n + kRB - 1) / kRB;
+    g = g > 1024 ? 1024 : g;
+    hipLaunchKernelGGL(k_update, dim3((unsigned)g), dim3(kRB), 0, s, v, idx, val, n, add_eps, from_td, serial);
+    return hipGetLastError();
+}
+
+hipError_t prepare_replay(int32_t max_batch) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_finish),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)replay_finish_lds(max_batch));
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_sample_replace),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)replay_replace_lds(max_batch));
+    return e;
+}
+
+}  // namespace f110

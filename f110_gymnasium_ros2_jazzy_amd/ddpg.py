@@ -1,0 +1,288 @@
+"""Data-parallel DDPG learner on PyTorch-ROCm.
+
+Mirrors rl_training/DDPG/agent.py: ``Actor`` (:25-62) and ``Critic``
+(:64-97) are the reference's networks (same layers, initialisation and seed
+order), and ``DDPGLearner`` is ``DDPGAgent`` (:105-460) for batches of
+envs on one GPU per rank:
+
+  remember      agent.py:223   -> DeviceReplayBuffer.add (batched, masked)
+  replay        agent.py:242   -> PER sample on the device, critic step, actor
+                                  step, priority update, soft target update
+  choose_action agent.py:350   -> actor + GaussianActionNoise (:507-539) on the
+                                  device for [N, obs_dim] observations
+  save_model / load_model      -> same checkpoint keys (weights_only loads)
+
+Data parallelism: one process per GPU (torch.distributed, backend "nccl" =
+RCCL over xGMI).  Every rank samples its own replay shard; the gradients of
+each network live in ONE flat fp32 buffer (the parameters' .grad are views
+into it), so a backward pass is followed by a single all-reduce of that
+bucket (critic: 156 289 floats, actor: 156 162 floats at obs_dim 1088), then
+the optimizer step.  The critic's all-reduce must finish before the actor's
+forward (the actor loss reads the updated critic), so the two buckets are two
+collectives.  Ranks start from rank 0's weights and stay identical.
+"""
+from __future__ import annotations
+
+import os
+from typing import Sequence
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class Actor(nn.Module):
+    """agent.py:25-62: obs -> 128 -> 128 -> act_dim, tanh scaled to [low, high]."""
+
+    def __init__(self, obs_dim, act_dim, action_low: Sequence[float], action_high: Sequence[float]):
+        super().__init__()
+        self.fc1 = nn.Linear(obs_dim, 128)
+        self.fc2 = nn.Linear(128, 128)
+        self.fc3 = nn.Linear(128, act_dim)
+        self.register_buffer("action_low", torch.tensor(action_low, dtype=torch.float32))
+        self.register_buffer("action_high", torch.tensor(action_high, dtype=torch.float32))
+        nn.init.kaiming_uniform_(self.fc1.weight, nonlinearity="relu")  # :41-47
+        nn.init.kaiming_uniform_(self.fc2.weight, nonlinearity="relu")
+        nn.init.uniform_(self.fc3.weight, -3e-3, 3e-3)
+        nn.init.zeros_(self.fc1.bias)
+        nn.init.zeros_(self.fc2.bias)
+        nn.init.zeros_(self.fc3.bias)
+
+    def forward(self, obs: torch.Tensor) -> torch.Tensor:
+        if obs.dim() == 1:
+            obs = obs.unsqueeze(0)
+        x = F.relu(self.fc1(obs))
+        x = F.relu(self.fc2(x))
+        t = torch.tanh(self.fc3(x))
+        low, high = self.action_low, self.action_high
+        return 0.5 * (high - low) * t + 0.5 * (high + low)  # :60-61
+
+
+class Critic(nn.Module):
+    """agent.py:64-97: obs -> 128, concat action -> 128 -> 1."""
+
+    def __init__(self, obs_dim: int, act_dim: int):
+        super().__init__()
+        self.fcs1 = nn.Linear(obs_dim, 128)
+        self.fcs2 = nn.Linear(128 + act_dim, 128)
+        self.q = nn.Linear(128, 1)
+        nn.init.kaiming_uniform_(self.fcs1.weight, nonlinearity="relu")  # :77-83
+        nn.init.kaiming_uniform_(self.fcs2.weight, nonlinearity="relu")
+        nn.init.uniform_(self.q.weight, -3e-3, 3e-3)
+        nn.init.zeros_(self.fcs1.bias)
+        nn.init.zeros_(self.fcs2.bias)
+        nn.init.zeros_(self.q.bias)
+
+    def forward(self, obs: torch.Tensor, act: torch.Tensor) -> torch.Tensor:
+        if obs.dim() == 1:
+            obs = obs.unsqueeze(0)
+        if act.dim() == 1:
+            act = act.unsqueeze(0)
+        z = F.relu(self.fcs1(obs))
+        z = torch.cat([z, act], dim=-1)
+        z = F.relu(self.fcs2(z))
+        return self.q(z)
+
+
+class GradBucket:
+    """The .grad of every parameter of a module as a view into one flat fp32
+    buffer: one all-reduce per backward (DDP's gradient-as-bucket-view)."""
+
+    def __init__(self, module: nn.Module, group=None):
+        self.params = [p for p in module.parameters()]
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in self.params:
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self.group = group
+        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+
+    def zero(self):
+        self.flat.zero_()  # optimizer.zero_grad(set_to_none=True) + backward == 0 + g
+
+    def all_reduce(self):
+        if self.world > 1:  # bucket mean over ranks (RCCL sum, then one scale)
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+            self.flat.mul_(1.0 / self.world)
+
+
+class DDPGLearner:
+    """DDPGAgent (agent.py:105) for batched envs, one GPU per rank."""
+
+    def __init__(self, obs_dim: int, act_dim: int, action_low, action_high, gamma: float = 0.99, tau: float = 0.005,
+                 actor_lr: float = 1e-4, critic_lr: float = 1e-3, memory_size: int = 1 << 20, batch_size: int = 128,
+                 alpha: float = 0.6, beta: float = 0.4, priority_epsilon: float = 1e-5,
+                 noise_sigma_start: float = 0.2, noise_sigma_min: float = 0.05, noise_decay: float = 0.999,
+                 seed: int = 42, device="cuda:0", replay="device", process_group=None, max_add: int | None = None,
+                 check_finite: bool = False, path: str | None = None):
+        self.device = torch.device(device)
+        self.obs_dim, self.act_dim = int(obs_dim), int(act_dim)
+        self.action_low = np.asarray(action_low, dtype=np.float32)
+        self.action_high = np.asarray(action_high, dtype=np.float32)
+        assert self.action_low.shape == (self.act_dim,) and self.action_high.shape == (self.act_dim,)
+        self.batch_size = int(batch_size)
+        self.gamma, self.tau, self.beta = float(gamma), float(tau), float(beta)
+        self.priority_epsilon = float(priority_epsilon)
+        self.check_finite = bool(check_finite)
+        self.path = path
+        # agent.py:176-184: seed, then the four networks in this order, built on
+        # the CPU generator so every device (and rank) starts from the same weights
+        torch.manual_seed(seed)
+        self.actor = Actor(self.obs_dim, self.act_dim, self.action_low, self.action_high)
+        self.critic = Critic(self.obs_dim, self.act_dim)
+        self.actor_target = Actor(self.obs_dim, self.act_dim, self.action_low, self.action_high)
+        self.critic_target = Critic(self.obs_dim, self.act_dim)
+        self.actor_target.load_state_dict(self.actor.state_dict())
+        self.critic_target.load_state_dict(self.critic.state_dict())
+        for net in (self.actor, self.critic, self.actor_target, self.critic_target):
+            net.to(self.device)
+        self.group = process_group
+        self.distributed = dist.is_available() and dist.is_initialized()
+        if self.distributed:  # every rank starts from rank 0's weights
+            for net in (self.actor, self.critic, self.actor_target, self.critic_target):
+                for t in list(net.parameters()) + list(net.buffers()):
+                    dist.broadcast(t.data, src=0, group=self.group)
+        self.actor_grads = GradBucket(self.actor, self.group)
+        self.critic_grads = GradBucket(self.critic, self.group)
+        fused = {"fused": True} if self.device.type == "cuda" else {}
+        self.actor_optim = torch.optim.Adam(self.actor.parameters(), lr=actor_lr, **fused)
+        self.critic_optim = torch.optim.Adam(self.critic.parameters(), lr=critic_lr, **fused)
+        self._online = list(self.actor.parameters()) + list(self.critic.parameters())
+        self._target = list(self.actor_target.parameters()) + list(self.critic_target.parameters())
+        self.memory = None
+        if replay == "device":
+            from .replay import DeviceReplayBuffer
+            self.memory = DeviceReplayBuffer(buffer_size=memory_size, batch_size=self.batch_size, alpha=alpha,
+                                             seed=seed + 7919 * (dist.get_rank() if self.distributed else 0),
+                                             obs_dim=self.obs_dim, act_dim=self.act_dim, device=self.device,
+                                             max_add=max_add)
+        elif replay is not None:
+            self.memory = replay
+        # GaussianActionNoise (agent.py:507-539) on the device
+        self.sigma = float(noise_sigma_start)
+        self.sigma_min, self.noise_decay = float(noise_sigma_min), float(noise_decay)
+        self._noise_gen = torch.Generator(device=self.device)
+        self._noise_gen.manual_seed(seed)
+        self._low = torch.as_tensor(self.action_low, device=self.device)
+        self._high = torch.as_tensor(self.action_high, device=self.device)
+        self._ready = False
+        self.global_step = 0
+
+    # ------------------------------------------------------------------
+    def remember(self, state, action, reward, next_state, done, mask=None):
+        """agent.py:223-237 for a batch of transitions (rows with mask == 0 skipped)."""
+        self.memory.add(state, action, reward, next_state, done, mask=mask)
+
+    def _finite(self, name, x):  # agent.py:291-296 (host sync; only with check_finite)
+        if self.check_finite and not bool(torch.isfinite(x).all()):
+            bad = (~torch.isfinite(x)).nonzero(as_tuple=False)[:10].cpu().numpy().tolist()
+            raise ValueError(f"Non-finite in {name}; examples idx={bad[:5]}")
+
+    def update(self, states, actions, rewards, next_states, dones, weights) -> dict:
+        """The learning part of replay() (agent.py:302-343) on one batch:
+        critic step, actor step, soft target update.  Returns device tensors
+        (critic_loss, actor_loss, td [B])."""
+        r = rewards.reshape(-1, 1)
+        d = dones.reshape(-1, 1)
+        w = weights.reshape(-1, 1)
+        for name, t in (("states", states), ("actions", actions), ("next_states", next_states), ("rewards", r),
+                        ("dones", d)):
+            self._finite(name, t)
+        with torch.no_grad():  # :302-308
+            a_next = self.actor_target(next_states)
+            q_next = self.critic_target(next_states, a_next)
+            target_y = r + self.gamma * (1.0 - d) * q_next
+            self._finite("target_y", target_y)
+        q_pred = self.critic(states, actions)  # :310-315
+        td = target_y - q_pred
+        critic_loss = (w * td ** 2).mean()
+        self.critic_grads.zero()               # :318-321
+        critic_loss.backward()
+        self.critic_grads.all_reduce()
+        self.critic_optim.step()
+        for p in self.critic.parameters():     # :324-334
+            p.requires_grad_(False)
+        actor_loss = -self.critic(states, self.actor(states)).mean()
+        self.actor_grads.zero()
+        actor_loss.backward()
+        self.actor_grads.all_reduce()
+        self.actor_optim.step()
+        for p in self.critic.parameters():
+            p.requires_grad_(True)
+        with torch.no_grad():                  # _soft_update (:340-341, :373-376)
+            torch._foreach_lerp_(self._target, self._online, self.tau)
+        self.global_step += 1
+        return {"critic_loss": critic_loss.detach(), "actor_loss": actor_loss.detach(), "td": td.detach()}
+
+    @staticmethod
+    def td_priorities(td: torch.Tensor, priority_epsilon: float) -> torch.Tensor:
+        """agent.py:337: new_priorities = |td| + priority_epsilon (float32)."""
+        return td.abs().reshape(-1) + priority_epsilon
+
+    def replay(self):
+        """agent.py:242-348: None until the memory holds batch_size rows."""
+        if not self._ready:  # len() syncs; once full enough it stays so (the ring never shrinks)
+            if len(self.memory) < self.batch_size:
+                return None
+            self._ready = True
+        idxs, b, w = self.memory.sample(beta=self.beta)
+        st = self.update(b["states"], b["actions"], b["rewards"], b["next_states"], b["dones"], w)
+        self.memory.update_priorities(idxs, st["td"], td_errors=True, add_eps=self.priority_epsilon)
+        return st
+
+    def choose_action(self, obs, training: bool = True) -> torch.Tensor:
+        """agent.py:350-370 for obs [N, obs_dim] (or [obs_dim]): actor output,
+        plus N(0, sigma^2) noise clipped to [low, high] when training; sigma
+        decays once per call (GaussianActionNoise.__call__, :520-539)."""
+        with torch.no_grad():
+            o = torch.as_tensor(obs, device=self.device, dtype=torch.float32)
+            a = self.actor(o)
+            if training:
+                noise = torch.randn(a.shape, generator=self._noise_gen, device=self.device) * self.sigma
+                a = torch.clamp(a + noise, self._low, self._high)
+                self.sigma = max(self.sigma * self.noise_decay, self.sigma_min)
+        return a
+
+    def hard_update(self):
+        self.actor_target.load_state_dict(self.actor.state_dict())
+        self.critic_target.load_state_dict(self.critic.state_dict())
+
+    # ---------------------------------------------------------- checkpoint --
+    def save_model(self, filename: str = "ddpg_checkpoint.pt"):
+        """agent.py:384-405 (same keys)."""
+        os.makedirs(self.path, exist_ok=True)
+        torch.save({
+            "actor": self.actor.state_dict(), "critic": self.critic.state_dict(),
+            "actor_target": self.actor_target.state_dict(), "critic_target": self.critic_target.state_dict(),
+            "actor_optim": self.actor_optim.state_dict(), "critic_optim": self.critic_optim.state_dict(),
+            "action_low": self.action_low.tolist(), "action_high": self.action_high.tolist(),
+            "gamma": self.gamma, "tau": self.tau, "obs_dim": self.obs_dim, "act_dim": self.act_dim,
+            "global_step": self.global_step, "torch_version": torch.__version__,
+        }, os.path.join(self.path, filename))
+
+    def load_model(self, filename: str = "ddpg_checkpoint.pt") -> bool:
+        """agent.py:407-460 with the safe loader only (weights_only=True)."""
+        model_path = os.path.join(self.path, filename)
+        if not os.path.exists(model_path):
+            return False
+        ckpt = torch.load(model_path, map_location=self.device, weights_only=True)
+        self.actor.load_state_dict(ckpt["actor"], strict=True)
+        self.critic.load_state_dict(ckpt["critic"], strict=True)
+        self.actor_target.load_state_dict(ckpt.get("actor_target", ckpt["actor"]), strict=False)
+        self.critic_target.load_state_dict(ckpt.get("critic_target", ckpt["critic"]), strict=False)
+        if "actor_optim" in ckpt:
+            self.actor_optim.load_state_dict(ckpt["actor_optim"])
+        if "critic_optim" in ckpt:
+            self.critic_optim.load_state_dict(ckpt["critic_optim"])
+        self.gamma = float(ckpt.get("gamma", self.gamma))
+        self.tau = float(ckpt.get("tau", self.tau))
+        self.global_step = int(ckpt.get("global_step", 0))
+        # the grads must stay views of the all-reduce buckets
+        self.actor_grads = GradBucket(self.actor, self.group)
+        self.critic_grads = GradBucket(self.critic, self.group)
+        return True

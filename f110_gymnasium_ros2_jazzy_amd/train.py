@@ -1,0 +1,126 @@
+"""Batched DDPG training loop (config 5): rl_training/train_ddpg.py's loop
+(:150-216) for N envs per GPU, one process per GPU.
+
+Per vector step, everything on the device:
+  ego action    random U(low, high) during warm-up (:162-163), else the actor
+                + Gaussian noise (:165)
+  opponent      gap_follow_action on its previous scan (:168), inside F110VectorEnv
+  env.step      (:174) with device autoreset (gymnasium NEXT_STEP)
+  reward        CenterlineSafetyProgressReward (:127-146, :179) on the device
+  remember      (:184) every transition except the reset rows of autoreset steps
+  replay        (:187-188) `updates_per_step` learner updates after warm-up,
+                gradients averaged over ranks by RCCL
+
+    python -m torch.distributed.run --nproc-per-node 8 -m f110_gymnasium_ros2_jazzy_amd.train --envs-per-gpu 4096
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+import torch
+
+from . import distributed as D
+
+# ddpg_config.yaml (agent_hyperparameters, action bounds)
+ACTION_LOW = [-0.4189, 0.0]
+ACTION_HIGH = [0.4189, 20.0]
+# train_ddpg.py:127-146 reward kwargs
+REWARD_KW = dict(w_prog=5.0, alive_bonus=0.5, grace_steps_wall=25, grace_steps_opp=175, w_lat=0.25, lat_cap=3.0,
+                 near_wall_dist=0.30 / 30, w_wall=0.30, wall_quantile=0.10, opp_safe_dist=0.60, w_opp=0.30,
+                 w_rel_lead=0.0)
+
+
+class VectorTrainer:
+    """One rank's share of the batched train_ddpg loop."""
+
+    def __init__(self, envs_per_rank: int, map_name: str = "Spielberg_map", batch_size: int = 4096,
+                 memory_size: int = 1 << 20, warmup_steps: int = 1000, updates_per_step: int = 1, seed: int = 42,
+                 device=None, env_offset: int = 0, rank_seed: int = 0):
+        from .ddpg import DDPGLearner
+        from .maps import MAP_DIR
+        from .reward import BatchedCenterlineReward, CenterlineTrack
+        from .vector_env import F110VectorEnv
+        self.device = torch.device(device or f"cuda:{torch.cuda.current_device()}")
+        self.N = int(envs_per_rank)
+        cl = np.load(os.path.join(MAP_DIR, map_name.replace("_map", "") + "_centerline.npz"))
+        self.track = CenterlineTrack(cl["xy"], cl["w_right"], cl["w_left"], device=self.device.index or 0)
+        self.reward_fn = BatchedCenterlineReward(self.N, dt=0.01, progress=self.track, device=self.device,
+                                                 **REWARD_KW)
+        self.env = F110VectorEnv(self.N, map=map_name, num_agents=2, seed=seed, device=self.device,
+                                 env_offset=env_offset, opponent="gap_follow", reward_fn=self.reward_fn)
+        self.agent = DDPGLearner(obs_dim=self.env.single_observation_space.shape[0], act_dim=2,
+                                 action_low=ACTION_LOW, action_high=ACTION_HIGH, gamma=0.99, tau=0.005,
+                                 actor_lr=1e-4, critic_lr=1e-3, memory_size=memory_size, batch_size=batch_size,
+                                 alpha=0.6, beta=0.4, priority_epsilon=1e-5, noise_sigma_start=0.20,
+                                 noise_sigma_min=0.02, noise_decay=0.9995, seed=seed, device=self.device,
+                                 max_add=self.N)
+        self.warmup = int(warmup_steps)
+        self.updates_per_step = int(updates_per_step)
+        self._gen = torch.Generator(device=self.device)
+        self._gen.manual_seed(seed * 1000003 + rank_seed)
+        self._low = torch.tensor(ACTION_LOW, device=self.device)
+        self._high = torch.tensor(ACTION_HIGH, device=self.device)
+        self.obs, self.info = self.env.reset(seed=seed + rank_seed)
+        self.global_step = 0
+        self.last = None
+
+    def step(self):
+        """One vector step of the loop (train_ddpg.py:160-192)."""
+        if self.global_step < self.warmup:  # :162-163
+            u = torch.rand(self.N, 2, generator=self._gen, device=self.device)
+            act = self._low + u * (self._high - self._low)
+        else:
+            act = self.agent.choose_action(self.obs, training=True)
+        next_obs, rew, term, trunc, info = self.env.step(act)
+        # NEXT_STEP autoreset: a reset row's obs is the previous episode's last
+        # observation and its next_obs the new episode's first -- not a transition
+        keep = ~info["reset"]
+        self.agent.remember(self.obs, act, rew.to(torch.float32), next_obs, term, mask=keep)
+        if self.global_step >= self.warmup:
+            for _ in range(self.updates_per_step):
+                self.last = self.agent.replay()
+        self.obs = next_obs
+        self.global_step += 1
+        return rew, term
+
+    def close(self):
+        self.env.close()
+        self.track.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs-per-gpu", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--memory", type=int, default=1 << 20)
+    ap.add_argument("--updates-per-step", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=42)
+    args = ap.parse_args()
+    rank, world, local = D.init()
+    torch.cuda.set_device(D.local_device_index(local))
+    shard = D.shard_range(args.envs_per_gpu * world, world, rank)
+    tr = VectorTrainer(shard.count, batch_size=args.batch, memory_size=args.memory, warmup_steps=args.warmup,
+                       updates_per_step=args.updates_per_step, seed=args.seed, env_offset=shard.offset,
+                       rank_seed=rank)
+    t0 = time.perf_counter()
+    ret = torch.zeros(shard.count, device=tr.device, dtype=torch.float64)
+    for k in range(args.steps):
+        rew, term = tr.step()
+        ret += rew
+        if rank == 0 and (k + 1) % 500 == 0:
+            st = tr.last or {}
+            print(json.dumps({"step": k + 1, "env_steps_per_s": shard.count * world * (k + 1) / (time.perf_counter() - t0),
+                              "critic_loss": float(st["critic_loss"]) if st else None,
+                              "mean_return": float(ret.mean())}), flush=True)
+    tr.close()
+    D.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -310,6 +310,67 @@ F110_API int f110_reward(const f110_track *track, const f110_reward_params *para
                          int32_t obs_len, int32_t n_beams, f110_reward_state *state, const uint8_t *reset_mask,
                          double *rewards, void *stream);
 
+/* ---- prioritized experience replay ---------------------------------------------
+ * Replaces rl_training/DDPG/replay_buffer.py:PrioritizedExperienceReplayBuffer
+ * (:6-135), the DDPG agent's memory (agent.py:194): a ring of transitions
+ * (state, action, reward, next_state, done) with one float32 priority each.
+ * All of it lives in device memory; every call below is asynchronous on
+ * `stream` and takes device pointers, except f110_replay_length /
+ * f110_replay_stats, which wait for the stream. */
+typedef struct f110_replay f110_replay;
+
+/* PrioritizedExperienceReplayBuffer(buffer_size=capacity, batch_size, alpha,
+ * seed, priority_epsilon=eps) (:18-40).  max_batch bounds the batch of
+ * f110_replay_sample (<= 8192) and max_add the rows of one f110_replay_add;
+ * obs_dim / act_dim are the state / action lengths (1088 / 2 in train_ddpg). */
+F110_API int f110_replay_create(f110_replay **out, int32_t device, int64_t capacity, int32_t obs_dim,
+                                int32_t act_dim, int32_t max_batch, int64_t max_add, double alpha, double eps,
+                                uint64_t seed);
+F110_API int f110_replay_destroy(f110_replay *rb);
+
+/* n calls of add(Experience(state, action, reward, next_state, done)) with
+ * priority=None (:48-71, agent.remember agent.py:223-237), in row order: the
+ * new rows get the current max priority (1.0 when empty).  obs / next_obs:
+ * rows of obs_dim floats at a stride of obs_stride / next_stride floats;
+ * act: act_dim floats per row at act_stride; reward [n] f32; done [n] u8
+ * (NULL = all 0).  priority [n] f32: add(exp, priority=p) (clipped to
+ * [1e-8, FLT_MAX]); NULL = priority=None.  mask [n] u8 (NULL = all rows):
+ * only rows with mask != 0 are stored (e.g. not the reset rows of an
+ * autoresetting vector env). */
+F110_API int f110_replay_add(f110_replay *rb, const float *obs, int64_t obs_stride, const float *act,
+                             int64_t act_stride, const float *reward, const float *next_obs, int64_t next_stride,
+                             const uint8_t *done, const float *priority, const uint8_t *mask, int64_t n,
+                             void *stream);
+
+/* sample(beta) (:76-116) of `batch` rows: without replacement when the buffer
+ * holds at least `batch` rows (distributed like numpy's
+ * Generator.choice(replace=False, p=...): successive draws, in draw order),
+ * i.i.d. otherwise.  Writes idx [batch] i64, weights [batch] f32 (normalised
+ * IS weights) and, when obs != NULL, the gathered batch agent.replay stacks
+ * (agent.py:257-270): obs / next_obs [batch][obs_dim], act [batch][act_dim],
+ * reward / done [batch] f32.  The caller must not sample an empty buffer
+ * (the reference raises ValueError, :83-84). */
+F110_API int f110_replay_sample(f110_replay *rb, int32_t batch, double beta, int64_t *idx, float *weights, float *obs,
+                                float *act, float *reward, float *next_obs, float *done, void *stream);
+
+/* update_priorities(idx, priorities) (:121-135): the priority of row idx[j]
+ * becomes clip(p_j, 1e-8, FLT_MAX) in float32 with NaN -> 1e-6, where
+ * p_j = values[j] (from_td == 0) or agent.replay's |values[j]| + add_eps
+ * (from_td != 0, values = TD errors, agent.py:337).  Repeated indices keep
+ * the last value. */
+F110_API int f110_replay_update_priorities(f110_replay *rb, const int64_t *idx, const float *values, int64_t n,
+                                           int32_t from_td, float add_eps, void *stream);
+
+/* len(buffer) (:42-43) and the ring pointer; waits for `stream`. */
+F110_API int f110_replay_length(f110_replay *rb, int64_t *length, int64_t *next_idx, void *stream);
+
+/* Device pointers of the stored arrays (read-only views for tests and
+ * checkpoints): priority [capacity] f32, obs / next_obs [capacity][obs_dim],
+ * act [capacity][act_dim], reward / done [capacity] f32.  Any out pointer
+ * may be NULL. */
+F110_API int f110_replay_arrays(f110_replay *rb, float **priority, float **obs, float **act, float **reward,
+                                float **next_obs, float **done);
+
 #ifdef __cplusplus
 }
 #endif

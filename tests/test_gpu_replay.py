@@ -1,0 +1,177 @@
+"""Device PER buffer (f110_replay_*) and the DDPG learner on the GPU, against
+the reference buffer's recorded state (tests/golden/per.npz), the CPU
+restatement (oracle/replay_oracle.py) and the reference DDPGAgent
+(tests/golden/ddpg.npz)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _rb(cap, batch, D=8, A=2, **kw):
+    from f110_gymnasium_ros2_jazzy_amd.replay import DeviceReplayBuffer
+    return DeviceReplayBuffer(buffer_size=cap, batch_size=batch, obs_dim=D, act_dim=A, device=0, **kw)
+
+
+def _rows(n, D=8, A=2, base=0.0):
+    v = torch.arange(n, dtype=torch.float32, device="cuda")[:, None] + base
+    return v.expand(n, D).contiguous(), v.expand(n, A).contiguous() * 2, v[:, 0] * 3, v.expand(n, D) + 0.5
+
+
+def test_replay_follows_reference_sequence(gpu):
+    from replay_oracle import PEROracle
+    from test_oracle_replay import replay_ops
+    d = golden("per.npz")
+    rb = _rb(16, 5)
+    o = PEROracle(16, 5, alpha=0.6)
+    betas = [0.4, 0.4, 0.7, 0.4, 0.4, 0.4, 0.4]
+    for t, op, arg in replay_ops(d):
+        if op in (0, 1):
+            s, a, r, s2 = _rows(1, base=float(t))
+            rb.add(s, a, r, s2, torch.zeros(1, device="cuda"), priority=None if op == 0 else [arg])
+            o.add(None if op == 0 else arg)
+        elif op == 2:
+            idx, batch, w = rb.sample(beta=betas[arg])
+            idx = idx.cpu().numpy()
+            assert ((idx >= 0) & (idx < o.length)).all()
+            if o.length >= 5:
+                assert len(set(idx.tolist())) == 5  # without replacement
+            np.testing.assert_allclose(w.cpu().numpy(), o.weights(idx, betas[arg]), rtol=2e-6)
+            st = rb.arrays(("states",))["states"].cpu().numpy()
+            np.testing.assert_array_equal(batch["states"].cpu().numpy(), st[idx])
+        else:  # the reference's own update (indices and raw priorities)
+            idx = d["upd_idx"][arg]
+            vals = d["upd_val"][arg][idx >= 0]
+            idx = idx[idx >= 0]
+            rb.update_priorities(idx, vals)
+            o.update_priorities(idx, vals)
+        np.testing.assert_array_equal(rb.priorities().cpu().numpy(), d["prio"][t], err_msg=f"op {t}")
+        assert len(rb) == d["length"][t]
+    rb.close()
+
+
+def test_replay_sampling_distribution(gpu):
+    """40 rows with the fixture's priorities, 20000 draws of 6: the first draw
+    is distributed as p (chi-square) and the inclusion counts agree with the
+    reference's own rng.choice counts."""
+    d = golden("per.npz")
+    n_draws, B = int(d["stat_draws"]), int(d["stat_batch"])
+    rb = _rb(40, B, seed=123)
+    s, a, r, s2 = _rows(40)
+    rb.add(s, a, r, s2, priority=torch.as_tensor(d["stat_prio"]))
+    incl = torch.zeros(40, dtype=torch.int64, device="cuda")
+    first = torch.zeros(40, dtype=torch.int64, device="cuda")
+    ones = torch.ones(B, dtype=torch.int64, device="cuda")
+    for _ in range(n_draws):
+        idx, _, _ = rb.sample(beta=0.4, gather=False)
+        incl.index_add_(0, idx, ones)
+        first.index_add_(0, idx[:1], ones[:1])
+    incl, first = incl.cpu().numpy(), first.cpu().numpy()
+    assert incl.sum() == n_draws * B and (incl <= n_draws).all()
+    exp = n_draws * d["stat_probs"]
+    chi2 = float(np.sum((first - exp) ** 2 / exp))
+    assert chi2 < 39 + 6 * np.sqrt(2 * 39), chi2
+    ref = d["stat_incl"]
+    z = np.abs(incl - ref) / np.sqrt(incl + ref + 1.0)
+    assert z.max() < 5.0, (incl, ref)
+    rb.close()
+
+
+def test_replay_masked_add_and_gather(gpu):
+    D, A = 1088, 2
+    rb = _rb(100, 32, D=D, A=A, max_add=64)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    S = torch.rand(60, D, device="cuda", generator=g)
+    S2 = torch.rand(60, D, device="cuda", generator=g)
+    Ac = torch.rand(60, A, device="cuda", generator=g)
+    R = torch.rand(60, device="cuda", generator=g)
+    done = torch.rand(60, device="cuda", generator=g) < 0.3
+    mask = torch.rand(60, device="cuda", generator=g) < 0.7
+    rb.add(S, Ac, R, S2, done, mask=mask)
+    rb.add(S, Ac, R, S2, done, mask=mask)     # wraps the 100-row ring
+    keep = torch.cat([mask.nonzero()[:, 0]] * 2)
+    k = keep.numel()
+    assert len(rb) == min(k, 100)
+    arr = rb.arrays()
+    slots = torch.arange(k, device="cuda") % 100
+    last = {int(s): i for i, s in enumerate(slots.tolist())}  # later rows overwrite earlier ones
+    rows = keep[torch.tensor([last[s] for s in range(min(k, 100))], device="cuda")]
+    torch.testing.assert_close(arr["states"][:len(rows)], S[rows], rtol=0, atol=0)
+    torch.testing.assert_close(arr["next_states"][:len(rows)], S2[rows], rtol=0, atol=0)
+    torch.testing.assert_close(arr["actions"][:len(rows)], Ac[rows], rtol=0, atol=0)
+    torch.testing.assert_close(arr["dones"][:len(rows)], done[rows].float(), rtol=0, atol=0)
+    idx, b, w = rb.sample(0.4)
+    torch.testing.assert_close(b["states"], arr["states"][idx], rtol=0, atol=0)
+    torch.testing.assert_close(b["rewards"], arr["rewards"][idx], rtol=0, atol=0)
+    assert float(w.max()) == 1.0
+    rb.close()
+
+
+def test_replay_full_size(gpu):
+    """train_ddpg-sized rows (1088 floats), 2^18 rows, batch 4096: distinct
+    indices inside the buffer, weights in (0, 1] with max 1, priority update
+    by TD errors (|td| + 1e-5) lands on the sampled rows."""
+    from replay_oracle import PEROracle
+    cap, B, D = 1 << 18, 4096, 1088
+    rb = _rb(cap, B, D=D, max_add=1 << 16)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for k in range(5):
+        S = torch.rand(1 << 16, D, device="cuda", generator=g)
+        rb.add(S, torch.rand(1 << 16, 2, device="cuda", generator=g), torch.rand(1 << 16, device="cuda"), S)
+    assert len(rb) == cap
+    td = torch.randn(B, device="cuda", generator=g)
+    for _ in range(3):
+        idx, b, w = rb.sample(0.4)
+        rb.update_priorities(idx, td, td_errors=True, add_eps=1e-5)
+    i = idx.cpu().numpy()
+    assert len(np.unique(i)) == B and i.min() >= 0 and i.max() < cap
+    wn = w.cpu().numpy()
+    assert wn.max() == 1.0 and (wn > 0).all()
+    pr = rb.priorities().cpu().numpy()
+    np.testing.assert_array_equal(pr[i], PEROracle.td_priorities(td.cpu().numpy(), 1e-5))
+    rb.close()
+
+
+def test_learner_on_gpu_matches_reference(gpu):
+    """The reference DDPGAgent's three replay() steps on the GPU learner
+    (hipBLASLt GEMMs, fused Adam): losses within 1e-4 relative, weights
+    within 2e-6 absolute of the reference's CPU result."""
+    from f110_gymnasium_ros2_jazzy_amd.ddpg import DDPGLearner
+    d = golden("ddpg.npz")
+    ln = DDPGLearner(obs_dim=12, act_dim=2, action_low=[-0.4189, 0.0], action_high=[0.4189, 20.0], seed=42,
+                     device="cuda:0", replay=None)
+    S, A, R, S2, Dn = (torch.from_numpy(np.asarray(d[k])).cuda() for k in ("S", "A", "R", "S2", "D"))
+    for step in range(3):
+        idx = torch.from_numpy(d["idx"][step]).cuda()
+        w = torch.from_numpy(d["w"][step]).cuda()
+        st = ln.update(S[idx], A[idx], R[idx], S2[idx], Dn[idx].float(), w)
+        np.testing.assert_allclose([float(st["critic_loss"]), float(st["actor_loss"])], d["losses"][step][:2],
+                                   rtol=1e-4)
+    for name, net in (("actor", ln.actor), ("critic", ln.critic), ("actor_target", ln.actor_target),
+                      ("critic_target", ln.critic_target)):
+        for k, v in net.state_dict().items():
+            if k in ("action_low", "action_high"):
+                continue
+            np.testing.assert_allclose(v.cpu().numpy(), d[f"final/{name}/{k}"], rtol=1e-4, atol=2e-6,
+                                       err_msg=f"{name}.{k}")
+
+
+def test_vector_trainer_loop(gpu):
+    """The batched train_ddpg loop: 256 two-agent envs, gap-follow opponent,
+    device reward, replay, learner updates after a 5-step warm-up."""
+    from f110_gymnasium_ros2_jazzy_amd.train import VectorTrainer
+    tr = VectorTrainer(256, batch_size=256, memory_size=4096, warmup_steps=5, seed=3)
+    stored = 0
+    for _ in range(30):
+        tr.step()
+        stored += int((tr.env.sim.out.was_reset == 0).sum())
+    assert len(tr.agent.memory) == min(stored, 4096)
+    st = tr.last
+    assert st is not None and torch.isfinite(st["critic_loss"]) and torch.isfinite(st["actor_loss"])
+    assert tr.agent.global_step == 25
+    for p in tr.agent.actor.parameters():
+        assert torch.isfinite(p).all()
+    tr.close()
