@@ -43,7 +43,81 @@ def parse():
     ap.add_argument("--cpu-envs", type=int, default=512)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=12345)
+    ap.add_argument("--workload", choices=["step", "ddpg"], default="step",
+                    help="step: the env step (headline); ddpg: config 5, the batched train_ddpg loop")
+    ap.add_argument("--ddpg-batch", type=int, default=4096)
+    ap.add_argument("--ddpg-memory", type=int, default=1 << 20)
     return ap.parse_args()
+
+
+def bench_ddpg(args):
+    """Config 5 (BASELINE.json): the batched train_ddpg loop, --envs-per-gpu
+    two-agent envs per GPU (gap-follow opponent, device reward, replay add,
+    one learner update of --ddpg-batch rows per vector step with the actor /
+    critic gradients all-reduced over the ranks by RCCL)."""
+    import torch
+    from f110_gymnasium_ros2_jazzy_amd import distributed as D
+    from f110_gymnasium_ros2_jazzy_amd.train import VectorTrainer
+    rank, world, local = D.init()
+    dev_index = D.local_device_index(local)
+    torch.cuda.set_device(dev_index)
+    shard = D.shard_range(args.envs_per_gpu * world, world, rank)
+    K, W = args.steps, args.warmup
+    # learner updates start once the memory holds a batch: ceil(batch / envs) steps
+    fill = -(-args.ddpg_batch // max(shard.count, 1)) + 1
+    tr = VectorTrainer(shard.count, batch_size=args.ddpg_batch, memory_size=args.ddpg_memory,
+                       warmup_steps=min(fill, W), seed=args.seed, env_offset=shard.offset, rank_seed=rank)
+    for _ in range(W):
+        tr.step()
+    assert tr.last is not None, "warm-up too short: no learner update ran"
+    torch.cuda.synchronize()
+    D.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        tr.step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    D.barrier()
+    elapsed = D.max_over_ranks(t1 - t0)
+    total = D.sum_over_ranks(shard.count * K)
+    # phase split (separate pass, events on the current stream; not part of `value`)
+    stream = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    KP = min(K, 100)
+    ph = {"env_step_reward_ms": 0.0, "replay_add_ms": 0.0, "learner_update_ms": 0.0}
+    for _ in range(KP):
+        act = tr.agent.choose_action(tr.obs, training=True)
+        ev[0].record(stream)
+        nxt, rew, term, _, info = tr.env.step(act)
+        ev[1].record(stream)
+        tr.agent.remember(tr.obs, act, rew.to(torch.float32), nxt, term, mask=~info["reset"])
+        ev[2].record(stream)
+        tr.last = tr.agent.replay()
+        ev[3].record(stream)
+        tr.obs = nxt
+        torch.cuda.synchronize()
+        ph["env_step_reward_ms"] += ev[0].elapsed_time(ev[1]) / KP
+        ph["replay_add_ms"] += ev[1].elapsed_time(ev[2]) / KP
+        ph["learner_update_ms"] += ev[2].elapsed_time(ev[3]) / KP
+    result = {
+        "metric": "env-steps/sec, end-to-end DDPG (BASELINE config 5)", "value": total / elapsed,
+        "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": W, "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64 env / f32 learner",
+        "data": "synthetic: Spielberg map, centerline spawns, actor + Gaussian noise actions",
+        "config": {"workload": f"{shard.count} two-agent envs per GPU (gap-follow opponent), device reward, "
+                               f"PER replay, 1 learner update of {args.ddpg_batch} rows per vector step",
+                   "envs_per_gpu": args.envs_per_gpu, "global_envs": args.envs_per_gpu * world,
+                   "batch_per_rank": args.ddpg_batch, "memory_per_rank": args.ddpg_memory,
+                   "parallelism": f"env-shard x{world}, DDPG data-parallel (RCCL all-reduce of grads)"},
+        "phases_ms": ph,
+        "learner": {"critic_loss": float(tr.last["critic_loss"]), "actor_loss": float(tr.last["actor_loss"]),
+                    "updates": tr.agent.global_step},
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    tr.close()
+    D.shutdown()
 
 
 def algorithmic_bytes_per_env_step(B: int, A: int, mean_lookups: float) -> float:
@@ -107,6 +181,8 @@ def cpu_baseline(track, spawn_poses, actions_np, args, gpu_sim):
 
 def main():
     args = parse()
+    if args.workload == "ddpg":
+        return bench_ddpg(args)
     import numpy as np
     import torch
     from f110_gymnasium_ros2_jazzy_amd import distributed as D
