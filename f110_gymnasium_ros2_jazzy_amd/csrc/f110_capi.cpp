@@ -50,7 +50,8 @@ struct f110_ctx {
     // device buffers
     double *dt_tiled = nullptr;
     int32_t wt = 0, tiles_h = 0;
-    int ray_kernel = 1;  // F110_RAY_KERNEL=0 selects the row-major k_rays (A/B)
+    int ray_kernel = 2;  // F110_RAY_KERNEL: 0 row-major k_rays, 1 tiled flat order, 2 tiled chunked (default)
+    uint8_t chunk_order[kMaxChunks] = {};
     double *dt = nullptr, *sines = nullptr, *cosines = nullptr, *angles = nullptr, *beam_cos = nullptr,
            *side = nullptr, *spawn = nullptr;
     double *start_rot = nullptr;
@@ -357,7 +358,35 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     c->inc = (double)C.theta_dis * (C.fov / (double)(C.n_beams - 1)) / (2. * kPi);  // laser_models.py:367-368
     c->beam_incr = C.fov / (double)(C.n_beams - 1);
     c->n_spawn = n_spawn;
-    if (const char *v = std::getenv("F110_RAY_KERNEL")) c->ray_kernel = std::atoi(v) == 0 ? 0 : 1;
+    if (const char *v = std::getenv("F110_RAY_KERNEL")) {
+        const int k = std::atoi(v);
+        c->ray_kernel = k == 0 ? 0 : (k == 2 ? 2 : 1);
+    }
+    {
+        // chunked dispatch order: descending beam chunks (the scan's left edge
+        // to its right edge), or F110_CHUNK_ORDER="16,15,...".  Measured
+        // against the flat order and five other chunk orders
+        // (scripts/chunk_ab.py): fastest at 4096 and 8192 envs,
+        // 1 and 2 agents.
+        const int nch = (C.n_beams + 63) / 64;
+        if (nch > kMaxChunks && c->ray_kernel == 2) c->ray_kernel = 1;
+        for (int i = 0; i < nch && i < kMaxChunks; ++i) c->chunk_order[i] = (uint8_t)(nch - 1 - i);
+        if (const char *v = std::getenv("F110_CHUNK_ORDER")) {
+            std::vector<int> seen(nch, 0), ord;
+            for (const char *q = v; *q;) {
+                char *end = nullptr;
+                long k = std::strtol(q, &end, 10);
+                if (end == q) break;
+                if (k >= 0 && k < nch && !seen[k]) {
+                    seen[k] = 1;
+                    ord.push_back((int)k);
+                }
+                q = *end ? end + 1 : end;
+            }
+            if ((int)ord.size() == nch)
+                for (int i = 0; i < nch; ++i) c->chunk_order[i] = (uint8_t)ord[i];
+        }
+    }
     const size_t EA = (size_t)C.n_envs * C.n_agents;
 
     auto cleanup = [&](int code, const std::string &msg) {
@@ -455,6 +484,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.map = map_view(c);
     a.tmap = tiled_view(c);
     a.ray_kernel = c->ray_kernel;
+    for (int i = 0; i < kMaxChunks; ++i) a.chunk_order[i] = c->chunk_order[i];
     a.sines = c->sines;
     a.cosines = c->cosines;
     a.angles = c->angles;

@@ -14,6 +14,7 @@ namespace f110 {
 // a 3.4 ms scan at 8192 envs); 256 slots make the adds contention-free.
 constexpr int kCtrSlots = 256;
 constexpr int kCtrStride = 16;  // u64 per slot (128 B)
+constexpr int kMaxChunks = 32;  // 64-beam chunks per scan (n_beams <= 2048) for the chunked ray dispatch
 
 // Everything one launch of the fused env-step kernel needs, passed by value.
 struct StepArgs {
@@ -24,7 +25,8 @@ struct StepArgs {
     f110_params p;                            // Simulator / F110Env params (GJK boxes, lidar_max)
     const f110_params *pa;                    // [A] RaceCar params (update_pose, ray_cast boxes)
     int32_t E, A, B, theta_dis, integrator, ego, autoreset, mode;  // mode 0 step, 1 reset
-    int32_t ray_kernel;       // 0: k_rays on the row-major EDT; 1: k_rays_tiled (default)
+    int32_t ray_kernel;       // 0: k_rays on the row-major EDT; 1: k_rays_tiled, flat ray order; 2: chunked
+    uint8_t chunk_order[kMaxChunks];  // beam-chunk dispatch order of the chunked ray kernel
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
     uint64_t seed;
     int64_t env_offset;
@@ -89,6 +91,9 @@ struct RayArgs {
     double *scans_f64;         // [EA][B] or null
     int32_t obs_len;
     float lidar_max;
+    // chunked dispatch (k_rays_tiled<.., CH = true>)
+    int32_t G4;                // blocks per chunk slot (4 cars per block)
+    uint8_t order[kMaxChunks]; // chunk of each slot
 };
 
 struct ScanArgs {

@@ -238,14 +238,37 @@ __device__ __forceinline__ const RayArgs *kernarg_rays() {
 // (k_post_single resolves the per-env state; no f64 scan hand-off at all).
 // With other cars in the env (HANDOFF) the f64 range also goes to
 // k_post_multi, whose agent ray_cast re-writes the entries it shortens.
-template <bool ROT, bool MASK, bool HANDOFF>
+//
+// CH (chunked dispatch): a wave traces 64 consecutive beams of ONE car (beam
+// chunk k of car g) instead of 64 consecutive rays of the flat ray index, and
+// the grid walks the chunks in a_order (the forward-looking, long-ray chunks
+// first), all cars of one chunk slot before the next.  Waves whose rays run
+// longest start first and the short side-looking chunks fill in behind them,
+// instead of a late long wave extending the tail of the launch.  With 4 cars
+// per block and G4 = ceil(EA/4) blocks per slot, block -> XCD (block % 8)
+// keeps all of a car's chunks on one XCD (and its L2) when G4 % 8 == 0.
+template <bool ROT, bool MASK, bool HANDOFF, bool CH>
 __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
     const int B = a.B;
-    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    int64_t r;
+    int g, b;
+    bool live;
+    if (CH) {
+        const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        const int slot = (int)blockIdx.x / a.G4;
+        const int cg = (int)blockIdx.x - slot * a.G4;
+        g = cg * 4 + wave;
+        b = (int)a.order[slot] * 64 + (int)(threadIdx.x & 63);
+        live = g < a.EA && b < B;
+        r = (int64_t)g * B + b;
+    } else {
+        r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+        live = r < (int64_t)a.EA * B;
+        g = (int)(r / B);
+        b = (int)(r - (int64_t)g * B);
+    }
     uint32_t n = 0;
-    if (r < (int64_t)a.EA * B) {
-        const int g = (int)(r / B);
-        const int b = (int)(r - (int64_t)g * B);
+    if (live) {
         const int e = g / a.A;
         if (!MASK || a.reset_mask[e]) {
             double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
@@ -731,18 +754,33 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         ra.scans_f64 = a.out.scans_f64;
         const bool rot = !(a.tmap.os == 0.0 && a.tmap.oc == 1.0);
         const bool mask = ra.reset_mask != nullptr;
-        const int v = (rot ? 4 : 0) + (mask ? 2 : 0) + (single ? 0 : 1);  // HANDOFF for A >= 2
-        const void *fn[8] = {
-            reinterpret_cast<const void *>(&k_rays_tiled<false, false, false>),
-            reinterpret_cast<const void *>(&k_rays_tiled<false, false, true>),
-            reinterpret_cast<const void *>(&k_rays_tiled<false, true, false>),
-            reinterpret_cast<const void *>(&k_rays_tiled<false, true, true>),
-            reinterpret_cast<const void *>(&k_rays_tiled<true, false, false>),
-            reinterpret_cast<const void *>(&k_rays_tiled<true, false, true>),
-            reinterpret_cast<const void *>(&k_rays_tiled<true, true, false>),
-            reinterpret_cast<const void *>(&k_rays_tiled<true, true, true>)};
+        const bool ch = a.ray_kernel == 2;
+        dim3 g2 = grid;
+        if (ch) {
+            ra.G4 = (EA + 3) / 4;
+            for (int i = 0; i < kMaxChunks; ++i) ra.order[i] = a.chunk_order[i];
+            g2 = dim3((unsigned)(ra.G4 * ((a.B + 63) / 64)));
+        }
+        const int v = (ch ? 8 : 0) + (rot ? 4 : 0) + (mask ? 2 : 0) + (single ? 0 : 1);  // HANDOFF for A >= 2
+        const void *fn[16] = {
+            reinterpret_cast<const void *>(&k_rays_tiled<false, false, false, false>),
+            reinterpret_cast<const void *>(&k_rays_tiled<false, false, true, false>),
+            reinterpret_cast<const void *>(&k_rays_tiled<false, true, false, false>),
+            reinterpret_cast<const void *>(&k_rays_tiled<false, true, true, false>),
+            reinterpret_cast<const void *>(&k_rays_tiled<true, false, false, false>),
+            reinterpret_cast<const void *>(&k_rays_tiled<true, false, true, false>),
+            reinterpret_cast<const void *>(&k_rays_tiled<true, true, false, false>),
+            reinterpret_cast<const void *>(&k_rays_tiled<true, true, true, false>),
+            reinterpret_cast<const void *>(&k_rays_tiled<false, false, false, true>),
+            reinterpret_cast<const void *>(&k_rays_tiled<false, false, true, true>),
+            reinterpret_cast<const void *>(&k_rays_tiled<false, true, false, true>),
+            reinterpret_cast<const void *>(&k_rays_tiled<false, true, true, true>),
+            reinterpret_cast<const void *>(&k_rays_tiled<true, false, false, true>),
+            reinterpret_cast<const void *>(&k_rays_tiled<true, false, true, true>),
+            reinterpret_cast<const void *>(&k_rays_tiled<true, true, false, true>),
+            reinterpret_cast<const void *>(&k_rays_tiled<true, true, true, true>)};
         void *args[] = {&ra};
-        if ((e = hipLaunchKernel(fn[v], grid, dim3(kBlock), args, 0, s)) != hipSuccess) return e;
+        if ((e = hipLaunchKernel(fn[v], g2, dim3(kBlock), args, 0, s)) != hipSuccess) return e;
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;

@@ -1,0 +1,108 @@
+"""A/B of the ray-kernel dispatch orders in one process (GPU box):
+flat ray order (F110_RAY_KERNEL=1) vs chunked centre-out (=2) vs chunked in
+the order of measured per-chunk cost.  Also per-chunk lookup statistics of the
+bench poses (mean lookups, mean wave max) and a bit-identity check of the
+variants' outputs.  Prints one JSON line."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns, load_map
+from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
+
+E = int(os.environ.get("AB_ENVS", 8192))
+A = int(os.environ.get("AB_AGENTS", 1))
+tm = load_map("Spielberg_map")
+sp = centerline_spawns("Spielberg", A)
+rng = np.random.default_rng(12345)
+p0 = sp[rng.integers(0, sp.shape[0], E)]
+
+# per-chunk cost of the bench poses (probe lookups per ray)
+os.environ["F110_RAY_KERNEL"] = "1"
+probe = BatchSim(tm, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp)
+poses = torch.as_tensor(p0[:, 0], device="cuda")
+look = None
+res = {}
+try:
+    out = probe.scan_batch(poses, probe=True)
+    look = out[1] if isinstance(out, tuple) else None
+except Exception as exc:  # probe API differences: record and continue
+    res["probe_error"] = repr(exc)
+if look is not None:
+    L = look.reshape(E, -1).cpu().numpy().astype(np.float64)
+    B = L.shape[1]
+    nch = (B + 63) // 64
+    mean_c, wmax_c = [], []
+    for k in range(nch):
+        blk = L[:, k * 64:(k + 1) * 64]
+        mean_c.append(float(blk.mean()))
+        wmax_c.append(float(blk.max(1).mean()))
+    res["chunk_mean_lookups"] = [round(x, 2) for x in mean_c]
+    res["chunk_mean_wave_max"] = [round(x, 2) for x in wmax_c]
+    order = list(np.argsort(-np.asarray(wmax_c), kind="stable"))
+    res["measured_order"] = [int(k) for k in order]
+    os.environ["F110_CHUNK_ORDER"] = ",".join(str(int(k)) for k in order)
+probe.close()
+
+variants = {"flat": ("1", None), "chunk_centre": ("2", ""), "chunk_measured": ("2", os.environ.get("F110_CHUNK_ORDER")),
+            "chunk_natural": ("2", ",".join(str(k) for k in range(17))),
+            "chunk_edges_first": ("2", "0,16,1,15,2,14,3,13,4,12,5,11,6,10,7,9,8"),
+            "chunk_sweep_from_centre": ("2", "8,9,10,11,12,13,14,15,16,7,6,5,4,3,2,1,0"),
+            "chunk_sweep_left_first": ("2", "8,7,6,5,4,3,2,1,0,9,10,11,12,13,14,15,16"),
+            "chunk_sweep_7_first": ("2", "7,8,9,10,11,12,13,14,15,16,6,5,4,3,2,1,0"),
+            "chunk_sweep_wrap": ("2", "8,9,10,11,12,13,14,15,16,0,1,2,3,4,5,6,7"),
+            "chunk_zigzag2": ("2", "8,9,7,10,11,6,5,12,13,4,3,14,15,2,1,16,0"),
+            "chunk_mono_desc": ("2", ",".join(str(k) for k in range(16, -1, -1))),
+            "chunk_light_first": ("2", "0,1,2,3,4,5,6,7,16,15,14,13,12,11,10,9,8"),
+            "chunk_9_first_desc": ("2", "9,10,11,12,13,14,15,16,8,7,6,5,4,3,2,1,0")}
+if os.environ.get("AB_ONLY"):
+    variants = {k: v for k, v in variants.items() if k in os.environ["AB_ONLY"].split(",")}
+sims = {}
+for name, (rk, order) in variants.items():
+    os.environ["F110_RAY_KERNEL"] = rk
+    if order is None or order == "":
+        os.environ.pop("F110_CHUNK_ORDER", None)
+    else:
+        os.environ["F110_CHUNK_ORDER"] = order
+    sims[name] = BatchSim(tm, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp,
+                          keep_f64_scans=True)
+
+g = torch.Generator(device="cuda").manual_seed(0)
+acts = torch.rand(200, E, A, 2, device="cuda", generator=g)
+acts[..., 0] = acts[..., 0] * 0.8378 - 0.4189
+acts[..., 1] *= 20
+for sm in sims.values():  # DVFS ramp + warm
+    sm.reset(p0)
+    for k in range(100):
+        sm.step(acts[k], minimal_outputs=True)
+torch.cuda.synchronize()
+for rnd in range(3):
+    for name, sm in sims.items():
+        sm.reset(p0)
+        for k in range(30):
+            sm.step(acts[k], minimal_outputs=True)
+        sm.profile_begin(150)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for k in range(150):
+            sm.step(acts[30 + k], minimal_outputs=True)
+        e1.record()
+        torch.cuda.synchronize()
+        pk = sm.profile_end()
+        res.setdefault(f"step_ms_{name}", []).append(round(e0.elapsed_time(e1) / 150, 4))
+        res.setdefault(f"rays_ms_{name}", []).append(round(pk["k_rays_ms"], 4))
+# bit identity of the variants after the same 40 steps
+outs = {}
+for name, sm in sims.items():
+    sm.reset(p0)
+    for k in range(40):
+        o = sm.step(acts[k])
+    torch.cuda.synchronize()
+    outs[name] = (o.scans_f64.clone(), o.obs.clone(), sm.agent_states().clone())
+ref = outs["flat"]
+res["variants_identical"] = all(all(torch.equal(a, b) for a, b in zip(ref, v)) for v in outs.values())
+print(json.dumps(res))
