@@ -69,6 +69,14 @@ struct f110_ctx {
     std::vector<hipEvent_t> prof_ev;  // 4 per recorded step
     int prof_max = 0, prof_n = 0;
     const double *noise_ext = nullptr;  // f110_set_scan_noise (caller-owned)
+    uint64_t *wtrace = nullptr;         // f110_debug_wave_trace buffer (diagnostics)
+    // heavy-first ray dispatch (chunked kernel)
+    uint8_t *wcost = nullptr;
+    uint32_t *heavy_list = nullptr, *heavy_mask = nullptr, *heavy_count = nullptr;
+    int32_t heavy_cap = 0, heavy_T = 24, nch = 0;  // F110_HEAVY_T; measured: 20-32 equal, 40 +1%, 16 +11%
+    uint64_t launch_n = 0;
+    int64_t wtrace_n = 0;
+    bool wtrace_armed = false;
 
     hipEvent_t *next_prof_events() {
         if (prof_n >= prof_max) return nullptr;
@@ -370,6 +378,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
         // 1 and 2 agents.
         const int nch = (C.n_beams + 63) / 64;
         if (nch > kMaxChunks && c->ray_kernel == 2) c->ray_kernel = 1;
+        c->nch = nch;
         for (int i = 0; i < nch && i < kMaxChunks; ++i) c->chunk_order[i] = (uint8_t)(nch - 1 - i);
         if (const char *v = std::getenv("F110_CHUNK_ORDER")) {
             std::vector<int> seen(nch, 0), ord;
@@ -433,6 +442,16 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     ALLOC(c->ctr, (size_t)kCtrSlots * kCtrStride);
     ALLOC(c->pa, (size_t)C.n_agents);
     if (spawn_poses && n_spawn > 0) ALLOC(c->spawn, (size_t)n_spawn * C.n_agents * 3);
+    if (const char *v = std::getenv("F110_HEAVY_T")) c->heavy_T = std::atoi(v);  // 0: no heavy-first dispatch
+    if (c->ray_kernel == 2 && c->heavy_T > 0) {
+        // up to 1/8 of the waves, in blocks of 4 (measured: ~7% of the waves
+        // have a ray longer than 40 lookups and carry ~46% of the wave-iterations)
+        c->heavy_cap = (int32_t)std::max<size_t>(64, (EA * (size_t)c->nch / 8 + 3) / 4 * 4);
+        ALLOC(c->wcost, EA * (size_t)c->nch);
+        ALLOC(c->heavy_list, 2 * (size_t)c->heavy_cap);
+        ALLOC(c->heavy_mask, EA);
+        ALLOC(c->heavy_count, 2);
+    }
 #undef ALLOC
 
     // dt = res * EDT (get_dt, laser_models.py:52) — bit-exact from the integer k.
@@ -535,6 +554,20 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.n_spawn = c->n_spawn;
     if (out) a.out = *out;
     a.ctr = c->ctr;
+    a.ray_nch = c->nch;
+    a.parity = (int32_t)(c->launch_n++ & 1);
+    if (c->wcost) {
+        a.wcost = c->wcost;
+        a.heavy_list = c->heavy_list;
+        a.heavy_mask = c->heavy_mask;
+        a.heavy_count = c->heavy_count;
+        a.heavy_cap = c->heavy_cap;
+        a.heavy_T = c->heavy_T;
+    }
+    if (c->wtrace_armed) {  // one traced ray launch
+        a.wtrace = c->wtrace;
+        c->wtrace_armed = false;
+    }
     return a;
 }
 
@@ -558,6 +591,7 @@ extern "C" int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dty
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     StepArgs a = make_step_args(ctx, out);
     a.mode = 0;
+    a.heavy_build = a.heavy_use = (a.wcost && a.ray_kernel == 2) ? 1 : 0;  // f110_reset launches do not use it
     if (actions_dtype == F110_F64)
         a.actions_f64 = static_cast<const double *>(actions);
     else
@@ -703,6 +737,31 @@ extern "C" int f110_profile_end(f110_ctx *ctx, double ms_out[3], int32_t *steps_
         for (int k = 0; k < 3; ++k) ms_out[k] = acc[k];
     if (steps_out) *steps_out = ctx->prof_n;
     ctx->free_prof();
+    return F110_OK;
+}
+
+extern "C" int f110_debug_wave_trace(f110_ctx *ctx, int32_t arm, uint64_t *host_out, int64_t max_waves,
+                                     int64_t *n_waves, void *stream) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_debug_wave_trace: null context");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    const int64_t EA = (int64_t)ctx->cfg.n_envs * ctx->cfg.n_agents;
+    const int64_t waves = ((EA + 3) / 4) * ((ctx->cfg.n_beams + 63) / 64) * (kRayBlock / 64);
+    if (!ctx->wtrace) {
+        void *q = nullptr;
+        HIP_TRY(hipMalloc(&q, (size_t)waves * 4 * sizeof(uint64_t)));
+        HIP_TRY(hipMemset(q, 0, (size_t)waves * 4 * sizeof(uint64_t)));
+        ctx->allocs.push_back(q);
+        ctx->wtrace = static_cast<uint64_t *>(q);
+        ctx->wtrace_n = waves;
+    }
+    if (n_waves) *n_waves = waves;
+    if (host_out) {
+        HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+        const int64_t n = max_waves < waves ? max_waves : waves;
+        HIP_TRY(hipMemcpy(host_out, ctx->wtrace, (size_t)n * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    }
+    if (arm) HIP_TRY(hipMemsetAsync(ctx->wtrace, 0, (size_t)waves * 4 * sizeof(uint64_t), (hipStream_t)stream));
+    ctx->wtrace_armed = arm != 0;
     return F110_OK;
 }
 

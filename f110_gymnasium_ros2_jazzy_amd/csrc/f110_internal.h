@@ -14,6 +14,7 @@ namespace f110 {
 // a 3.4 ms scan at 8192 envs); 256 slots make the adds contention-free.
 constexpr int kCtrSlots = 256;
 constexpr int kCtrStride = 16;  // u64 per slot (128 B)
+constexpr int kRayBlock = 256; // threads per block of the ray kernels
 constexpr int kMaxChunks = 32;  // 64-beam chunks per scan (n_beams <= 2048) for the chunked ray dispatch
 
 // Everything one launch of the fused env-step kernel needs, passed by value.
@@ -27,6 +28,14 @@ struct StepArgs {
     int32_t E, A, B, theta_dis, integrator, ego, autoreset, mode;  // mode 0 step, 1 reset
     int32_t ray_kernel;       // 0: k_rays on the row-major EDT; 1: k_rays_tiled, flat ray order; 2: chunked
     uint8_t chunk_order[kMaxChunks];  // beam-chunk dispatch order of the chunked ray kernel
+    uint64_t *wtrace;         // diagnostic wave trace of the next ray launch (f110_debug_wave_trace) or null
+    // heavy-first ray dispatch (chunked kernel): per (car, chunk) wave cost of
+    // the previous ray launch, this step's list of predicted-heavy waves
+    uint8_t *wcost;           // [EA][nch] min(255, longest ray of the wave) or null
+    uint32_t *heavy_list;     // [2][heavy_cap] (car << 8 | chunk), by step parity
+    uint32_t *heavy_mask;     // [EA] chunks of the car that are in the heavy list
+    uint32_t *heavy_count;    // [2] list lengths, by step parity
+    int32_t heavy_cap, heavy_T, heavy_build, heavy_use, parity, ray_nch;
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
     uint64_t seed;
     int64_t env_offset;
@@ -94,6 +103,13 @@ struct RayArgs {
     // chunked dispatch (k_rays_tiled<.., CH = true>)
     int32_t G4;                // blocks per chunk slot (4 cars per block)
     uint8_t order[kMaxChunks]; // chunk of each slot
+    uint64_t *wtrace;          // diagnostic wave trace [waves][4] or null
+    // heavy-first dispatch: HB leading blocks run the listed heavy waves
+    uint8_t *wcost;            // [EA][nch] written by every chunked launch (or null)
+    const uint32_t *heavy_list;
+    const uint32_t *heavy_mask;
+    const uint32_t *heavy_count;
+    int32_t HB, nch;
 };
 
 struct ScanArgs {

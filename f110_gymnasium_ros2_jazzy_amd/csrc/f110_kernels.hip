@@ -23,7 +23,7 @@
 
 namespace f110 {
 
-constexpr int kBlock = 256;
+constexpr int kBlock = kRayBlock;
 
 static_assert(sizeof(BeamRun) == 24, "BeamRun layout");
 
@@ -88,9 +88,55 @@ __device__ __forceinline__ double trace(const MapView &m, double x, double y, do
 
 // ------------------------------------------------------------------------
 // k_agents: one thread per car.
+// Heavy-first ray dispatch: the (car, chunk) waves whose longest ray took at
+// least heavy_T lookups in the previous ray launch are listed (up to
+// heavy_cap) for the leading blocks of this step's chunked ray kernel, so the
+// rare long waves (grazing beams, up to ~400 lookups) start first instead of
+// extending the launch's tail.  One atomic per wave of cars.
+__device__ __forceinline__ void build_heavy_list(const StepArgs &a, int g, bool valid) {
+    uint32_t hm = 0;
+    int h = 0;
+    if (valid) {
+        const uint8_t *wc = a.wcost + (size_t)g * a.ray_nch;
+        for (int k = 0; k < a.ray_nch; ++k)
+            if (wc[k] >= a.heavy_T) {
+                hm |= 1u << k;
+                ++h;
+            }
+    }
+    const int lane = threadIdx.x & 63;
+    int incl = h;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int up = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += up;
+    }
+    const int total = __shfl(incl, 63, 64);
+    uint32_t base = 0;
+    if (lane == 63 && total > 0) base = atomicAdd(a.heavy_count + a.parity, (uint32_t)total);
+    base = __shfl(base, 63, 64);
+    uint32_t pos = base + (uint32_t)(incl - h), keep = 0;
+    uint32_t *list = a.heavy_list + (size_t)a.parity * a.heavy_cap;
+    for (uint32_t m = hm; m; m &= m - 1) {
+        const int k = __builtin_ctz(m);
+        if (pos < (uint32_t)a.heavy_cap) {
+            list[pos] = ((uint32_t)g << 8) | (uint32_t)k;
+            keep |= 1u << k;
+        }
+        ++pos;
+    }
+    if (valid) a.heavy_mask[g] = keep;
+}
+
+// The next step's heavy list starts empty (its counter is the other parity).
+__device__ __forceinline__ void reset_next_heavy(const StepArgs &a) {
+    if (a.heavy_count && blockIdx.x == 0 && threadIdx.x == 0) a.heavy_count[a.parity ^ 1] = 0;
+}
+
 __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
     const int g = blockIdx.x * 64 + threadIdx.x;
     const int EA = a.E * a.A;
+    if (a.heavy_build) build_heavy_list(a, g, g < EA);  // block-uniform branch, before any return
     if (g >= EA) return;
     const int A = a.A;
     const int e = g / A;
@@ -247,18 +293,36 @@ __device__ __forceinline__ const RayArgs *kernarg_rays() {
 // instead of a late long wave extending the tail of the launch.  With 4 cars
 // per block and G4 = ceil(EA/4) blocks per slot, block -> XCD (block % 8)
 // keeps all of a car's chunks on one XCD (and its L2) when G4 % 8 == 0.
-template <bool ROT, bool MASK, bool HANDOFF, bool CH>
+//
+// TRACE (diagnostic build only, f110_debug_wave_trace): lane 0 of every wave
+// records its start / end time (s_memrealtime, 100 MHz), hardware id, XCC,
+// chunk slot and car to a buffer nothing else reads.
+template <bool ROT, bool MASK, bool HANDOFF, bool CH, bool TRACE = false>
 __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
+    uint64_t t_start = 0;
+    if (TRACE) t_start = __builtin_amdgcn_s_memrealtime();
     const int B = a.B;
     int64_t r;
     int g, b;
     bool live;
     if (CH) {
         const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-        const int slot = (int)blockIdx.x / a.G4;
-        const int cg = (int)blockIdx.x - slot * a.G4;
-        g = cg * 4 + wave;
-        b = (int)a.order[slot] * 64 + (int)(threadIdx.x & 63);
+        int k;
+        if ((int)blockIdx.x < a.HB) {  // heavy-first blocks: the listed waves
+            const uint32_t item = (uint32_t)blockIdx.x * 4 + wave;
+            if (item >= *a.heavy_count) return;  // wave-uniform: nothing listed here
+            const uint32_t v = __builtin_amdgcn_readfirstlane(a.heavy_list[item]);
+            g = (int)(v >> 8);
+            k = (int)(v & 255u);
+        } else {
+            const int blk = (int)blockIdx.x - a.HB;
+            const int slot = blk / a.G4;
+            const int cg = blk - slot * a.G4;
+            g = cg * 4 + wave;
+            k = (int)a.order[slot];
+            if (a.HB && g < a.EA && ((a.heavy_mask[g] >> k) & 1u)) return;  // ran in a heavy block
+        }
+        b = k * 64 + (int)(threadIdx.x & 63);
         live = g < a.EA && b < B;
         r = (int64_t)g * B + b;
     } else {
@@ -320,6 +384,26 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
         }
     }
     count_rays(kernarg_rays()->ctr, n);
+    if (CH) {  // this wave's cost, the next step's heavy-first prediction
+        uint32_t m = n;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+        uint8_t *wc = kernarg_rays()->wcost;
+        if (wc && (threadIdx.x & 63) == 0 && g < a.EA)
+            wc[(size_t)g * a.nch + (b >> 6)] = (uint8_t)(m < 255u ? m : 255u);
+    }
+    if (TRACE && (threadIdx.x & 63) == 0) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        const int64_t w = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+        uint64_t *o = kernarg_rays()->wtrace + 4 * w;
+        o[0] = t_start;
+        o[1] = t_end;
+        o[2] = ((uint64_t)xcc << 32) | hw;
+        o[3] = ((uint64_t)(CH ? (int)blockIdx.x / a.G4 : 0) << 32) | (uint32_t)g;
+    }
 }
 
 // F110Env.step's time + _check_done (f110_env.py:404-406, :310-352) and the
@@ -387,6 +471,7 @@ size_t post_lds_bytes(int A, int B) { return sizeof(PostShared) + sizeof(double)
 
 // k_post: one workgroup per env: Simulator.step's collision stage + F110Env's epilogue.
 __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
+    reset_next_heavy(a);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     PostShared &sh = *reinterpret_cast<PostShared *>(smem);
     double *scan = reinterpret_cast<double *>(smem + sizeof(PostShared));
@@ -511,6 +596,7 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
 // env: the TTC response (RaceCar.check_ttc, base_classes.py:246-249), the
 // pose part of the observation, collisions and the env epilogue.
 __global__ void __launch_bounds__(64) k_post_single(StepArgs a) {
+    reset_next_heavy(a);
     const int e = blockIdx.x * 64 + threadIdx.x;
     if (e >= a.E) return;
     if (a.mode == 1 && a.reset_mask && !a.reset_mask[e]) return;
@@ -565,6 +651,7 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 __global__ void __launch_bounds__(kMultiBlock) k_post_multi(StepArgs a) {
+    reset_next_heavy(a);
     __shared__ MultiShared sh;
     const int e = blockIdx.x;
     const int tid = threadIdx.x;
@@ -758,8 +845,16 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         dim3 g2 = grid;
         if (ch) {
             ra.G4 = (EA + 3) / 4;
+            ra.nch = (a.B + 63) / 64;
             for (int i = 0; i < kMaxChunks; ++i) ra.order[i] = a.chunk_order[i];
-            g2 = dim3((unsigned)(ra.G4 * ((a.B + 63) / 64)));
+            ra.wcost = a.wcost;
+            if (a.heavy_use && !mask) {
+                ra.HB = (a.heavy_cap + 3) / 4;
+                ra.heavy_list = a.heavy_list + (size_t)a.parity * a.heavy_cap;
+                ra.heavy_mask = a.heavy_mask;
+                ra.heavy_count = a.heavy_count + a.parity;
+            }
+            g2 = dim3((unsigned)(ra.HB + ra.G4 * ra.nch));
         }
         const int v = (ch ? 8 : 0) + (rot ? 4 : 0) + (mask ? 2 : 0) + (single ? 0 : 1);  // HANDOFF for A >= 2
         const void *fn[16] = {
@@ -780,7 +875,12 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
             reinterpret_cast<const void *>(&k_rays_tiled<true, true, false, true>),
             reinterpret_cast<const void *>(&k_rays_tiled<true, true, true, true>)};
         void *args[] = {&ra};
-        if ((e = hipLaunchKernel(fn[v], g2, dim3(kBlock), args, 0, s)) != hipSuccess) return e;
+        const void *f = fn[v];
+        if (a.wtrace && ch && !rot && !mask)  // diagnostic wave trace (f110_debug_wave_trace)
+            f = single ? reinterpret_cast<const void *>(&k_rays_tiled<false, false, false, true, true>)
+                       : reinterpret_cast<const void *>(&k_rays_tiled<false, false, true, true, true>);
+        ra.wtrace = a.wtrace;
+        if ((e = hipLaunchKernel(f, g2, dim3(kBlock), args, 0, s)) != hipSuccess) return e;
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;

@@ -209,6 +209,15 @@ F110_API int f110_reset_counters(f110_ctx *ctx, void *stream);
 F110_API int f110_profile_begin(f110_ctx *ctx, int32_t max_steps);
 F110_API int f110_profile_end(f110_ctx *ctx, double ms_out[3], int32_t *steps_out);
 
+/* ---- diagnostics -------------------------------------------------------------
+ * Wave trace of the ray kernel (chunked dispatch, axis-aligned map, no reset
+ * mask): arm != 0 records the next f110_step's ray launch -- per wave
+ * {start, end} s_memrealtime ticks (100 MHz), {XCC id << 32 | HW_ID},
+ * {chunk slot << 32 | car}.  host_out [max_waves][4] (or NULL) receives the
+ * last trace (waits for `stream`); n_waves gets the wave count of a launch. */
+F110_API int f110_debug_wave_trace(f110_ctx *ctx, int32_t arm, uint64_t *host_out, int64_t max_waves,
+                                   int64_t *n_waves, void *stream);
+
 /* ---- opponent policy -------------------------------------------------------
  * Replaces gap_follow_action (rl_training/utils/gap_follow.py:3-58), the
  * rule-based opponent train_ddpg.py:168 computes on the host each step from

@@ -48,26 +48,27 @@ if look is not None:
     os.environ["F110_CHUNK_ORDER"] = ",".join(str(int(k)) for k in order)
 probe.close()
 
-variants = {"flat": ("1", None), "chunk_centre": ("2", ""), "chunk_measured": ("2", os.environ.get("F110_CHUNK_ORDER")),
-            "chunk_natural": ("2", ",".join(str(k) for k in range(17))),
-            "chunk_edges_first": ("2", "0,16,1,15,2,14,3,13,4,12,5,11,6,10,7,9,8"),
-            "chunk_sweep_from_centre": ("2", "8,9,10,11,12,13,14,15,16,7,6,5,4,3,2,1,0"),
-            "chunk_sweep_left_first": ("2", "8,7,6,5,4,3,2,1,0,9,10,11,12,13,14,15,16"),
-            "chunk_sweep_7_first": ("2", "7,8,9,10,11,12,13,14,15,16,6,5,4,3,2,1,0"),
-            "chunk_sweep_wrap": ("2", "8,9,10,11,12,13,14,15,16,0,1,2,3,4,5,6,7"),
-            "chunk_zigzag2": ("2", "8,9,7,10,11,6,5,12,13,4,3,14,15,2,1,16,0"),
-            "chunk_mono_desc": ("2", ",".join(str(k) for k in range(16, -1, -1))),
-            "chunk_light_first": ("2", "0,1,2,3,4,5,6,7,16,15,14,13,12,11,10,9,8"),
-            "chunk_9_first_desc": ("2", "9,10,11,12,13,14,15,16,8,7,6,5,4,3,2,1,0")}
+DESC = ",".join(str(k) for k in range(16, -1, -1))
+variants = {"flat": {"F110_RAY_KERNEL": "1"},
+            "chunk_desc": {"F110_RAY_KERNEL": "2", "F110_CHUNK_ORDER": DESC, "F110_HEAVY_T": "0"},
+            "chunk_asc": {"F110_RAY_KERNEL": "2", "F110_CHUNK_ORDER": ",".join(str(k) for k in range(17)),
+                          "F110_HEAVY_T": "0"},
+            "heavy12": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "12"},
+            "heavy16": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "16"},
+            "heavy20": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "20"},
+            "heavy24": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "24"},
+            "heavy32": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "32"},
+            "heavy40": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "40"},
+            "heavy64": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "64"},
+            "heavy40_asc": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "40",
+                            "F110_CHUNK_ORDER": ",".join(str(k) for k in range(17))}}
 if os.environ.get("AB_ONLY"):
     variants = {k: v for k, v in variants.items() if k in os.environ["AB_ONLY"].split(",")}
 sims = {}
-for name, (rk, order) in variants.items():
-    os.environ["F110_RAY_KERNEL"] = rk
-    if order is None or order == "":
-        os.environ.pop("F110_CHUNK_ORDER", None)
-    else:
-        os.environ["F110_CHUNK_ORDER"] = order
+for name, env in variants.items():
+    for k in ("F110_RAY_KERNEL", "F110_CHUNK_ORDER", "F110_HEAVY_T"):
+        os.environ.pop(k, None)
+    os.environ.update(env)
     sims[name] = BatchSim(tm, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp,
                           keep_f64_scans=True)
 
@@ -103,6 +104,6 @@ for name, sm in sims.items():
         o = sm.step(acts[k])
     torch.cuda.synchronize()
     outs[name] = (o.scans_f64.clone(), o.obs.clone(), sm.agent_states().clone())
-ref = outs["flat"]
+ref = next(iter(outs.values()))
 res["variants_identical"] = all(all(torch.equal(a, b) for a, b in zip(ref, v)) for v in outs.values())
 print(json.dumps(res))

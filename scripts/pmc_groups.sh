@@ -2,7 +2,7 @@
 # counter groups for k_rays analysis; one rocprofv3 --pmc pass per group
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/pmc_groups${MB_AGENTS:+_a$MB_AGENTS}
+OUT=$R/gpurun_out/pmc_groups${MB_AGENTS:+_a$MB_AGENTS}${PMC_TAG:+_$PMC_TAG}
 mkdir -p $OUT
 timeout -k 10 60 rocprofv3 -L > $OUT/counters_list.txt 2>&1
 i=0
