@@ -288,6 +288,54 @@ F110_HD int32_t tiled_cell(const TiledMapView &m, double x, double y) {
     return inb ? tiled_index(m.wt, r, c) : m.oob;
 }
 
+// The ray loop's form of tiled_cell (same cell, bit for bit): the tile index
+// in 24-bit multiplies, the IEEE-divide fallback behind a wave-uniform
+// branch (taken only when some lane sits within 1e-9 of a cell edge, so the
+// common iteration carries no exec-mask juggling), and the EDT read as a
+// 32-bit byte offset from the table base (SGPR-base global load).
+__device__ __forceinline__ uint32_t tiled_index_u24(int32_t wt, int32_t r, int32_t c) {
+    return ((__umul24((uint32_t)r >> 2, (uint32_t)wt) + ((uint32_t)c >> 2)) << 4) | (((uint32_t)r & 3u) << 2) |
+           ((uint32_t)c & 3u);
+}
+
+template <bool ROT>
+__device__ __forceinline__ double tiled_lookup(const TiledMapView &m, double x, double y) {
+    double xr = x - m.ox;
+    double yr = y - m.oy;
+    if (ROT) {
+        const double xt = xr, yt = yr;
+        xr = xt * m.oc + yt * m.os;
+        yr = -xt * m.os + yt * m.oc;
+    }
+    const bool inb = (xr >= 0) & (xr < m.wres) & (yr >= 0) & (yr < m.hres);  // false for NaN
+    const double qx = xr * m.inv_res, qy = yr * m.inv_res;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double fx = __builtin_amdgcn_fract(qx), fy = __builtin_amdgcn_fract(qy);
+#else
+    const double fx = qx - floor(qx), fy = qy - floor(qy);
+#endif
+    const double band = fmax(fabs(fx - 0.5), fabs(fy - 0.5));
+    const bool slow = inb && band > 0.5 - 1e-9;
+    const uint32_t fast = tiled_index_u24(m.wt, (int32_t)qy, (int32_t)qx);  // garbage off-map, masked below
+    const uint32_t sel = 0u - (uint32_t)inb;  // branchless select: no exec-mask split per iteration
+    uint32_t idx = (fast & sel) | ((uint32_t)m.oob & ~sel);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (__builtin_amdgcn_ballot_w64(slow))  // wave-uniform, rare: the guard band of trunc_div
+#endif
+    {
+        if (slow) {
+            int32_t c = (int32_t)(xr / m.res);
+            int32_t r = (int32_t)(yr / m.res);
+            if (c >= m.W) {  // see tiled_cell
+                c = 0;
+                ++r;
+            }
+            idx = r >= m.H ? (uint32_t)m.oob : tiled_index_u24(m.wt, r, c);
+        }
+    }
+    return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(m.dt) + (idx << 3));
+}
+
 // ------------------------------------------------------ beam index runs --
 // get_scan's beam index (laser_models.py:167-184) is a SEQUENTIAL float
 // accumulation t_{i+1} = wrap(fl(t_i + inc)).  Inside one binade [2^(e-1), 2^e)

@@ -360,7 +360,7 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
             while (d > eps && tot <= mr) {  // :133
                 x += d * c;                 // :135
                 y += d * s;                 // :136
-                d = a.m.dt[tiled_cell<ROT>(a.m, x, y)];
+                d = tiled_lookup<ROT>(a.m, x, y);
                 tot += d;                   // :141
                 ++k;
             }
