@@ -377,11 +377,15 @@ F110_HD int build_beam_runs(double t, double inc, int theta_dis, int B, BeamRun 
                 double rem = inc - delta;    // exact (|rem| <= u/2, u >= 2^-52)
                 double half_u = ldexp(1.0, e - 54);
                 bool tie = fabs(rem) == half_u;
-                bool even = fmod(ldexp(t, 52 - e), 1.0) == 0.0;  // t/u even
+                bool even = (((int64_t)ldexp(t, 53 - e)) & 1) == 0;  // t/u (an integer < 2^53) even
                 if (!tie || even) {
                     int64_t span_u = (int64_t)ldexp(lim - t, 53 - e);
                     int64_t d_u = (int64_t)ldexp(delta, 53 - e);
-                    int64_t kmax = (span_u - 1) / d_u;
+                    // kmax = (span_u - 1) / d_u without a 64-bit integer divide:
+                    // both < 2^53, the fp64 quotient is within 1 of it, fixed up exactly
+                    int64_t kmax = (int64_t)((double)(span_u - 1) / (double)d_u);
+                    if (kmax * d_u > span_u - 1) --kmax;
+                    else if ((kmax + 1) * d_u <= span_u - 1) ++kmax;
                     int64_t left = (int64_t)(B - i - 1);
                     run = 1 + (int)(kmax < left ? kmax : left);
                 }
