@@ -170,11 +170,11 @@ struct ReplayHdr {
     int64_t next;       // _next_idx
     uint64_t draws;     // sample() calls so far (Philox counter)
     double den;         // sum of (p + eps)^alpha at the last sample
-    uint32_t maxbits;   // f32 bits of the max stored priority (add)
     int32_t replace;    // the last sample drew with replacement
+    int32_t pad0_;
     uint32_t prefix;    // radix select: threshold key so far
     uint32_t kleft;     //   rank still to select below/at the prefix
-    uint32_t n_lt, n_tie;  // keys below / equal to the threshold (cleared per sample)
+    uint32_t n_lt, n_tie;  // keys below / equal to the threshold (n_tie zeroed by k_finish)
     uint32_t overflow;  // samples whose tie list overflowed kTieCap
     uint32_t pad_;
 };
@@ -187,7 +187,8 @@ struct ReplayView {
     uint32_t *keys;      // [cap] exponential-race keys
     uint32_t *hist;      // [4][256]
     double *den_part;    // [kReplayMaxGrid]
-    uint64_t *sel;       // [kReplayMaxBatch] (key << 32 | index) below the threshold
+    uint32_t *part;      // [kReplayMaxGrid] per-block max priority (add) / selected count (sample)
+    uint64_t *sel;       // [kReplayMaxBatch] indices of the keys below the threshold, in index order
     uint32_t *tie;       // [kTieCap]
     int64_t *pos;        // [max rows per add] ring slot of each added row (-1: not stored)
     double alpha;

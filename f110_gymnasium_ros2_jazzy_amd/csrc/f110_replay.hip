@@ -6,8 +6,8 @@
 // numpy rng.choice on the host every update.  Here the ring of transitions
 // lives on the device as flat arrays and every operation is a few kernels:
 //
-//   add     (replay_buffer.py:48-71)   k_prio_max (max priority over the
-//           buffer) -> k_add_scan (one workgroup: ring slots of the masked
+//   add     (replay_buffer.py:48-71)   k_prio_max (per-block max priority)
+//           -> k_add_scan (one workgroup: the max, ring slots of the masked
 //           rows, their priority) -> k_add_copy (one block per row).
 //   sample  (replay_buffer.py:76-116)  Sampling WITHOUT replacement from
 //           p_i = (prio_i + eps)^alpha / sum_j (...) by the exponential race
@@ -18,8 +18,11 @@
 //           drops repeats in draw order and redraws the rest from the
 //           renormalised p).  The B smallest 32-bit key patterns are found by
 //           a 4-pass radix select (8-bit digits, LDS histograms); ties at the
-//           threshold go to the lowest indices; one workgroup then sorts the B
-//           (key, index) pairs and computes the IS weights.  With fewer stored
+//           threshold go to the lowest indices; the selection is compacted in
+//           index order (two passes, no sort) and one workgroup computes the
+//           IS weights.  As a set the batch has the distribution of the
+//           reference's draws; it is returned in index order, not draw order
+//           (agent.replay only averages over it).  With fewer stored
 //           rows than B (replace=True, :97) one workgroup draws i.i.d. by
 //           inverse CDF.
 //   update  (replay_buffer.py:121-135) clip, NaN -> 1e-6, scatter.
@@ -51,10 +54,10 @@ __device__ __forceinline__ double prio_weight(float p, float eps, double alpha) 
 }
 
 // p0 of add() (replay_buffer.py:52-63) from the max priority.
-__device__ __forceinline__ float add_priority(const ReplayHdr *h) {
+__device__ __forceinline__ float add_priority(int64_t length, uint32_t maxbits) {
     double p0 = 1.0;
-    if (h->length > 0) {
-        p0 = (double)__uint_as_float(h->maxbits);
+    if (length > 0) {
+        p0 = (double)__uint_as_float(maxbits);
         if (!isfinite(p0) || p0 <= 0.0) p0 = 1.0;
     }
     p0 = p0 < 1e-8 ? 1e-8 : p0;
@@ -84,21 +87,34 @@ __device__ __forceinline__ double block_sum_f64(double v, double *sh) {
 // Stored priorities are finite and positive (add and update clamp them), so
 // their u32 patterns order like the floats.
 __global__ void __launch_bounds__(kRB) k_prio_max(ReplayView v) {
+    __shared__ uint32_t wm[kRB / 64];
     const int64_t len = v.hdr->length;
     uint32_t m = 0;
     for (int64_t i = (int64_t)blockIdx.x * kRB + threadIdx.x; i < len; i += (int64_t)gridDim.x * kRB)
         m = max(m, f32_bits(v.prio[i]));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
-    if ((threadIdx.x & 63) == 0 && m) atomicMax(&v.hdr->maxbits, m);
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // one partial per block, reduced by k_add_scan (no hot-spot atomics)
+        uint32_t b = wm[0];
+        for (int w = 1; w < kRB / 64; ++w) b = max(b, wm[w]);
+        v.part[blockIdx.x] = b;
+    }
 }
 
 // Ring slots of the rows to store (mask[i] != 0, or all) in row order, as the
 // reference's one add() per transition (agent.remember) would fill them.
 __global__ void __launch_bounds__(kOneBlock) k_add_scan(ReplayView v, const uint8_t *mask, const float *priority,
-                                                        int64_t n) {
+                                                        int64_t n, int n_part) {
     __shared__ int64_t part[kOneBlock];
+    __shared__ uint32_t mx;
     const int t = threadIdx.x;
+    if (t == 0) {  // the max priority from k_prio_max's partials
+        uint32_t m = 0;
+        for (int k = 0; k < n_part; ++k) m = max(m, v.part[k]);
+        mx = m;
+    }
     const int64_t chunk = (n + kOneBlock - 1) / kOneBlock;
     const int64_t r0 = min((int64_t)t * chunk, n), r1 = min(r0 + chunk, n);
     int64_t cnt = 0;
@@ -114,7 +130,7 @@ __global__ void __launch_bounds__(kOneBlock) k_add_scan(ReplayView v, const uint
     const int64_t total = part[kOneBlock - 1];
     int64_t rank = part[t] - cnt;
     const int64_t cap = v.capacity, next = v.hdr->next;
-    const float p0 = add_priority(v.hdr);
+    const float p0 = add_priority(v.hdr->length, mx);
     for (int64_t i = r0; i < r1; ++i) {
         if (!mask || mask[i]) {
             const int64_t slot = (next + rank) % cap;
@@ -230,6 +246,7 @@ __global__ void __launch_bounds__(256) k_select(ReplayView v, int32_t batch, int
     const uint32_t kleft = pass == 0 ? (uint32_t)batch : v.hdr->kleft;
     const uint32_t prefix = pass == 0 ? 0u : v.hdr->prefix;
     inc[t] = v.hist[pass * 256 + t];
+    v.hist[pass * 256 + t] = 0;  // consumed: zero for the next sample
     __syncthreads();
     for (int o = 1; o < 256; o <<= 1) {
         const uint32_t add = t >= o ? inc[t - o] : 0u;
@@ -244,40 +261,74 @@ __global__ void __launch_bounds__(256) k_select(ReplayView v, int32_t batch, int
     }
 }
 
-// Keys below the threshold key T go to the selection; keys equal to T to the
-// tie list, of which the kleft lowest indices are taken.
-__global__ void __launch_bounds__(kRB) k_collect(ReplayView v, int32_t batch) {
+// The selection: every key below the threshold key T, plus the lowest-index
+// kleft of the keys equal to T (tie list).  It is written in INDEX order
+// (deterministic, no sort): block b owns the contiguous index range
+// [b*chunk, (b+1)*chunk); k_count counts its keys below T (and lists the
+// ties), k_place writes them at the sum of the preceding blocks' counts.
+__device__ __forceinline__ int64_t block_chunk(int64_t len) {
+    return (len + gridDim.x - 1) / gridDim.x;
+}
+
+__global__ void __launch_bounds__(kRB) k_count(ReplayView v, int32_t batch) {
+    __shared__ uint32_t wc[kRB / 64];
     const int64_t len = v.hdr->length;
     if (len < batch) return;
     const uint32_t T = v.hdr->prefix;
-    for (int64_t i = (int64_t)blockIdx.x * kRB + threadIdx.x; i < len; i += (int64_t)gridDim.x * kRB) {
+    const int64_t chunk = block_chunk(len);
+    const int64_t i0 = (int64_t)blockIdx.x * chunk, i1 = min(i0 + chunk, len);
+    uint32_t c = 0;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kRB) {
         const uint32_t key = v.keys[i];
-        if (key < T) {
-            const uint32_t s = atomicAdd(&v.hdr->n_lt, 1u);
-            if (s < (uint32_t)batch) v.sel[s] = ((uint64_t)key << 32) | (uint64_t)i;
-        } else if (key == T) {
-            const uint32_t s = atomicAdd(&v.hdr->n_tie, 1u);
+        c += key < T ? 1u : 0u;
+        if (key == T) {
+            const uint32_t s = atomicAdd(&v.hdr->n_tie, 1u);  // rare
             if (s < (uint32_t)kTieCap) v.tie[s] = (uint32_t)i;
         }
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) v.part[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
 }
 
-__device__ void bitonic_sort_u64(uint64_t *a, int P) {
-    for (int k = 2; k <= P; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < P; i += blockDim.x) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const uint64_t x = a[i], y = a[l];
-                    const bool up = (i & k) == 0;
-                    if ((x > y) == up) {
-                        a[i] = y;
-                        a[l] = x;
-                    }
-                }
-            }
-            __syncthreads();
+__global__ void __launch_bounds__(kRB) k_place(ReplayView v, int32_t batch) {
+    __shared__ uint32_t base, wsum[kRB / 64];
+    const int64_t len = v.hdr->length;
+    if (len < batch) return;
+    const uint32_t T = v.hdr->prefix;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    {  // this block's offset: the counts of the blocks before it
+        uint32_t acc = 0;
+        for (int k = t; k < (int)blockIdx.x; k += kRB) acc += v.part[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+        if (lane == 0) wsum[wave] = acc;
+        __syncthreads();
+        if (t == 0) base = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+    }
+    const int64_t chunk = block_chunk(len);
+    const int64_t i0 = (int64_t)blockIdx.x * chunk, i1 = min(i0 + chunk, len);
+    uint32_t off = base;
+    for (int64_t j0 = i0; j0 < i1; j0 += kRB) {  // tiles of kRB indices, in order
+        const int64_t i = j0 + t;
+        const bool sel = i < i1 && v.keys[i] < T;
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(sel);
+        const uint32_t before = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        __syncthreads();
+        if (lane == 0) wsum[wave] = (uint32_t)__builtin_popcountll(bal);
+        __syncthreads();
+        uint32_t pre = 0;
+        for (int w = 0; w < wave; ++w) pre += wsum[w];
+        if (sel) {
+            const uint32_t s = off + pre + before;
+            if (s < (uint32_t)batch) v.sel[s] = (uint64_t)i;
         }
+        off += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    }
+    if (blockIdx.x == gridDim.x - 1 && t == 0) v.hdr->n_lt = off;  // total below T
 }
 
 // IS weights (replay_buffer.py:103-113) of the selected rows.
@@ -304,39 +355,56 @@ __device__ void write_weights(const ReplayView &v, const int64_t *idx, int32_t b
     }
 }
 
-// Without replacement: resolve the ties, sort the batch by (key, index) --
-// the draw order -- and write indices and weights.
+// Without replacement: merge the chosen ties (the lowest-index `need` keys
+// equal to T) into the index-ordered selection; weights.
 __global__ void __launch_bounds__(kOneBlock) k_finish(ReplayView v, int32_t batch, double beta, int64_t *idx_out,
                                                       float *w_out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int64_t len = v.hdr->length;
     if (len < batch) return;
-    int P = 1;
-    while (P < batch) P <<= 1;
-    uint64_t *a = reinterpret_cast<uint64_t *>(smem);  // [P]
-    int64_t *idx = reinterpret_cast<int64_t *>(a + P);  // [batch]
+    int64_t *idx = reinterpret_cast<int64_t *>(smem);     // [batch]
     double *wsh = reinterpret_cast<double *>(idx + batch);  // [batch]
-    const uint32_t T = v.hdr->prefix;
+    __shared__ uint32_t chosen[64];
+    __shared__ uint32_t n_ch;
     const uint32_t n_lt = min(v.hdr->n_lt, (uint32_t)batch);
     const uint32_t n_tie = min(v.hdr->n_tie, (uint32_t)kTieCap);
     const uint32_t need = (uint32_t)batch - n_lt;
-    for (int j = threadIdx.x; j < P; j += blockDim.x) a[j] = j < (int)n_lt ? v.sel[j] : ~0ull;
+    if (threadIdx.x == 0) n_ch = 0;
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < n_tie; t += blockDim.x) {  // rank among the ties by index
         const uint32_t mine = v.tie[t];
         uint32_t rank = 0;
         for (uint32_t u = 0; u < n_tie; ++u) rank += v.tie[u] < mine ? 1u : 0u;
-        if (rank < need) a[n_lt + rank] = ((uint64_t)T << 32) | (uint64_t)mine;
+        if (rank < need) {
+            if (rank < 64) chosen[rank] = mine;
+            atomicAdd(&n_ch, 1u);
+        }
     }
     __syncthreads();
-    bitonic_sort_u64(a, P);
-    for (int j = threadIdx.x; j < batch; j += blockDim.x) idx[j] = (int64_t)(a[j] & 0xffffffffull);
+    const uint32_t nc = min(n_ch, 64u);  // kTieCap ties, of which need (typically 1) are taken
+    for (uint32_t j = threadIdx.x; j < n_lt; j += blockDim.x) {  // main rows shift past smaller ties
+        const uint64_t i = v.sel[j];
+        uint32_t k = 0;
+        for (uint32_t c = 0; c < nc; ++c) k += chosen[c] < i ? 1u : 0u;
+        idx[j + k] = (int64_t)i;
+    }
+    for (uint32_t c = threadIdx.x; c < nc; c += blockDim.x) {  // ties after the smaller main rows
+        const uint32_t ti = chosen[c];
+        uint32_t lo = 0, hi = n_lt;  // first main row with index > ti
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (v.sel[mid] < ti) lo = mid + 1;
+            else hi = mid;
+        }
+        idx[lo + c] = (int64_t)ti;
+    }
     __syncthreads();
     write_weights(v, idx, batch, len, v.hdr->den, beta, wsh, idx_out, w_out);
     if (threadIdx.x == 0) {
         v.hdr->draws += 1;
         v.hdr->replace = 0;
-        if (v.hdr->n_tie > (uint32_t)kTieCap) v.hdr->overflow += 1;
+        if (v.hdr->n_tie > (uint32_t)kTieCap || n_ch > 64u) v.hdr->overflow += 1;
+        v.hdr->n_tie = 0;  // consumed: zero for the next sample
     }
 }
 
@@ -447,21 +515,16 @@ int replay_grid(int64_t capacity) {
     return (int)(g < 1 ? 1 : (g > kReplayMaxGrid ? kReplayMaxGrid : g));
 }
 
-size_t replay_finish_lds(int32_t batch) {
-    size_t P = 1;
-    while (P < (size_t)batch) P <<= 1;
-    return P * 8 + (size_t)batch * 16;
-}
+size_t replay_finish_lds(int32_t batch) { return (size_t)batch * 16; }
 
 size_t replay_replace_lds(int32_t batch) { return (size_t)batch * 24; }
 
 hipError_t launch_replay_add(const ReplayView &v, const ReplayRows &in, const uint8_t *mask, int64_t n,
                              hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(&v.hdr->maxbits, 0, sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_prio_max, dim3(replay_grid(v.capacity)), dim3(kRB), 0, s, v);
-    hipLaunchKernelGGL(k_add_scan, dim3(1), dim3(kOneBlock), 0, s, v, mask, in.priority, n);
+    const int grid = replay_grid(v.capacity);
+    hipLaunchKernelGGL(k_prio_max, dim3(grid), dim3(kRB), 0, s, v);
+    hipLaunchKernelGGL(k_add_scan, dim3(1), dim3(kOneBlock), 0, s, v, mask, in.priority, n, grid);
     hipLaunchKernelGGL(k_add_copy, dim3((unsigned)n), dim3(kRB), 0, s, v, in, n);
     return hipGetLastError();
 }
@@ -469,16 +532,16 @@ hipError_t launch_replay_add(const ReplayView &v, const ReplayRows &in, const ui
 hipError_t launch_replay_sample(const ReplayView &v, int32_t batch, double beta, int64_t *idx, float *w,
                                 const ReplayBatch &out, hipStream_t s) {
     const int grid = replay_grid(v.capacity);
-    hipError_t e = hipMemsetAsync(v.hist, 0, 4 * 256 * sizeof(uint32_t), s);  // histograms
-    if (e == hipSuccess) e = hipMemsetAsync(&v.hdr->n_lt, 0, 2 * sizeof(uint32_t), s);  // n_lt, n_tie
-    if (e != hipSuccess) return e;
+    // histograms and tie count are cleared by k_select of the previous sample
+    // (and at create), so a sample is kernels only
     hipLaunchKernelGGL(k_keys, dim3(grid), dim3(kRB), 0, s, v, batch);
     hipLaunchKernelGGL(k_select, dim3(1), dim3(256), 0, s, v, batch, 0, grid);
     for (int pass = 1; pass < 4; ++pass) {
         hipLaunchKernelGGL(k_hist, dim3(grid), dim3(kRB), 0, s, v, batch, pass);
         hipLaunchKernelGGL(k_select, dim3(1), dim3(256), 0, s, v, batch, pass, grid);
     }
-    hipLaunchKernelGGL(k_collect, dim3(grid), dim3(kRB), 0, s, v, batch);
+    hipLaunchKernelGGL(k_count, dim3(grid), dim3(kRB), 0, s, v, batch);
+    hipLaunchKernelGGL(k_place, dim3(grid), dim3(kRB), 0, s, v, batch);
     hipLaunchKernelGGL(k_finish, dim3(1), dim3(kOneBlock), replay_finish_lds(batch), s, v, batch, beta, idx, w);
     hipLaunchKernelGGL(k_sample_replace, dim3(1), dim3(kOneBlock), replay_replace_lds(batch), s, v, batch, beta,
                        idx, w);
