@@ -119,7 +119,7 @@ class DDPGLearner:
                  alpha: float = 0.6, beta: float = 0.4, priority_epsilon: float = 1e-5,
                  noise_sigma_start: float = 0.2, noise_sigma_min: float = 0.05, noise_decay: float = 0.999,
                  seed: int = 42, device="cuda:0", replay="device", process_group=None, max_add: int | None = None,
-                 check_finite: bool = False, path: str | None = None):
+                 check_finite: bool = False, path: str | None = None, graphs: bool = False):
         self.device = torch.device(device)
         self.obs_dim, self.act_dim = int(obs_dim), int(act_dim)
         self.action_low = np.asarray(action_low, dtype=np.float32)
@@ -149,7 +149,11 @@ class DDPGLearner:
                     dist.broadcast(t.data, src=0, group=self.group)
         self.actor_grads = GradBucket(self.actor, self.group)
         self.critic_grads = GradBucket(self.critic, self.group)
-        fused = {"fused": True} if self.device.type == "cuda" else {}
+        # HIP graphs (replay with graphs=True) need the device-side step counters
+        self.graphs = bool(graphs) and self.device.type == "cuda" and replay is not None
+        fused = {"fused": True, "capturable": self.graphs} if self.device.type == "cuda" else {}
+        self._graphs, self._graph_out, self._eager_left = None, None, 3
+        self._side = torch.cuda.Stream(self.device) if self.graphs else None
         self.actor_optim = torch.optim.Adam(self.actor.parameters(), lr=actor_lr, **fused)
         self.critic_optim = torch.optim.Adam(self.critic.parameters(), lr=critic_lr, **fused)
         self._online = list(self.actor.parameters()) + list(self.critic.parameters())
@@ -183,10 +187,10 @@ class DDPGLearner:
             bad = (~torch.isfinite(x)).nonzero(as_tuple=False)[:10].cpu().numpy().tolist()
             raise ValueError(f"Non-finite in {name}; examples idx={bad[:5]}")
 
-    def update(self, states, actions, rewards, next_states, dones, weights) -> dict:
-        """The learning part of replay() (agent.py:302-343) on one batch:
-        critic step, actor step, soft target update.  Returns device tensors
-        (critic_loss, actor_loss, td [B])."""
+    # The update is three phases split at the two gradient all-reduces, so a
+    # HIP graph can hold each phase while the RCCL collectives stay eager.
+    def _phase_critic(self, states, actions, rewards, next_states, dones, weights):
+        """agent.py:302-319: TD target, critic loss, critic backward."""
         r = rewards.reshape(-1, 1)
         d = dones.reshape(-1, 1)
         w = weights.reshape(-1, 1)
@@ -201,23 +205,39 @@ class DDPGLearner:
         q_pred = self.critic(states, actions)  # :310-315
         td = target_y - q_pred
         critic_loss = (w * td ** 2).mean()
-        self.critic_grads.zero()               # :318-321
+        self.critic_grads.zero()               # :318-319
         critic_loss.backward()
-        self.critic_grads.all_reduce()
+        return critic_loss.detach(), td.detach()
+
+    def _phase_actor(self, states):
+        """agent.py:321-331: critic step, actor loss through the frozen critic."""
         self.critic_optim.step()
-        for p in self.critic.parameters():     # :324-334
+        for p in self.critic.parameters():
             p.requires_grad_(False)
         actor_loss = -self.critic(states, self.actor(states)).mean()
         self.actor_grads.zero()
         actor_loss.backward()
-        self.actor_grads.all_reduce()
-        self.actor_optim.step()
         for p in self.critic.parameters():
             p.requires_grad_(True)
-        with torch.no_grad():                  # _soft_update (:340-341, :373-376)
+        return actor_loss.detach()
+
+    def _phase_finish(self):
+        """agent.py:331, :340-341: actor step, soft target update."""
+        self.actor_optim.step()
+        with torch.no_grad():
             torch._foreach_lerp_(self._target, self._online, self.tau)
+
+    def update(self, states, actions, rewards, next_states, dones, weights) -> dict:
+        """The learning part of replay() (agent.py:302-343) on one batch:
+        critic step, actor step, soft target update.  Returns device tensors
+        (critic_loss, actor_loss, td [B])."""
+        critic_loss, td = self._phase_critic(states, actions, rewards, next_states, dones, weights)
+        self.critic_grads.all_reduce()
+        actor_loss = self._phase_actor(states)
+        self.actor_grads.all_reduce()
+        self._phase_finish()
         self.global_step += 1
-        return {"critic_loss": critic_loss.detach(), "actor_loss": actor_loss.detach(), "td": td.detach()}
+        return {"critic_loss": critic_loss, "actor_loss": actor_loss, "td": td}
 
     @staticmethod
     def td_priorities(td: torch.Tensor, priority_epsilon: float) -> torch.Tensor:
@@ -225,15 +245,73 @@ class DDPGLearner:
         return td.abs().reshape(-1) + priority_epsilon
 
     def replay(self):
-        """agent.py:242-348: None until the memory holds batch_size rows."""
+        """agent.py:242-348: None until the memory holds batch_size rows.
+        With graphs=True the sample + update + priority update run as HIP
+        graph replays (captured after a few eager updates): one launch per
+        phase instead of ~150 kernel launches from Python."""
         if not self._ready:  # len() syncs; once full enough it stays so (the ring never shrinks)
             if len(self.memory) < self.batch_size:
                 return None
             self._ready = True
+        if self.graphs:
+            return self._replay_graphed()
+        return self._replay_eager()
+
+    def _replay_eager(self):
         idxs, b, w = self.memory.sample(beta=self.beta)
         st = self.update(b["states"], b["actions"], b["rewards"], b["next_states"], b["dones"], w)
         self.memory.update_priorities(idxs, st["td"], td_errors=True, add_eps=self.priority_epsilon)
         return st
+
+    def _graph_phases(self):
+        """The replay() body as three callables split at the all-reduces."""
+        m = self.memory
+        out = {}
+
+        def a():
+            idxs, b, w = m.sample(beta=self.beta)
+            out["critic_loss"], out["td"] = self._phase_critic(b["states"], b["actions"], b["rewards"],
+                                                               b["next_states"], b["dones"], w)
+
+        def b_():
+            out["actor_loss"] = self._phase_actor(m.batch["states"])
+
+        def c():
+            self._phase_finish()
+            m.update_priorities(m.idx, out["td"], td_errors=True, add_eps=self.priority_epsilon)
+        return (a, b_, c), out
+
+    def _replay_graphed(self):
+        cur = torch.cuda.current_stream(self.device)
+        if self._graphs is None:
+            phases, out = self._graph_phases()
+            if self._eager_left > 0:  # warm-up: real updates on a side stream (allocator, optimizer state)
+                side = self._side
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    phases[0]()
+                    self.critic_grads.all_reduce()
+                    phases[1]()
+                    self.actor_grads.all_reduce()
+                    phases[2]()
+                cur.wait_stream(side)
+                self._eager_left -= 1
+                self.global_step += 1
+                return dict(out)
+            graphs = [torch.cuda.CUDAGraph() for _ in phases]
+            pool = torch.cuda.graph_pool_handle()
+            for g, ph in zip(graphs, phases):  # capture records, it does not run
+                with torch.cuda.graph(g, pool=pool, stream=self._side):
+                    ph()
+            self._graphs, self._graph_out = graphs, out
+        g = self._graphs
+        g[0].replay()
+        self.critic_grads.all_reduce()
+        g[1].replay()
+        self.actor_grads.all_reduce()
+        g[2].replay()
+        self.global_step += 1
+        return self._graph_out
 
     def choose_action(self, obs, training: bool = True) -> torch.Tensor:
         """agent.py:350-370 for obs [N, obs_dim] (or [obs_dim]): actor output,

@@ -39,7 +39,7 @@ class VectorTrainer:
 
     def __init__(self, envs_per_rank: int, map_name: str = "Spielberg_map", batch_size: int = 4096,
                  memory_size: int = 1 << 20, warmup_steps: int = 1000, updates_per_step: int = 1, seed: int = 42,
-                 device=None, env_offset: int = 0, rank_seed: int = 0):
+                 device=None, env_offset: int = 0, rank_seed: int = 0, graphs: bool = True):
         from .ddpg import DDPGLearner
         from .maps import MAP_DIR
         from .reward import BatchedCenterlineReward, CenterlineTrack
@@ -57,7 +57,7 @@ class VectorTrainer:
                                  actor_lr=1e-4, critic_lr=1e-3, memory_size=memory_size, batch_size=batch_size,
                                  alpha=0.6, beta=0.4, priority_epsilon=1e-5, noise_sigma_start=0.20,
                                  noise_sigma_min=0.02, noise_decay=0.9995, seed=seed, device=self.device,
-                                 max_add=self.N)
+                                 max_add=self.N, graphs=graphs)
         self.warmup = int(warmup_steps)
         self.updates_per_step = int(updates_per_step)
         self._gen = torch.Generator(device=self.device)

@@ -174,3 +174,34 @@ def test_vector_trainer_loop(gpu):
     for p in tr.agent.actor.parameters():
         assert torch.isfinite(p).all()
     tr.close()
+
+
+def test_learner_graphs_match_eager(gpu):
+    """replay() as HIP-graph replays (graphs=True: 3 eager warm-up updates,
+    then captured phases) follows the eager learner: same PER draws (device
+    Philox counter), same losses and weights within fp32 tolerance."""
+    from f110_gymnasium_ros2_jazzy_amd.ddpg import DDPGLearner
+    g = torch.Generator(device="cuda").manual_seed(5)
+    D = 64
+    S = torch.randn(512, D, device="cuda", generator=g)
+    A = torch.rand(512, 2, device="cuda", generator=g) * torch.tensor([0.8378, 20.0], device="cuda") - \
+        torch.tensor([0.4189, 0.0], device="cuda")
+    R = torch.randn(512, device="cuda", generator=g)
+    S2 = S + 0.1 * torch.randn(512, D, device="cuda", generator=g)
+    Dn = torch.rand(512, device="cuda", generator=g) < 0.1
+    runs = []
+    for graphs in (False, True):
+        ln = DDPGLearner(obs_dim=D, act_dim=2, action_low=[-0.4189, 0.0], action_high=[0.4189, 20.0], seed=3,
+                         device="cuda:0", memory_size=1024, batch_size=128, graphs=graphs)
+        ln.remember(S, A, R, S2, Dn)
+        losses = []
+        for _ in range(8):
+            st = ln.replay()
+            losses.append((float(st["critic_loss"]), float(st["actor_loss"])))
+        runs.append((losses, [p.detach().clone() for p in ln.actor.parameters()],
+                     ln.memory.priorities().clone()))
+        ln.memory.close()
+    np.testing.assert_allclose(runs[0][0], runs[1][0], rtol=1e-4)
+    for a, b in zip(runs[0][1], runs[1][1]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(runs[0][2], runs[1][2], rtol=1e-3, atol=1e-6)
