@@ -863,7 +863,52 @@ extern "C" int f110_track_create(f110_track **out, int32_t device, const double 
         *dst = static_cast<const double *>(q);
         return hipMemcpy(q, src, cnt * sizeof(double), hipMemcpyHostToDevice);
     };
+    // uniform grid over the segment midpoints (reward kernel's kd.query):
+    // 4 m cells (the centerline spacing is ~1 m, the 5th nearest midpoint
+    // is typically within 2.5 m), one cell of margin on every side
+    std::vector<int32_t> cstart, citems;
+    if (!host_only && n >= 2) {
+        double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
+        for (int32_t i = 0; i + 1 < n; ++i) {
+            mnx = std::min(mnx, t->mid[2 * (size_t)i]);
+            mxx = std::max(mxx, t->mid[2 * (size_t)i]);
+            mny = std::min(mny, t->mid[2 * (size_t)i + 1]);
+            mxy = std::max(mxy, t->mid[2 * (size_t)i + 1]);
+        }
+        const double h = 4.0;
+        if (std::isfinite(mnx) && std::isfinite(mny) && std::isfinite(mxx) && std::isfinite(mxy) &&
+            (mxx - mnx) / h < 4096 && (mxy - mny) / h < 4096) {
+            t->v.gh = h;
+            t->v.gx0 = mnx - h;
+            t->v.gy0 = mny - h;
+            t->v.gnx = (int32_t)((mxx - t->v.gx0) / h) + 2;
+            t->v.gny = (int32_t)((mxy - t->v.gy0) / h) + 2;
+            const size_t nc = (size_t)t->v.gnx * t->v.gny;
+            std::vector<int32_t> cell((size_t)n - 1);
+            cstart.assign(nc + 1, 0);
+            for (int32_t i = 0; i + 1 < n; ++i) {
+                const int32_t ci = (int32_t)((t->mid[2 * (size_t)i] - t->v.gx0) / h);
+                const int32_t cj = (int32_t)((t->mid[2 * (size_t)i + 1] - t->v.gy0) / h);
+                cell[(size_t)i] = cj * t->v.gnx + ci;
+                ++cstart[(size_t)cell[(size_t)i] + 1];
+            }
+            for (size_t c = 0; c < nc; ++c) cstart[c + 1] += cstart[c];
+            citems.assign((size_t)n - 1, 0);
+            std::vector<int32_t> fill(cstart.begin(), cstart.end() - 1);
+            for (int32_t i = 0; i + 1 < n; ++i) citems[(size_t)fill[(size_t)cell[(size_t)i]]++] = i;
+        }
+    }
+    auto up_i = [&](const std::vector<int32_t> &src, const int32_t **dst) -> hipError_t {
+        void *q = nullptr;
+        hipError_t e = hipMalloc(&q, src.size() * sizeof(int32_t));
+        if (e != hipSuccess) return e;
+        t->allocs.push_back(q);
+        *dst = static_cast<const int32_t *>(q);
+        return hipMemcpy(q, src.data(), src.size() * sizeof(int32_t), hipMemcpyHostToDevice);
+    };
     hipError_t e = up(xy, 2 * (size_t)n, &t->v.xy);
+    if (e == hipSuccess && !cstart.empty()) e = up_i(cstart, &t->v.cell_start);
+    if (e == hipSuccess && !citems.empty()) e = up_i(citems, &t->v.cell_items);
     if (e == hipSuccess) e = up(t->s.data(), t->s.size(), &t->v.s);
     if (e == hipSuccess) e = up(t->tan.data(), t->tan.size(), &t->v.tan);
     if (e == hipSuccess) e = up(t->nrm.data(), t->nrm.size(), &t->v.nrm);

@@ -146,6 +146,12 @@ struct TrackView {
     const double *wR, *wL;  // [n] lane widths or null
     int32_t n, closed;
     double L;
+    // uniform grid over the midpoints (kd.query acceleration): cell (i, j) of
+    // size gh at (gx0 + i*gh, gy0 + j*gh) holds midpoints cell_items[cell_start[c] ..
+    // cell_start[c+1]), c = j*gnx + i
+    const int32_t *cell_start, *cell_items;
+    int32_t gnx, gny;
+    double gx0, gy0, gh;
 };
 
 struct RewardArgs {

@@ -37,6 +37,8 @@ __device__ __forceinline__ bool cand_less(double d2a, int32_t ia, double d2b, in
     return d2a < d2b || (d2a == d2b && ia < ib);
 }
 
+__device__ void merge_top(const Cand (&t)[kTop], int lane, Cand out[kTop]);
+
 // The kTop midpoints nearest to (px, py), ascending; every lane gets the same list.
 __device__ void nearest_mids(const double *mid, int32_t M, double px, double py, int lane, Cand out[kTop]) {
     Cand t[kTop];
@@ -56,6 +58,11 @@ __device__ void nearest_mids(const double *mid, int32_t M, double px, double py,
                 }
         }
     }
+    merge_top(t, lane, out);
+}
+
+// The wave-wide kTop smallest of the lanes' sorted lists (every lane gets them).
+__device__ void merge_top(const Cand (&t)[kTop], int lane, Cand out[kTop]) {
     int head = 0;
 #pragma unroll
     for (int r = 0; r < kTop; ++r) {
@@ -90,10 +97,54 @@ struct Proj {
 // np.dot of two 2-vectors / np.linalg.norm of one (OpenBLAS pattern)
 __device__ __forceinline__ double bdot(double a0, double a1, double b0, double b1) { return fma(a1, b1, a0 * b0); }
 
+// nearest_mids through the grid: the midpoints of the 3x3 cells around the
+// query, merged as above; the result is final when every midpoint outside
+// those cells is provably farther than the 5th found one (distance to the
+// 3x3 block's edge, less a margin, above it), otherwise the full scan runs.
+// The same 5 (and order) as the full scan.
+__device__ void nearest_mids_grid(const TrackView &T, double px, double py, int lane, Cand out[kTop]) {
+    const int32_t M = T.n - 1;
+    const double fx = (px - T.gx0) / T.gh, fy = (py - T.gy0) / T.gh;
+    bool ok = T.cell_start && fx >= 1.0 && fy >= 1.0 && fx < (double)(T.gnx - 1) && fy < (double)(T.gny - 1);
+    if (ok) {
+        const int32_t ci = (int32_t)fx, cj = (int32_t)fy;
+        Cand t[kTop];
+#pragma unroll
+        for (int k = 0; k < kTop; ++k) t[k] = Cand{INFINITY, INT32_MAX};
+        for (int dj = -1; dj <= 1; ++dj)
+            for (int di = -1; di <= 1; ++di) {
+                const int32_t c = (cj + dj) * T.gnx + (ci + di);
+                for (int32_t q = T.cell_start[c] + lane; q < T.cell_start[c + 1]; q += 64) {
+                    const int32_t m = T.cell_items[q];
+                    const double dx = T.mid[2 * m] - px, dy = T.mid[2 * m + 1] - py;
+                    const double d2 = dx * dx + dy * dy;
+                    if (cand_less(d2, m, t[kTop - 1].d2, t[kTop - 1].i)) {
+                        Cand cc{d2, m};
+#pragma unroll
+                        for (int k = 0; k < kTop; ++k)
+                            if (cand_less(cc.d2, cc.i, t[k].d2, t[k].i)) {
+                                const Cand o = t[k];
+                                t[k] = cc;
+                                cc = o;
+                            }
+                    }
+                }
+            }
+        merge_top(t, lane, out);
+        // distance from the query to the 3x3 block's edge (a lower bound for
+        // every midpoint outside it), with a relative margin for rounding
+        const double bx0 = T.gx0 + (double)(ci - 1) * T.gh, by0 = T.gy0 + (double)(cj - 1) * T.gh;
+        const double lb = fmin(fmin(px - bx0, bx0 + 3.0 * T.gh - px), fmin(py - by0, by0 + 3.0 * T.gh - py));
+        const double lbm = lb * (1.0 - 1e-9) - 1e-9;
+        ok = out[kTop - 1].i != INT32_MAX && lbm > 0.0 && out[kTop - 1].d2 < lbm * lbm;
+    }
+    if (!ok) nearest_mids(T.mid, M, px, py, lane, out);  // off the grid or a sparse neighbourhood
+}
+
 // CenterlineProgress.project_xy (track_progress.py:58-97)
 __device__ Proj project_xy(const TrackView &T, double x, double y, int lane) {
     Cand c[kTop];
-    nearest_mids(T.mid, T.n - 1, x, y, lane, c);
+    nearest_mids_grid(T, x, y, lane, c);
     bool have = false;
     double bn = 0.0, bs = 0.0, bt = 0.0;
 #pragma unroll
