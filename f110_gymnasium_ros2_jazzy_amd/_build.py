@@ -13,7 +13,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libf110.so")
-SOURCES = ["f110_kernels.hip", "f110_opponent.hip", "f110_reward.hip", "f110_replay.hip", "f110_capi.cpp",
+SOURCES = ["f110_kernels.hip", "f110_opponent.hip", "f110_reward.hip", "f110_replay.hip", "f110_adam.hip",
+           "f110_capi.cpp",
            "f110_replay_capi.cpp"]
 HEADERS = ["f110_device.h", "f110_internal.h"]
 ARCH = os.environ.get("F110_OFFLOAD_ARCH", "gfx950")

@@ -62,7 +62,7 @@ EXPORTS = [
     "f110_host_window_ranges", "f110_track_create", "f110_track_destroy", "f110_track_arrays",
     "f110_default_reward_params", "f110_reward", "f110_replay_create", "f110_replay_destroy", "f110_replay_add",
     "f110_replay_sample", "f110_replay_update_priorities", "f110_replay_length", "f110_replay_arrays",
-    "f110_debug_wave_trace",
+    "f110_debug_wave_trace", "f110_adam_step",
 ]
 
 _lib = None
@@ -140,6 +140,8 @@ def load(build_if_missing: bool = True):
     L.f110_replay_length.argtypes = [_P, ctypes.POINTER(i64), ctypes.POINTER(i64), _P]
     L.f110_replay_arrays.argtypes = [_P] + [ctypes.POINTER(_P)] * 6
     L.f110_debug_wave_trace.argtypes = [_P, i32, _P, i64, ctypes.POINTER(i64), _P]
+    L.f110_adam_step.argtypes = [_P, _P, _P, _P, i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                 ctypes.c_double, _P, _P]
     for name in EXPORTS:
         if name not in ("f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config",
                         "f110_host_tables", "f110_host_window_ranges", "f110_track_arrays",

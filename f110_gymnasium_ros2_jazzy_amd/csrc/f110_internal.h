@@ -224,6 +224,17 @@ hipError_t launch_replay_update(const ReplayView &v, const int64_t *idx, const f
 hipError_t prepare_replay(int32_t max_batch);
 int replay_grid(int64_t capacity);
 
+// ---- flat Adam (f110_adam.hip) --------------------------------------------
+struct AdamArgs {
+    float *param, *exp_avg, *exp_avg_sq;
+    const float *grad;
+    int64_t n;
+    double lr, beta1, beta2, eps;
+    int64_t *step;     // device step counter
+    uint32_t *done;    // device: blocks finished (last one advances step)
+};
+hipError_t launch_adam(const AdamArgs &a, hipStream_t s);
+
 size_t step_lds_bytes(int A, int B);
 hipError_t prepare_env_step(size_t lds_bytes);
 hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev = nullptr);  // ev: 4 events or null

@@ -1,6 +1,7 @@
-// f110_replay_capi.cpp — host side of the prioritized replay buffer
-// (include/f110.h, "prioritized experience replay"): argument checks, the
-// device allocation at create, and the launches of f110_replay.hip.
+// f110_replay_capi.cpp — host side of the learner's device components
+// (include/f110.h, "prioritized experience replay" and "learner
+// optimizer"): argument checks, the device allocation at create, and the
+// launches of f110_replay.hip / f110_adam.hip.
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -177,5 +178,26 @@ extern "C" int f110_replay_arrays(f110_replay *rb, float **priority, float **obs
     if (reward) *reward = rb->v.reward;
     if (next_obs) *next_obs = rb->v.next_obs;
     if (done) *done = rb->v.done;
+    return F110_OK;
+}
+
+extern "C" int f110_adam_step(float *param, float *exp_avg, float *exp_avg_sq, const float *grad, int64_t n,
+                              double lr, double beta1, double beta2, double eps, void *state, void *stream) {
+    if (n < 0 || (n > 0 && (!param || !exp_avg || !exp_avg_sq || !grad || !state)))
+        return fail(F110_E_INVALID, "f110_adam_step: bad arguments");
+    AdamArgs a{};
+    a.param = param;
+    a.exp_avg = exp_avg;
+    a.exp_avg_sq = exp_avg_sq;
+    a.grad = grad;
+    a.n = n;
+    a.lr = lr;
+    a.beta1 = beta1;
+    a.beta2 = beta2;
+    a.eps = eps;
+    a.step = static_cast<int64_t *>(state);
+    a.done = reinterpret_cast<uint32_t *>(static_cast<int64_t *>(state) + 1);
+    hipError_t e = launch_adam(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(F110_E_HIP, std::string("f110_adam_step: ") + hipGetErrorString(e));
     return F110_OK;
 }

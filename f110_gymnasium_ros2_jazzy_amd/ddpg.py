@@ -13,11 +13,10 @@ envs on one GPU per rank:
   save_model / load_model      -> same checkpoint keys (weights_only loads)
 
 Data parallelism: one process per GPU (torch.distributed, backend "nccl" =
-RCCL over xGMI).  Every rank samples its own replay shard; the gradients of
-each network live in ONE flat fp32 buffer (the parameters' .grad are views
-into it), so a backward pass is followed by a single all-reduce of that
-bucket (critic: 156 289 floats, actor: 156 162 floats at obs_dim 1088), then
-the optimizer step.  The critic's all-reduce must finish before the actor's
+RCCL over xGMI).  Every rank samples its own replay shard; after a backward
+pass the gradients of a network are packed into ONE flat fp32 bucket and
+all-reduced in a single collective (critic: 156 289 floats, actor: 156 162
+floats at obs_dim 1088), then the optimizer step.  The critic's all-reduce must finish before the actor's
 forward (the actor loss reads the updated critic), so the two buckets are two
 collectives.  Ranks start from rank 0's weights and stay identical.
 """
@@ -87,28 +86,115 @@ class Critic(nn.Module):
 
 
 class GradBucket:
-    """The .grad of every parameter of a module as a view into one flat fp32
-    buffer: one all-reduce per backward (DDP's gradient-as-bucket-view)."""
+    """Gradient all-reduce of one network as ONE flat fp32 bucket.
 
-    def __init__(self, module: nn.Module, group=None):
+    Backward writes fresh .grad tensors (set_to_none semantics, no
+    accumulate kernels); with more than one rank they are gathered into the
+    flat bucket by one cat, all-reduced by RCCL (sum, then one scale) and the
+    parameters' .grad become views of the averaged bucket for the optimizer
+    step."""
+
+    def __init__(self, module: nn.Module, group=None, always_pack: bool = False):
+        self.always_pack = always_pack  # flat-Adam path: the optimizer reads self.flat
         self.params = [p for p in module.parameters()]
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.views = []
         off = 0
         for p in self.params:
-            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            self.views.append(self.flat[off:off + p.numel()].view_as(p))
             off += p.numel()
         self.group = group
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
 
     def zero(self):
-        self.flat.zero_()  # optimizer.zero_grad(set_to_none=True) + backward == 0 + g
+        for p in self.params:  # optimizer.zero_grad(set_to_none=True) (agent.py:318, :329)
+            p.grad = None
 
-    def all_reduce(self):
-        if self.world > 1:  # bucket mean over ranks (RCCL sum, then one scale)
+    # pack / reduce / unpack: in graph mode pack ends one captured phase,
+    # reduce runs eagerly (RCCL) and unpack starts the next captured phase
+    def pack(self):
+        if self.world > 1 or self.always_pack:
+            torch.cat([p.grad.reshape(-1) for p in self.params], out=self.flat)
+
+    def reduce(self):
+        if self.world > 1:
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
             self.flat.mul_(1.0 / self.world)
+
+    def unpack(self):
+        if self.world > 1 and not self.always_pack:
+            torch._foreach_copy_([p.grad for p in self.params], self.views)
+
+    def all_reduce(self):
+        self.pack()
+        self.reduce()
+        self.unpack()
+
+
+def flatten_params(module: nn.Module) -> torch.Tensor:
+    """Re-home a module's parameters into ONE flat fp32 buffer (the
+    nn.Parameters become views of it) and return the buffer."""
+    params = list(module.parameters())
+    flat = torch.cat([p.detach().reshape(-1) for p in params]).contiguous()
+    off = 0
+    for p in params:
+        p.data = flat[off:off + p.numel()].view_as(p)
+        off += p.numel()
+    return flat
+
+
+class FlatAdam:
+    """torch.optim.Adam (agent.py:187-188) over a flat parameter buffer: one
+    libf110 f110_adam_step launch per network and step (the step counter lives
+    on the device, so it can run inside a HIP graph).  state_dict() /
+    load_state_dict() use torch.optim.Adam's per-parameter layout, so
+    checkpoints stay interchangeable with the reference agent's."""
+
+    def __init__(self, module: nn.Module, flat: torch.Tensor, lr: float, betas=(0.9, 0.999), eps: float = 1e-8):
+        from . import _lib
+        self.L = _lib.load()
+        self._check = _lib.check
+        self.params = list(module.parameters())
+        self.flat = flat
+        self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
+        self.exp_avg = torch.zeros_like(flat)
+        self.exp_avg_sq = torch.zeros_like(flat)
+        self.state = torch.zeros(2, dtype=torch.int64, device=flat.device)  # [step, scratch]
+
+    def step(self, flat_grad: torch.Tensor):
+        import ctypes
+        s = torch.cuda.current_stream(self.flat.device).cuda_stream
+        vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        self._check(self.L.f110_adam_step(vp(self.flat), vp(self.exp_avg), vp(self.exp_avg_sq), vp(flat_grad),
+                                          self.flat.numel(), self.lr, self.betas[0], self.betas[1], self.eps,
+                                          vp(self.state), ctypes.c_void_p(s)), "f110_adam_step")
+
+    def _views(self, flat):
+        out, off = [], 0
+        for p in self.params:
+            out.append(flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        return out
+
+    def state_dict(self):
+        step = float(self.state[0].item())
+        st = {i: {"step": torch.tensor(step), "exp_avg": a.detach().clone(), "exp_avg_sq": b.detach().clone()}
+              for i, (a, b) in enumerate(zip(self._views(self.exp_avg), self._views(self.exp_avg_sq)))}
+        return {"state": st, "param_groups": [{"lr": self.lr, "betas": self.betas, "eps": self.eps,
+                                               "weight_decay": 0, "amsgrad": False,
+                                               "params": list(range(len(self.params)))}]}
+
+    def load_state_dict(self, sd):
+        with torch.no_grad():
+            for i, (a, b) in enumerate(zip(self._views(self.exp_avg), self._views(self.exp_avg_sq))):
+                if i in sd["state"]:
+                    a.copy_(sd["state"][i]["exp_avg"])
+                    b.copy_(sd["state"][i]["exp_avg_sq"])
+            steps = [float(v["step"]) for v in sd["state"].values()]
+            self.state[0] = int(max(steps)) if steps else 0
+        self.lr = float(sd["param_groups"][0].get("lr", self.lr))
 
 
 class DDPGLearner:
@@ -147,17 +233,30 @@ class DDPGLearner:
             for net in (self.actor, self.critic, self.actor_target, self.critic_target):
                 for t in list(net.parameters()) + list(net.buffers()):
                     dist.broadcast(t.data, src=0, group=self.group)
-        self.actor_grads = GradBucket(self.actor, self.group)
-        self.critic_grads = GradBucket(self.critic, self.group)
-        # HIP graphs (replay with graphs=True) need the device-side step counters
+        # On the GPU each network is one flat buffer (parameters are views):
+        # its gradient bucket feeds one flat Adam launch and the soft target
+        # update is one lerp over the buffers.  The CPU path keeps
+        # torch.optim.Adam (the reference's own optimizer, for parity tests).
+        self.flat = self.device.type == "cuda"
+        if self.flat:
+            self._flat = {n: flatten_params(net) for n, net in (("actor", self.actor), ("critic", self.critic),
+                                                                 ("actor_target", self.actor_target),
+                                                                 ("critic_target", self.critic_target))}
+        self.actor_grads = GradBucket(self.actor, self.group, always_pack=self.flat)
+        self.critic_grads = GradBucket(self.critic, self.group, always_pack=self.flat)
         self.graphs = bool(graphs) and self.device.type == "cuda" and replay is not None
-        fused = {"fused": True, "capturable": self.graphs} if self.device.type == "cuda" else {}
         self._graphs, self._graph_out, self._eager_left = None, None, 3
         self._side = torch.cuda.Stream(self.device) if self.graphs else None
-        self.actor_optim = torch.optim.Adam(self.actor.parameters(), lr=actor_lr, **fused)
-        self.critic_optim = torch.optim.Adam(self.critic.parameters(), lr=critic_lr, **fused)
-        self._online = list(self.actor.parameters()) + list(self.critic.parameters())
-        self._target = list(self.actor_target.parameters()) + list(self.critic_target.parameters())
+        if self.flat:
+            self.actor_optim = FlatAdam(self.actor, self._flat["actor"], lr=actor_lr)
+            self.critic_optim = FlatAdam(self.critic, self._flat["critic"], lr=critic_lr)
+            self._online = [self._flat["actor"], self._flat["critic"]]
+            self._target = [self._flat["actor_target"], self._flat["critic_target"]]
+        else:
+            self.actor_optim = torch.optim.Adam(self.actor.parameters(), lr=actor_lr)
+            self.critic_optim = torch.optim.Adam(self.critic.parameters(), lr=critic_lr)
+            self._online = list(self.actor.parameters()) + list(self.critic.parameters())
+            self._target = list(self.actor_target.parameters()) + list(self.critic_target.parameters())
         self.memory = None
         if replay == "device":
             from .replay import DeviceReplayBuffer
@@ -209,9 +308,15 @@ class DDPGLearner:
         critic_loss.backward()
         return critic_loss.detach(), td.detach()
 
+    def _optim_step(self, optim, bucket):
+        if self.flat:
+            optim.step(bucket.flat)
+        else:
+            optim.step()
+
     def _phase_actor(self, states):
         """agent.py:321-331: critic step, actor loss through the frozen critic."""
-        self.critic_optim.step()
+        self._optim_step(self.critic_optim, self.critic_grads)
         for p in self.critic.parameters():
             p.requires_grad_(False)
         actor_loss = -self.critic(states, self.actor(states)).mean()
@@ -223,7 +328,7 @@ class DDPGLearner:
 
     def _phase_finish(self):
         """agent.py:331, :340-341: actor step, soft target update."""
-        self.actor_optim.step()
+        self._optim_step(self.actor_optim, self.actor_grads)
         with torch.no_grad():
             torch._foreach_lerp_(self._target, self._online, self.tau)
 
@@ -272,11 +377,15 @@ class DDPGLearner:
             idxs, b, w = m.sample(beta=self.beta)
             out["critic_loss"], out["td"] = self._phase_critic(b["states"], b["actions"], b["rewards"],
                                                                b["next_states"], b["dones"], w)
+            self.critic_grads.pack()
 
         def b_():
+            self.critic_grads.unpack()
             out["actor_loss"] = self._phase_actor(m.batch["states"])
+            self.actor_grads.pack()
 
         def c():
+            self.actor_grads.unpack()
             self._phase_finish()
             m.update_priorities(m.idx, out["td"], td_errors=True, add_eps=self.priority_epsilon)
         return (a, b_, c), out
@@ -290,9 +399,9 @@ class DDPGLearner:
                 side.wait_stream(cur)
                 with torch.cuda.stream(side):
                     phases[0]()
-                    self.critic_grads.all_reduce()
+                    self.critic_grads.reduce()
                     phases[1]()
-                    self.actor_grads.all_reduce()
+                    self.actor_grads.reduce()
                     phases[2]()
                 cur.wait_stream(side)
                 self._eager_left -= 1
@@ -306,9 +415,9 @@ class DDPGLearner:
             self._graphs, self._graph_out = graphs, out
         g = self._graphs
         g[0].replay()
-        self.critic_grads.all_reduce()
+        self.critic_grads.reduce()  # eager RCCL between the captured phases
         g[1].replay()
-        self.actor_grads.all_reduce()
+        self.actor_grads.reduce()
         g[2].replay()
         self.global_step += 1
         return self._graph_out
@@ -360,7 +469,4 @@ class DDPGLearner:
         self.gamma = float(ckpt.get("gamma", self.gamma))
         self.tau = float(ckpt.get("tau", self.tau))
         self.global_step = int(ckpt.get("global_step", 0))
-        # the grads must stay views of the all-reduce buckets
-        self.actor_grads = GradBucket(self.actor, self.group)
-        self.critic_grads = GradBucket(self.critic, self.group)
         return True

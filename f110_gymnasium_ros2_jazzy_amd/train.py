@@ -51,7 +51,8 @@ class VectorTrainer:
         self.reward_fn = BatchedCenterlineReward(self.N, dt=0.01, progress=self.track, device=self.device,
                                                  **REWARD_KW)
         self.env = F110VectorEnv(self.N, map=map_name, num_agents=2, seed=seed, device=self.device,
-                                 env_offset=env_offset, opponent="gap_follow", reward_fn=self.reward_fn)
+                                 env_offset=env_offset, opponent="gap_follow", reward_fn=self.reward_fn,
+                                 infos="minimal")
         self.agent = DDPGLearner(obs_dim=self.env.single_observation_space.shape[0], act_dim=2,
                                  action_low=ACTION_LOW, action_high=ACTION_HIGH, gamma=0.99, tau=0.005,
                                  actor_lr=1e-4, critic_lr=1e-3, memory_size=memory_size, batch_size=batch_size,

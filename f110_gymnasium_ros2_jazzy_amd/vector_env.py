@@ -44,7 +44,7 @@ class F110VectorEnv:
                  params: dict | None = None, seed: int = 42, timestep: float = 0.01, device=0,
                  spawn_poses: np.ndarray | None = None, noise_std: float = 0.01, env_offset: int = 0,
                  ego_idx: int = 0, as_numpy: bool = False, autoreset: bool = True, opponent: str | None = None,
-                 opponent_idx: int = 1, reward_fn=None, **kwargs):
+                 opponent_idx: int = 1, reward_fn=None, infos: str = "full", **kwargs):
         self.num_envs = int(num_envs)
         self.num_agents = int(num_agents)
         self.params = dict(params or DEFAULT_PARAMS)
@@ -72,6 +72,11 @@ class F110VectorEnv:
         # reward_fn: a BatchedCenterlineReward (reward.py) evaluated on the device
         # from every step's observations, as train_ddpg.py:176 does per env
         self.reward_fn = reward_fn
+        # infos="minimal": only "reset" (+ "opponent_actions"), no per-step copies
+        # of the scans and poses (the batched trainer reads nothing else)
+        if infos not in ("full", "minimal"):
+            raise ValueError("infos must be 'full' or 'minimal'")
+        self.infos_mode = infos
         if reward_fn is not None and reward_fn.n_envs != self.num_envs:
             raise ValueError("reward_fn must be built for num_envs envs")
         if opponent is not None:
@@ -90,6 +95,11 @@ class F110VectorEnv:
 
     # ------------------------------------------------------------------
     def _infos(self, out):
+        if self.infos_mode == "minimal":
+            infos = {"reset": out.was_reset.bool()}
+            if self.opponent is not None:
+                infos["opponent_actions"] = self._act[:, self.opponent_idx]
+            return {k: v.cpu().numpy() for k, v in infos.items()} if self.as_numpy else infos
         st = self.sim.agent_states()  # [E, A, 7]
         infos = {
             "poses_x": st[..., 0].float(), "poses_y": st[..., 1].float(), "poses_theta": st[..., 4].float(),

@@ -380,6 +380,16 @@ F110_API int f110_replay_length(f110_replay *rb, int64_t *length, int64_t *next_
 F110_API int f110_replay_arrays(f110_replay *rb, float **priority, float **obs, float **act, float **reward,
                                 float **next_obs, float **done);
 
+/* ---- learner optimizer ----------------------------------------------------------
+ * One torch.optim.Adam step (agent.py:187-188: Adam(params, lr), betas
+ * (0.9, 0.999), eps 1e-8, no weight decay, no amsgrad) over a network whose
+ * parameters, gradients and moments are flat float32 device buffers of n
+ * elements.  state: device int64 step counter followed by a uint32 scratch
+ * word (both zero initially); the step is advanced on the device, so the
+ * call can be captured in a HIP graph.  Async on stream. */
+F110_API int f110_adam_step(float *param, float *exp_avg, float *exp_avg_sq, const float *grad, int64_t n, double lr,
+                            double beta1, double beta2, double eps, void *state, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -205,3 +205,30 @@ def test_learner_graphs_match_eager(gpu):
     for a, b in zip(runs[0][1], runs[1][1]):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(runs[0][2], runs[1][2], rtol=1e-3, atol=1e-6)
+
+
+def test_flat_adam_matches_torch_adam(gpu):
+    """f110_adam_step over a flat buffer == torch.optim.Adam's single-tensor
+    update (agent.py:187-188) on CPU, five steps, float32 tolerance."""
+    import ctypes
+    from f110_gymnasium_ros2_jazzy_amd import _lib
+    L = _lib.load()
+    g = torch.Generator().manual_seed(0)
+    p0 = torch.randn(5000, generator=g)
+    grads = [torch.randn(5000, generator=g) * 10 ** (k - 2) for k in range(5)]
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([ref], lr=1e-3)
+    dev = p0.cuda()
+    m, v = torch.zeros_like(dev), torch.zeros_like(dev)
+    state = torch.zeros(2, dtype=torch.int64, device="cuda")
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    for gr in grads:
+        ref.grad = gr.clone()
+        opt.step()
+        gd = gr.cuda()
+        _lib.check(L.f110_adam_step(vp(dev), vp(m), vp(v), vp(gd), dev.numel(), 1e-3, 0.9, 0.999, 1e-8, vp(state),
+                                    ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "adam")
+    torch.cuda.synchronize()
+    assert int(state[0]) == 5
+    torch.testing.assert_close(dev.cpu(), ref.detach(), rtol=2e-6, atol=1e-7)
+    torch.testing.assert_close(m.cpu(), opt.state[ref]["exp_avg"], rtol=1e-5, atol=1e-7)  # CPU lerp may fuse (1 ulp)
