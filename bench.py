@@ -100,6 +100,9 @@ def bench_ddpg(args):
         ph["env_step_reward_ms"] += ev[0].elapsed_time(ev[1]) / KP
         ph["replay_add_ms"] += ev[1].elapsed_time(ev[2]) / KP
         ph["learner_update_ms"] += ev[2].elapsed_time(ev[3]) / KP
+    # data-parallel consistency: every rank must hold the same weights
+    wsum = float(sum(float(p.double().sum()) for p in tr.agent.actor.parameters()))
+    in_sync = D.max_over_ranks(wsum) == -D.max_over_ranks(-wsum)
     result = {
         "metric": "env-steps/sec, end-to-end DDPG (BASELINE config 5)", "value": total / elapsed,
         "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": W, "ms_per_step": elapsed / K * 1e3,
@@ -112,7 +115,7 @@ def bench_ddpg(args):
                    "parallelism": f"env-shard x{world}, DDPG data-parallel (RCCL all-reduce of grads)"},
         "phases_ms": ph,
         "learner": {"critic_loss": float(tr.last["critic_loss"]), "actor_loss": float(tr.last["actor_loss"]),
-                    "updates": tr.agent.global_step},
+                    "updates": tr.agent.global_step, "ranks_in_sync": in_sync},
     }
     if rank == 0:
         print(json.dumps(result), flush=True)
