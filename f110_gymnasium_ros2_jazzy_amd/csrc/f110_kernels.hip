@@ -269,6 +269,60 @@ __device__ __forceinline__ const RayArgs *kernarg_rays() {
 #endif
 }
 
+// One lane's ray of k_rays_tiled: beam index, trace_ray's loop
+// (laser_models.py:106-146) with the given EDT lookup, clamp, noise, TTC
+// flag, outputs.  Returns the lookups made.
+template <bool HANDOFF, class Lookup>
+__device__ __forceinline__ uint32_t trace_lane(const RayArgs &a, int g, int b, int e, int64_t r, Lookup lookup) {
+    const int B = a.B;
+    double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
+    int ti = (int)t;  // int(theta_index), laser_models.py:124
+    if (ti >= a.theta_dis) ti = 0;
+    const double c = a.cosines[ti], s = a.sines[ti];
+    double x = a.ray0[g], y = a.ray0[a.EA + g];
+    double d = a.ray0[2 * a.EA + g];  // :129
+    double tot = d;                   // :130
+    // the TTC operands are loaded before the loop, which hides their
+    // latency (the epilogue would otherwise wait on them)
+    const double v = a.vel[g], bcos = a.beam_cos[b], side = a.side[b];
+    // the ray's scan noise does not depend on the trace: drawn (or loaded)
+    // here, it overlaps the set-up loads above
+    double noise = 0.0;
+    {
+        const RayArgs &K = *kernarg_rays();
+        if (K.noise_ext)
+            noise = K.noise_ext[(size_t)e * B + b];
+        else if (K.noise_std > 0.0)
+            noise = K.noise_std * (double)beam_normal(K.seed, (uint64_t)(K.env_offset + e), K.noise_step[e], b);
+    }
+    uint32_t k = 1;
+    const double eps = a.eps, mr = a.max_range;
+    while (d > eps && tot <= mr) {  // :133
+        x += d * c;                 // :135
+        y += d * s;                 // :136
+        d = lookup(x, y);
+        tot += d;                   // :141
+        ++k;
+    }
+    // Epilogue fields are read through the kernarg pointer HERE, after the
+    // loop: argument loads would otherwise sit at kernel entry and stay live
+    // in SGPRs across the loop (84 instead of 68 SGPRs: 7 instead of 8
+    // blocks per CU).
+    const RayArgs &K = *kernarg_rays();
+    double range = tot > mr ? mr : tot;  // :143-144
+    if (K.noise_ext || K.noise_std > 0.0) range += noise;  // noise after the clamp (see store_ray)
+    // state[3] after update_pose; check_ttc_jit on the noisy scan, before the
+    // agent ray_cast (base_classes.py:597-599)
+    if (v != 0.0 && ttc_fires(range, side, v * bcos, K.ttc_thresh)) K.ttc_hit[g] = 1;
+    // outputs straight from the ray; with other cars in the env (HANDOFF)
+    // k_post_multi patches the beams its ray_cast shortens
+    if (K.obs && g == e * a.A) K.obs[(size_t)e * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
+    if (K.scans_f32) K.scans_f32[r] = (float)range;
+    if (K.scans_f64) K.scans_f64[r] = range;
+    if (HANDOFF) K.scan[r] = range;
+    return k;
+}
+
 // ------------------------------------------------------------------------
 // k_rays_tiled: one thread per ray on the 4x4-tiled EDT, with the rotation
 // compiled out for axis-aligned maps.  Same results as k_rays, bit for bit.
@@ -334,54 +388,8 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
     uint32_t n = 0;
     if (live) {
         const int e = g / a.A;
-        if (!MASK || a.reset_mask[e]) {
-            double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
-            int ti = (int)t;  // int(theta_index), laser_models.py:124
-            if (ti >= a.theta_dis) ti = 0;
-            const double c = a.cosines[ti], s = a.sines[ti];
-            double x = a.ray0[g], y = a.ray0[a.EA + g];
-            double d = a.ray0[2 * a.EA + g];  // :129
-            double tot = d;                   // :130
-            // the TTC operands are loaded before the loop, which hides their
-            // latency (the epilogue would otherwise wait on them)
-            const double v = a.vel[g], bcos = a.beam_cos[b], side = a.side[b];
-            // the ray's scan noise does not depend on the trace: drawn (or
-            // loaded) here, it overlaps the set-up loads above
-            double noise = 0.0;
-            {
-                const RayArgs &K = *kernarg_rays();
-                if (K.noise_ext)
-                    noise = K.noise_ext[(size_t)e * B + b];
-                else if (K.noise_std > 0.0)
-                    noise = K.noise_std * (double)beam_normal(K.seed, (uint64_t)(K.env_offset + e), K.noise_step[e], b);
-            }
-            uint32_t k = 1;
-            const double eps = a.eps, mr = a.max_range;
-            while (d > eps && tot <= mr) {  // :133
-                x += d * c;                 // :135
-                y += d * s;                 // :136
-                d = tiled_lookup<ROT>(a.m, x, y);
-                tot += d;                   // :141
-                ++k;
-            }
-            n = k;
-            // Epilogue fields are read through the kernarg pointer HERE, after
-            // the loop: argument loads would otherwise sit at kernel entry and
-            // stay live in SGPRs across the loop (84 instead of 68 SGPRs:
-            // 7 instead of 8 blocks per CU).
-            const RayArgs &K = *kernarg_rays();
-            double range = tot > mr ? mr : tot;  // :143-144
-            if (K.noise_ext || K.noise_std > 0.0) range += noise;  // noise after the clamp (see store_ray)
-            // state[3] after update_pose; check_ttc_jit on the noisy scan,
-            // before the agent ray_cast (base_classes.py:597-599)
-            if (v != 0.0 && ttc_fires(range, side, v * bcos, K.ttc_thresh)) K.ttc_hit[g] = 1;
-            // outputs straight from the ray; with other cars in the env
-            // (HANDOFF) k_post_multi patches the beams its ray_cast shortens
-            if (K.obs && g == e * a.A) K.obs[(size_t)e * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
-            if (K.scans_f32) K.scans_f32[r] = (float)range;
-            if (K.scans_f64) K.scans_f64[r] = range;
-            if (HANDOFF) K.scan[r] = range;
-        }
+        if (!MASK || a.reset_mask[e])
+            n = trace_lane<HANDOFF>(a, g, b, e, r, [&](double x, double y) { return tiled_lookup<ROT>(a.m, x, y); });
     }
     count_rays(kernarg_rays()->ctr, n);
     if (CH) {  // this wave's cost, the next step's heavy-first prediction
@@ -405,6 +413,7 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
         o[3] = ((uint64_t)(CH ? (int)blockIdx.x / a.G4 : 0) << 32) | (uint32_t)g;
     }
 }
+
 
 // F110Env.step's time + _check_done (f110_env.py:404-406, :310-352) and the
 // env's autoreset / episode / noise bookkeeping, for env e.  stl: post-TTC
