@@ -189,6 +189,37 @@ def corridor_poses(s, rng):
     return poses
 
 
+ROT_YAW = 0.35
+
+
+def gen_scans_rotated(rng):
+    """Spielberg with a map-origin yaw of 0.35 rad (every bundled map has yaw
+    0): xy_2_rc's rotation (laser_models.py:75-76) on the reference's own
+    ScanSimulator2D, origin fields overridden after set_map."""
+    s = scan_sim("Spielberg_map")
+    s.orig_c, s.orig_s = np.cos(ROT_YAW), np.sin(ROT_YAW)
+    free = np.argwhere(s.map_img > 0)
+    pick = free[rng.choice(len(free), 20, replace=False)]
+    poses = []
+    for r, c in pick:
+        xr = (c + rng.uniform(0.05, 0.95)) * s.map_resolution
+        yr = (r + rng.uniform(0.05, 0.95)) * s.map_resolution
+        xt = xr * s.orig_c - yr * s.orig_s
+        yt = xr * s.orig_s + yr * s.orig_c
+        poses.append([xt + s.orig_x, yt + s.orig_y, rng.uniform(-np.pi, np.pi)])
+    poses += [[s.orig_x, s.orig_y, 0.2], [-300.0, 10.0, 0.0], [s.orig_x + 1.0, s.orig_y - 0.5, 2.5]]
+    scans, counts, rcs = [], [], []
+    for p in poses:
+        with RayProbe() as pr:
+            sc = s.scan(np.asarray(p, dtype=np.float64), None)
+        scans.append(sc)
+        counts.append(pr.counts)
+        rcs.append(pr.lasts)
+    save("scans_Spielberg_rot.npz", poses=np.asarray(poses, np.float64), scans=np.asarray(scans),
+         lookups=np.asarray(counts, np.int32), hit_rc=np.asarray(rcs, np.int32),
+         origin=np.array([s.orig_x, s.orig_y, ROT_YAW]))
+
+
 # -------------------------------------------------------------- dynamics ----
 def gen_dynamics(rng):
     P = [DEFAULT_PARAMS[k] for k in PKEYS]
@@ -686,6 +717,7 @@ def main():
     gen_gap_follow()
     gen_env_gapfollow(cl)
     gen_reward(cl)
+    gen_scans_rotated(np.random.default_rng(35))
 
 
 if __name__ == "__main__":
@@ -694,6 +726,7 @@ if __name__ == "__main__":
         for name in sys.argv[1:]:
             {"env_noise": lambda c: gen_env_noise(c), "env_params": lambda c: gen_env_params(c),
              "gap_follow": lambda c: gen_gap_follow(), "env_gapfollow": gen_env_gapfollow,
-             "reward": gen_reward}[name](_cl)
+             "reward": gen_reward,
+             "scans_rot": lambda c: gen_scans_rotated(np.random.default_rng(35))}[name](_cl)
     else:
         main()

@@ -53,6 +53,18 @@ def test_scans(oracle_scanners, m):
     assert np.array_equal(rc, g["hit_rc"])
 
 
+def test_scans_rotated_origin(oracle_mod):
+    """Map-origin yaw != 0 (xy_2_rc's rotation, laser_models.py:75-76): the
+    reference's ScanSimulator2D with yaw 0.35 on Spielberg."""
+    g = golden("scans_Spielberg_rot.npz")
+    free, res, _ = oracle_mod.load_map(os.path.join(MAPS, "Spielberg_map.yaml"))
+    sc = oracle_mod.OracleScanner(free, res, g["origin"])
+    out, look, rc = sc.scan(g["poses"], with_probe=True)
+    assert np.array_equal(out, g["scans"])
+    assert np.array_equal(look, g["lookups"])
+    assert np.array_equal(rc, g["hit_rc"])
+
+
 def test_dynamics(oracle_mod):
     d = golden("dynamics.npz")
     P = oracle_mod.make_params(dict(zip(PKEYS, d["params"])))
