@@ -136,30 +136,55 @@ __device__ __forceinline__ void reset_next_heavy(const StepArgs &a) {
 __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
     const int g = blockIdx.x * 64 + threadIdx.x;
     const int EA = a.E * a.A;
-    if (a.heavy_build) build_heavy_list(a, g, g < EA);  // block-uniform branch, before any return
-    if (g >= EA) return;
+    const bool valid = g < EA;
     const int A = a.A;
-    const int e = g / A;
+    const int e = valid ? g / A : 0;
     const int ag = g - e * A;
+    // Every input of the car is loaded first, before the heavy-list atomic
+    // and before anything waits: one memory round trip for the whole prologue.
+    double s[7];
+    double b0 = 0.0, b1 = 0.0, raw_steer = 0.0, vel = 0.0;
+    int cnt = 0, gate = 0;
+    uint32_t episode = 0;
+    uint64_t nstep = 0;
+    if (valid) {
+        if (ag == 0) nstep = a.nstep[e];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) s[k] = a.st[(size_t)k * EA + g];
+        b0 = a.sb[g];
+        b1 = a.sb[EA + g];
+        cnt = a.scnt[g];
+        if (a.mode == 1) {
+            gate = a.reset_mask ? a.reset_mask[e] : 1;
+        } else {
+            gate = a.autoreset ? a.pending[e] : 0;
+            episode = a.episode[e];
+            if (a.actions_f64) {
+                raw_steer = a.actions_f64[(size_t)g * 2];
+                vel = a.actions_f64[(size_t)g * 2 + 1];
+            } else {
+                raw_steer = (double)a.actions[(size_t)g * 2];
+                vel = (double)a.actions[(size_t)g * 2 + 1];
+            }
+        }
+    }
+    if (a.heavy_build) build_heavy_list(a, g, valid);  // block-uniform branch, before any return
+    if (!valid) return;
     const uint64_t genv = (uint64_t)(a.env_offset + e);
     int do_reset;
     if (a.mode == 1) {
-        if (a.reset_mask && !a.reset_mask[e]) return;
+        if (!gate) return;
         do_reset = 1;
     } else {
-        do_reset = (a.autoreset && a.pending[e]) ? 1 : 0;
+        do_reset = gate ? 1 : 0;
     }
-    double s[7];
-    double b0, b1;
-    int cnt;
-    double raw_steer, vel;
     if (do_reset) {
         // RaceCar.reset (base_classes.py:183-204), then F110Env.reset's zero-action step (f110_env.py:457)
         const double *pz;
         if (a.mode == 1) {
             pz = a.reset_poses + (size_t)g * 3;
         } else {
-            uint32_t k = spawn_draw(a.seed, genv, a.episode[e]) % (uint32_t)a.n_spawn;
+            uint32_t k = spawn_draw(a.seed, genv, episode) % (uint32_t)a.n_spawn;
             pz = a.spawn + ((size_t)k * A + ag) * 3;
         }
 #pragma unroll
@@ -182,19 +207,6 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
         a.near_start[g] = 1;
         a.lap_times[g] = 0.0f;
         a.lap_counts[g] = 0.0f;
-    } else {
-#pragma unroll
-        for (int k = 0; k < 7; ++k) s[k] = a.st[(size_t)k * EA + g];
-        b0 = a.sb[g];
-        b1 = a.sb[EA + g];
-        cnt = a.scnt[g];
-        if (a.actions_f64) {
-            raw_steer = a.actions_f64[(size_t)g * 2];
-            vel = a.actions_f64[(size_t)g * 2 + 1];
-        } else {
-            raw_steer = (double)a.actions[(size_t)g * 2];
-            vel = (double)a.actions[(size_t)g * 2 + 1];
-        }
     }
     update_pose(s, b0, b1, cnt, raw_steer, vel, a.pa[ag], a.dt, a.integrator);  // RaceCar.params (per agent)
 #pragma unroll
@@ -217,7 +229,7 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
     a.ttc_hit[g] = 0;
     if (ag == 0) {
         a.reset_flag[e] = (uint8_t)do_reset;
-        a.noise_step[e] = do_reset ? 0ull : a.nstep[e];
+        a.noise_step[e] = do_reset ? 0ull : nstep;
     }
 }
 
@@ -416,22 +428,53 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
 
 
 // F110Env.step's time + _check_done (f110_env.py:404-406, :310-352) and the
-// env's autoreset / episode / noise bookkeeping, for env e.  stl: post-TTC
-// state rows of its A agents (x at [i*stride], y at [i*stride + 1]); col:
-// collision flags.
+// env's autoreset / episode / noise bookkeeping, for env e.  Split in two so
+// the kernels issue every load of it at their start, together with their own
+// loads: one memory round trip instead of a chain of dependent ones (the
+// stores in between would otherwise keep the compiler from hoisting them).
+struct EpiCar {  // per car: lap bookkeeping
+    double sx, sy;
+    int32_t tg;
+    float lt;
+    uint32_t ns;
+};
+struct EpiEnv {  // per env
+    double tprev, ct, st;
+    uint64_t nstep;
+    uint32_t episode;
+};
+
+__device__ __forceinline__ void epilogue_load_car(const StepArgs &a, int g, EpiCar &c) {
+    const int EA = a.E * a.A;
+    c.sx = a.start[g];
+    c.sy = a.start[EA + g];
+    c.tg = a.toggles[g];
+    c.ns = a.near_start[g];
+    c.lt = a.lap_times[g];
+}
+
+__device__ __forceinline__ void epilogue_load_env(const StepArgs &a, int e, EpiEnv &v) {
+    v.tprev = a.sim_time[e];
+    v.ct = a.start_rot[e];  // cos(-th), sin(-th) of the ego start yaw
+    v.st = a.start_rot[a.E + e];
+    v.nstep = a.noise_step[e];  // written by this step's k_agents
+    v.episode = a.mode == 0 ? a.episode[e] : 0u;
+}
+
+// stl: post-TTC state rows of its A agents (x at [i*stride], y at
+// [i*stride + 1]); col: collision flags; cars / env: the prefetched inputs.
 __device__ void env_epilogue(const StepArgs &a, int e, const double *stl, int stride, const int32_t *col,
-                             int do_reset) {
+                             int do_reset, const EpiEnv &v, const EpiCar *cars) {
     const int A = a.A;
-    const int EA = a.E * A;
-    double tnow = (do_reset ? 0.0 : a.sim_time[e]) + a.dt;
+    const double tnow = (do_reset ? 0.0 : v.tprev) + a.dt;
     a.sim_time[e] = tnow;
-    const double ct = a.start_rot[e], st = a.start_rot[a.E + e];  // cos(-th), sin(-th) of the ego start yaw
-    const double r00 = ct, r01 = -st, r10 = st, r11 = ct;
+    const double r00 = v.ct, r01 = -v.st, r10 = v.st, r11 = v.ct;
     bool all4 = true;
     for (int i = 0; i < A; ++i) {
         const int g = e * A + i;
-        double px = stl[i * stride] - a.start[g];
-        double py = stl[i * stride + 1] - a.start[EA + g];
+        const EpiCar &c = cars[i];
+        double px = stl[i * stride] - c.sx;
+        double py = stl[i * stride + 1] - c.sy;
         double dx = r00 * px + r01 * py;
         double dy = r10 * px + r11 * py;
         double ty;
@@ -439,14 +482,14 @@ __device__ void env_epilogue(const StepArgs &a, int e, const double *stl, int st
         else if (dy < -2.0) ty = -2.0 - dy;
         else ty = 0.0;
         bool close = dx * dx + ty * ty <= 0.1;
-        int tg = a.toggles[g];
-        uint8_t ns = a.near_start[g];
+        int tg = c.tg;
+        uint32_t ns = c.ns;
         if (close && !ns) { ns = 1; ++tg; }
         else if (!close && ns) { ns = 0; ++tg; }
         a.toggles[g] = tg;
-        a.near_start[g] = ns;
+        a.near_start[g] = (uint8_t)ns;
         float lc = (float)(tg / 2);
-        float lt = tg < 4 ? (float)tnow : a.lap_times[g];
+        float lt = tg < 4 ? (float)tnow : c.lt;
         a.lap_counts[g] = lc;
         a.lap_times[g] = lt;
         if (a.out.lap_counts) a.out.lap_counts[g] = lc;
@@ -458,8 +501,8 @@ __device__ void env_epilogue(const StepArgs &a, int e, const double *stl, int st
     if (a.out.was_reset) a.out.was_reset[e] = (uint8_t)do_reset;
     if (a.out.sim_time) a.out.sim_time[e] = tnow;
     a.pending[e] = (a.autoreset && term) ? 1 : 0;
-    if (do_reset && a.mode == 0) a.episode[e] += 1;
-    a.nstep[e] = a.noise_step[e] + 1;
+    if (do_reset && a.mode == 0) a.episode[e] = v.episode + 1;
+    a.nstep[e] = v.nstep + 1;
 }
 
 // ------------------------------------------------------------------------
@@ -472,7 +515,9 @@ struct PostShared {
     int32_t col[kMaxAgents];     // collisions (GJK | TTC)
     double wcen[kMaxAgents * (kMaxAgents - 1)], whalf[kMaxAgents * (kMaxAgents - 1)];  // box_beam_window
     int32_t blo[kMaxAgents * kMaxAgents], bhi[kMaxAgents * kMaxAgents];
-    int32_t do_reset, pad_[3];
+    EpiCar epi[kMaxAgents];      // env_epilogue inputs, prefetched at kernel start
+    EpiEnv epe;
+    int32_t do_reset, pad_[1];
 };
 static_assert(sizeof(PostShared) % 16 == 0, "LDS carve alignment");
 
@@ -500,11 +545,15 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
         sh.pose0[tid][0] = sh.stl[tid][0];
         sh.pose0[tid][1] = sh.stl[tid][1];
         sh.pose0[tid][2] = sh.stl[tid][4];
+        epilogue_load_car(a, g, sh.epi[tid]);
         get_vertices(sh.stl[tid][0], sh.stl[tid][1], sh.stl[tid][4], a.p.length, a.p.width, sh.verts[tid]);
         sh.hit[tid] = 0;
         sh.col[tid] = 0;
     }
-    if (tid == 0) sh.do_reset = a.reset_flag[e];
+    if (tid == 0) {
+        sh.do_reset = a.reset_flag[e];
+        epilogue_load_env(a, e, sh.epe);
+    }
     __syncthreads();
 
     // TTC against the environment (check_ttc_jit, laser_models.py:188-217) on the noisy scan
@@ -598,7 +647,7 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
         for (int id = tid; id < A * B; id += kBlock) o[id] = scan[id];
     }
     if (a.out.collisions && tid < A) a.out.collisions[(size_t)e * A + tid] = (uint8_t)sh.col[tid];
-    if (tid == 0) env_epilogue(a, e, &sh.stl[0][0], 7, sh.col, sh.do_reset);
+    if (tid == 0) env_epilogue(a, e, &sh.stl[0][0], 7, sh.col, sh.do_reset, sh.epe, sh.epi);
 }
 
 // k_post_single: single-agent envs after the FUSED ray kernel, one thread per
@@ -610,9 +659,15 @@ __global__ void __launch_bounds__(64) k_post_single(StepArgs a) {
     if (e >= a.E) return;
     if (a.mode == 1 && a.reset_mask && !a.reset_mask[e]) return;
     const int EA = a.E;  // A == 1: car g == env e
+    // every input first (one memory round trip), then the stores
     double stl[2] = {a.st[e], a.st[EA + e]};
     double yaw = a.st[(size_t)4 * EA + e];
     int32_t col = a.ttc_hit[e];
+    const int do_reset = a.reset_flag[e];
+    EpiCar car;
+    EpiEnv env;
+    epilogue_load_car(a, e, car);
+    epilogue_load_env(a, e, env);
     if (col) {  // state[3:] = 0 (yaw included)
 #pragma unroll
         for (int k = 3; k < 7; ++k) a.st[(size_t)k * EA + e] = 0.0;
@@ -626,7 +681,7 @@ __global__ void __launch_bounds__(64) k_post_single(StepArgs a) {
         o[3] = col ? 1.0f : 0.0f;
     }
     if (a.out.collisions) a.out.collisions[e] = (uint8_t)col;
-    env_epilogue(a, e, stl, 2, &col, a.reset_flag[e]);
+    env_epilogue(a, e, stl, 2, &col, do_reset, env, &car);
 }
 
 // k_post_multi: multi-agent envs after the tiled ray kernel (TTC flags are
@@ -649,6 +704,8 @@ struct MultiShared {
     int32_t blo[kMaxAgents * (kMaxAgents - 1)], bhi[kMaxAgents * (kMaxAgents - 1)];
     int32_t rng[kMaxAgents * (kMaxAgents - 1)][4]; // window_beam_ranges, clipped to [blo, bhi]
     int32_t col[kMaxAgents];
+    EpiCar epi[kMaxAgents];  // env_epilogue inputs, prefetched at kernel start
+    EpiEnv epe;
     int32_t do_reset;
 };
 
@@ -675,6 +732,7 @@ __global__ void __launch_bounds__(kMultiBlock) k_post_multi(StepArgs a) {
         sh.pose0[tid][0] = sh.stl[tid][0];
         sh.pose0[tid][1] = sh.stl[tid][1];
         sh.pose0[tid][2] = sh.stl[tid][4];
+        epilogue_load_car(a, g, sh.epi[tid]);
         get_vertices(sh.stl[tid][0], sh.stl[tid][1], sh.stl[tid][4], a.p.length, a.p.width, sh.verts[tid]);
         const int hit = a.ttc_hit[g];
         sh.col[tid] = hit;  // Simulator.step :601-602
@@ -686,7 +744,10 @@ __global__ void __launch_bounds__(kMultiBlock) k_post_multi(StepArgs a) {
             }
         }
     }
-    if (tid == 0) sh.do_reset = a.reset_flag[e];
+    if (tid == 0) {
+        sh.do_reset = a.reset_flag[e];
+        epilogue_load_env(a, e, sh.epe);
+    }
     __syncthreads();
     if (tid == 0) {  // collision_multiple (collision_models.py:184-212)
         for (int i = 0; i < A - 1; ++i)
@@ -789,7 +850,7 @@ __global__ void __launch_bounds__(kMultiBlock) k_post_multi(StepArgs a) {
         o[3] = sh.col[tid] ? 1.0f : 0.0f;
     }
     if (a.out.collisions && tid < A) a.out.collisions[(size_t)e * A + tid] = (uint8_t)sh.col[tid];
-    if (tid == 0) env_epilogue(a, e, &sh.stl[0][0], 7, sh.col, sh.do_reset);
+    if (tid == 0) env_epilogue(a, e, &sh.stl[0][0], 7, sh.col, sh.do_reset, sh.epe, sh.epi);
 }
 
 hipError_t prepare_env_step(size_t lds_bytes) {
