@@ -864,9 +864,11 @@ extern "C" int f110_track_create(f110_track **out, int32_t device, const double 
         return hipMemcpy(q, src, cnt * sizeof(double), hipMemcpyHostToDevice);
     };
     // uniform grid over the segment midpoints (reward kernel's kd.query):
-    // 4 m cells (the centerline spacing is ~1 m, the 5th nearest midpoint
-    // is typically within 2.5 m), one cell of margin on every side
+    // cells of 16 median segment lengths (a 3x3 block then holds ~50
+    // midpoints of a centerline through it; the kernel widens the block when
+    // the 5th nearest is not provably inside), one cell of margin on every side
     std::vector<int32_t> cstart, citems;
+    std::vector<double> cmid;
     if (!host_only && n >= 2) {
         double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
         for (int32_t i = 0; i + 1 < n; ++i) {
@@ -875,8 +877,15 @@ extern "C" int f110_track_create(f110_track **out, int32_t device, const double 
             mny = std::min(mny, t->mid[2 * (size_t)i + 1]);
             mxy = std::max(mxy, t->mid[2 * (size_t)i + 1]);
         }
-        const double h = 4.0;
-        if (std::isfinite(mnx) && std::isfinite(mny) && std::isfinite(mxx) && std::isfinite(mxy) &&
+        std::vector<double> seg;
+        for (int32_t i = 0; i + 1 < n; ++i)
+            seg.push_back(std::hypot(xy[2 * (size_t)i + 2] - xy[2 * (size_t)i], xy[2 * (size_t)i + 3] - xy[2 * (size_t)i + 1]));
+        std::nth_element(seg.begin(), seg.begin() + seg.size() / 2, seg.end());
+        const double med = seg[seg.size() / 2];
+        const double ext = std::max(mxx - mnx, mxy - mny);
+        // at most 4096 cells a side; a degenerate spacing falls back to ext / 64
+        const double h = std::max(std::isfinite(med) && med > 0.0 ? 16.0 * med : ext / 64.0, ext / 4000.0);
+        if (h > 0.0 && std::isfinite(h) && std::isfinite(mnx) && std::isfinite(mny) && std::isfinite(mxx) && std::isfinite(mxy) &&
             (mxx - mnx) / h < 4096 && (mxy - mny) / h < 4096) {
             t->v.gh = h;
             t->v.gx0 = mnx - h;
@@ -896,6 +905,11 @@ extern "C" int f110_track_create(f110_track **out, int32_t device, const double 
             citems.assign((size_t)n - 1, 0);
             std::vector<int32_t> fill(cstart.begin(), cstart.end() - 1);
             for (int32_t i = 0; i + 1 < n; ++i) citems[(size_t)fill[(size_t)cell[(size_t)i]]++] = i;
+            cmid.resize(2 * citems.size());
+            for (size_t q = 0; q < citems.size(); ++q) {
+                cmid[2 * q] = t->mid[2 * (size_t)citems[q]];
+                cmid[2 * q + 1] = t->mid[2 * (size_t)citems[q] + 1];
+            }
         }
     }
     auto up_i = [&](const std::vector<int32_t> &src, const int32_t **dst) -> hipError_t {
@@ -909,6 +923,7 @@ extern "C" int f110_track_create(f110_track **out, int32_t device, const double 
     hipError_t e = up(xy, 2 * (size_t)n, &t->v.xy);
     if (e == hipSuccess && !cstart.empty()) e = up_i(cstart, &t->v.cell_start);
     if (e == hipSuccess && !citems.empty()) e = up_i(citems, &t->v.cell_items);
+    if (e == hipSuccess && !cmid.empty()) e = up(cmid.data(), cmid.size(), &t->v.cell_mid);
     if (e == hipSuccess) e = up(t->s.data(), t->s.size(), &t->v.s);
     if (e == hipSuccess) e = up(t->tan.data(), t->tan.size(), &t->v.tan);
     if (e == hipSuccess) e = up(t->nrm.data(), t->nrm.size(), &t->v.nrm);

@@ -150,6 +150,7 @@ struct TrackView {
     // size gh at (gx0 + i*gh, gy0 + j*gh) holds midpoints cell_items[cell_start[c] ..
     // cell_start[c+1]), c = j*gnx + i
     const int32_t *cell_start, *cell_items;
+    const double *cell_mid;  // [n-1][2]: mid[cell_items[q]], in cell order (no indirection)
     int32_t gnx, gny;
     double gx0, gy0, gh;
 };

@@ -37,14 +37,19 @@ __device__ __forceinline__ bool cand_less(double d2a, int32_t ia, double d2b, in
     return d2a < d2b || (d2a == d2b && ia < ib);
 }
 
-__device__ void merge_top(const Cand (&t)[kTop], int lane, Cand out[kTop]);
+__device__ void merge_top(const Cand (&t)[kTop], int sub, Cand out[kTop]);
 
-// The kTop midpoints nearest to (px, py), ascending; every lane gets the same list.
-__device__ void nearest_mids(const double *mid, int32_t M, double px, double py, int lane, Cand out[kTop]) {
+// Each half-wave (32 lanes) projects its own point: the ego car's on lanes
+// 0-31, the opponent's on 32-63, so the two dependent load chains overlap.
+// `sub` is the lane within the half; cross-lane steps stay inside it.
+constexpr int kHalf = 32;
+
+// The kTop midpoints nearest to (px, py), ascending; every lane of the half gets the same list.
+__device__ void nearest_mids(const double *mid, int32_t M, double px, double py, int sub, Cand out[kTop]) {
     Cand t[kTop];
 #pragma unroll
     for (int k = 0; k < kTop; ++k) t[k] = Cand{INFINITY, INT32_MAX};
-    for (int32_t m = lane; m < M; m += 64) {
+    for (int32_t m = sub; m < M; m += kHalf) {
         const double dx = mid[2 * m] - px, dy = mid[2 * m + 1] - py;
         const double d2 = dx * dx + dy * dy;  // cKDTree's squared euclidean distance
         if (cand_less(d2, m, t[kTop - 1].d2, t[kTop - 1].i)) {
@@ -58,11 +63,11 @@ __device__ void nearest_mids(const double *mid, int32_t M, double px, double py,
                 }
         }
     }
-    merge_top(t, lane, out);
+    merge_top(t, sub, out);
 }
 
-// The wave-wide kTop smallest of the lanes' sorted lists (every lane gets them).
-__device__ void merge_top(const Cand (&t)[kTop], int lane, Cand out[kTop]) {
+// The half-wide kTop smallest of the lanes' sorted lists (every lane gets them).
+__device__ void merge_top(const Cand (&t)[kTop], int sub, Cand out[kTop]) {
     int head = 0;
 #pragma unroll
     for (int r = 0; r < kTop; ++r) {
@@ -77,7 +82,7 @@ __device__ void merge_top(const Cand (&t)[kTop], int lane, Cand out[kTop]) {
         double bd = hd;
         int32_t bi = hi;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
+        for (int o = kHalf / 2; o > 0; o >>= 1) {
             const double od = __shfl_xor(bd, o, 64);
             const int32_t oi = __shfl_xor(bi, o, 64);
             if (cand_less(od, oi, bd, bi)) {
@@ -92,61 +97,89 @@ __device__ void merge_top(const Cand (&t)[kTop], int lane, Cand out[kTop]) {
 
 struct Proj {
     double s, t;
+    int32_t seg;  // the segment (or node) s was taken from: seg_at's first guess
 };
 
 // np.dot of two 2-vectors / np.linalg.norm of one (OpenBLAS pattern)
 __device__ __forceinline__ double bdot(double a0, double a1, double b0, double b1) { return fma(a1, b1, a0 * b0); }
 
-// nearest_mids through the grid: the midpoints of the 3x3 cells around the
-// query, merged as above; the result is final when every midpoint outside
-// those cells is provably farther than the 5th found one (distance to the
-// 3x3 block's edge, less a margin, above it), otherwise the full scan runs.
-// The same 5 (and order) as the full scan.
-__device__ void nearest_mids_grid(const TrackView &T, double px, double py, int lane, Cand out[kTop]) {
+// nearest_mids through the grid: the midpoints of the (2r+1)^2 cells around
+// the query, merged as above; the result is final when every midpoint
+// outside the block is provably farther than the 5th found one (distance to
+// the block's edge, less a margin, above it).  r = 1, then 2, then 4; past
+// that (or off the grid) the full scan runs.  The same 5 (and order) as the
+// full scan.  A grid row's cells are consecutive in cell order, so a block is
+// 2r+1 item ranges: their bounds load together, every lane then takes items
+// of the concatenated ranges from the cell-ordered midpoint copy.
+constexpr int kMaxBlockRows = 9;
+
+__device__ void nearest_mids_grid(const TrackView &T, double px, double py, int sub, Cand out[kTop]) {
     const int32_t M = T.n - 1;
     const double fx = (px - T.gx0) / T.gh, fy = (py - T.gy0) / T.gh;
-    bool ok = T.cell_start && fx >= 1.0 && fy >= 1.0 && fx < (double)(T.gnx - 1) && fy < (double)(T.gny - 1);
-    if (ok) {
+    bool ok = false;
+    if (T.cell_start && fx >= 0.0 && fy >= 0.0 && fx < (double)T.gnx && fy < (double)T.gny) {
         const int32_t ci = (int32_t)fx, cj = (int32_t)fy;
-        Cand t[kTop];
+        for (int32_t r = 1; r <= (kMaxBlockRows - 1) / 2 && !ok; r *= 2) {
+            // the block clipped to the grid: a clipped side needs no bound
+            const int32_t i0 = ci - r < 0 ? 0 : ci - r, i1 = ci + r >= T.gnx ? T.gnx - 1 : ci + r;
+            const int32_t j0 = cj - r < 0 ? 0 : cj - r, j1 = cj + r >= T.gny ? T.gny - 1 : cj + r;
+            const int32_t nrow = j1 - j0 + 1;
+            int32_t r0[kMaxBlockRows], pre[kMaxBlockRows];
+            int32_t K = 0;
 #pragma unroll
-        for (int k = 0; k < kTop; ++k) t[k] = Cand{INFINITY, INT32_MAX};
-        for (int dj = -1; dj <= 1; ++dj)
-            for (int di = -1; di <= 1; ++di) {
-                const int32_t c = (cj + dj) * T.gnx + (ci + di);
-                for (int32_t q = T.cell_start[c] + lane; q < T.cell_start[c + 1]; q += 64) {
-                    const int32_t m = T.cell_items[q];
-                    const double dx = T.mid[2 * m] - px, dy = T.mid[2 * m + 1] - py;
-                    const double d2 = dx * dx + dy * dy;
-                    if (cand_less(d2, m, t[kTop - 1].d2, t[kTop - 1].i)) {
-                        Cand cc{d2, m};
-#pragma unroll
-                        for (int k = 0; k < kTop; ++k)
-                            if (cand_less(cc.d2, cc.i, t[k].d2, t[k].i)) {
-                                const Cand o = t[k];
-                                t[k] = cc;
-                                cc = o;
-                            }
-                    }
+            for (int t = 0; t < kMaxBlockRows; ++t) {
+                r0[t] = 0;
+                pre[t] = K;
+                if (t < nrow) {
+                    const int32_t c = (j0 + t) * T.gnx;
+                    r0[t] = T.cell_start[c + i0];
+                    K += T.cell_start[c + i1 + 1] - r0[t];
                 }
             }
-        merge_top(t, lane, out);
-        // distance from the query to the 3x3 block's edge (a lower bound for
-        // every midpoint outside it), with a relative margin for rounding
-        const double bx0 = T.gx0 + (double)(ci - 1) * T.gh, by0 = T.gy0 + (double)(cj - 1) * T.gh;
-        const double lb = fmin(fmin(px - bx0, bx0 + 3.0 * T.gh - px), fmin(py - by0, by0 + 3.0 * T.gh - py));
-        const double lbm = lb * (1.0 - 1e-9) - 1e-9;
-        ok = out[kTop - 1].i != INT32_MAX && lbm > 0.0 && out[kTop - 1].d2 < lbm * lbm;
+            Cand tp[kTop];
+#pragma unroll
+            for (int k = 0; k < kTop; ++k) tp[k] = Cand{INFINITY, INT32_MAX};
+            for (int32_t j = sub; j < K; j += kHalf) {
+                int32_t q = r0[0] + j;
+#pragma unroll
+                for (int t = 1; t < kMaxBlockRows; ++t)
+                    if (t < nrow && j >= pre[t]) q = r0[t] + (j - pre[t]);
+                const int32_t m = T.cell_items[q];
+                const double dx = T.cell_mid[2 * q] - px, dy = T.cell_mid[2 * q + 1] - py;
+                const double d2 = dx * dx + dy * dy;
+                if (cand_less(d2, m, tp[kTop - 1].d2, tp[kTop - 1].i)) {
+                    Cand cc{d2, m};
+#pragma unroll
+                    for (int k = 0; k < kTop; ++k)
+                        if (cand_less(cc.d2, cc.i, tp[k].d2, tp[k].i)) {
+                            const Cand o = tp[k];
+                            tp[k] = cc;
+                            cc = o;
+                        }
+                }
+            }
+            merge_top(tp, sub, out);
+            // distance from the query to the block's unclipped edges (a lower
+            // bound for every midpoint outside the block), with a margin
+            double lb = INFINITY;
+            if (ci - r >= 0) lb = fmin(lb, px - (T.gx0 + (double)i0 * T.gh));
+            if (ci + r < T.gnx) lb = fmin(lb, T.gx0 + (double)(i1 + 1) * T.gh - px);
+            if (cj - r >= 0) lb = fmin(lb, py - (T.gy0 + (double)j0 * T.gh));
+            if (cj + r < T.gny) lb = fmin(lb, T.gy0 + (double)(j1 + 1) * T.gh - py);
+            const double lbm = lb * (1.0 - 1e-9) - 1e-9;
+            ok = out[kTop - 1].i != INT32_MAX && lbm > 0.0 && out[kTop - 1].d2 < lbm * lbm;
+        }
     }
-    if (!ok) nearest_mids(T.mid, M, px, py, lane, out);  // off the grid or a sparse neighbourhood
+    if (!ok) nearest_mids(T.mid, M, px, py, sub, out);  // off the grid or a sparse neighbourhood
 }
 
 // CenterlineProgress.project_xy (track_progress.py:58-97)
-__device__ Proj project_xy(const TrackView &T, double x, double y, int lane) {
+__device__ Proj project_xy(const TrackView &T, double x, double y, int sub) {
     Cand c[kTop];
-    nearest_mids_grid(T, x, y, lane, c);
+    nearest_mids_grid(T, x, y, sub, c);
     bool have = false;
     double bn = 0.0, bs = 0.0, bt = 0.0;
+    int32_t bseg = 0;
 #pragma unroll
     for (int r = 0; r < kTop; ++r) {
         const int32_t idx = c[r].i;
@@ -168,12 +201,13 @@ __device__ Proj project_xy(const TrackView &T, double x, double y, int lane) {
             bn = nrm;
             bs = s_proj;
             bt = t_signed;
+            bseg = idx;
         }
     }
     if (!have) {  // degenerate fallback: nearest node (:93-95)
         double bd = INFINITY;
         int32_t bj = INT32_MAX;
-        for (int32_t j = lane; j < T.n; j += 64) {
+        for (int32_t j = sub; j < T.n; j += kHalf) {
             const double d0 = T.xy[2 * j] - x, d1 = T.xy[2 * j + 1] - y;
             const double d = sqrt(d0 * d0 + d1 * d1);
             if (cand_less(d, j, bd, bj)) {
@@ -182,7 +216,7 @@ __device__ Proj project_xy(const TrackView &T, double x, double y, int lane) {
             }
         }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
+        for (int o = kHalf / 2; o > 0; o >>= 1) {
             const double od = __shfl_xor(bd, o, 64);
             const int32_t oi = __shfl_xor(bj, o, 64);
             if (cand_less(od, oi, bd, bj)) {
@@ -190,14 +224,23 @@ __device__ Proj project_xy(const TrackView &T, double x, double y, int lane) {
                 bj = oi;
             }
         }
-        return Proj{T.s[bj], 0.0};
+        return Proj{T.s[bj], 0.0, bj};
     }
-    return Proj{bs, bt};
+    return Proj{bs, bt, bseg};
 }
 
 // np.searchsorted(s, v, side="right") - 1 clipped to [0, n-2] (rewards.py:112-114, :262-264)
-__device__ int32_t seg_at(const TrackView &T, double v) {
+// guess: the segment the projection came from; the answer is checked on it
+// and its successor (s is non-decreasing: i is the answer iff s[i] <= v and
+// s[i+1] > v or i = n-1) before the binary search runs.
+__device__ int32_t seg_at(const TrackView &T, double v, int32_t guess) {
     int32_t lo = 0, hi = T.n;  // first index with s[i] > v
+    if (guess >= 0 && guess + 1 < T.n) {
+        const double s0 = T.s[guess], s1 = T.s[guess + 1];
+        const double s2 = guess + 2 < T.n ? T.s[guess + 2] : INFINITY;
+        if (s0 <= v && s1 > v) lo = hi = guess + 1;
+        else if (s1 <= v && (guess + 2 >= T.n || s2 > v)) lo = hi = guess + 2;
+    }
     while (lo < hi) {
         const int32_t m = (lo + hi) >> 1;
         if (T.s[m] > v) hi = m;
@@ -231,21 +274,87 @@ constexpr int kRwPerLane = 32;  // n_beams <= 64 * 32 = 2048
 
 constexpr uint32_t kNoValue = 0xFFFFFFFFu;  // empty slot: above every value
 
+// wave-wide count of held values <= x: one compare per slot, whose lane mask
+// is counted on the scalar unit (no cross-lane reduction); every lane of the
+// wave must be active.  Empty slots hold kNoValue, above every query.
+template <int NQ>
+__device__ __forceinline__ int32_t wave_count_le(const uint32_t (&v)[NQ], uint32_t x) {
+    int32_t c = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) c += __popcll(__ballot(v[q] <= x));
+    return c;
+}
+
 // k-th smallest (0-based) of the values held across the wave (non-negative
-// floats by bit pattern, kRwPerLane slots per lane, empty = kNoValue), by
-// bisection on the bit pattern; every answer lies in [0, hi_bits].
-__device__ uint32_t kth_bits(const uint32_t (&v)[kRwPerLane], int nq, uint32_t hi_bits, int32_t k) {
-    uint32_t lo = 0, hi = hi_bits;
+// floats by bit pattern, NQ slots per lane), by bisection on the bit pattern
+// between the smallest and the largest held value.  (A 4-pass 8-bit radix
+// select over an LDS histogram measured slower: the few exponent values put
+// most of a wave's atomics on the same bins.)
+template <int NQ>
+__device__ __forceinline__ uint32_t kth_bits(const uint32_t (&v)[NQ], uint32_t lo, uint32_t hi, int32_t k) {
     while (lo < hi) {
         const uint32_t mid = lo + ((hi - lo) >> 1);
-        int32_t c = 0;
-#pragma unroll
-        for (int q = 0; q < kRwPerLane; ++q)
-            if (q < nq) c += v[q] <= mid;
-        if (wave_count(c) >= k + 1) hi = mid;
+        if (wave_count_le<NQ>(v, mid) >= k + 1) hi = mid;
         else lo = mid + 1;
     }
     return lo;
+}
+
+// The wall term's np.quantile(clip(where(x <= 0 | ~finite, lmax, x), 0, lmax), q)
+// in float32 (rewards.py:312-320): q cast to float32, virtual index (n-1)*q,
+// numpy's _lerp in float32.  NQ slots of 64 beams per lane (B <= 64 * NQ).
+template <int NQ>
+__device__ float wall_quantile(const float *o, int B, float lmax, float qf, int lane) {
+    uint32_t v[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int b = lane + 64 * q;
+        v[q] = kNoValue;
+        if (b < B) {
+            float x = o[b];
+            if (x <= 0.0f || !isfinite(x)) x = lmax;  // np.where(...)
+            x = x < 0.0f ? 0.0f : (x > lmax ? lmax : x);  // np.clip
+            v[q] = __float_as_uint(x);
+        }
+    }
+    // the answer lies between the smallest and the largest value (kNoValue
+    // fillers excluded from the max)
+    uint32_t vmin = kNoValue, vmax = 0u;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        vmin = v[q] < vmin ? v[q] : vmin;
+        vmax = v[q] != kNoValue && v[q] > vmax ? v[q] : vmax;
+    }
+#pragma unroll
+    for (int s2 = 32; s2 > 0; s2 >>= 1) {
+        const uint32_t a = __shfl_xor(vmin, s2, 64), b = __shfl_xor(vmax, s2, 64);
+        vmin = a < vmin ? a : vmin;
+        vmax = b > vmax ? b : vmax;
+    }
+    const float vi = (float)(B - 1) * qf;
+    if (vi >= (float)(B - 1)) return __uint_as_float(kth_bits<NQ>(v, vmin, vmax, B - 1));
+    const float pv = floorf(vi < 0.0f ? 0.0f : vi);
+    const int32_t k = (int32_t)pv;
+    const float g = vi - pv;
+    const uint32_t ab = kth_bits<NQ>(v, vmin, vmax, k);
+    uint32_t bb;
+    if (wave_count_le<NQ>(v, ab) >= k + 2) {
+        bb = ab;
+    } else {  // the smallest value above a
+        uint32_t m = kNoValue;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+            if (v[q] > ab && v[q] < m) m = v[q];
+#pragma unroll
+        for (int s2 = 32; s2 > 0; s2 >>= 1) {
+            const uint32_t om = __shfl_xor(m, s2, 64);
+            m = om < m ? om : m;
+        }
+        bb = m;
+    }
+    const float fa = __uint_as_float(ab), fb = __uint_as_float(bb);
+    const float diff = fb - fa;
+    return g >= 0.5f ? fb - diff * (1.0f - g) : fa + diff * g;
 }
 
 }  // namespace
@@ -283,15 +392,25 @@ __global__ void __launch_bounds__(64 * kRwWaves) k_reward(RewardArgs a) {
     } else {
         // ---- progress: _Prog.update (:125-172) or _ProgFallback.update (:73-79)
         double de, dop, s_ego = 0.0, t_ego = 0.0;
+        int32_t seg_ego = -1;
         const double xs[2] = {ex, ox}, ys[2] = {ey, oy};
         double dd[2];
         if (P.use_progress) {
             const TrackView &T = a.track;
             Proj pj[2];
-            pj[0] = project_xy(T, ex, ey, lane);
-            pj[1] = project_xy(T, ox, oy, lane);
+            {  // ego on lanes 0-31, opponent on 32-63
+                const bool lo_half = lane < kHalf;
+                const Proj mine = project_xy(T, lo_half ? ex : ox, lo_half ? ey : oy, lane & (kHalf - 1));
+#pragma unroll
+                for (int w = 0; w < 2; ++w) {
+                    pj[w].s = __shfl(mine.s, w * kHalf, 64);
+                    pj[w].t = __shfl(mine.t, w * kHalf, 64);
+                    pj[w].seg = __shfl(mine.seg, w * kHalf, 64);
+                }
+            }
             s_ego = pj[0].s;
             t_ego = pj[0].t;
+            seg_ego = pj[0].seg;
 #pragma unroll
             for (int w = 0; w < 2; ++w) {
                 if (!(st.flags & (1 << w))) {  // init
@@ -310,7 +429,7 @@ __global__ void __launch_bounds__(64 * kRwWaves) k_reward(RewardArgs a) {
                     const double dx = xs[w] - st.px[w], dy = ys[w] - st.py[w];
                     st.px[w] = xs[w];
                     st.py[w] = ys[w];
-                    const int32_t idx = seg_at(T, pj[w].s);
+                    const int32_t idx = seg_at(T, pj[w].s, pj[w].seg);
                     const double ds_sign = dx * T.tan[2 * idx] + dy * T.tan[2 * idx + 1];
                     ds = copysign(fabs(ds_geom), fabs(ds_sign) > 1e-6 ? ds_sign : ds_geom);
                 }
@@ -370,7 +489,7 @@ __global__ void __launch_bounds__(64 * kRwWaves) k_reward(RewardArgs a) {
             const TrackView &T = a.track;
             double wR = P.default_half_width, wL = P.default_half_width;
             if (T.wR) {
-                const int32_t idx = seg_at(T, s_ego);
+                const int32_t idx = seg_at(T, s_ego, seg_ego);
                 wR = T.wR[idx];
                 wL = T.wL[idx];
             }
@@ -382,54 +501,9 @@ __global__ void __launch_bounds__(64 * kRwWaves) k_reward(RewardArgs a) {
         double r_wall = 0.0;
         if (B > 0 && st.steps >= P.grace_steps_wall) {  // wall term (:312-320)
             const float lmax = (float)P.lidar_max;
-            const int nq = (B + 63) / 64;  // wave-uniform
-            uint32_t v[kRwPerLane];
-#pragma unroll
-            for (int q = 0; q < kRwPerLane; ++q) {
-                const int b = lane + 64 * q;
-                v[q] = kNoValue;
-                if (q < nq && b < B) {
-                    float x = o[b];
-                    if (x <= 0.0f || !isfinite(x)) x = lmax;  // np.where(...)
-                    x = x < 0.0f ? 0.0f : (x > lmax ? lmax : x);  // np.clip
-                    v[q] = __float_as_uint(x);
-                }
-            }
-            // np.quantile(rng, q): q cast to float32, index (n-1)*q, _lerp in float32
             const float qf = (float)P.wall_quantile;
-            const float vi = (float)(B - 1) * qf;
-            float dmin_f;
-            const uint32_t top = __float_as_uint(lmax);
-            if (vi >= (float)(B - 1)) {
-                dmin_f = __uint_as_float(kth_bits(v, nq, top, B - 1));
-            } else {
-                const float pv = floorf(vi < 0.0f ? 0.0f : vi);
-                const int32_t k = (int32_t)pv;
-                const float g = vi - pv;
-                const uint32_t ab = kth_bits(v, nq, top, k);
-                int32_t c = 0;
-#pragma unroll
-                for (int q = 0; q < kRwPerLane; ++q)
-                    if (q < nq) c += v[q] <= ab;
-                uint32_t bb;
-                if (wave_count(c) >= k + 2) {
-                    bb = ab;
-                } else {  // the smallest value above a
-                    uint32_t m = kNoValue;
-#pragma unroll
-                    for (int q = 0; q < kRwPerLane; ++q)
-                        if (q < nq && v[q] > ab && v[q] < m) m = v[q];
-#pragma unroll
-                    for (int s2 = 32; s2 > 0; s2 >>= 1) {
-                        const uint32_t om = __shfl_xor(m, s2, 64);
-                        m = om < m ? om : m;
-                    }
-                    bb = m;
-                }
-                const float fa = __uint_as_float(ab), fb = __uint_as_float(bb);
-                const float diff = fb - fa;
-                dmin_f = g >= 0.5f ? fb - diff * (1.0f - g) : fa + diff * g;
-            }
+            const float dmin_f = B <= 64 * 17 ? wall_quantile<17>(o, B, lmax, qf, lane)
+                                              : wall_quantile<kRwPerLane>(o, B, lmax, qf, lane);
             const double dmin = (double)dmin_f;
             if (dmin < P.near_wall_dist) {
                 const double x = (P.near_wall_dist - dmin) / pymax(1e-6, P.near_wall_dist);
