@@ -62,7 +62,9 @@ EXPORTS = [
     "f110_host_window_ranges", "f110_track_create", "f110_track_destroy", "f110_track_arrays",
     "f110_default_reward_params", "f110_reward", "f110_replay_create", "f110_replay_destroy", "f110_replay_add",
     "f110_replay_sample", "f110_replay_update_priorities", "f110_replay_length", "f110_replay_arrays",
-    "f110_debug_wave_trace", "f110_adam_step",
+    "f110_debug_wave_trace", "f110_adam_step", "f110_ddpg_scratch_floats", "f110_ddpg_actor_head",
+    "f110_ddpg_actor_head_bwd", "f110_ddpg_td_target", "f110_ddpg_critic_loss", "f110_ddpg_critic_loss_bwd",
+    "f110_ddpg_q_mean", "f110_ddpg_q_mean_bwd",
 ]
 
 _lib = None
@@ -142,11 +144,21 @@ def load(build_if_missing: bool = True):
     L.f110_debug_wave_trace.argtypes = [_P, i32, _P, i64, ctypes.POINTER(i64), _P]
     L.f110_adam_step.argtypes = [_P, _P, _P, _P, i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                  ctypes.c_double, _P, _P]
+    f32 = ctypes.c_float
+    L.f110_ddpg_scratch_floats.argtypes = [i32, i32, i32]
+    L.f110_ddpg_actor_head.argtypes = [_P] * 5 + [i32] * 3 + [_P] * 3
+    L.f110_ddpg_actor_head_bwd.argtypes = [_P] * 5 + [i32] * 3 + [_P] * 5
+    L.f110_ddpg_td_target.argtypes = [_P] * 5 + [f32, i32, i32, _P, _P]
+    L.f110_ddpg_critic_loss.argtypes = [_P] * 5 + [i32] * 2 + [_P] * 4
+    L.f110_ddpg_critic_loss_bwd.argtypes = [_P] * 5 + [i32] * 2 + [_P] * 5
+    L.f110_ddpg_q_mean.argtypes = [_P] * 3 + [f32, i32, i32] + [_P] * 3
+    L.f110_ddpg_q_mean_bwd.argtypes = [_P] * 3 + [f32, i32, i32] + [_P] * 5
     for name in EXPORTS:
         if name not in ("f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config",
                         "f110_host_tables", "f110_host_window_ranges", "f110_track_arrays",
-                        "f110_default_reward_params"):
+                        "f110_default_reward_params", "f110_ddpg_scratch_floats"):
             getattr(L, name).restype = ctypes.c_int
+    L.f110_ddpg_scratch_floats.restype = i64
     if L.f110_abi_version() != 1:
         raise F110Error("libf110.so ABI version mismatch")
     _lib = L

@@ -108,12 +108,21 @@ __global__ void __launch_bounds__(kRB) k_prio_max(ReplayView v) {
 __global__ void __launch_bounds__(kOneBlock) k_add_scan(ReplayView v, const uint8_t *mask, const float *priority,
                                                         int64_t n, int n_part) {
     __shared__ int64_t part[kOneBlock];
+    __shared__ uint32_t wmx[kOneBlock / 64];
     __shared__ uint32_t mx;
     const int t = threadIdx.x;
-    if (t == 0) {  // the max priority from k_prio_max's partials
+    {  // the max priority from k_prio_max's partials, spread over the block
         uint32_t m = 0;
-        for (int k = 0; k < n_part; ++k) m = max(m, v.part[k]);
-        mx = m;
+        for (int k = t; k < n_part; k += kOneBlock) m = max(m, v.part[k]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+        if ((t & 63) == 0) wmx[t >> 6] = m;
+        __syncthreads();
+        if (t == 0) {
+            uint32_t b = wmx[0];
+            for (int w = 1; w < kOneBlock / 64; ++w) b = max(b, wmx[w]);
+            mx = b;
+        }
     }
     const int64_t chunk = (n + kOneBlock - 1) / kOneBlock;
     const int64_t r0 = min((int64_t)t * chunk, n), r1 = min(r0 + chunk, n);

@@ -31,6 +31,39 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
+# On a HIP device the networks' hidden layers run as GEMMs with the bias and
+# ReLU fused into the BLAS epilogue (torch._addmm_activation: the same values
+# as relu(linear(x))) and their output layers as the fused learner heads of
+# ddpg_heads.py.  F110_DDPG_FUSED=0 keeps the plain torch modules (A/B runs).
+FUSED = os.environ.get("F110_DDPG_FUSED", "1") != "0"
+
+
+def _fused(x: torch.Tensor) -> bool:
+    return FUSED and x.is_cuda
+
+
+class _LinearReLU(torch.autograd.Function):
+    """relu(x W^T + b) with the ReLU in the GEMM epilogue; backward as
+    autograd does it for relu(linear): threshold on the result, two GEMMs
+    and a bias sum (only the ones whose inputs need a gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        y = torch._addmm_activation(b, x, W.t())
+        ctx.save_for_backward(x, W, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W, y = ctx.saved_tensors
+        gz = torch.ops.aten.threshold_backward(gy, y, 0)
+        nx, nw, nb = ctx.needs_input_grad
+        return (gz.mm(W) if nx else None, gz.t().mm(x) if nw else None, gz.sum(0) if nb else None)
+
+
+def _linear_relu(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
+    return _LinearReLU.apply(x, lin.weight, lin.bias)
+
 
 class Actor(nn.Module):
     """agent.py:25-62: obs -> 128 -> 128 -> act_dim, tanh scaled to [low, high]."""
@@ -52,11 +85,26 @@ class Actor(nn.Module):
     def forward(self, obs: torch.Tensor) -> torch.Tensor:
         if obs.dim() == 1:
             obs = obs.unsqueeze(0)
+        if _fused(obs):
+            from .ddpg_heads import actor_head
+            x = _linear_relu(self.fc2, _linear_relu(self.fc1, obs))
+            return actor_head(x, self.fc3.weight, self.fc3.bias, *self._affine())
         x = F.relu(self.fc1(obs))
         x = F.relu(self.fc2(x))
         t = torch.tanh(self.fc3(x))
         low, high = self.action_low, self.action_high
         return 0.5 * (high - low) * t + 0.5 * (high + low)  # :60-61
+
+    def _affine(self):
+        """0.5*(high-low), 0.5*(high+low) as forward computes them (:60-61),
+        cached until the bounds change (the learner's eager warm-up fills the
+        cache before any graph capture)."""
+        low, high = self.action_low, self.action_high
+        key = (low.data_ptr(), high.data_ptr(), low._version, high._version)
+        if getattr(self, "_aff_key", None) != key:
+            self._aff = (0.5 * (high - low), 0.5 * (high + low))
+            self._aff_key = key
+        return self._aff
 
 
 class Critic(nn.Module):
@@ -79,10 +127,16 @@ class Critic(nn.Module):
             obs = obs.unsqueeze(0)
         if act.dim() == 1:
             act = act.unsqueeze(0)
+        return self.q(self.hidden(obs, act))
+
+    def hidden(self, obs: torch.Tensor, act: torch.Tensor) -> torch.Tensor:
+        """The input of the q layer (agent.py:93-96)."""
+        if _fused(obs):
+            z = torch.cat([_linear_relu(self.fcs1, obs), act], dim=-1)
+            return _linear_relu(self.fcs2, z)
         z = F.relu(self.fcs1(obs))
         z = torch.cat([z, act], dim=-1)
-        z = F.relu(self.fcs2(z))
-        return self.q(z)
+        return F.relu(self.fcs2(z))
 
 
 class GradBucket:
@@ -296,15 +350,26 @@ class DDPGLearner:
         for name, t in (("states", states), ("actions", actions), ("next_states", next_states), ("rewards", r),
                         ("dones", d)):
             self._finite(name, t)
+        fused = _fused(states)
         with torch.no_grad():  # :302-308
             a_next = self.actor_target(next_states)
-            q_next = self.critic_target(next_states, a_next)
-            target_y = r + self.gamma * (1.0 - d) * q_next
+            if fused:
+                from .ddpg_heads import td_target
+                ct = self.critic_target
+                target_y = td_target(ct.hidden(next_states, a_next), ct.q.weight, ct.q.bias, r, d, self.gamma)
+            else:
+                q_next = self.critic_target(next_states, a_next)
+                target_y = r + self.gamma * (1.0 - d) * q_next
             self._finite("target_y", target_y)
-        q_pred = self.critic(states, actions)  # :310-315
-        td = target_y - q_pred
-        critic_loss = (w * td ** 2).mean()
         self.critic_grads.zero()               # :318-319
+        if fused:  # :310-316
+            from .ddpg_heads import critic_loss as fused_loss
+            critic_loss, td = fused_loss(self.critic.hidden(states, actions), self.critic.q.weight,
+                                         self.critic.q.bias, target_y, w)
+        else:
+            q_pred = self.critic(states, actions)  # :310-315
+            td = target_y - q_pred
+            critic_loss = (w * td ** 2).mean()
         critic_loss.backward()
         return critic_loss.detach(), td.detach()
 
@@ -319,7 +384,12 @@ class DDPGLearner:
         self._optim_step(self.critic_optim, self.critic_grads)
         for p in self.critic.parameters():
             p.requires_grad_(False)
-        actor_loss = -self.critic(states, self.actor(states)).mean()
+        if _fused(states):
+            from .ddpg_heads import q_mean
+            actor_loss = q_mean(self.critic.hidden(states, self.actor(states)), self.critic.q.weight,
+                                self.critic.q.bias, -1.0)
+        else:
+            actor_loss = -self.critic(states, self.actor(states)).mean()
         self.actor_grads.zero()
         actor_loss.backward()
         for p in self.critic.parameters():
@@ -330,7 +400,8 @@ class DDPGLearner:
         """agent.py:331, :340-341: actor step, soft target update."""
         self._optim_step(self.actor_optim, self.actor_grads)
         with torch.no_grad():
-            torch._foreach_lerp_(self._target, self._online, self.tau)
+            for tgt, src in zip(self._target, self._online):  # one launch per flat network
+                tgt.lerp_(src, self.tau)
 
     def update(self, states, actions, rewards, next_states, dones, weights) -> dict:
         """The learning part of replay() (agent.py:302-343) on one batch:

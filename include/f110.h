@@ -390,6 +390,42 @@ F110_API int f110_replay_arrays(f110_replay *rb, float **priority, float **obs, 
 F110_API int f110_adam_step(float *param, float *exp_avg, float *exp_avg_sq, const float *grad, int64_t n, double lr,
                             double beta1, double beta2, double eps, void *state, void *stream);
 
+/* ---- learner heads -------------------------------------------------------------
+ * The DDPG networks' output layers fused with what follows them
+ * (rl_training agent.py: Actor.fc3 + tanh + action-box map :56-61, Critic.q
+ * :93-97, replay()'s TD target :302-308, weighted MSE :310-316, actor loss
+ * -mean(q) :321-326), replacing torch's skinny GEMM + elementwise launches.
+ * Row-major float32 device buffers: h [B][K] (the last hidden layer), W
+ * [nout][K], b [nout]; K <= 255, nout <= 4 (nout = 1 for the critic).
+ * scratch: f110_ddpg_scratch_floats(B, K, nout) floats.  dh / dW / db
+ * outputs may be null (not wanted).  g: device scalar, the gradient of the
+ * loss (autograd's grad_output).  Deterministic; async on stream. */
+F110_API int64_t f110_ddpg_scratch_floats(int32_t B, int32_t K, int32_t nout);
+/* t = tanh(h W^T + b); act = scale * t + shift  (act, t: [B][nout]) */
+F110_API int f110_ddpg_actor_head(const float *h, const float *W, const float *b, const float *scale,
+                                  const float *shift, int32_t B, int32_t K, int32_t nout, float *act, float *t,
+                                  void *stream);
+/* dz = (dact * scale) * (1 - t*t); dh = dz W; dW = dz^T h; db = sum_rows dz */
+F110_API int f110_ddpg_actor_head_bwd(const float *h, const float *W, const float *t, const float *scale,
+                                      const float *dact, int32_t B, int32_t K, int32_t nout, float *dh, float *dW,
+                                      float *db, float *scratch, void *stream);
+/* y = r + (gamma * (1 - d)) * (h W^T + b) */
+F110_API int f110_ddpg_td_target(const float *h, const float *W, const float *b, const float *r, const float *d,
+                                 float gamma, int32_t B, int32_t K, float *y, void *stream);
+/* td = y - (h W^T + b); loss = mean(w * td * td)  (loss: device scalar) */
+F110_API int f110_ddpg_critic_loss(const float *h, const float *W, const float *b, const float *y, const float *w,
+                                   int32_t B, int32_t K, float *td, float *loss, float *scratch, void *stream);
+/* dq = -((g / B) * w) * (2 td); dh, dW, db from dq */
+F110_API int f110_ddpg_critic_loss_bwd(const float *h, const float *W, const float *td, const float *w,
+                                       const float *g, int32_t B, int32_t K, float *dh, float *dW, float *db,
+                                       float *scratch, void *stream);
+/* loss = sign * mean(h W^T + b)  (sign -1: the actor loss) */
+F110_API int f110_ddpg_q_mean(const float *h, const float *W, const float *b, float sign, int32_t B, int32_t K,
+                              float *loss, float *scratch, void *stream);
+/* dq = sign * (g / B); dh, dW, db from dq (h only needed for dW / db) */
+F110_API int f110_ddpg_q_mean_bwd(const float *h, const float *W, const float *g, float sign, int32_t B, int32_t K,
+                                  float *dh, float *dW, float *db, float *scratch, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
