@@ -507,20 +507,24 @@ F110_HD bool gjk_collision(const double *v1, const double *v2) {
     return false;
 }
 
+// RaceCar.scan_angles[k] (base_classes.py:122-126), the value f110_host_tables
+// stores: computed instead of loaded (same operations, no contraction)
+F110_HD double beam_angle(int k, double fov, double incr) { return -fov / 2. + (double)k * incr; }
+
 // argmin_k |angles[k] - a| over the uniform beam grid angles[k] = -fov/2 + k*incr
 // (get_blocked_view_indices, laser_models.py:310-313).  The grid is strictly
 // increasing, so |angles[k]-a| is V-shaped: test the analytic guess +-2 with
 // NumPy's first-minimum tie break instead of a 1080-long scan.
-F110_HD int nearest_beam(const double *angles, int B, double fov, double incr, double a) {
+F110_HD int nearest_beam(int B, double fov, double incr, double a) {
     if (a != a) return 0;  // np.argmin of an all-NaN array
     double g = (a + fov / 2.0) / incr;
     int k0 = g < 0 ? 0 : (g > (double)(B - 1) ? B - 1 : (int)(g + 0.5));
     int lo = k0 - 2 < 0 ? 0 : k0 - 2;
     int hi = k0 + 2 > B - 1 ? B - 1 : k0 + 2;
     int best = lo;
-    double bd = fabs(angles[lo] - a);
+    double bd = fabs(beam_angle(lo, fov, incr) - a);
     for (int k = lo + 1; k <= hi; ++k) {
-        double d = fabs(angles[k] - a);
+        double d = fabs(beam_angle(k, fov, incr) - a);
         if (d < bd) { bd = d; best = k; }
     }
     return best;
@@ -529,8 +533,8 @@ F110_HD int nearest_beam(const double *angles, int B, double fov, double incr, d
 // One vertex of get_blocked_view_indices (laser_models.py:282-315): the beam
 // nearest to the vertex bearing, relative to ego = atan2(sin(yaw), cos(yaw)).
 // phi receives the vertex bearing atan2(uy, ux) (used by box_beam_window).
-F110_HD int blocked_vertex_beam(double px, double py, double ego, double vx0, double vy0, const double *angles, int B,
-                                double fov, double incr, double &phi) {
+F110_HD int blocked_vertex_beam(double px, double py, double ego, double vx0, double vy0, int B, double fov,
+                                double incr, double &phi) {
     double vx = vx0 - px, vy = vy0 - py;
     double nrm = sqrt(vx * vx + vy * vy);
     double ux = vx / nrm, uy = vy / nrm;
@@ -538,12 +542,12 @@ F110_HD int blocked_vertex_beam(double px, double py, double ego, double vx0, do
     double angle = ego - phi;
     if (angle > kPi) angle = angle - 2 * kPi;
     else if (angle < -kPi) angle = angle + 2 * kPi;
-    return nearest_beam(angles, B, fov, incr, -angle);
+    return nearest_beam(B, fov, incr, -angle);
 }
 
 // get_blocked_view_indices, laser_models.py:282-315
-F110_HD void blocked_range(double px, double py, double pth, const double v[8], const double *angles, int B,
-                           double fov, double incr, int &lo, int &hi) {
+F110_HD void blocked_range(double px, double py, double pth, const double v[8], int B, double fov, double incr,
+                           int &lo, int &hi) {
     double ex = cos(pth), ey = sin(pth);
     double ego = atan2(ey, ex);
     int mn = 0, mx = 0;
@@ -555,7 +559,7 @@ F110_HD void blocked_range(double px, double py, double pth, const double v[8], 
         double angle = ego - atan2(uy, ux);
         if (angle > kPi) angle = angle - 2 * kPi;
         else if (angle < -kPi) angle = angle + 2 * kPi;
-        int k = nearest_beam(angles, B, fov, incr, -angle);
+        int k = nearest_beam(B, fov, incr, -angle);
         if (i == 0 || k < mn) mn = k;
         if (i == 0 || k > mx) mx = k;
     }

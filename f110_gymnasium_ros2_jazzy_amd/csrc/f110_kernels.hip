@@ -591,7 +591,7 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
         const f110_params &pi = a.pa[i];
         get_vertices(sh.pose0[j][0], sh.pose0[j][1], sh.pose0[j][2], pi.length, pi.width, v);
         int lo, hi;
-        blocked_range(sh.stl[i][0], sh.stl[i][1], sh.stl[i][4], v, a.angles, B, a.fov, a.beam_incr, lo, hi);
+        blocked_range(sh.stl[i][0], sh.stl[i][1], sh.stl[i][4], v, B, a.fov, a.beam_incr, lo, hi);
         box_beam_window(sh.stl[i][0], sh.stl[i][1], v, nullptr, sh.wcen[tid], sh.whalf[tid]);
         sh.blo[tid] = lo;
         sh.bhi[tid] = hi;
@@ -609,8 +609,9 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
                 // beams that cannot reach the box keep their range (see box_beam_window);
                 // get_blocked_view_indices' min..max spans most of the scan for an
                 // opponent behind the car, the filter keeps ~the box's own beams
-                if (!(fabs(wrap_pm_pi(oth + a.angles[b] - wc)) <= wh)) continue;
-                double bt = oth + a.angles[b] + kPi / 2.;
+                const double ang = beam_angle(b, a.fov, a.beam_incr);
+                if (!(fabs(wrap_pm_pi(oth + ang - wc)) <= wh)) continue;
+                double bt = oth + ang + kPi / 2.;
                 double v30 = cos(bt), v31 = sin(bt);
                 double cur = scan[i * B + b];
 #pragma unroll
@@ -709,6 +710,13 @@ struct MultiShared {
     int32_t do_reset;
 };
 
+// beams of pair pr's ray_cast pass (window_beam_ranges clipped to lo..hi)
+__device__ __forceinline__ int pass_beams(const MultiShared &sh, int pr) {
+    const int n0 = sh.rng[pr][1] - sh.rng[pr][0] + 1;
+    const int n1 = sh.rng[pr][3] - sh.rng[pr][2] + 1;
+    return (n0 > 0 ? n0 : 0) + (n1 > 0 ? n1 : 0);
+}
+
 // LDS hand-off between the lanes of ONE wave (no workgroup barrier).
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -777,7 +785,7 @@ __global__ void __launch_bounds__(kMultiBlock) k_post_multi(StepArgs a) {
             const int pr = w >> 2, q = w & 3;
             const int i = pr / (A - 1);
             sh.kq[pr][q] = blocked_vertex_beam(sh.stl[i][0], sh.stl[i][1], sh.ego[i], sh.rv[pr][2 * q],
-                                               sh.rv[pr][2 * q + 1], a.angles, B, a.fov, a.beam_incr, sh.phi[pr][q]);
+                                               sh.rv[pr][2 * q + 1], B, a.fov, a.beam_incr, sh.phi[pr][q]);
         }
         wave_sync();
         for (int pr = lane; pr < NP; pr += 64) {
@@ -804,37 +812,41 @@ __global__ void __launch_bounds__(kMultiBlock) k_post_multi(StepArgs a) {
     }
     __syncthreads();
     // agent ray_cast (base_classes.py:206-227; laser_models.py:318-346), one
-    // opponent at a time per car (each pass min-updates the same beams);
-    // only the beams of lo..hi that the box's window can hold are visited
+    // opponent at a time per car (each pass min-updates the same beams), all
+    // cars' passes of one round in one sweep over the block; only the beams
+    // of lo..hi that the box's window can hold are visited
     for (int jj = 0; jj < A - 1; ++jj) {
-        for (int i = 0; i < A; ++i) {
+        int total = 0;
+        for (int i = 0; i < A; ++i) total += pass_beams(sh, i * (A - 1) + jj);
+        for (int item = tid; item < total; item += kMultiBlock) {
+            int i = 0, k = item;
+            for (int n = pass_beams(sh, jj); k >= n; n = pass_beams(sh, i * (A - 1) + jj)) {
+                k -= n;
+                ++i;
+            }
             const int pr = i * (A - 1) + jj;
             const int n0 = sh.rng[pr][1] - sh.rng[pr][0] + 1;
-            const int n1 = sh.rng[pr][3] - sh.rng[pr][2] + 1;
-            const int nb = (n0 > 0 ? n0 : 0) + (n1 > 0 ? n1 : 0);
+            const int b = k < (n0 > 0 ? n0 : 0) ? sh.rng[pr][0] + k : sh.rng[pr][2] + k - (n0 > 0 ? n0 : 0);
             const double ox = sh.stl[i][0], oy = sh.stl[i][1], oth = sh.stl[i][4];
             const double *v = sh.rv[pr];
-            const double wc = sh.wcen[pr], wh = sh.whalf[pr];
-            for (int k = tid; k < nb; k += kMultiBlock) {
-                const int b = k < (n0 > 0 ? n0 : 0) ? sh.rng[pr][0] + k : sh.rng[pr][2] + k - (n0 > 0 ? n0 : 0);
-                if (!(fabs(wrap_pm_pi(oth + a.angles[b] - wc)) <= wh)) continue;  // box_beam_window
-                const double bt = oth + a.angles[b] + kPi / 2.;
-                const double v30 = cos(bt), v31 = sin(bt);
-                double cur = scan[i * B + b];
-                const double cur0 = cur;
+            const double ang = beam_angle(b, a.fov, a.beam_incr);
+            if (!(fabs(wrap_pm_pi(oth + ang - sh.wcen[pr])) <= sh.whalf[pr])) continue;  // box_beam_window
+            const double bt = oth + ang + kPi / 2.;
+            const double v30 = cos(bt), v31 = sin(bt);
+            double cur = scan[i * B + b];
+            const double cur0 = cur;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int q1 = (q + 1) & 3;
-                    const double rr = get_range(ox, oy, v30, v31, v[2 * q], v[2 * q + 1], v[2 * q1], v[2 * q1 + 1]);
-                    if (rr < cur) cur = rr;
-                }
-                if (cur != cur0) {  // patch the ray pass's outputs for this beam
-                    scan[i * B + b] = cur;
-                    const size_t o = ((size_t)e * A + i) * B + b;
-                    if (a.out.scans) a.out.scans[o] = (float)cur;
-                    if (a.out.scans_f64) a.out.scans_f64[o] = cur;
-                    if (i == 0 && a.out.obs) a.out.obs[(size_t)e * (B + 4 * A) + b] = obs_scan_value(cur, (float)a.p.lidar_max);
-                }
+            for (int q = 0; q < 4; ++q) {
+                const int q1 = (q + 1) & 3;
+                const double rr = get_range(ox, oy, v30, v31, v[2 * q], v[2 * q + 1], v[2 * q1], v[2 * q1 + 1]);
+                if (rr < cur) cur = rr;
+            }
+            if (cur != cur0) {  // patch the ray pass's outputs for this beam
+                scan[i * B + b] = cur;
+                const size_t o = ((size_t)e * A + i) * B + b;
+                if (a.out.scans) a.out.scans[o] = (float)cur;
+                if (a.out.scans_f64) a.out.scans_f64[o] = cur;
+                if (i == 0 && a.out.obs) a.out.obs[(size_t)e * (B + 4 * A) + b] = obs_scan_value(cur, (float)a.p.lidar_max);
             }
         }
         __syncthreads();
