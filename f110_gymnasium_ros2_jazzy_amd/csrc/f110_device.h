@@ -298,8 +298,19 @@ __device__ __forceinline__ uint32_t tiled_index_u24(int32_t wt, int32_t r, int32
            ((uint32_t)c & 3u);
 }
 
+// the same cell as a byte offset into the f64 table (the << 3 folded into
+// the bit assembly)
+__device__ __forceinline__ uint32_t tiled_offset_u24(int32_t wt, int32_t r, int32_t c) {
+    const uint32_t tile = (__umul24((uint32_t)r >> 2, (uint32_t)wt) + ((uint32_t)c >> 2)) << 7;
+    const uint32_t rc = (((uint32_t)r & 3u) << 2) | ((uint32_t)c & 3u);  // 4-bit cell within the tile
+    return tile | (rc << 3);
+}
+
+// oob8: the byte offset of m.oob (m.oob << 3), passed by the caller so that a
+// loop can keep it in a VGPR (the select below cannot read it from an SGPR
+// next to its VCC condition)
 template <bool ROT>
-__device__ __forceinline__ double tiled_lookup(const TiledMapView &m, double x, double y) {
+__device__ __forceinline__ double tiled_lookup(const TiledMapView &m, double x, double y, uint32_t oob8) {
     double xr = x - m.ox;
     double yr = y - m.oy;
     if (ROT) {
@@ -315,25 +326,27 @@ __device__ __forceinline__ double tiled_lookup(const TiledMapView &m, double x, 
     const double fx = qx - floor(qx), fy = qy - floor(qy);
 #endif
     const double band = fmax(fabs(fx - 0.5), fabs(fy - 0.5));
-    const bool slow = inb && band > 0.5 - 1e-9;
-    const uint32_t fast = tiled_index_u24(m.wt, (int32_t)qy, (int32_t)qx);  // garbage off-map, masked below
+    const bool near = band > 0.5 - 1e-9;  // the guard band of trunc_div (off-map lanes filtered inside)
+    const uint32_t fast = tiled_offset_u24(m.wt, (int32_t)qy, (int32_t)qx);  // garbage off-map, masked below
     const uint32_t sel = 0u - (uint32_t)inb;  // branchless select: no exec-mask split per iteration
-    uint32_t idx = (fast & sel) | ((uint32_t)m.oob & ~sel);
+    uint32_t off = (fast & sel) | (oob8 & ~sel);
 #if defined(__HIP_DEVICE_COMPILE__)
-    if (__builtin_amdgcn_ballot_w64(slow))  // wave-uniform, rare: the guard band of trunc_div
+    // wave-uniform, rare; the ballot of a bare compare is its lane mask (no
+    // VGPR round trip, as a ballot of (inb && near) would need)
+    if (__builtin_amdgcn_ballot_w64(near))
 #endif
     {
-        if (slow) {
+        if (near && inb) {
             int32_t c = (int32_t)(xr / m.res);
             int32_t r = (int32_t)(yr / m.res);
             if (c >= m.W) {  // see tiled_cell
                 c = 0;
                 ++r;
             }
-            idx = r >= m.H ? (uint32_t)m.oob : tiled_index_u24(m.wt, r, c);
+            off = r >= m.H ? oob8 : tiled_offset_u24(m.wt, r, c);
         }
     }
-    return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(m.dt) + (idx << 3));
+    return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(m.dt) + off);
 }
 
 // ------------------------------------------------------ beam index runs --

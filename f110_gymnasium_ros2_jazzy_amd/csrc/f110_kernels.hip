@@ -281,45 +281,71 @@ __device__ __forceinline__ const RayArgs *kernarg_rays() {
 #endif
 }
 
-// One lane's ray of k_rays_tiled: beam index, trace_ray's loop
-// (laser_models.py:106-146) with the given EDT lookup, clamp, noise, TTC
-// flag, outputs.  Returns the lookups made.
+// Lookup statistics of one wave's trace, the same in every lane: lookups
+// made, lanes that traced a ray, the longest ray's lookups.
+struct WaveLookups {
+    uint32_t total, lanes, max;
+};
+
+// One wave's rays of k_rays_tiled (a lane traces when `has`): beam index,
+// trace_ray's loop (laser_models.py:106-146) with the given EDT lookup,
+// clamp, noise, TTC flag, outputs.  The loop runs on wave-uniform control
+// (while any lane is still tracing), so its counters live in SGPRs: no
+// per-lane lookup counter in the loop body.
 template <bool HANDOFF, class Lookup>
-__device__ __forceinline__ uint32_t trace_lane(const RayArgs &a, int g, int b, int e, int64_t r, Lookup lookup) {
+__device__ __forceinline__ WaveLookups trace_wave(const RayArgs &a, bool has, int g, int b, int e, int64_t r,
+                                                  Lookup lookup) {
+    const uint64_t hm = __builtin_amdgcn_ballot_w64(has);
+    WaveLookups w{0u, (uint32_t)__popcll(hm), 0u};
+    if (!hm) return w;
     const int B = a.B;
-    double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
-    int ti = (int)t;  // int(theta_index), laser_models.py:124
-    if (ti >= a.theta_dis) ti = 0;
-    const double c = a.cosines[ti], s = a.sines[ti];
-    double x = a.ray0[g], y = a.ray0[a.EA + g];
-    double d = a.ray0[2 * a.EA + g];  // :129
-    double tot = d;                   // :130
-    // the TTC operands are loaded before the loop, which hides their
-    // latency (the epilogue would otherwise wait on them)
-    const double v = a.vel[g], bcos = a.beam_cos[b], side = a.side[b];
-    // the ray's scan noise does not depend on the trace: drawn (or loaded)
-    // here, it overlaps the set-up loads above
-    double noise = 0.0;
-    {
+    double c = 0.0, s = 0.0, x = 0.0, y = 0.0, d = 0.0, v = 0.0, bcos = 0.0, side = 0.0, noise = 0.0;
+    if (has) {
+        double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
+        int ti = (int)t;  // int(theta_index), laser_models.py:124
+        if (ti >= a.theta_dis) ti = 0;
+        c = a.cosines[ti];
+        s = a.sines[ti];
+        x = a.ray0[g];
+        y = a.ray0[a.EA + g];
+        d = a.ray0[2 * a.EA + g];  // :129
+        // the TTC operands are loaded before the loop, which hides their
+        // latency (the epilogue would otherwise wait on them)
+        v = a.vel[g];
+        bcos = a.beam_cos[b];
+        side = a.side[b];
+        // the ray's scan noise does not depend on the trace: drawn (or
+        // loaded) here, it overlaps the set-up loads above
         const RayArgs &K = *kernarg_rays();
         if (K.noise_ext)
             noise = K.noise_ext[(size_t)e * B + b];
         else if (K.noise_std > 0.0)
             noise = K.noise_std * (double)beam_normal(K.seed, (uint64_t)(K.env_offset + e), K.noise_step[e], b);
     }
-    uint32_t k = 1;
+    double tot = d;  // :130 (lanes without a ray: d = 0, never traced)
     const double eps = a.eps, mr = a.max_range;
-    while (d > eps && tot <= mr) {  // :133
-        x += d * c;                 // :135
-        y += d * s;                 // :136
-        d = lookup(x, y);
-        tot += d;                   // :141
-        ++k;
+    uint32_t iters = 0, lane_iters = 0;
+    for (;;) {
+        const bool act = d > eps && tot <= mr;  // :133 (no loop-carried mask)
+        // ballots of the bare compares are their lane masks (a ballot of the
+        // conjunction would go through a VGPR)
+        const uint64_t m = __builtin_amdgcn_ballot_w64(d > eps) & __builtin_amdgcn_ballot_w64(tot <= mr);
+        if (!m) break;
+        ++iters;
+        lane_iters += (uint32_t)__popcll(m);
+        if (act) {
+            x += d * c;  // :135
+            y += d * s;  // :136
+            d = lookup(x, y);
+            tot += d;    // :141
+        }
     }
+    w.total = w.lanes + lane_iters;  // the first lookup of every ray came from k_agents
+    w.max = 1u + iters;
+    if (!has) return w;
     // Epilogue fields are read through the kernarg pointer HERE, after the
     // loop: argument loads would otherwise sit at kernel entry and stay live
-    // in SGPRs across the loop (84 instead of 68 SGPRs: 7 instead of 8
-    // blocks per CU).
+    // in SGPRs across the loop.
     const RayArgs &K = *kernarg_rays();
     double range = tot > mr ? mr : tot;  // :143-144
     if (K.noise_ext || K.noise_std > 0.0) range += noise;  // noise after the clamp (see store_ray)
@@ -332,7 +358,7 @@ __device__ __forceinline__ uint32_t trace_lane(const RayArgs &a, int g, int b, i
     if (K.scans_f32) K.scans_f32[r] = (float)range;
     if (K.scans_f64) K.scans_f64[r] = range;
     if (HANDOFF) K.scan[r] = range;
-    return k;
+    return w;
 }
 
 // ------------------------------------------------------------------------
@@ -397,17 +423,21 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
         g = (int)(r / B);
         b = (int)(r - (int64_t)g * B);
     }
-    uint32_t n = 0;
-    if (live) {
-        const int e = g / a.A;
-        if (!MASK || a.reset_mask[e])
-            n = trace_lane<HANDOFF>(a, g, b, e, r, [&](double x, double y) { return tiled_lookup<ROT>(a.m, x, y); });
+    const int e = live ? g / a.A : 0;
+    const bool has = live && (!MASK || a.reset_mask[e]);
+    // the off-map cell index in a VGPR for the whole trace (an opaque copy:
+    // otherwise it is re-materialised by a v_mov in every loop iteration)
+    uint32_t oobv;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(oobv) : "s"((uint32_t)a.m.oob << 3));
+    const WaveLookups w = trace_wave<HANDOFF>(a, has, g, b, e, r,
+                                              [&](double x, double y) { return tiled_lookup<ROT>(a.m, x, y, oobv); });
+    if ((threadIdx.x & 63) == 0 && w.lanes) {  // one (lookups, rays) atomic pair per wave
+        unsigned long long *slot = kernarg_rays()->ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+        atomicAdd(slot, (unsigned long long)w.total);
+        atomicAdd(slot + 1, (unsigned long long)w.lanes);
     }
-    count_rays(kernarg_rays()->ctr, n);
     if (CH) {  // this wave's cost, the next step's heavy-first prediction
-        uint32_t m = n;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+        const uint32_t m = w.lanes ? w.max : 0u;
         uint8_t *wc = kernarg_rays()->wcost;
         if (wc && (threadIdx.x & 63) == 0 && g < a.EA)
             wc[(size_t)g * a.nch + (b >> 6)] = (uint8_t)(m < 255u ? m : 255u);
