@@ -272,6 +272,80 @@ __global__ void __launch_bounds__(kHB) k_wgrad_finish(HeadArgs a) {
     }
 }
 
+// ReLU backward of a hidden layer fused with its bias gradient: gz =
+// threshold_backward(gy, y, 0) (gy where y > 0, else 0) and db = sum_rows gz
+// (per-block partials over kWRows rows, thread: column quad x row lane, then
+// k_colsum_finish).  Replaces torch's threshold_backward + sum(0) launches.
+__global__ void __launch_bounds__(kHB) k_relu_bwd(const float *gy, const float *y, float *gz, float *part, int32_t B,
+                                                  int32_t K) {
+    __shared__ float red[kHB][4];
+    const int Q = (K + 3) / 4;
+    const int lanes = kHB / Q;
+    const int q = threadIdx.x % Q, rl = threadIdx.x / Q;
+    const int64_t r0 = (int64_t)blockIdx.x * kWRows;
+    const int64_t r1 = r0 + kWRows < B ? r0 + kWRows : B;
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (rl < lanes) {
+        const int k = 4 * q;
+        for (int64_t r = r0 + rl; r < r1; r += lanes) {
+            float g4[4], y4[4];
+            if ((K & 3) == 0) {
+                const float4 gv = *reinterpret_cast<const float4 *>(gy + r * K + k);
+                const float4 yv = *reinterpret_cast<const float4 *>(y + r * K + k);
+                g4[0] = gv.x, g4[1] = gv.y, g4[2] = gv.z, g4[3] = gv.w;
+                y4[0] = yv.x, y4[1] = yv.y, y4[2] = yv.z, y4[3] = yv.w;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    g4[i] = k + i < K ? gy[r * K + k + i] : 0.0f;
+                    y4[i] = k + i < K ? y[r * K + k + i] : 0.0f;
+                }
+            }
+            float z4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                z4[i] = y4[i] > 0.0f ? g4[i] : 0.0f;
+                acc[i] += z4[i];
+            }
+            if ((K & 3) == 0) {
+                *reinterpret_cast<float4 *>(gz + r * K + k) = make_float4(z4[0], z4[1], z4[2], z4[3]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (k + i < K) gz[r * K + k + i] = z4[i];
+            }
+        }
+    }
+    if (!part) return;  // block-uniform
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[threadIdx.x][i] = acc[i];
+    __syncthreads();
+    if (threadIdx.x < Q) {
+        float sum[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sum[i] = red[threadIdx.x][i];
+        for (int l2 = 1; l2 < lanes; ++l2)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sum[i] += red[l2 * Q + threadIdx.x][i];
+        const int k = 4 * threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (k + i < K) part[(size_t)blockIdx.x * K + k + i] = sum[i];
+    }
+}
+
+// out[c] = sum of the nblk partials of column c (one wave per column, fixed order)
+__global__ void __launch_bounds__(kHB) k_colsum_finish(const float *part, int32_t nblk, int32_t K, float *out) {
+    const int64_t c = (int64_t)blockIdx.x * (kHB / 64) + (threadIdx.x >> 6);
+    if (c >= K) return;  // whole wave
+    const int lane = threadIdx.x & 63;
+    float s = 0.0f;
+    for (int i = lane; i < nblk; i += 64) s += part[(size_t)i * K + c];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (lane == 0) out[c] = s;
+}
+
 template <class F>
 hipError_t with_nout(int nout, F f) {
     switch (nout) {
@@ -318,6 +392,28 @@ extern "C" int64_t f110_ddpg_scratch_floats(int32_t B, int32_t K, int32_t nout) 
     const int64_t nblk_r = (B + kRowsPerBlock - 1) / kRowsPerBlock;
     const int64_t part = nblk_w * nout * (K + 1) > nblk_r ? nblk_w * nout * (K + 1) : nblk_r;
     return (int64_t)B * nout + part;
+}
+
+extern "C" int64_t f110_ddpg_relu_bwd_scratch_floats(int32_t B, int32_t K) {
+    if (B <= 0 || K <= 0 || K > 4 * kHB) return -1;
+    return (int64_t)((B + kWRows - 1) / kWRows) * K;
+}
+
+extern "C" int f110_ddpg_relu_bwd(const float *gy, const float *y, int32_t B, int32_t K, float *gz, float *db,
+                                  float *scratch, void *stream) {
+    if (B <= 0 || K <= 0 || K > 4 * kHB || (K + 3) / 4 > kHB || !gy || !y || !gz || (db && !scratch))
+        return fail_arg("f110_ddpg_relu_bwd");
+    const int nblk = (B + kWRows - 1) / kWRows;
+    hipLaunchKernelGGL(k_relu_bwd, dim3((unsigned)nblk), dim3(kHB), 0, (hipStream_t)stream, gy, y, gz,
+                       db ? scratch : nullptr, B, K);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && db) {
+        const int per = kHB / 64;
+        hipLaunchKernelGGL(k_colsum_finish, dim3((unsigned)((K + per - 1) / per)), dim3(kHB), 0, (hipStream_t)stream,
+                           scratch, nblk, K, db);
+        e = hipGetLastError();
+    }
+    return e == hipSuccess ? 0 : fail_hip("f110_ddpg_relu_bwd", e);
 }
 
 extern "C" int f110_ddpg_actor_head(const float *h, const float *W, const float *b, const float *scale,

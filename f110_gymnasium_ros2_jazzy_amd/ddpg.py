@@ -56,9 +56,10 @@ class _LinearReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, W, y = ctx.saved_tensors
-        gz = torch.ops.aten.threshold_backward(gy, y, 0)
         nx, nw, nb = ctx.needs_input_grad
-        return (gz.mm(W) if nx else None, gz.t().mm(x) if nw else None, gz.sum(0) if nb else None)
+        from .ddpg_heads import relu_bwd
+        gz, db = relu_bwd(gy, y, nb)  # one HIP pass: threshold_backward + the bias gradient's column sums
+        return (gz.mm(W) if nx else None, gz.t().mm(x) if nw else None, db)
 
 
 def _linear_relu(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:

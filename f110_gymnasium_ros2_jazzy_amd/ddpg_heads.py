@@ -167,3 +167,19 @@ def td_target(h, W, b, r, d, gamma: float):
     _lib.check(L.f110_ddpg_td_target(_p(h), _p(W), _p(b), _p(r), _p(d), float(gamma), B, K, _p(y), _stream(h)),
                "f110_ddpg_td_target")
     return y
+
+
+def relu_bwd(gy, y, need_db: bool = True):
+    """(threshold_backward(gy, y, 0), its column sums or None) in one pass."""
+    L = _lib.load()
+    gy, y = gy.contiguous(), y.contiguous()
+    B, K = y.shape
+    gz = torch.empty_like(y)
+    db = torch.empty(K, dtype=torch.float32, device=y.device) if need_db else None
+    m = L.f110_ddpg_relu_bwd_scratch_floats(B, K)
+    if m < 0:
+        raise _lib.F110Error(f"relu_bwd: unsupported shape B={B} K={K}")
+    scratch = torch.empty(int(m), dtype=torch.float32, device=y.device) if need_db else None
+    _lib.check(L.f110_ddpg_relu_bwd(_p(gy), _p(y), B, K, _p(gz), _p(db), _p(scratch), _stream(y)),
+               "f110_ddpg_relu_bwd")
+    return gz, db

@@ -422,6 +422,13 @@ F110_API int f110_ddpg_critic_loss_bwd(const float *h, const float *W, const flo
 /* loss = sign * mean(h W^T + b)  (sign -1: the actor loss) */
 F110_API int f110_ddpg_q_mean(const float *h, const float *W, const float *b, float sign, int32_t B, int32_t K,
                               float *loss, float *scratch, void *stream);
+/* A hidden layer's ReLU backward with its bias gradient (agent.py's F.relu(fc(x))
+ * under autograd): gz = gy where y > 0 else 0 (torch threshold_backward), db =
+ * sum_rows gz (db may be null).  gy, y, gz: [B][K]; K <= 1024; scratch:
+ * f110_ddpg_relu_bwd_scratch_floats(B, K) floats. */
+F110_API int64_t f110_ddpg_relu_bwd_scratch_floats(int32_t B, int32_t K);
+F110_API int f110_ddpg_relu_bwd(const float *gy, const float *y, int32_t B, int32_t K, float *gz, float *db,
+                                float *scratch, void *stream);
 /* dq = sign * (g / B); dh, dW, db from dq (h only needed for dW / db) */
 F110_API int f110_ddpg_q_mean_bwd(const float *h, const float *W, const float *g, float sign, int32_t B, int32_t K,
                                   float *dh, float *dW, float *db, float *scratch, void *stream);
