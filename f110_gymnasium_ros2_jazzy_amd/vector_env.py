@@ -86,6 +86,10 @@ class F110VectorEnv:
                 raise ValueError("opponent needs num_agents >= 2 and 0 <= opponent_idx < num_agents")
             self._act = torch.zeros(self.num_envs, A, 2, dtype=torch.float32, device=self.device)
             self._others = [i for i in range(A) if i != self.opponent_idx]
+            # a contiguous run of caller-driven agents is written with a slice
+            # copy (one strided copy kernel) instead of an index_put
+            o = self._others
+            self._others_sl = slice(o[0], o[-1] + 1) if o and o == list(range(o[0], o[-1] + 1)) else o
 
     def _opponent_next(self, out):
         """Next step's opponent action from this step's scans (train_ddpg.py:168)."""
@@ -134,8 +138,8 @@ class F110VectorEnv:
             if a.dim() == 2:
                 a = a.reshape(self.num_envs, len(self._others), 2)
             if a.shape[1] == self.num_agents:
-                a = a[:, self._others]
-            self._act[:, self._others] = a.to(torch.float32)
+                a = a[:, self._others_sl]
+            self._act[:, self._others_sl] = a
             a = self._act
         elif a.dim() == 2 and self.num_agents == 1:
             a = a.unsqueeze(1)
