@@ -28,6 +28,14 @@ def _p(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+
+def _as_u8(t: torch.Tensor) -> torch.Tensor:
+    """Flat uint8 flags; a contiguous bool tensor is reinterpreted (no copy)."""
+    t = t.reshape(-1)
+    if t.dtype == torch.bool and t.is_contiguous():
+        return t.view(torch.uint8)
+    return t.to(torch.uint8).contiguous()
+
 class DeviceReplayBuffer:
     def __init__(self, buffer_size: int, batch_size: int, alpha: float = 0.6, seed: int = 42,
                  priority_epsilon: float = 1e-6, obs_dim: int = 1088, act_dim: int = 2, device=0,
@@ -84,8 +92,8 @@ class DeviceReplayBuffer:
         a = self._rows(actions, self.act_dim)
         n = s.shape[0]
         r = torch.as_tensor(rewards, device=self.device).reshape(-1).to(torch.float32).contiguous()
-        d = None if dones is None else torch.as_tensor(dones, device=self.device).reshape(-1).to(torch.uint8).contiguous()
-        m = None if mask is None else torch.as_tensor(mask, device=self.device).reshape(-1).to(torch.uint8).contiguous()
+        d = None if dones is None else _as_u8(torch.as_tensor(dones, device=self.device))
+        m = None if mask is None else _as_u8(torch.as_tensor(mask, device=self.device))
         pr = None if priority is None else \
             torch.as_tensor(priority, device=self.device).reshape(-1).to(torch.float32).contiguous()
         if (pr is not None and pr.shape[0] != n) or ns.shape[0] != n or a.shape[0] != n or r.shape[0] != n or (d is not None and d.shape[0] != n) or \

@@ -143,7 +143,8 @@ class BatchedCenterlineReward:
         o = o.reshape(self.n_envs, -1).contiguous()
         m = None
         if reset_mask is not None:
-            m = torch.as_tensor(reset_mask, device=self.device).to(torch.uint8).contiguous()
+            m = torch.as_tensor(reset_mask, device=self.device).reshape(-1)
+            m = m.view(torch.uint8) if m.dtype == torch.bool and m.is_contiguous() else m.to(torch.uint8).contiguous()
         self._keep = (o, m)
         s = torch.cuda.current_stream(self.device).cuda_stream
         _lib.check(self.L_lib.f110_reward(

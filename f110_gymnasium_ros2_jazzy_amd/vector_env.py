@@ -145,11 +145,10 @@ class F110VectorEnv:
             a = a.unsqueeze(1)
         out = self.sim.step(a)
         self._opponent_next(out)
-        reset = out.was_reset.bool()
-        if self.reward_fn is not None:  # reset envs: reward_fn.reset(), reward 0
-            rewards = self.reward_fn(out.obs, reset_mask=reset).clone()
+        if self.reward_fn is not None:  # reset envs: reward_fn.reset(), reward 0 (the u8 flags as they are)
+            rewards = self.reward_fn(out.obs, reset_mask=out.was_reset).clone()
         else:
-            rewards = torch.where(reset, torch.zeros((), dtype=torch.float64, device=self.device),
+            rewards = torch.where(out.was_reset.bool(), torch.zeros((), dtype=torch.float64, device=self.device),
                                   torch.full((), self.timestep, dtype=torch.float64, device=self.device))
         term = out.terminated.bool()
         trunc = torch.zeros_like(term)
