@@ -107,7 +107,7 @@ __device__ __forceinline__ double bdot(double a0, double a1, double b0, double b
 // the query, merged as above; the result is final when every midpoint
 // outside the block is provably farther than the 5th found one (distance to
 // the block's edge, less a margin, above it).  r = 1, then 2, then 4; past
-// that (or off the grid) the full scan runs.  The same 5 (and order) as the
+// that the full scan runs.  The same 5 (and order) as the
 // full scan.  A grid row's cells are consecutive in cell order, so a block is
 // 2r+1 item ranges: their bounds load together, every lane then takes items
 // of the concatenated ranges from the cell-ordered midpoint copy.
@@ -117,8 +117,12 @@ __device__ void nearest_mids_grid(const TrackView &T, double px, double py, int 
     const int32_t M = T.n - 1;
     const double fx = (px - T.gx0) / T.gh, fy = (py - T.gy0) / T.gh;
     bool ok = false;
-    if (T.cell_start && fx >= 0.0 && fy >= 0.0 && fx < (double)T.gnx && fy < (double)T.gny) {
-        const int32_t ci = (int32_t)fx, cj = (int32_t)fy;
+    // a point off the grid searches from the nearest edge cell: the block's
+    // sides on the grid border are clipped (no midpoints beyond them) and
+    // the point lies inside every other side, so the bound below still holds
+    if (T.cell_start && fx == fx && fy == fy) {
+        const int32_t ci = fx < 0.0 ? 0 : (fx >= (double)(T.gnx - 1) ? T.gnx - 1 : (int32_t)fx);
+        const int32_t cj = fy < 0.0 ? 0 : (fy >= (double)(T.gny - 1) ? T.gny - 1 : (int32_t)fy);
         for (int32_t r = 1; r <= (kMaxBlockRows - 1) / 2 && !ok; r *= 2) {
             // the block clipped to the grid: a clipped side needs no bound
             const int32_t i0 = ci - r < 0 ? 0 : ci - r, i1 = ci + r >= T.gnx ? T.gnx - 1 : ci + r;
