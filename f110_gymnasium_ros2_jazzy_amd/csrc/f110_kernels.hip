@@ -754,7 +754,7 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ void __launch_bounds__(kMultiBlock) k_post_multi(StepArgs a) {
+__global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
     reset_next_heavy(a);
     __shared__ MultiShared sh;
     const int e = blockIdx.x;
