@@ -13,7 +13,8 @@
 //   find_max_gap     :21-39 runs of p > 0.5; first run of maximal end-start
 //   best point / action :41-58
 //
-// The 1080 beams are split into 64 contiguous lane chunks.  The run search is
+// Each wave keeps one LDS row (the preprocessed scan) and synchronises only
+// itself.  The 1080 beams are split into 64 contiguous lane chunks.  The run search is
 // a two-pass chunked scan: each lane finds the last run start in its chunk, a
 // wave-wide exclusive prefix max hands every lane the start of the run that
 // enters its chunk, and each lane then measures the runs that end inside it.
@@ -33,6 +34,14 @@ struct MinAt {
 };
 
 __device__ __forceinline__ int32_t shfl_xor_i(int32_t v, int m) { return __shfl_xor(v, m, 64); }
+
+// LDS hand-off between the lanes of ONE wave (each wave owns its scan: no
+// workgroup barrier)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __device__ __forceinline__ float shfl_xor_f(float v, int m) { return __shfl_xor(v, m, 64); }
 
 }  // namespace
@@ -42,30 +51,26 @@ __global__ void __launch_bounds__(64 * kGfWaves) k_gap_follow(GapFollowArgs a) {
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int B = a.B;
-    float *r = reinterpret_cast<float *>(smem) + (size_t)wave * 2 * B;
-    float *p = r + B;
+    float *p = reinterpret_cast<float *>(smem) + (size_t)wave * B;  // one LDS row per wave (scan)
     const int64_t m = (int64_t)blockIdx.x * kGfWaves + wave;
     const bool live = m < a.M;  // wave-uniform
     const float *scan = a.scans + (live ? m : 0) * a.scan_stride;
 
-    if (live)
-        for (int i = lane; i < B; i += 64) r[i] = scan[i];
-    __syncthreads();
-    // preprocess_lidar (:3-12)
+    // preprocess_lidar (:3-12), the window read straight from the scan (L1 hits)
     if (live)
         for (int i = lane; i < B; i += 64) {
             const int s = i - 2 > 0 ? i - 2 : 0;
             const int e = i + 2 < B - 1 ? i + 2 : B - 1;
             float sum = 0.0f;
             for (int j = s; j <= e; ++j) {
-                float v = r[j];
+                float v = scan[j];
                 v = v < 0.0f ? 0.0f : v;  // np.clip(x, 0, 3.0); NaN passes through
                 v = v > 3.0f ? 3.0f : v;
                 sum = sum + v;
             }
             p[i] = __fdiv_rn(sum, (float)(e - s + 1));
         }
-    __syncthreads();
+    wave_lds_sync();
 
     const int C = (B + 63) / 64;  // chunk per lane
     const int c0 = lane * C;
@@ -92,11 +97,11 @@ __global__ void __launch_bounds__(64 * kGfWaves) k_gap_follow(GapFollowArgs a) {
     const int cp = nan_i != INT32_MAX ? nan_i : (mn.i != INT32_MAX ? mn.i : 0);
     const int bs = cp - 30 > 0 ? cp - 30 : 0;
     const int be = cp + 30 < B - 1 ? cp + 30 : B - 1;
-    __syncthreads();
+    wave_lds_sync();
     if (live)
         for (int i = lane; i < B; i += 64)
             if (i >= bs && i <= be) p[i] = 0.0f;
-    __syncthreads();
+    wave_lds_sync();
 
     // find_max_gap (:21-39)
     auto mask = [&](int i) { return i >= 0 && i < B && p[i] > 0.5f; };
@@ -155,7 +160,7 @@ __global__ void __launch_bounds__(64 * kGfWaves) k_gap_follow(GapFollowArgs a) {
     }
 }
 
-size_t gap_follow_lds_bytes(int B) { return sizeof(float) * 2 * (size_t)B * kGfWaves; }
+size_t gap_follow_lds_bytes(int B) { return sizeof(float) * (size_t)B * kGfWaves; }
 
 hipError_t launch_gap_follow(const GapFollowArgs &a, hipStream_t s) {
     if (a.M <= 0) return hipSuccess;
