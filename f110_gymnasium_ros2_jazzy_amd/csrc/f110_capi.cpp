@@ -75,6 +75,7 @@ struct f110_ctx {
     uint32_t *heavy_list = nullptr, *heavy_mask = nullptr, *heavy_count = nullptr;
     int32_t heavy_cap = 0, heavy_T = 24, nch = 0;  // F110_HEAVY_T; measured: 20-32 equal, 40 +1%, 16 +11%
     uint64_t launch_n = 0;
+    int ray_wpb = 1;  // F110_RAY_WPB: 1 (one-wave blocks, default) or 4
     int64_t wtrace_n = 0;
     bool wtrace_armed = false;
 
@@ -442,6 +443,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     ALLOC(c->ctr, (size_t)kCtrSlots * kCtrStride);
     ALLOC(c->pa, (size_t)C.n_agents);
     if (spawn_poses && n_spawn > 0) ALLOC(c->spawn, (size_t)n_spawn * C.n_agents * 3);
+    if (const char *v = std::getenv("F110_RAY_WPB")) c->ray_wpb = std::atoi(v) == 1 ? 1 : 4;
     if (const char *v = std::getenv("F110_HEAVY_T")) c->heavy_T = std::atoi(v);  // 0: no heavy-first dispatch
     if (c->ray_kernel == 2 && c->heavy_T > 0) {
         // up to 1/8 of the waves, in blocks of 4 (measured: ~7% of the waves
@@ -503,6 +505,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.map = map_view(c);
     a.tmap = tiled_view(c);
     a.ray_kernel = c->ray_kernel;
+    a.ray_wpb = c->ray_wpb;
     for (int i = 0; i < kMaxChunks; ++i) a.chunk_order[i] = c->chunk_order[i];
     a.sines = c->sines;
     a.cosines = c->cosines;

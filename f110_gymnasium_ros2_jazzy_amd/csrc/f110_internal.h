@@ -26,6 +26,7 @@ struct StepArgs {
     f110_params p;                            // Simulator / F110Env params (GJK boxes, lidar_max)
     const f110_params *pa;                    // [A] RaceCar params (update_pose, ray_cast boxes)
     int32_t E, A, B, theta_dis, integrator, ego, autoreset, mode;  // mode 0 step, 1 reset
+    int32_t ray_wpb;          // chunked ray kernel: waves (cars) per block, 1 or 4 (F110_RAY_WPB)
     int32_t ray_kernel;       // 0: k_rays on the row-major EDT; 1: k_rays_tiled, flat ray order; 2: chunked
     uint8_t chunk_order[kMaxChunks];  // beam-chunk dispatch order of the chunked ray kernel
     uint64_t *wtrace;         // diagnostic wave trace of the next ray launch (f110_debug_wave_trace) or null
@@ -110,6 +111,7 @@ struct RayArgs {
     const uint32_t *heavy_mask;
     const uint32_t *heavy_count;
     int32_t HB, nch;
+    int32_t wpb;  // chunked: waves (cars) per block
 };
 
 struct ScanArgs {

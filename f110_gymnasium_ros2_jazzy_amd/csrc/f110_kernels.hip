@@ -401,7 +401,7 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
         const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
         int k;
         if ((int)blockIdx.x < a.HB) {  // heavy-first blocks: the listed waves
-            const uint32_t item = (uint32_t)blockIdx.x * 4 + wave;
+            const uint32_t item = (uint32_t)blockIdx.x * a.wpb + wave;
             if (item >= *a.heavy_count) return;  // wave-uniform: nothing listed here
             const uint32_t v = __builtin_amdgcn_readfirstlane(a.heavy_list[item]);
             g = (int)(v >> 8);
@@ -410,7 +410,7 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
             const int blk = (int)blockIdx.x - a.HB;
             const int slot = blk / a.G4;
             const int cg = blk - slot * a.G4;
-            g = cg * 4 + wave;
+            g = cg * a.wpb + wave;
             k = (int)a.order[slot];
             if (a.HB && g < a.EA && ((a.heavy_mask[g] >> k) & 1u)) return;  // ran in a heavy block
         }
@@ -956,12 +956,13 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         const bool ch = a.ray_kernel == 2;
         dim3 g2 = grid;
         if (ch) {
-            ra.G4 = (EA + 3) / 4;
+            ra.wpb = a.ray_wpb;
+            ra.G4 = (EA + ra.wpb - 1) / ra.wpb;
             ra.nch = (a.B + 63) / 64;
             for (int i = 0; i < kMaxChunks; ++i) ra.order[i] = a.chunk_order[i];
             ra.wcost = a.wcost;
             if (a.heavy_use && !mask) {
-                ra.HB = (a.heavy_cap + 3) / 4;
+                ra.HB = (a.heavy_cap + ra.wpb - 1) / ra.wpb;
                 ra.heavy_list = a.heavy_list + (size_t)a.parity * a.heavy_cap;
                 ra.heavy_mask = a.heavy_mask;
                 ra.heavy_count = a.heavy_count + a.parity;
@@ -992,7 +993,8 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
             f = single ? reinterpret_cast<const void *>(&k_rays_tiled<false, false, false, true, true>)
                        : reinterpret_cast<const void *>(&k_rays_tiled<false, false, true, true, true>);
         ra.wtrace = a.wtrace;
-        if ((e = hipLaunchKernel(f, g2, dim3(kBlock), args, 0, s)) != hipSuccess) return e;
+        const unsigned bdim = ch ? 64u * (unsigned)ra.wpb : (unsigned)kBlock;
+        if ((e = hipLaunchKernel(f, g2, dim3(bdim), args, 0, s)) != hipSuccess) return e;
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;

@@ -57,6 +57,7 @@ variants = {"flat": {"F110_RAY_KERNEL": "1"},
             "heavy16": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "16"},
             "heavy20": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "20"},
             "heavy24": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "24"},
+            "heavy24_wpb4": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "24", "F110_RAY_WPB": "4"},
             "heavy32": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "32"},
             "heavy40": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "40"},
             "heavy64": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "64"},
@@ -66,7 +67,7 @@ if os.environ.get("AB_ONLY"):
     variants = {k: v for k, v in variants.items() if k in os.environ["AB_ONLY"].split(",")}
 sims = {}
 for name, env in variants.items():
-    for k in ("F110_RAY_KERNEL", "F110_CHUNK_ORDER", "F110_HEAVY_T"):
+    for k in ("F110_RAY_KERNEL", "F110_CHUNK_ORDER", "F110_HEAVY_T", "F110_RAY_WPB"):
         os.environ.pop(k, None)
     os.environ.update(env)
     sims[name] = BatchSim(tm, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp,
