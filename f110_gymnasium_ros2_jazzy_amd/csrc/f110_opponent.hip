@@ -26,7 +26,7 @@ namespace f110 {
 
 namespace {
 
-constexpr int kGfWaves = 4;  // scans per 256-thread block
+constexpr int kGfWaves = 1;  // scans per block (one-wave blocks)
 
 struct MinAt {
     float v;

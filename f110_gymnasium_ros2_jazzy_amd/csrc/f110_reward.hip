@@ -25,7 +25,7 @@ namespace f110 {
 
 namespace {
 
-constexpr int kRwWaves = 4;  // envs per 256-thread block
+constexpr int kRwWaves = 1;  // envs per block: one-wave blocks free their slot as the env finishes
 constexpr int kTop = 5;      // kd.query(p, k=5)
 
 struct Cand {
