@@ -58,6 +58,10 @@ variants = {"flat": {"F110_RAY_KERNEL": "1"},
             "heavy20": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "20"},
             "heavy24": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "24"},
             "heavy24_wpb4": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "24", "F110_RAY_WPB": "4"},
+            "heavy24_asc": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "24",
+                            "F110_CHUNK_ORDER": ",".join(str(k) for k in range(17))},
+            "heavy24_centre": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "24",
+                               "F110_CHUNK_ORDER": "8,9,7,10,6,11,5,12,4,13,3,14,2,15,1,16,0"},
             "heavy32": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "32"},
             "heavy40": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "40"},
             "heavy64": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "64"},
