@@ -160,6 +160,144 @@ __global__ void __launch_bounds__(64 * kGfWaves) k_gap_follow(GapFollowArgs a) {
     }
 }
 
+// The same policy with the chunk passes in registers (B <= 64 * kGfMaxC):
+// the scan is staged in LDS once (coalesced), lane l computes the window
+// means of its beams [l*C, (l+1)*C), C = ceil(B/64), into registers, and the
+// bubble / run passes work on those and a per-lane bit mask (runs of
+// p > 0.5), the neighbours' edge bits coming by shuffle.  One wave per
+// scan, no workgroup barrier; same arithmetic and tie rules as k_gap_follow.
+constexpr int kGfMaxC = 17;
+
+__global__ void __launch_bounds__(64) k_gap_follow_reg(GapFollowArgs a) {
+    __shared__ float r[64 * kGfMaxC];  // the scan, then the window means
+    __shared__ float pm[64 * kGfMaxC];
+    const int lane = threadIdx.x;
+    const int B = a.B;
+    const int64_t m = blockIdx.x;
+    const float *gscan = a.scans + m * a.scan_stride;
+    for (int i = lane; i < B; i += 64) r[i] = gscan[i];
+    wave_lds_sync();
+    // preprocess_lidar (:3-12) in the coalesced layout
+    for (int i = lane; i < B; i += 64) {
+        const int s = i - 2 > 0 ? i - 2 : 0;
+        const int e = i + 2 < B - 1 ? i + 2 : B - 1;
+        float sum = 0.0f;
+        for (int q = s; q <= e; ++q) {
+            float v = r[q];
+            v = v < 0.0f ? 0.0f : v;  // np.clip(x, 0, 3.0); NaN passes through
+            v = v > 3.0f ? 3.0f : v;
+            sum = sum + v;
+        }
+        pm[i] = __fdiv_rn(sum, (float)(e - s + 1));
+    }
+    wave_lds_sync();
+    const int C = (B + 63) / 64;
+    const int c0 = lane * C;
+    const int c1 = c0 + C < B ? c0 + C : B;
+    const int n = c1 > c0 ? c1 - c0 : 0;  // beams of this lane
+    // this lane's chunk into registers (stride C across lanes, C odd for
+    // B = 1080: no bank conflicts)
+    float p[kGfMaxC];
+#pragma unroll
+    for (int j = 0; j < kGfMaxC; ++j) p[j] = j < n ? pm[c0 + j] : 0.0f;
+    // create_bubble (:14-19): np.argmin -> first NaN if any, else first minimum
+    int32_t nan_i = INT32_MAX;
+    MinAt mn{INFINITY, INT32_MAX};
+#pragma unroll
+    for (int j = 0; j < kGfMaxC; ++j)
+        if (j < n) {
+            const float v = p[j];
+            if (v != v) {
+                if (c0 + j < nan_i) nan_i = c0 + j;
+            } else if (mn.i == INT32_MAX || v < mn.v) {
+                mn = MinAt{v, c0 + j};
+            }
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        nan_i = min(nan_i, shfl_xor_i(nan_i, o));
+        const float ov = shfl_xor_f(mn.v, o);
+        const int32_t oi = shfl_xor_i(mn.i, o);
+        if (oi != INT32_MAX && (mn.i == INT32_MAX || ov < mn.v || (ov == mn.v && oi < mn.i))) mn = MinAt{ov, oi};
+    }
+    const int cp = nan_i != INT32_MAX ? nan_i : (mn.i != INT32_MAX ? mn.i : 0);
+    const int bs = cp - 30 > 0 ? cp - 30 : 0;
+    const int be = cp + 30 < B - 1 ? cp + 30 : B - 1;
+    // runs of p > 0.5 after the bubble: bit j = beam c0 + j
+    uint32_t mk = 0;
+#pragma unroll
+    for (int j = 0; j < kGfMaxC; ++j) {
+        const int i = c0 + j;
+        const bool bubble = i >= bs && i <= be;
+        if (j < n && !bubble && p[j] > 0.5f) mk |= 1u << j;
+    }
+    // mask(c0 - 1): the previous lane's last beam; mask(c1): the next lane's first
+    const uint32_t prev_mk = __shfl_up(mk, 1, 64), prev_n = (uint32_t)__shfl_up(n, 1, 64);
+    const bool before = lane > 0 && prev_n > 0 && ((prev_mk >> (prev_n - 1)) & 1u);
+    const uint32_t next_mk = __shfl_down(mk, 1, 64);
+    const bool after = lane < 63 && (next_mk & 1u);
+    // find_max_gap (:21-39): the last run start in this lane's chunk
+    int32_t last_start = -1;
+#pragma unroll
+    for (int j = 0; j < kGfMaxC; ++j) {
+        const bool mi = (mk >> j) & 1u;
+        const bool mp = j == 0 ? before : ((mk >> (j - 1)) & 1u);
+        if (j < n && mi && !mp) last_start = c0 + j;
+    }
+    int32_t incl = last_start;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t up = __shfl_up(incl, o, 64);
+        if (lane >= o) incl = max(incl, up);
+    }
+    int32_t cur = __shfl_up(incl, 1, 64);
+    if (lane == 0) cur = -1;
+    int32_t best_len = -1, best_start = INT32_MAX;
+#pragma unroll
+    for (int j = 0; j < kGfMaxC; ++j) {
+        if (j < n) {
+            const bool mi = (mk >> j) & 1u;
+            const bool mp = j == 0 ? before : ((mk >> (j - 1)) & 1u);
+            const bool mx = j == n - 1 ? after : ((mk >> (j + 1)) & 1u);
+            if (mi && !mp) cur = c0 + j;
+            if (mi && !mx) {
+                const int32_t len = c0 + j - cur;
+                if (len > best_len) {
+                    best_len = len;
+                    best_start = cur;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int32_t ol = shfl_xor_i(best_len, o);
+        const int32_t os = shfl_xor_i(best_start, o);
+        if (ol > best_len || (ol == best_len && os < best_start)) {
+            best_len = ol;
+            best_start = os;
+        }
+    }
+    if (lane == 0) {
+        int32_t g0 = 0, g1 = B - 1;  // no gap: the whole scan (:36-37)
+        if (best_len >= 0) {
+            g0 = best_start;
+            g1 = best_start + best_len;
+        }
+        const int32_t best = (g0 + g1) / 2;                                  // :41-42
+        const double steer = a.angle_min + (double)best * a.angle_increment;  // :47
+        const double sa = fabs(steer);
+        const double speed = sa < 10.0 * (kPi / 180.0) ? 2.5 : (sa < 20.0 * (kPi / 180.0) ? 2.0 : 1.5);  // :49-54
+        float *act = a.actions + m * a.action_stride;
+        act[0] = (float)steer;  // train_ddpg.py:168 .astype(np.float32)
+        act[1] = (float)speed;
+        if (a.gaps) {
+            a.gaps[2 * m] = g0;
+            a.gaps[2 * m + 1] = g1;
+        }
+    }
+}
+
 size_t gap_follow_lds_bytes(int B) { return sizeof(float) * (size_t)B * kGfWaves; }
 
 hipError_t launch_gap_follow(const GapFollowArgs &a, hipStream_t s) {
@@ -169,6 +307,10 @@ hipError_t launch_gap_follow(const GapFollowArgs &a, hipStream_t s) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_gap_follow),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
+    }
+    if (a.B <= 64 * kGfMaxC) {  // register-resident scan
+        hipLaunchKernelGGL(k_gap_follow_reg, dim3((unsigned)a.M), dim3(64), 0, s, a);
+        return hipGetLastError();
     }
     const dim3 grid((unsigned)((a.M + kGfWaves - 1) / kGfWaves));
     hipLaunchKernelGGL(k_gap_follow, grid, dim3(64 * kGfWaves), lds, s, a);
