@@ -73,7 +73,7 @@ struct f110_ctx {
     // heavy-first ray dispatch (chunked kernel)
     uint8_t *wcost = nullptr;
     uint32_t *heavy_list = nullptr, *heavy_mask = nullptr, *heavy_count = nullptr;
-    int32_t heavy_cap = 0, heavy_T = 24, nch = 0;  // F110_HEAVY_T; measured: 20-32 equal, 40 +1%, 16 +11%
+    int32_t heavy_cap = 0, heavy_T = 16, nch = 0;  // F110_HEAVY_T (with one-wave blocks and a 1/6 list: 16 best)
     uint64_t launch_n = 0;
     int ray_wpb = 1;  // F110_RAY_WPB: 1 (one-wave blocks, default) or 4
     int64_t wtrace_n = 0;
@@ -448,7 +448,9 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (c->ray_kernel == 2 && c->heavy_T > 0) {
         // up to 1/8 of the waves, in blocks of 4 (measured: ~7% of the waves
         // have a ray longer than 40 lookups and carry ~46% of the wave-iterations)
-        c->heavy_cap = (int32_t)std::max<size_t>(64, (EA * (size_t)c->nch / 8 + 3) / 4 * 4);
+        size_t div = 6;  // F110_HEAVY_DIV: list capacity = 1/div of the waves
+        if (const char *v = std::getenv("F110_HEAVY_DIV")) div = (size_t)std::max(1, std::atoi(v));
+        c->heavy_cap = (int32_t)std::max<size_t>(64, (EA * (size_t)c->nch / div + 3) / 4 * 4);
         ALLOC(c->wcost, EA * (size_t)c->nch);
         ALLOC(c->heavy_list, 2 * (size_t)c->heavy_cap);
         ALLOC(c->heavy_mask, EA);

@@ -58,6 +58,12 @@ variants = {"flat": {"F110_RAY_KERNEL": "1"},
             "heavy20": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "20"},
             "heavy24": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "24"},
             "heavy24_wpb4": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "24", "F110_RAY_WPB": "4"},
+            "heavy24_div12": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "24", "F110_HEAVY_DIV": "12"},
+            "heavy24_div16": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "24", "F110_HEAVY_DIV": "16"},
+            "heavy20_div8": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "20"},
+            "heavy16_div6": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "16", "F110_HEAVY_DIV": "6"},
+            "heavy20_div6": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "20", "F110_HEAVY_DIV": "6"},
+            "heavy16_div4": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "16", "F110_HEAVY_DIV": "4"},
             "heavy24_asc": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "24",
                             "F110_CHUNK_ORDER": ",".join(str(k) for k in range(17))},
             "heavy24_centre": {"F110_RAY_KERNEL": "2", "F110_HEAVY_T": "24",
@@ -71,7 +77,7 @@ if os.environ.get("AB_ONLY"):
     variants = {k: v for k, v in variants.items() if k in os.environ["AB_ONLY"].split(",")}
 sims = {}
 for name, env in variants.items():
-    for k in ("F110_RAY_KERNEL", "F110_CHUNK_ORDER", "F110_HEAVY_T", "F110_RAY_WPB"):
+    for k in ("F110_RAY_KERNEL", "F110_CHUNK_ORDER", "F110_HEAVY_T", "F110_RAY_WPB", "F110_HEAVY_DIV"):
         os.environ.pop(k, None)
     os.environ.update(env)
     sims[name] = BatchSim(tm, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp,
