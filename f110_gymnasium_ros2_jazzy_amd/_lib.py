@@ -64,7 +64,7 @@ EXPORTS = [
     "f110_replay_sample", "f110_replay_update_priorities", "f110_replay_length", "f110_replay_arrays",
     "f110_debug_wave_trace", "f110_adam_step", "f110_ddpg_scratch_floats", "f110_ddpg_actor_head",
     "f110_ddpg_actor_head_bwd", "f110_ddpg_td_target", "f110_ddpg_critic_loss", "f110_ddpg_critic_loss_bwd",
-    "f110_ddpg_q_mean", "f110_ddpg_q_mean_bwd", "f110_ddpg_relu_bwd_scratch_floats", "f110_ddpg_relu_bwd",
+    "f110_ddpg_q_mean", "f110_ddpg_q_mean_bwd", "f110_ddpg_relu_bwd_scratch_floats", "f110_ddpg_relu_bwd", "f110_ddpg_linear_relu",
 ]
 
 _lib = None
@@ -155,6 +155,7 @@ def load(build_if_missing: bool = True):
     L.f110_ddpg_q_mean_bwd.argtypes = [_P] * 3 + [f32, i32, i32] + [_P] * 5
     L.f110_ddpg_relu_bwd_scratch_floats.argtypes = [i32, i32]
     L.f110_ddpg_relu_bwd.argtypes = [_P, _P, i32, i32, _P, _P, _P, _P]
+    L.f110_ddpg_linear_relu.argtypes = [_P, _P, _P, i32, i32, i32, _P, _P]
     for name in EXPORTS:
         if name not in ("f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config",
                         "f110_host_tables", "f110_host_window_ranges", "f110_track_arrays",

@@ -36,6 +36,12 @@ import torch.nn.functional as F
 # as relu(linear(x))) and their output layers as the fused learner heads of
 # ddpg_heads.py.  F110_DDPG_FUSED=0 keeps the plain torch modules (A/B runs).
 FUSED = os.environ.get("F110_DDPG_FUSED", "1") != "0"
+# F110_DDPG_MFMA=1: hidden layers with K % 32 == 0 and 32-multiple widths
+# (fc1, fc2, fcs1) run forward on csrc/f110_ddpg.hip's fp32 matrix-core
+# kernel instead of BLAS.  Off by default: it ties hipBLASLt at the learner's
+# batch (20.0 vs 20.6 us, M = 4096, K = 1088) and loses at M = 8192 and at
+# K = 128 (learner).
+MFMA_HIDDEN = os.environ.get("F110_DDPG_MFMA", "0") == "1"
 
 
 def _fused(x: torch.Tensor) -> bool:
@@ -49,7 +55,11 @@ class _LinearReLU(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, W, b):
-        y = torch._addmm_activation(b, x, W.t())
+        from .ddpg_heads import linear_relu, linear_relu_ok
+        if MFMA_HIDDEN and linear_relu_ok(x, W):
+            y = linear_relu(x, W, b)  # csrc/f110_ddpg.hip k_linear_relu (matrix cores, fp32)
+        else:
+            y = torch._addmm_activation(b, x, W.t())
         ctx.save_for_backward(x, W, y)
         return y
 

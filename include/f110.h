@@ -422,6 +422,11 @@ F110_API int f110_ddpg_critic_loss_bwd(const float *h, const float *W, const flo
 /* loss = sign * mean(h W^T + b)  (sign -1: the actor loss) */
 F110_API int f110_ddpg_q_mean(const float *h, const float *W, const float *b, float sign, int32_t B, int32_t K,
                               float *loss, float *scratch, void *stream);
+/* A hidden layer's forward, y = relu(x W^T + b) on the fp32 matrix cores
+ * (replaces F.relu(self.fc1(obs)) etc., rl_training/DDPG/agent.py:55-56, :93, :95):
+ * x [M][K], W [N][K], b [N], y [M][N]; K a multiple of 32, N of 32. */
+F110_API int f110_ddpg_linear_relu(const float *x, const float *W, const float *b, int32_t M, int32_t K, int32_t N,
+                                   float *y, void *stream);
 /* A hidden layer's ReLU backward with its bias gradient (agent.py's F.relu(fc(x))
  * under autograd): gz = gy where y > 0 else 0 (torch threshold_backward), db =
  * sum_rows gz (db may be null).  gy, y, gz: [B][K]; K <= 1024; scratch:
