@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--cpu-envs", type=int, default=512)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=12345)
+    ap.add_argument("--streams", type=int, default=2,
+                    help="sub-shards of the GPU's envs on concurrent dedicated-queue streams "
+                         "(streams.StreamShards); 1 = one context on the current stream")
     ap.add_argument("--workload", choices=["step", "ddpg"], default="step",
                     help="step: the env step (headline); ddpg: config 5, the batched train_ddpg loop")
     ap.add_argument("--ddpg-batch", type=int, default=4096)
@@ -219,28 +222,45 @@ def main():
     acts[..., 0] = acts[..., 0] * (2 * 0.4189) - 0.4189   # steer in [-0.4189, 0.4189]
     acts[..., 1] = acts[..., 1] * 20.0                   # speed in [0, 20] (ddpg_config.yaml:19-20)
     stream = torch.cuda.current_stream(dev)
+    S = max(1, args.streams)
+    runner = sim
+    if S > 1:
+        from f110_gymnasium_ros2_jazzy_amd.streams import StreamShards
+        runner = StreamShards(track, n_envs=shard.count, n_streams=S, env_offset=shard.offset, n_agents=A,
+                              device=dev, seed=args.seed, noise_std=0.0 if args.no_noise else 0.01,
+                              autoreset=True, spawn_poses=spawn)
 
-    sim.reset(poses0)
-    for w in range(W):
-        sim.step(acts[w], minimal_outputs=True)
-    torch.cuda.synchronize(dev)
-    sim.reset_counters()
-    D.barrier()
-    torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for k in range(K):
-        sim.step(acts[W + k], minimal_outputs=True)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    D.barrier()
-    elapsed = D.max_over_ranks(t1 - t0)
-    kernel_ms = ev0.elapsed_time(ev1) / K
-    lookups, rays = sim.read_counters()
+    def timed(r):
+        """W untimed steps, then K steps between barrier + synchronize (max over ranks)."""
+        r.reset(poses0)
+        for w in range(W):
+            r.step(acts[w], minimal_outputs=True)
+        torch.cuda.synchronize(dev)
+        r.reset_counters()
+        D.barrier()
+        torch.cuda.synchronize(dev)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for k in range(K):
+            r.step(acts[W + k], minimal_outputs=True)
+        if r is not sim:
+            r.join()
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        D.barrier()
+        return D.max_over_ranks(t1 - t0), ev0.elapsed_time(ev1) / K, r.read_counters()
+
+    elapsed, kernel_ms, (lookups, rays) = timed(runner)
     mean_look = lookups / max(rays, 1)
     total_env_steps = D.sum_over_ranks(shard.count * K)
+    single = None
+    if runner is not sim:
+        # the same workload on one context / one stream, for comparison (not `value`)
+        el1, _, _ = timed(sim)
+        single = {"value": total_env_steps / el1, "ms_per_step": el1 / K * 1e3}
+        runner.close()
 
     # second, separate pass: per-kernel HIP-event timing (not part of `value`)
     KP = min(K, 300)
@@ -276,6 +296,7 @@ def main():
             "envs_per_gpu": E, "global_envs": E * world, "agents": A, "beams": B, "map": args.map,
             "integrator": "RK4", "scan_noise": not args.no_noise, "autoreset": True,
             "parallelism": f"env-shard x{world} (no collectives)",
+            "streams_per_gpu": S,
         },
         "roofline": {
             "kernel": "k_rays", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -287,6 +308,8 @@ def main():
             "step_algorithmic_bytes_per_env": bytes_launch / max(shard.count, 1),
         },
     }
+    if single is not None:
+        result["single_stream"] = single
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(track, poses0, acts[:64].cpu().numpy(), args, sim)

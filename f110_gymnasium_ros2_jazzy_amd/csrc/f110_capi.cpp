@@ -70,6 +70,8 @@ struct f110_ctx {
     int prof_max = 0, prof_n = 0;
     const double *noise_ext = nullptr;  // f110_set_scan_noise (caller-owned)
     uint64_t *wtrace = nullptr;         // f110_debug_wave_trace buffer (diagnostics)
+    hipEvent_t gate_wait = nullptr;     // f110_set_ray_gate (caller-owned events)
+    hipEvent_t gate_record = nullptr;
     // heavy-first ray dispatch (chunked kernel)
     uint8_t *wcost = nullptr;
     uint32_t *heavy_list = nullptr, *heavy_mask = nullptr, *heavy_count = nullptr;
@@ -569,6 +571,8 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
         a.heavy_cap = c->heavy_cap;
         a.heavy_T = c->heavy_T;
     }
+    a.gate_wait = c->gate_wait;
+    a.gate_record = c->gate_record;
     if (c->wtrace_armed) {  // one traced ray launch
         a.wtrace = c->wtrace;
         c->wtrace_armed = false;
@@ -602,6 +606,13 @@ extern "C" int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dty
     else
         a.actions = static_cast<const float *>(actions);
     HIP_TRY(launch_env_step(a, (hipStream_t)stream, ctx->next_prof_events()));
+    return F110_OK;
+}
+
+extern "C" int f110_set_ray_gate(f110_ctx *ctx, void *wait_event, void *record_event) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_gate: null context");
+    ctx->gate_wait = static_cast<hipEvent_t>(wait_event);
+    ctx->gate_record = static_cast<hipEvent_t>(record_event);
     return F110_OK;
 }
 

@@ -30,6 +30,8 @@ struct StepArgs {
     int32_t ray_kernel;       // 0: k_rays on the row-major EDT; 1: k_rays_tiled, flat ray order; 2: chunked
     uint8_t chunk_order[kMaxChunks];  // beam-chunk dispatch order of the chunked ray kernel
     uint64_t *wtrace;         // diagnostic wave trace of the next ray launch (f110_debug_wave_trace) or null
+    hipEvent_t gate_wait;     // f110_set_ray_gate: waited on before the ray launch, or null
+    hipEvent_t gate_record;   // f110_set_ray_gate: recorded after the ray launch, or null
     // heavy-first ray dispatch (chunked kernel): per (car, chunk) wave cost of
     // the previous ray launch, this step's list of predicted-heavy waves
     uint8_t *wcost;           // [EA][nch] min(255, longest ray of the wave) or null

@@ -911,6 +911,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     hipLaunchKernelGGL(k_agents, dim3((EA + 63) / 64), dim3(64), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
+    if (a.gate_wait && (e = hipStreamWaitEvent(s, a.gate_wait, 0)) != hipSuccess) return e;
     const int64_t R = (int64_t)EA * a.B;
     const dim3 grid((unsigned)((R + kBlock - 1) / kBlock));
     // tiled kernel: TTC in the ray pass; single-agent envs also write their
@@ -997,6 +998,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         if ((e = hipLaunchKernel(f, g2, dim3(bdim), args, 0, s)) != hipSuccess) return e;
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (a.gate_record && (e = hipEventRecord(a.gate_record, s)) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;
     if (single)
         hipLaunchKernelGGL(k_post_single, dim3((a.E + 63) / 64), dim3(64), 0, s, a);

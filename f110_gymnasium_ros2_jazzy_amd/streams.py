@@ -1,0 +1,128 @@
+"""Sub-shards of one GPU's env batch stepped on concurrent HIP streams.
+
+Envs never interact across env ids, so a GPU's shard of E envs
+can be stepped as S contiguous sub-shards, one `BatchSim` context each, on S
+streams that are never joined between steps.  Sub-shard s then starts step
+t+1 while another is still tracing step t: the latency-bound launches
+(k_agents / k_post_single, one thread per car) and the ray kernel's tail
+(the few grazing-beam waves) run beside another sub-shard's ray
+pass instead of leaving CUs idle.  Results are those of one E-env context:
+the RNG streams are keyed by global env id (`env_offset`), so every
+sub-shard reproduces its slice of the single-context run bit for bit
+(`tests/test_gpu_env.py::test_stream_shards_match_single_context`).
+
+Each stream is created with a full CU mask (`hipExtStreamCreateWithCUMask`),
+which gives it a hardware queue of its own: streams handed out round-robin
+from a shared pool can land on one queue, which serialises the sub-shards in
+submission order and runs them in lock-step (measured 27-33 M env-steps/s
+instead of 41; `scripts/stream_split.py`).
+
+This is a throughput mode for callers whose actions are already resident
+(random-action rollouts, the bench): a consumer that reads the obs of step t
+before choosing the actions of step t+1 joins every step, which measured
+slower than one context (`scripts/stream_split.py --join 1`).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from .sim import BatchSim
+
+_hip = None
+
+
+def _hip_lib():
+    global _hip
+    if _hip is None:
+        _hip = ctypes.CDLL("libamdhip64.so")
+    return _hip
+
+
+def dedicated_stream(device: torch.device) -> torch.cuda.ExternalStream:
+    """A stream with a hardware queue of its own (full CU mask)."""
+    hip = _hip_lib()
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    words = (ncu + 31) // 32
+    mask = (ctypes.c_uint32 * words)(*([0xFFFFFFFF] * words))
+    h = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(words), mask)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    return torch.cuda.ExternalStream(h.value, device=device)
+
+
+class StreamShards:
+    """S BatchSim sub-shards of an E-env batch on S dedicated streams.
+
+    `step(actions[E, A, 2])` launches every sub-shard on its own stream and
+    returns without joining; `join()` makes the caller's current stream wait
+    for all of them (do that before reading `obs`)."""
+
+    def __init__(self, track, n_envs: int, n_streams: int = 2, env_offset: int = 0, **kw):
+        if n_streams < 1 or n_envs % n_streams:
+            raise ValueError(f"n_envs ({n_envs}) must split evenly into n_streams ({n_streams})")
+        self.S = n_streams
+        self.E = n_envs
+        self.Es = n_envs // n_streams
+        self.device = torch.device(kw.get("device", "cuda"))
+        self.streams = [dedicated_stream(self.device) for _ in range(self.S)]
+        self.sims = []
+        for s in range(self.S):
+            with torch.cuda.stream(self.streams[s]):
+                self.sims.append(BatchSim(track, n_envs=self.Es, env_offset=env_offset + s * self.Es, **kw))
+        self._sl = [slice(s * self.Es, (s + 1) * self.Es) for s in range(self.S)]
+        self._fork()
+
+    def _fork(self):
+        # whatever the caller's stream produced so far (inputs) precedes every sub-shard's work
+        ev = torch.cuda.current_stream(self.device).record_event()
+        for st in self.streams:
+            st.wait_event(ev)
+
+    def reset(self, poses):
+        self._fork()
+        for s in range(self.S):
+            with torch.cuda.stream(self.streams[s]):
+                self.sims[s].reset(poses[self._sl[s]])
+
+    def step(self, actions, minimal_outputs: bool = True):
+        for s in range(self.S):
+            with torch.cuda.stream(self.streams[s]):
+                self.sims[s].step(actions[self._sl[s]], minimal_outputs=minimal_outputs)
+
+    def join(self):
+        cur = torch.cuda.current_stream(self.device)
+        for st in self.streams:
+            cur.wait_event(st.record_event())
+
+    @property
+    def obs(self) -> torch.Tensor:
+        self.join()
+        return torch.cat([sm.out.obs for sm in self.sims], 0)
+
+    def read_counters(self):
+        self.join()
+        lk = rays = 0
+        for sm in self.sims:
+            a, b = sm.read_counters()
+            lk += a
+            rays += b
+        return lk, rays
+
+    def reset_counters(self):
+        self._fork()
+        for s in range(self.S):
+            with torch.cuda.stream(self.streams[s]):
+                self.sims[s].reset_counters()
+
+    def close(self):
+        torch.cuda.synchronize(self.device)
+        for sm in self.sims:
+            sm.close()
+        hip = _hip_lib()
+        for st in self.streams:
+            hip.hipStreamDestroy(ctypes.c_void_p(st.cuda_stream))
+        self.streams = []

@@ -218,6 +218,16 @@ F110_API int f110_profile_end(f110_ctx *ctx, double ms_out[3], int32_t *steps_ou
 F110_API int f110_debug_wave_trace(f110_ctx *ctx, int32_t arm, uint64_t *host_out, int64_t max_waves,
                                    int64_t *n_waves, void *stream);
 
+/* Ray gate for sub-shards stepped on concurrent streams (one context per
+ * sub-shard, one stream each).  A non-null wait_event is waited on (stream
+ * side) before every following f110_step / f110_reset ray launch of this
+ * context; a non-null record_event is recorded right after it.  Chaining
+ * the sub-shards' events in a ring keeps their ray passes in order (never two
+ * ray grids competing for the CUs) while their k_agents / k_post launches run
+ * beside another sub-shard's ray pass.  Events are caller-owned hipEvent_t;
+ * NULL, NULL turns the gate off.  Scheduling only: results are unchanged. */
+F110_API int f110_set_ray_gate(f110_ctx *ctx, void *wait_event, void *record_event);
+
 /* ---- opponent policy -------------------------------------------------------
  * Replaces gap_follow_action (rl_training/utils/gap_follow.py:3-58), the
  * rule-based opponent train_ddpg.py:168 computes on the host each step from

@@ -6,7 +6,8 @@
 
 1. kernel trace + stats of `bench.py` (same command as the headline, fewer
    steps, no cpu leg) -> profiles/<tag>_kernel_stats.csv (+ summary json)
-2. PMC passes, one counter group per run (FETCH_SIZE, WRITE_SIZE,
+   (+ k_rays averages split by grid size: sub-shard vs isolated launches)
+2. PMC passes (bench --streams 1: every k_rays launch is the isolated E-car one), one counter group per run (FETCH_SIZE, WRITE_SIZE,
    TCC_HIT/TCC_MISS): per-launch HBM-side bytes of k_rays -> profiles/pmc_traffic.json
    FETCH_SIZE/WRITE_SIZE are in KiB per dispatch (rocprofv3 derived counters).
 The parent process never touches the GPU; rocprofv3 launches python itself.
@@ -23,12 +24,12 @@ BENCH = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "300", "--wa
 env = dict(os.environ, TMPDIR="/tmp")
 
 
-def run(name, extra, timeout=400):
+def run(name, extra, timeout=400, bench_extra=()):
     d = os.path.join(OUT, name)
     if COLLECT:
         return d
     shutil.rmtree(d, ignore_errors=True)
-    cmd = ["rocprofv3"] + extra + ["--output-format", "csv", "-d", d, "-o", "run", "--"] + BENCH
+    cmd = ["rocprofv3"] + extra + ["--output-format", "csv", "-d", d, "-o", "run", "--"] + BENCH + list(bench_extra)
     print(" ".join(cmd), flush=True)
     with open(os.path.join(OUT, f"{name}.log"), "w") as log:
         subprocess.run(["timeout", "-k", "10", str(timeout)] + cmd, cwd="/tmp", env=env, stdout=log,
@@ -68,13 +69,29 @@ with open(stats) as f:
     for row in csv.DictReader(f):
         summary[row["Name"][:80]] = {k: row[k] for k in ("Calls", "TotalDurationNs", "AverageNs", "Percentage")
                                      if k in row}
+# the default bench launches k_rays at two grid sizes: the timed region's
+# sub-shards (E/S cars each, concurrent streams) and the isolated full-shard
+# roofline pass (E cars, one stream).  Split the averages by grid size so the
+# roofline's kernel_ms can be matched against the E-car launches.
+trace = find(d, "kernel_trace.csv")
+by_grid = {}
+with open(trace) as f:
+    for row in csv.DictReader(f):
+        if "k_rays" not in row.get("Kernel_Name", ""):
+            continue
+        g = next((row[k] for k in ("Grid_Size_X", "Grid_Size", "Grid_X") if k in row), "?")
+        dur = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+        e = by_grid.setdefault(str(g), [0, 0.0])
+        e[0] += 1
+        e[1] += dur
+summary["k_rays_by_grid_size"] = {g: {"Calls": n, "AverageNs": t / n} for g, (n, t) in by_grid.items()}
 json.dump(summary, open(os.path.join(PROF, f"{tag}_kernel_stats.json"), "w"), indent=1)
 
 res = {"kernel": "k_rays", "envs": 8192, "agents": 1}
 for grp in (["FETCH_SIZE"], ["WRITE_SIZE"], ["TCC_HIT_sum", "TCC_MISS_sum"]):
     name = "pmc_" + "_".join(g.lower() for g in grp)
     try:
-        dd = run(name, ["--pmc"] + grp)
+        dd = run(name, ["--pmc"] + grp, bench_extra=("--streams", "1"))  # the isolated E-car launch
         res.update(counters(dd, os.path.join(PROF, f"{tag}_{name}.csv")))
     except Exception as exc:  # record, do not hide
         res[name + "_error"] = repr(exc)

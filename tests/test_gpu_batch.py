@@ -154,3 +154,28 @@ def test_ray_kernel_dispatch_variants_identical(tracks, gpu, monkeypatch, A):
         for t, (a, b) in enumerate(zip(outs[0], rec)):
             for x, y in zip(a, b):
                 assert torch.equal(x, y), f"step {t}"
+
+
+def test_stream_shards_match_single_context(tracks, gpu):
+    """streams.StreamShards (bench.py's default timed runner): 4 sub-shards on
+    4 dedicated-queue streams, never joined between steps, end bit-identical
+    to one context stepping all envs (noise and autoreset on; the actions are
+    resident before the loop, as in the bench)."""
+    from f110_gymnasium_ros2_jazzy_amd.streams import StreamShards
+    E, A, T = 256, 1, 60
+    sp = _spawns(A)
+    rng = np.random.default_rng(11)
+    poses = sp[rng.integers(0, sp.shape[0], E)]
+    acts = torch.tensor(np.stack([rng.uniform(-0.4189, 0.4189, (T, E, A)), rng.uniform(0, 20, (T, E, A))], -1),
+                        dtype=torch.float32, device=gpu)
+    full = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=9)
+    sh = StreamShards(tracks("Spielberg_map"), n_envs=E, n_streams=4,
+                      n_agents=A, device=gpu, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=9)
+    full.reset(poses)
+    sh.reset(poses)
+    for t in range(T):
+        full.step(acts[t], minimal_outputs=True)
+        sh.step(acts[t], minimal_outputs=True)
+    assert torch.equal(sh.obs, full.out.obs)
+    assert sh.read_counters() == full.read_counters()
+    sh.close()
