@@ -70,6 +70,7 @@ struct f110_ctx {
     int prof_max = 0, prof_n = 0;
     const double *noise_ext = nullptr;  // f110_set_scan_noise (caller-owned)
     uint64_t *wtrace = nullptr;         // f110_debug_wave_trace buffer (diagnostics)
+    bool heavy_off = false;             // f110_disable_heavy_first
     hipEvent_t gate_wait = nullptr;     // f110_set_ray_gate (caller-owned events)
     hipEvent_t gate_record = nullptr;
     // heavy-first ray dispatch (chunked kernel)
@@ -600,12 +601,18 @@ extern "C" int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dty
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     StepArgs a = make_step_args(ctx, out);
     a.mode = 0;
-    a.heavy_build = a.heavy_use = (a.wcost && a.ray_kernel == 2) ? 1 : 0;  // f110_reset launches do not use it
+    a.heavy_build = a.heavy_use = (a.wcost && a.ray_kernel == 2 && !ctx->heavy_off) ? 1 : 0;  // not on resets
     if (actions_dtype == F110_F64)
         a.actions_f64 = static_cast<const double *>(actions);
     else
         a.actions = static_cast<const float *>(actions);
     HIP_TRY(launch_env_step(a, (hipStream_t)stream, ctx->next_prof_events()));
+    return F110_OK;
+}
+
+extern "C" int f110_disable_heavy_first(f110_ctx *ctx) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_disable_heavy_first: null context");
+    ctx->heavy_off = true;
     return F110_OK;
 }
 

@@ -9,7 +9,7 @@ t+1 while another is still tracing step t: the latency-bound launches
 pass instead of leaving CUs idle.  Results are those of one E-env context:
 the RNG streams are keyed by global env id (`env_offset`), so every
 sub-shard reproduces its slice of the single-context run bit for bit
-(`tests/test_gpu_env.py::test_stream_shards_match_single_context`).
+(`tests/test_gpu_batch.py::test_stream_shards_match_single_context`).
 
 Each stream is created with a full CU mask (`hipExtStreamCreateWithCUMask`),
 which gives it a hardware queue of its own: streams handed out round-robin
@@ -28,6 +28,7 @@ import ctypes
 
 import torch
 
+from . import _lib
 from .sim import BatchSim
 
 _hip = None
@@ -61,7 +62,8 @@ class StreamShards:
     returns without joining; `join()` makes the caller's current stream wait
     for all of them (do that before reading `obs`)."""
 
-    def __init__(self, track, n_envs: int, n_streams: int = 2, env_offset: int = 0, **kw):
+    def __init__(self, track, n_envs: int, n_streams: int = 2, env_offset: int = 0, heavy_first: bool = False,
+                 **kw):
         if n_streams < 1 or n_envs % n_streams:
             raise ValueError(f"n_envs ({n_envs}) must split evenly into n_streams ({n_streams})")
         self.S = n_streams
@@ -72,7 +74,12 @@ class StreamShards:
         self.sims = []
         for s in range(self.S):
             with torch.cuda.stream(self.streams[s]):
-                self.sims.append(BatchSim(track, n_envs=self.Es, env_offset=env_offset + s * self.Es, **kw))
+                sm = BatchSim(track, n_envs=self.Es, env_offset=env_offset + s * self.Es, **kw)
+                if not heavy_first and n_streams > 1:
+                    # the other sub-shard's ray pass fills this one's tail; heavy-first's list
+                    # upkeep then costs more than it saves (42.5 vs 41.8 M env-steps/s)
+                    _lib.check(sm.L.f110_disable_heavy_first(sm.ctx), "f110_disable_heavy_first")
+                self.sims.append(sm)
         self._sl = [slice(s * self.Es, (s + 1) * self.Es) for s in range(self.S)]
         self._fork()
 

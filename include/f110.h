@@ -228,6 +228,14 @@ F110_API int f110_debug_wave_trace(f110_ctx *ctx, int32_t arm, uint64_t *host_ou
  * NULL, NULL turns the gate off.  Scheduling only: results are unchanged. */
 F110_API int f110_set_ray_gate(f110_ctx *ctx, void *wait_event, void *record_event);
 
+/* Turns the heavy-first ray dispatch off for the following f110_step calls of
+ * this context (permanent).  Heavy-first starts the previous
+ * step's long waves first so one ray grid does not end on them; when another
+ * sub-shard's ray pass runs beside this one on a concurrent stream, that
+ * tail is filled anyway and the list upkeep is the larger cost.
+ * Scheduling only: results are unchanged. */
+F110_API int f110_disable_heavy_first(f110_ctx *ctx);
+
 /* ---- opponent policy -------------------------------------------------------
  * Replaces gap_follow_action (rl_training/utils/gap_follow.py:3-58), the
  * rule-based opponent train_ddpg.py:168 computes on the host each step from
