@@ -101,3 +101,14 @@ def test_gloo_world2_sharding_and_reductions():
         p.join(timeout=60)
     assert [r[1] for r in res] == [0, 8] and [r[2] for r in res] == [8, 8]
     assert all(r[3] == 1.5 for r in res) and all(r[4] == 160 for r in res)
+
+
+def test_stream_shards_rejects_uneven_split():
+    """streams.StreamShards splits the shard into equal contiguous sub-shards
+    (bench.py --streams); an uneven split is refused before any device work."""
+    import pytest
+    from f110_gymnasium_ros2_jazzy_amd.streams import StreamShards
+    with pytest.raises(ValueError):
+        StreamShards(None, n_envs=10, n_streams=3)
+    with pytest.raises(ValueError):
+        StreamShards(None, n_envs=8, n_streams=0)
