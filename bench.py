@@ -2,11 +2,15 @@
 """bench.py — env-steps/s of the batched F1TENTH step on MI355X.
 
 Metric (BASELINE.json): env-steps/sec at 65536 parallel envs, 1080-beam
-lidar; scan L2 vs CPU ref.  Weak scaling: every GPU steps the same shard of
---envs-per-gpu single-agent envs (8192 -> 65536 envs at 8 GPUs, the
-metric's configuration).  One "step" = one f110_step launch: ST dynamics
-(RK4) + 1080-beam EDT sphere-trace + TTC/GJK/ray_cast + obs pack for every
-env of the shard, with scan noise and device-side autoreset on.
+lidar; scan L2 vs CPU ref.  The job steps --global-envs (65536) single-agent
+envs split over the ranks (strong scaling: 65536 on one MI355X, 8192 per GPU
+at 8).  One "step" = one f110_step launch: ST dynamics (RK4) + 1080-beam EDT
+sphere-trace + TTC/GJK/ray_cast + obs pack for every env of the shard, with
+scan noise and device-side autoreset on.  At N=1 the line also carries the
+8192-env C3 shard and the 4096-env C2 workload (`secondary`), the one-stream
+runner a policy loop uses (`single_stream`), the scan check of the timed
+kernel against the CPU oracle (`scan_check`), the roofline and the CPU
+baseline.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -27,6 +31,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "env-steps/sec at 65536 parallel envs, 1080-beam lidar; scan L2 vs CPU ref"
+GLOBAL_ENVS = 65536
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -35,13 +40,19 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--envs-per-gpu", type=int, default=8192)
+    ap.add_argument("--global-envs", type=int, default=GLOBAL_ENVS,
+                    help="envs of the whole job, split over the ranks (the metric's 65536; strong scaling)")
+    ap.add_argument("--envs-per-gpu", type=int, default=None,
+                    help="fixed envs per rank instead (weak scaling); --workload ddpg defaults to 4096")
     ap.add_argument("--agents", type=int, default=1)
     ap.add_argument("--map", default="Spielberg_map")
     ap.add_argument("--no-noise", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-envs", type=int, default=512)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the C3-shard (8192) / C2 (4096) secondary lines at N=1")
+    ap.add_argument("--cpu-envs", type=int, default=4096)
+    ap.add_argument("--cpu-steps", type=int, default=1000)
+    ap.add_argument("--cpu-warmup", type=int, default=100)
     ap.add_argument("--seed", type=int, default=12345)
     ap.add_argument("--streams", type=int, default=2,
                     help="sub-shards of the GPU's envs on concurrent dedicated-queue streams "
@@ -64,7 +75,8 @@ def bench_ddpg(args):
     rank, world, local = D.init()
     dev_index = D.local_device_index(local)
     torch.cuda.set_device(dev_index)
-    shard = D.shard_range(args.envs_per_gpu * world, world, rank)
+    per_gpu = args.envs_per_gpu or 4096  # C5: 32768 envs over 8 GPUs
+    shard = D.shard_range(per_gpu * world, world, rank)
     K, W = args.steps, args.warmup
     # learner updates start once the memory holds a batch: ceil(batch / envs) steps
     fill = -(-args.ddpg_batch // max(shard.count, 1)) + 1
@@ -113,7 +125,7 @@ def bench_ddpg(args):
         "data": "synthetic: Spielberg map, centerline spawns, actor + Gaussian noise actions",
         "config": {"workload": f"{shard.count} two-agent envs per GPU (gap-follow opponent), device reward, "
                                f"PER replay, 1 learner update of {args.ddpg_batch} rows per vector step",
-                   "envs_per_gpu": args.envs_per_gpu, "global_envs": args.envs_per_gpu * world,
+                   "envs_per_gpu": per_gpu, "global_envs": per_gpu * world,
                    "batch_per_rank": args.ddpg_batch, "memory_per_rank": args.ddpg_memory,
                    "parallelism": f"env-shard x{world}, DDPG data-parallel (RCCL all-reduce of grads)"},
         "phases_ms": ph,
@@ -133,56 +145,96 @@ def algorithmic_bytes_per_env_step(B: int, A: int, mean_lookups: float) -> float
     return A * (B * (4.0 * mean_lookups + 4.0) + 120.0)
 
 
-def load_pmc_traffic(E: int, A: int):
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        if int(d.get("envs")) == E and int(d.get("agents")) == A:
-            return float(d["bytes_per_launch"]), d
-    except Exception:
-        pass
-    return None, None
+def load_profile(kind: str, E: int, A: int):
+    """A profiles/ summary recorded at this exact configuration (or None):
+    pmc_traffic (FETCH/WRITE bytes per k_rays launch, scripts/profile_round.py)
+    or pmc_busy (VALU busy / wave occupancy, scripts/profile_round.py)."""
+    for name in (f"{kind}_E{E}_A{A}.json", f"{kind}.json"):
+        path = os.path.join(REPO, "profiles", name)
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            if int(d.get("envs")) == E and int(d.get("agents")) == A:
+                d["file"] = "profiles/" + name
+                return d
+        except Exception:
+            pass
+    return None
 
 
-def cpu_baseline(track, spawn_poses, actions_np, args, gpu_sim):
-    """Oracle (C restatement, OpenMP) on the host cores; bounded sample."""
-    import numpy as np
+def cpu_threads() -> int:
+    t = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    return max(1, min(t, os.cpu_count() or t))
+
+
+def oracle_module():
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O  # noqa: E402  (test infrastructure: the checker, never the product)
     O.build()
-    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or threads))
-    sc = O.OracleScanner(track.free_mask, track.resolution, track.origin)
-    E = min(args.cpu_envs, spawn_poses.shape[0])
+    return O
+
+
+def cpu_baseline(O, scanner, poses, acts_np, args):
+    """The C oracle (oracle/f110_oracle.c, OpenMP over envs) on the host cores:
+    BASELINE.md §3's plan -- cpu_envs envs, cpu_warmup + cpu_steps steps, the
+    GPU run's seeded spawn poses and actions, scan noise on (a host draw)."""
+    threads = cpu_threads()
+    E = min(args.cpu_envs, poses.shape[0])
     A = args.agents
-    sim = O.OracleSim(sc, E, A)
-    sim.reset(spawn_poses[:E])
+    sim = O.OracleSim(scanner, E, A)
+    sim.set_noise(0.0 if args.no_noise else 0.01, args.seed)
+    sim.reset(poses[:E])
+    T = acts_np.shape[0]
+    for k in range(args.cpu_warmup):
+        sim.step(acts_np[k % T, :E], threads=threads)
     t0 = time.perf_counter()
-    sim.step(actions_np[0, :E], threads=threads)
-    t1 = time.perf_counter()
-    per = max(t1 - t0, 1e-4)
-    steps = int(max(2, min(2000, args.cpu_seconds / per)))
-    sim.reset(spawn_poses[:E])
-    t0 = time.perf_counter()
-    for k in range(steps):
-        sim.step(actions_np[k % actions_np.shape[0], :E], threads=threads)
+    for k in range(args.cpu_steps):
+        sim.step(acts_np[(args.cpu_warmup + k) % T, :E], threads=threads)
     dt = time.perf_counter() - t0
-    # scan parity at the GPU's current poses (the metric's "scan L2 vs CPU ref")
-    import torch
-    st = gpu_sim.agent_states()[:64].reshape(-1, 7).cpu().numpy()
-    poses = np.stack([st[:, 0], st[:, 1], st[:, 4]], 1)
-    g = gpu_sim.scan_batch(poses).cpu().numpy()
-    ref = sc.scan(poses, threads=threads)
-    diff = g - ref
     return {
-        "value": E * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-        "sample": f"{E} envs x {steps} steps ({args.agents} agent, {args.map}, RK4, noise-free), "
-                  f"C oracle oracle/f110_oracle.c, OpenMP over envs, {dt:.1f} s",
-        "scan_l2_vs_cpu": float(np.sqrt(np.sum(diff * diff))),
-        "scan_max_abs_vs_cpu": float(np.max(np.abs(diff))),
-        "scan_rays_compared": int(diff.size),
+        "value": E * args.cpu_steps / dt, "unit": "env-steps/s", "cores": threads, "nproc": os.cpu_count(),
+        "kind": "port",
+        "sample": f"{E} envs x {args.cpu_steps} steps after {args.cpu_warmup} warm-up ({A} agent, {args.map}, RK4, "
+                  f"noise {'off' if args.no_noise else 'on'}, the GPU run's spawn poses and actions), C oracle "
+                  f"oracle/f110_oracle.c, OpenMP over envs on {threads} threads, {dt:.1f} s timed",
     }
+
+
+def scan_check(O, scanner, runner, act, threads):
+    """Scan L2 of the TIMED kernel against the CPU oracle: one more step of the
+    timed runner (k_rays_tiled, same dispatch) with its f64 scan output on and
+    the noise zeroed through the caller-noise input (range + 0.0 is exact),
+    compared with oracle scans at the cars' post-step poses (the scan pose:
+    lidar_dist = 0).  Cars whose TTC fired are skipped: the collision response
+    zeroed their yaw after the scan (base_classes.py:246-249)."""
+    import numpy as np
+    import torch
+    sims = getattr(runner, "sims", [runner])
+    if sims[0].A != 1:
+        return {"skipped": "multi-agent: the agent ray_cast edits scans after the trace"}
+    for sm in sims:
+        sm.set_scan_noise(torch.zeros(sm.E, sm.B, dtype=torch.float64, device=sm.device))
+    runner.step(act, minimal_outputs=False)
+    if hasattr(runner, "join"):
+        runner.join()
+    torch.cuda.synchronize()
+    g, poses, skipped = [], [], 0
+    for sm in sims:
+        st = sm.agent_states().reshape(-1, 7).cpu().numpy()
+        col = sm.out.collisions.reshape(-1).cpu().numpy().astype(bool)
+        sc = sm.out.scans_f64.reshape(-1, sm.B).cpu().numpy()
+        sm.set_scan_noise(None)
+        skipped += int(col.sum())
+        g.append(sc[~col])
+        poses.append(np.stack([st[~col, 0], st[~col, 1], st[~col, 4]], 1))
+    g = np.concatenate(g)
+    poses = np.concatenate(poses)
+    ref = scanner.scan(poses, threads=threads)
+    diff = g - ref
+    return {"kernel": "k_rays_tiled (the timed runner, one extra step)", "cars": int(poses.shape[0]),
+            "cars_skipped_ttc": skipped, "rays": int(diff.size),
+            "l2": float(np.sqrt(np.sum(diff * diff))), "max_abs": float(np.max(np.abs(diff))),
+            "bit_exact_fraction": float(np.mean(diff == 0.0))}
 
 
 def main():
@@ -194,6 +246,7 @@ def main():
     from f110_gymnasium_ros2_jazzy_amd import distributed as D
     from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns, load_map
     from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
+    from f110_gymnasium_ros2_jazzy_amd.streams import StreamShards
 
     rank, world, local = D.init()
     if world != args.gpus and rank == 0:
@@ -201,68 +254,82 @@ def main():
     dev_index = D.local_device_index(local)
     torch.cuda.set_device(dev_index)
     dev = torch.device(f"cuda:{dev_index}")
-    E, A = args.envs_per_gpu, args.agents
-    shard = D.shard_range(E * world, world, rank)
+    A = args.agents
+    weak = args.envs_per_gpu is not None
+    G = args.envs_per_gpu * world if weak else args.global_envs
+    shard = D.shard_range(G, world, rank)
+    E = shard.count
+    K, W = args.steps, args.warmup
+    S = max(1, args.streams)
+    noise = 0.0 if args.no_noise else 0.01
 
     track = load_map(args.map)
     track.ensure_edt()
     spawn = centerline_spawns(args.map.replace("_map", ""), A)
     # initial spawn per GLOBAL env id (independent of GPU count)
     rng = np.random.default_rng(args.seed)
-    gidx = rng.integers(0, spawn.shape[0], size=E * world)[shard.offset:shard.offset + shard.count]
+    gidx = rng.integers(0, spawn.shape[0], size=G)[shard.offset:shard.offset + E]
     poses0 = spawn[gidx]
-    sim = BatchSim(track, n_envs=shard.count, n_agents=A, device=dev, seed=args.seed,
-                   noise_std=0.0 if args.no_noise else 0.01, autoreset=True, spawn_poses=spawn,
-                   env_offset=shard.offset)
 
-    K, W = args.steps, args.warmup
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1000003 * 0 + shard.offset)
-    acts = torch.rand(W + K, shard.count, A, 2, device=dev, generator=gen, dtype=torch.float32)
-    acts[..., 0] = acts[..., 0] * (2 * 0.4189) - 0.4189   # steer in [-0.4189, 0.4189]
-    acts[..., 1] = acts[..., 1] * 20.0                   # speed in [0, 20] (ddpg_config.yaml:19-20)
+    def actions(n_steps, n_envs, offset):
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(offset)
+        a = torch.rand(n_steps, n_envs, A, 2, device=dev, generator=gen, dtype=torch.float32)
+        a[..., 0] = a[..., 0] * (2 * 0.4189) - 0.4189   # steer in [-0.4189, 0.4189]
+        a[..., 1] = a[..., 1] * 20.0                   # speed in [0, 20] (ddpg_config.yaml:19-20)
+        return a
+
+    acts = actions(W + K + 1, E, shard.offset)
     stream = torch.cuda.current_stream(dev)
-    S = max(1, args.streams)
-    runner = sim
-    if S > 1:
-        from f110_gymnasium_ros2_jazzy_amd.streams import StreamShards
-        runner = StreamShards(track, n_envs=shard.count, n_streams=S, env_offset=shard.offset, n_agents=A,
-                              device=dev, seed=args.seed, noise_std=0.0 if args.no_noise else 0.01,
-                              autoreset=True, spawn_poses=spawn)
 
-    def timed(r):
+    def make(n_envs, offset, s):
+        kw = dict(n_agents=A, device=dev, seed=args.seed, noise_std=noise, autoreset=True, spawn_poses=spawn,
+                  keep_f64_scans=True)
+        if s > 1 and n_envs % s == 0:
+            return StreamShards(track, n_envs=n_envs, n_streams=s, env_offset=offset, **kw)
+        return BatchSim(track, n_envs=n_envs, env_offset=offset, **kw)
+
+    def timed(r, p0, a, minimal=True):
         """W untimed steps, then K steps between barrier + synchronize (max over ranks)."""
-        r.reset(poses0)
+        r.reset(p0)
         for w in range(W):
-            r.step(acts[w], minimal_outputs=True)
+            r.step(a[w], minimal_outputs=minimal)
         torch.cuda.synchronize(dev)
         r.reset_counters()
         D.barrier()
         torch.cuda.synchronize(dev)
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
-        ev0.record(stream)
         for k in range(K):
-            r.step(acts[W + k], minimal_outputs=True)
-        if r is not sim:
+            r.step(a[W + k], minimal_outputs=minimal)
+        if hasattr(r, "join"):
             r.join()
-        ev1.record(stream)
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         D.barrier()
-        return D.max_over_ranks(t1 - t0), ev0.elapsed_time(ev1) / K, r.read_counters()
+        return D.max_over_ranks(t1 - t0), r.read_counters()
 
-    elapsed, kernel_ms, (lookups, rays) = timed(runner)
+    runner = make(E, shard.offset, S)
+    elapsed, (lookups, rays) = timed(runner, poses0, acts)
     mean_look = lookups / max(rays, 1)
-    total_env_steps = D.sum_over_ranks(shard.count * K)
+    total_env_steps = D.sum_over_ranks(E * K)
+    sim = runner if isinstance(runner, BatchSim) else make(E, shard.offset, 1)
     single = None
-    if runner is not sim:
-        # the same workload on one context / one stream, for comparison (not `value`)
-        el1, _, _ = timed(sim)
-        single = {"value": total_env_steps / el1, "ms_per_step": el1 / K * 1e3}
-        runner.close()
+    if sim is not runner:  # the same workload on one context / one stream (what a policy loop steps)
+        el1, _ = timed(sim, poses0, acts)
+        single = {"value": total_env_steps / el1, "ms_per_step": el1 / K * 1e3,
+                  "runner": "one BatchSim context on the caller's stream, minimal outputs"}
+    el_full, _ = timed(sim, poses0, acts, minimal=False)
+    full_outputs = {"value": total_env_steps / el_full, "ms_per_step": el_full / K * 1e3,
+                    "runner": "one context, every output (f32 + f64 scans, laps, sim_time, was_reset)"}
 
-    # second, separate pass: per-kernel HIP-event timing (not part of `value`)
+    O = scanner = None
+    checks = None
+    if rank == 0:
+        O = oracle_module()
+        scanner = O.OracleScanner(track.free_mask, track.resolution, track.origin)
+        checks = scan_check(O, scanner, runner, acts[W + K], cpu_threads())
+
+    # second, separate pass: per-kernel HIP-event timing on the one-context run (not part of `value`)
     KP = min(K, 300)
     sim.profile_begin(KP)
     for k in range(KP):
@@ -273,10 +340,33 @@ def main():
     # k_rays (the dominant kernel): per ray 4 B per EDT lookup (exact uint32 k
     # cell) + 4 B of f32 range out; the 120 B/agent of state I/O
     # belong to k_agents.
-    rays_bytes_launch = shard.count * A * B * (4.0 * mean_look + 4.0)
-    achieved = rays_bytes_launch / (per_kernel["k_rays_ms"] * 1e-3) / 1e9
-    bytes_launch = shard.count * algorithmic_bytes_per_env_step(B, A, mean_look)
-    traffic, _ = load_pmc_traffic(shard.count, A)
+    rays_bytes_launch = E * A * B * (4.0 * mean_look + 4.0)
+    k_ms = per_kernel["k_rays_ms"]
+    achieved = rays_bytes_launch / (k_ms * 1e-3) / 1e9
+    pmc = load_profile("pmc_traffic", E, A)
+    busy = load_profile("pmc_busy", E, A)
+    traffic = pmc.get("bytes_per_launch") if pmc else None
+    roof = {
+        "kernel": "k_rays", "bound": "gather-latency/VALU-issue (HBM is not the limit: see hbm_traffic_frac)",
+        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic, "kernel_ms": k_ms, "algorithmic_bytes_per_launch": rays_bytes_launch,
+        "mean_lookups_per_ray": mean_look,
+        "step_kernels_ms": {"k_agents": per_kernel["k_agents_ms"], "k_rays": k_ms, "k_post": per_kernel["k_post_ms"]},
+        "step_algorithmic_bytes_per_env": algorithmic_bytes_per_env_step(B, A, mean_look),
+    }
+    if pmc and traffic:
+        roof["hbm_traffic_gbs"] = traffic / (k_ms * 1e-3) / 1e9
+        roof["hbm_traffic_frac"] = roof["hbm_traffic_gbs"] / HBM_PEAK_GBS
+        if pmc.get("write_bytes"):
+            roof["write_ratio"] = pmc["write_bytes"] / (E * A * B * 4.0)
+        roof["l2_hit_rate"] = pmc.get("l2_hit_rate")
+        roof["traffic_source"] = pmc["file"]
+    if busy:
+        for k in ("valu_busy", "waves_per_simd", "simt_efficiency"):
+            if k in busy:
+                roof[k] = busy[k]
+        roof["busy_source"] = busy["file"]
+
     result = {
         "metric": METRIC,
         "value": total_env_steps / elapsed,
@@ -286,38 +376,59 @@ def main():
         "warmup": W,
         "ms_per_step": elapsed / K * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: i.i.d. uniform random actions, centerline spawn poses, Spielberg map",
         "config": {
-            "workload": f"{E} single-agent envs per GPU ({E * world} total); C3 shard at 8 GPUs = 65536 envs"
-            if A == 1 else f"{E} {A}-agent envs per GPU",
-            "envs_per_gpu": E, "global_envs": E * world, "agents": A, "beams": B, "map": args.map,
+            "workload": f"{G} {'single' if A == 1 else f'{A}'}-agent envs"
+                        + (f" ({E} per GPU x {world})" if world > 1 else " on one GPU"),
+            "global_envs": G, "envs_per_gpu": E, "agents": A, "beams": B, "map": args.map,
             "integrator": "RK4", "scan_noise": not args.no_noise, "autoreset": True,
             "parallelism": f"env-shard x{world} (no collectives)",
-            "streams_per_gpu": S,
+            "streams_per_gpu": S if not isinstance(runner, BatchSim) else 1,
+            "runner": ("StreamShards: S unjoined stream sub-shards, actions resident in HBM" if S > 1 else
+                       "one BatchSim context") + "; minimal outputs (obs, collisions, terminated): no f32 "
+                       "info['scans'] copy, lap_times/counts, sim_time, was_reset",
         },
-        "roofline": {
-            "kernel": "k_rays", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel_ms": per_kernel["k_rays_ms"], "algorithmic_bytes_per_launch": rays_bytes_launch,
-            "mean_lookups_per_ray": mean_look,
-            "step_kernels_ms": {"k_agents": per_kernel["k_agents_ms"], "k_rays": per_kernel["k_rays_ms"],
-                                "k_post": per_kernel["k_post_ms"], "stream_per_step": kernel_ms},
-            "step_algorithmic_bytes_per_env": bytes_launch / max(shard.count, 1),
-        },
+        "single_stream": single,
+        "single_stream_full_outputs": full_outputs,
+        "scan_l2_vs_cpu": checks["l2"] if checks and "l2" in checks else None,
+        "scan_check": checks,
+        "roofline": roof,
     }
-    if single is not None:
-        result["single_stream"] = single
+    if rank == 0 and world == 1 and not args.no_secondary:
+        sec = {}
+        for label, n in (("C3_shard_8192", 8192), ("C2_4096", 4096)):
+            if n >= E:
+                continue
+            r2 = make(n, 0, S)
+            el2, _ = timed(r2, spawn[rng.integers(0, spawn.shape[0], size=n)], actions(W + K, n, 0))
+            line = {"envs": n, "value": n * K / el2, "ms_per_step": el2 / K * 1e3,
+                    "streams": S if not isinstance(r2, BatchSim) else 1}
+            if not isinstance(r2, BatchSim):
+                r2.close()
+                r1 = make(n, 0, 1)
+                el1, _ = timed(r1, spawn[rng.integers(0, spawn.shape[0], size=n)], actions(W + K, n, 0))
+                line["single_stream"] = {"value": n * K / el1, "ms_per_step": el1 / K * 1e3}
+                r1.close()
+            else:
+                r2.close()
+            sec[label] = line
+        result["secondary"] = sec
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            result["cpu_baseline"] = cpu_baseline(track, poses0, acts[:64].cpu().numpy(), args, sim)
+            T = args.cpu_warmup + args.cpu_steps
+            a_cpu = acts if acts.shape[0] >= T else actions(T, E, shard.offset)
+            n = min(args.cpu_envs, E)
+            result["cpu_baseline"] = cpu_baseline(O, scanner, poses0[:n], a_cpu[:T, :n].cpu().numpy(), args)
         except Exception as exc:  # report, never hide
             result["cpu_baseline"] = {"error": repr(exc)}
     if rank == 0:
         print(json.dumps(result), flush=True)
-    sim.close()
+    if sim is not runner:
+        sim.close()
+    runner.close()
     D.shutdown()
 
 

@@ -24,6 +24,7 @@ slower than one context (`scripts/stream_split.py --join 1`).
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 
 import torch
@@ -69,12 +70,23 @@ class StreamShards:
         self.S = n_streams
         self.E = n_envs
         self.Es = n_envs // n_streams
-        self.device = torch.device(kw.get("device", "cuda"))
-        self.streams = [dedicated_stream(self.device) for _ in range(self.S)]
+        self.streams = []
         self.sims = []
+        self._inflight = collections.deque()
+        self._free_ev = []
+        # one explicit device index for the CU-masked streams AND the contexts
+        # ('cuda' alone would mean device 0 to BatchSim but the current device
+        # to the stream constructor)
+        dev = kw.pop("device", None)
+        dev = torch.device(f"cuda:{dev}" if isinstance(dev, int) else (dev if dev is not None else "cuda"))
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        self.n_agents = int(kw.get("n_agents", 2))
+        self.streams = [dedicated_stream(self.device) for _ in range(self.S)]
         for s in range(self.S):
             with torch.cuda.stream(self.streams[s]):
-                sm = BatchSim(track, n_envs=self.Es, env_offset=env_offset + s * self.Es, **kw)
+                sm = BatchSim(track, n_envs=self.Es, env_offset=env_offset + s * self.Es, device=self.device, **kw)
                 if not heavy_first and n_streams > 1:
                     # the other sub-shard's ray pass fills this one's tail; heavy-first's list
                     # upkeep then costs more than it saves (42.5 vs 41.8 M env-steps/s)
@@ -83,27 +95,83 @@ class StreamShards:
         self._sl = [slice(s * self.Es, (s + 1) * self.Es) for s in range(self.S)]
         self._fork()
 
+    def _caller(self):
+        """The caller's current stream, or None when it is the legacy null
+        stream.  The sub-streams are blocking streams (hipExtStreamCreate-
+        WithCUMask takes no flags), so null-stream work is ordered against
+        them implicitly in both directions: sub-stream kernels start after
+        earlier null-stream work (actions drawn there), and later null-stream
+        work (obs reads, a reuse of a freed action block) waits for them.
+        Recording an event there would also wait for every sub-stream, i.e.
+        serialise the sub-shards, so nothing is recorded on it."""
+        cur = torch.cuda.current_stream(self.device)
+        return None if cur.cuda_stream == 0 else cur
+
+    def _event(self):
+        return self._free_ev.pop() if self._free_ev else torch.cuda.Event()
+
     def _fork(self):
         # whatever the caller's stream produced so far (inputs) precedes every sub-shard's work
-        ev = torch.cuda.current_stream(self.device).record_event()
+        cur = self._caller()
+        if cur is None:
+            return
+        ev = self._event()
+        ev.record(cur)
         for st in self.streams:
             st.wait_event(ev)
+        self._free_ev.append(ev)  # re-recording later is safe: the waits are already enqueued
+
+    def _hold(self, t):
+        """Keep a caller tensor that the sub-streams read alive until their
+        kernels are done with it, so the caching allocator cannot hand its
+        block to the caller's (non-null) stream while a sub-stream still
+        reads it.  One event per sub-stream marks the end of the reads; the
+        reference is dropped once they have completed.  (Tensor.record_stream
+        on these external streams crashed at hipStreamDestroy.)"""
+        if self._caller() is None:
+            return
+        evs = []
+        for st in self.streams:
+            ev = self._event()
+            ev.record(st)
+            evs.append(ev)
+        self._inflight.append((t, evs))
+        while self._inflight and all(e.query() for e in self._inflight[0][1]):
+            self._free_ev.extend(self._inflight.popleft()[1])
 
     def reset(self, poses):
+        p = torch.as_tensor(poses, dtype=torch.float64, device=self.device)
+        if p.dim() == 2:  # [A, 3] broadcast to every env (as BatchSim.reset)
+            p = p.unsqueeze(0).expand(self.E, p.shape[0], 3)
+        if p.shape[0] != self.E:
+            raise ValueError(f"poses must be [{self.E}, A, 3] or [A, 3]; got {tuple(p.shape)}")
         self._fork()
         for s in range(self.S):
             with torch.cuda.stream(self.streams[s]):
-                self.sims[s].reset(poses[self._sl[s]])
+                self.sims[s].reset(p[self._sl[s]])
+        self._hold(p)
 
     def step(self, actions, minimal_outputs: bool = True):
+        """Launch every sub-shard's step on its stream (not joined).  The
+        sub-streams first wait for the caller's stream: actions produced there
+        (a policy, torch.rand) and any reads of the previous obs queued there
+        (`obs`, a torch.cat) are ordered before this step's kernels."""
+        a = torch.as_tensor(actions, device=self.device)
+        self._fork()
         for s in range(self.S):
             with torch.cuda.stream(self.streams[s]):
-                self.sims[s].step(actions[self._sl[s]], minimal_outputs=minimal_outputs)
+                self.sims[s].step(a[self._sl[s]], minimal_outputs=minimal_outputs)
+        self._hold(a)
 
     def join(self):
-        cur = torch.cuda.current_stream(self.device)
+        cur = self._caller()
+        if cur is None:
+            return  # the null stream waits for the sub-streams by itself
         for st in self.streams:
-            cur.wait_event(st.record_event())
+            ev = self._event()
+            ev.record(st)
+            cur.wait_event(ev)
+            self._free_ev.append(ev)
 
     @property
     def obs(self) -> torch.Tensor:
@@ -126,10 +194,23 @@ class StreamShards:
                 self.sims[s].reset_counters()
 
     def close(self):
+        if not self.streams and not self.sims:
+            return
         torch.cuda.synchronize(self.device)
+        self._inflight.clear()
         for sm in self.sims:
             sm.close()
+        # the contexts' output tensors were allocated under these streams:
+        # release them (to the caching allocator) before the streams go away
+        self.sims = []
+        torch.cuda.synchronize(self.device)
         hip = _hip_lib()
         for st in self.streams:
             hip.hipStreamDestroy(ctypes.c_void_p(st.cuda_stream))
         self.streams = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -609,18 +609,54 @@ typedef struct {
     const double *angles, *beam_cos, *side;
     double dt, lidar_dist, ttc_thresh;
     int32_t n_agents, integrator;
+    /* scan noise (ScanSimulator2D.scan, laser_models.py:450-452): 0 = the
+     * parity setting (scan_rng = None).  > 0 only for the bench's CPU
+     * baseline, where the host does the per-step draw the reference does:
+     * B normals per env per step, shared by the env's agents (all RaceCars
+     * seed alike, base_classes.py:119,204).  The stream (splitmix64 +
+     * Box-Muller) is not NumPy's PCG64; only the cost of the draw matters. */
+    double noise_std;
+    uint64_t noise_seed, step_no;
 } or_sim;
 
-static void or_sim_step_env(const or_sim *S, double *state, double *buf, int32_t *cnt, const double *act,
-                            double *scans, double *collisions) {
+static inline uint64_t or_splitmix(uint64_t *s) {
+    uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static void or_scan_noise(const or_sim *S, int64_t env, double *noise, int B) {
+    /* Marsaglia's polar method: one log + one sqrt per pair of normals */
+    uint64_t st = S->noise_seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(env + 1)) ^ (S->step_no << 20);
+    for (int b = 0; b < B; b += 2) {
+        double u, v, q;
+        do {
+            u = (double)(or_splitmix(&st) >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+            v = (double)(or_splitmix(&st) >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+            q = u * u + v * v;
+        } while (q >= 1.0 || q == 0.0);
+        const double f = S->noise_std * sqrt(-2.0 * log(q) / q);
+        noise[b] = u * f;
+        if (b + 1 < B) noise[b + 1] = v * f;
+    }
+}
+
+static void or_sim_step_env(const or_sim *S, int64_t env, double *state, double *buf, int32_t *cnt,
+                            const double *act, double *scans, double *collisions) {
     const int A = S->n_agents, B = S->sc->num_beams;
     double agent_poses[16][3];
     double verts[16][8] = {{0}};
+    double noise[4096];
+    const int noisy = S->noise_std > 0.0 && B <= 4096;
+    if (noisy) or_scan_noise(S, env, noise, B);
     for (int i = 0; i < A; ++i) { /* :581-587 */
         double *st = state + 7 * i;
         or_update_pose(st, buf + 2 * i, cnt + i, act[2 * i], act[2 * i + 1], S->p, S->dt, S->integrator);
         double scan_pose[3] = {st[0] + S->lidar_dist * cos(st[4]), st[1] + S->lidar_dist * sin(st[4]), st[4]};
         or_get_scan(S->sc, scan_pose, scans + (size_t)i * B, NULL, NULL);
+        if (noisy) /* after the clamp, laser_models.py:450-452 */
+            for (int b = 0; b < B; ++b) scans[(size_t)i * B + b] += noise[b];
         agent_poses[i][0] = st[0];
         agent_poses[i][1] = st[1];
         agent_poses[i][2] = st[4];
@@ -653,7 +689,7 @@ OR_API void or_sim_step(const or_sim *S, int64_t n_envs, double *state, double *
     const int64_t A = S->n_agents, B = S->sc->num_beams;
 #pragma omp parallel for schedule(dynamic, 2) num_threads(threads > 0 ? threads : 1)
     for (int64_t e = 0; e < n_envs; ++e)
-        or_sim_step_env(S, state + 7 * A * e, buf + 2 * A * e, cnt + A * e, actions + 2 * A * e,
+        or_sim_step_env(S, e, state + 7 * A * e, buf + 2 * A * e, cnt + A * e, actions + 2 * A * e,
                         scans + A * B * e, collisions + A * e);
 }
 

@@ -39,7 +39,8 @@ class Scanner(ctypes.Structure):
 class Sim(ctypes.Structure):
     _fields_ = [("sc", ctypes.POINTER(Scanner)), ("p", ctypes.POINTER(Params)), ("angles", _D),
                 ("beam_cos", _D), ("side", _D), ("dt", ctypes.c_double), ("lidar_dist", ctypes.c_double),
-                ("ttc_thresh", ctypes.c_double), ("n_agents", ctypes.c_int32), ("integrator", ctypes.c_int32)]
+                ("ttc_thresh", ctypes.c_double), ("n_agents", ctypes.c_int32), ("integrator", ctypes.c_int32),
+                ("noise_std", ctypes.c_double), ("noise_seed", ctypes.c_uint64), ("step_no", ctypes.c_uint64)]
 
 
 DEFAULT_PARAMS = {'mu': 1.0489, 'C_Sf': 4.718, 'C_Sr': 5.4562, 'lf': 0.15875, 'lr': 0.17145,
@@ -242,7 +243,13 @@ class OracleSim:
         poses = _f64(poses).reshape(self.E * self.A, 3)
         lib().or_sim_reset(self.E * self.A, _p(self.state), _p(self.buf), _p(self.cnt, _I32), _p(poses))
 
+    def set_noise(self, std: float, seed: int = 0):
+        """Host-drawn scan noise (timing baseline only; parity runs keep 0)."""
+        self.sim.noise_std = float(std)
+        self.sim.noise_seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+
     def step(self, actions, threads=1):
+        self.sim.step_no += 1
         actions = _f64(actions).reshape(self.E * self.A, 2)
         scans = np.empty((self.E * self.A, self.scanner.num_beams))
         cols = np.empty(self.E * self.A)

@@ -179,3 +179,57 @@ def test_stream_shards_match_single_context(tracks, gpu):
     assert torch.equal(sh.obs, full.out.obs)
     assert sh.read_counters() == full.read_counters()
     sh.close()
+
+
+@pytest.mark.parametrize("caller", ["null", "torch_stream"])
+def test_stream_shards_policy_loop(tracks, gpu, caller):
+    """A policy-style loop on StreamShards: actions drawn with torch.rand on
+    the caller's stream every step (then freed), obs read (torch.cat on the
+    caller's stream) every step.  On the legacy null stream the ordering is
+    implicit; on a torch stream step() orders the sub-streams after it and
+    holds the action tensor until their kernels are done.  Either way every
+    per-step obs equals one BatchSim's, bit for bit."""
+    import contextlib
+    from f110_gymnasium_ros2_jazzy_amd.streams import StreamShards
+    ctx = torch.cuda.stream(torch.cuda.Stream(device=gpu)) if caller == "torch_stream" else contextlib.nullcontext()
+    with ctx:
+        _policy_loop(tracks, gpu, StreamShards)
+
+
+def _policy_loop(tracks, gpu, StreamShards):
+    E, A, T = 512, 1, 40
+    sp = _spawns(A)
+    rng = np.random.default_rng(12)
+    poses = sp[rng.integers(0, sp.shape[0], E)]
+    full = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=3)
+    sh = StreamShards(tracks("Spielberg_map"), n_envs=E, n_streams=2,
+                      n_agents=A, device=gpu, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=3)
+    full.reset(poses)
+    sh.reset(poses)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(5)
+    for t in range(T):
+        a = torch.rand(E, A, 2, device=gpu, generator=g)
+        a[..., 0] = a[..., 0] * 0.8378 - 0.4189
+        a[..., 1] *= 20
+        o_sh = sh.step(a) or sh.obs          # the obs of THIS step (join + cat on the caller's stream)
+        o_full = full.step(a.clone()).obs.clone()
+        del a                                 # freed on the caller's stream while the sub-streams may still read it
+        junk = torch.full((E, A, 2), float("nan"), device=gpu)  # would land in the freed block
+        assert torch.equal(o_sh, o_full), f"step {t}"
+        del junk
+    sh.close()
+    sh.close()  # idempotent
+
+
+def test_stream_shards_broadcast_reset(tracks, gpu):
+    """StreamShards.reset accepts BatchSim's broadcast [A, 3] pose."""
+    from f110_gymnasium_ros2_jazzy_amd.streams import StreamShards
+    E, A = 64, 2
+    sp = _spawns(A)
+    sh = StreamShards(tracks("Spielberg_map"), n_envs=E, n_streams=2, n_agents=A, device=gpu, noise_std=0.0)
+    full = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.0)
+    sh.reset(sp[100])
+    full.reset(sp[100])
+    assert torch.equal(sh.obs, full.out.obs)
+    sh.close()
