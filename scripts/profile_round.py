@@ -20,16 +20,24 @@ OUT = os.path.join(REPO, "gpurun_out", f"prof_{tag}")
 COLLECT = "--collect" in sys.argv
 # only gpurun_out/ comes back from the box: write there, copy into profiles/ locally
 PROF = os.path.join(REPO, "profiles") if COLLECT else os.path.join(OUT, "summary")
-BENCH = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "300", "--warmup", "50", "--no-cpu-baseline"]
+ENVS = int(os.environ.get("PROFILE_ENVS", "65536"))  # the headline configuration (bench.py default)
+BENCH = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "300", "--warmup", "50", "--no-cpu-baseline",
+         "--no-secondary", "--global-envs", str(ENVS)]
 env = dict(os.environ, TMPDIR="/tmp")
 
 
-def run(name, extra, timeout=400, bench_extra=()):
+# PMC target: the headline's ray kernel alone (one BatchSim context, minimal outputs, 100 steps):
+# the bench also runs full-output passes whose extra scan writes would mix into the averages
+RAYPMC = [sys.executable, os.path.join(REPO, "scripts", "ray_pmc.py")]
+env["MB_ENVS"] = str(ENVS)
+
+
+def run(name, extra, timeout=400, bench_extra=(), target=None):
     d = os.path.join(OUT, name)
     if COLLECT:
         return d
     shutil.rmtree(d, ignore_errors=True)
-    cmd = ["rocprofv3"] + extra + ["--output-format", "csv", "-d", d, "-o", "run", "--"] + BENCH + list(bench_extra)
+    cmd = ["rocprofv3"] + extra + ["--output-format", "csv", "-d", d, "-o", "run", "--"] + (target or BENCH + list(bench_extra))
     print(" ".join(cmd), flush=True)
     with open(os.path.join(OUT, f"{name}.log"), "w") as log:
         subprocess.run(["timeout", "-k", "10", str(timeout)] + cmd, cwd="/tmp", env=env, stdout=log,
@@ -87,11 +95,11 @@ with open(trace) as f:
 summary["k_rays_by_grid_size"] = {g: {"Calls": n, "AverageNs": t / n} for g, (n, t) in by_grid.items()}
 json.dump(summary, open(os.path.join(PROF, f"{tag}_kernel_stats.json"), "w"), indent=1)
 
-res = {"kernel": "k_rays", "envs": 8192, "agents": 1}
+res = {"kernel": "k_rays", "envs": ENVS, "agents": 1}
 for grp in (["FETCH_SIZE"], ["WRITE_SIZE"], ["TCC_HIT_sum", "TCC_MISS_sum"]):
     name = "pmc_" + "_".join(g.lower() for g in grp)
     try:
-        dd = run(name, ["--pmc"] + grp, bench_extra=("--streams", "1"))  # the isolated E-car launch
+        dd = run(name, ["--pmc"] + grp, target=RAYPMC)  # the isolated E-car launch
         res.update(counters(dd, os.path.join(PROF, f"{tag}_{name}.csv")))
     except Exception as exc:  # record, do not hide
         res[name + "_error"] = repr(exc)
@@ -104,5 +112,25 @@ if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
                    "counted by these TCC_EA counters")
 if "TCC_HIT_sum" in res:
     res["l2_hit_rate"] = res["TCC_HIT_sum"] / max(1.0, res["TCC_HIT_sum"] + res["TCC_MISS_sum"])
-json.dump(res, open(os.path.join(PROF, "pmc_traffic.json"), "w"), indent=1)
+json.dump(res, open(os.path.join(PROF, f"pmc_traffic_E{ENVS}_A1.json"), "w"), indent=1)
 print(json.dumps(res))
+
+# 3. issue / occupancy pass: VALU busy and resident waves per SIMD of the isolated E-car launch.
+#    SQ_* cycle counters are quad-cycles summed over waves; GRBM_GUI_ACTIVE is summed over the 8 XCDs
+#    (MI355X_MICROARCH.md), so kernel cycles = GRBM_GUI_ACTIVE / 8 and SIMDs = CUs x 4.
+busy = {"kernel": "k_rays", "envs": ENVS, "agents": 1}
+grp = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+       "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"]
+try:
+    dd = run("pmc_busy", ["--pmc"] + grp, target=RAYPMC)
+    busy.update(counters(dd, os.path.join(PROF, f"{tag}_pmc_busy.csv")))
+    simds = 256 * 4
+    cyc = busy["GRBM_GUI_ACTIVE"] / 8.0
+    busy["valu_busy"] = busy["SQ_ACTIVE_INST_VALU"] * 4.0 / (simds * cyc)
+    busy["waves_per_simd"] = busy["SQ_WAVE_CYCLES"] * 4.0 / (simds * cyc)
+    busy["note"] = ("valu_busy = SQ_ACTIVE_INST_VALU*4 / (1024 SIMDs * GRBM_GUI_ACTIVE/8); waves_per_simd = "
+                    "SQ_WAVE_CYCLES*4 / (1024 * GRBM_GUI_ACTIVE/8); mean per k_rays dispatch, scripts/ray_pmc.py (minimal outputs)")
+except Exception as exc:
+    busy["error"] = repr(exc)
+json.dump(busy, open(os.path.join(PROF, f"pmc_busy_E{ENVS}_A1.json"), "w"), indent=1)
+print(json.dumps(busy))
