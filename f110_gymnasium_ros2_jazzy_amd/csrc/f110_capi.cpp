@@ -50,7 +50,8 @@ struct f110_ctx {
     // device buffers
     double *dt_tiled = nullptr;
     int32_t wt = 0, tiles_h = 0;
-    int ray_kernel = 2;  // F110_RAY_KERNEL: 0 row-major k_rays, 1 tiled flat order, 2 tiled chunked (default)
+    int ray_kernel = 3;  // F110_RAY_KERNEL: 0 row-major k_rays, 1 tiled flat order, 2 tiled chunked,
+                         // 3 chunked k_rays_fx (default; falls back to 2 where its preconditions fail)
     uint8_t chunk_order[kMaxChunks] = {};
     double *dt = nullptr, *sines = nullptr, *cosines = nullptr, *angles = nullptr, *beam_cos = nullptr,
            *side = nullptr, *spawn = nullptr;
@@ -327,6 +328,23 @@ static TiledMapView make_tiled_view(const MapView &m, const double *dt_tiled) {
     return t;
 }
 
+// k_rays_fx's preconditions (f110_kernels.hip): an axis-aligned map (origin
+// yaw 0: cos 1, sin 0 exactly, so x_rot == x_trans), one-wave blocks, H and W
+// below 2^21 and |origin / res| below 2^20 (on-map t = 1.5*2^22 + q stays in
+// [2^22, 2^23)), and every EDT entry 0 or above eps (the loop's d > eps is
+// then d != 0; the smallest non-zero entry is res * sqrt(1)).
+static bool fx_eligible(int32_t H, int32_t W, double res, const double origin[3], double eps, const uint32_t *edt_k,
+                        int32_t wpb) {
+    if (origin[2] != 0.0 || wpb != 1) return false;
+    if (H >= (1 << 21) || W >= (1 << 21)) return false;
+    const double ir = 1.0 / res;
+    if (!(std::fabs(origin[0] * ir) < 1048576.0) || !(std::fabs(origin[1] * ir) < 1048576.0)) return false;
+    uint32_t kmin = 0;
+    for (size_t i = 0, n = (size_t)H * W; i < n; ++i)
+        if (edt_k[i] && (!kmin || edt_k[i] < kmin)) kmin = edt_k[i];
+    return !kmin || res * std::sqrt((double)kmin) > eps;
+}
+
 static MapView map_view(const f110_ctx *c) { return make_map_view(c->dt, c->H, c->W, c->res, c->origin); }
 
 static int use_device(const f110_ctx *c) {
@@ -372,7 +390,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     c->n_spawn = n_spawn;
     if (const char *v = std::getenv("F110_RAY_KERNEL")) {
         const int k = std::atoi(v);
-        c->ray_kernel = k == 0 ? 0 : (k == 2 ? 2 : 1);
+        c->ray_kernel = k == 0 ? 0 : (k >= 2 && k <= 3 ? k : 1);
     }
     {
         // chunked dispatch order: descending beam chunks (the scan's left edge
@@ -381,7 +399,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
         // (scripts/chunk_ab.py): fastest at 4096 and 8192 envs,
         // 1 and 2 agents.
         const int nch = (C.n_beams + 63) / 64;
-        if (nch > kMaxChunks && c->ray_kernel == 2) c->ray_kernel = 1;
+        if (nch > kMaxChunks && c->ray_kernel >= 2) c->ray_kernel = 1;
         c->nch = nch;
         for (int i = 0; i < nch && i < kMaxChunks; ++i) c->chunk_order[i] = (uint8_t)(nch - 1 - i);
         if (const char *v = std::getenv("F110_CHUNK_ORDER")) {
@@ -448,7 +466,8 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (spawn_poses && n_spawn > 0) ALLOC(c->spawn, (size_t)n_spawn * C.n_agents * 3);
     if (const char *v = std::getenv("F110_RAY_WPB")) c->ray_wpb = std::atoi(v) == 1 ? 1 : 4;
     if (const char *v = std::getenv("F110_HEAVY_T")) c->heavy_T = std::atoi(v);  // 0: no heavy-first dispatch
-    if (c->ray_kernel == 2 && c->heavy_T > 0) {
+    if (c->ray_kernel == 3 && !fx_eligible(H, W, resolution, origin, C.eps, edt_k, c->ray_wpb)) c->ray_kernel = 2;
+    if (c->ray_kernel >= 2 && c->heavy_T > 0) {
         // up to 1/8 of the waves, in blocks of 4 (measured: ~7% of the waves
         // have a ray longer than 40 lookups and carry ~46% of the wave-iterations)
         size_t div = 6;  // F110_HEAVY_DIV: list capacity = 1/div of the waves
@@ -601,13 +620,18 @@ extern "C" int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dty
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     StepArgs a = make_step_args(ctx, out);
     a.mode = 0;
-    a.heavy_build = a.heavy_use = (a.wcost && a.ray_kernel == 2 && !ctx->heavy_off) ? 1 : 0;  // not on resets
+    a.heavy_build = a.heavy_use = (a.wcost && a.ray_kernel >= 2 && !ctx->heavy_off) ? 1 : 0;  // not on resets
     if (actions_dtype == F110_F64)
         a.actions_f64 = static_cast<const double *>(actions);
     else
         a.actions = static_cast<const float *>(actions);
     HIP_TRY(launch_env_step(a, (hipStream_t)stream, ctx->next_prof_events()));
     return F110_OK;
+}
+
+extern "C" int f110_ray_kernel(const f110_ctx *ctx) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_ray_kernel: null context");
+    return ctx->ray_kernel;
 }
 
 extern "C" int f110_disable_heavy_first(f110_ctx *ctx) {

@@ -718,21 +718,46 @@ F110_HD double u01_open(uint32_t hi, uint32_t lo) {  // (0, 1], 53 bits
     return ((double)v + 1.0) * (1.0 / 9007199254740992.0);
 }
 
-// N(0,1) for beam b of the env's stream at `step`: one Philox block per beam
-// pair, Box-Muller on 24-bit uniforms in fp32 (hardware v_log/v_sin/v_cos:
-// the noise is a statistical quantity, its ~1e-7 relative precision is far
-// below the 0.01 m std it scales; tails are cut at 5.8 sigma).  Even beams
-// take the cos branch, odd beams the sin branch.
+// Philox2x32-10 (Salmon et al., SC'11; passes BigCrush): one 32x32->64
+// multiply and one xor3 per round, half the work of Philox4x32 for the 48
+// random bits one normal needs.
+struct U2 { uint32_t x, y; };
+
+F110_HD U2 philox2x32(uint32_t L, uint32_t R, uint32_t k) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p = (uint64_t)0xD256D193u * L;
+        const uint32_t hi = (uint32_t)(p >> 32);
+        L = hi ^ k ^ R;
+        R = (uint32_t)p;
+        k += 0x9E3779B9u;
+    }
+    return {L, R};
+}
+
+// the noise key of (seed, env): distinct envs of one seed get distinct keys
+// (an odd multiplier is a bijection mod 2^32)
+F110_HD uint32_t noise_key(uint64_t seed, uint64_t env) {
+    return (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x85EBCA6Bu) ^ ((uint32_t)env * 0x9E3779B9u) ^
+           ((uint32_t)(env >> 32) * 0xC2B2AE35u);
+}
+
+// N(0,1) for beam b of the env's stream at `step`: one Philox2x32 block per
+// beam (counter (step, b | step_hi << 16), key noise_key(seed, env)),
+// Box-Muller on 24-bit uniforms in fp32 hardware transcendentals (v_log,
+// v_sqrt, v_cos: the noise is a statistical quantity, its ~1e-7 relative
+// precision is far below the 0.01 m std it scales; tails are cut at 5.8
+// sigma).  The key is per env: wave-uniform in the chunked ray kernels.
+F110_D float beam_normal_k(uint32_t key, uint64_t step, int b) {
+    const U2 r = philox2x32((uint32_t)step, (uint32_t)b | ((uint32_t)(step >> 32) << 16), key);
+    const float u1 = ((float)(r.x >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
+    const float u2 = (float)(r.y >> 8) * (1.0f / 16777216.0f);           // [0, 1)
+    const float rad = __builtin_amdgcn_sqrtf(-2.0f * 0.69314718055994531f * __builtin_amdgcn_logf(u1));
+    return rad * __builtin_amdgcn_cosf(u2);  // cos(2 pi u2)
+}
+
 F110_D float beam_normal(uint64_t seed, uint64_t env, uint64_t step, int b) {
-    U4 c = {(uint32_t)(b >> 1), (uint32_t)step, (uint32_t)(step >> 32), 0x5CA77u};
-    uint32_t k0 = (uint32_t)seed ^ (uint32_t)env;
-    uint32_t k1 = (uint32_t)(seed >> 32) ^ ((uint32_t)(env >> 32) * 0x85EBCA6Bu) ^ 0x3C6EF372u;
-    U4 r = philox(c, k0, k1);
-    float u1 = ((float)(r.x >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
-    float u2 = (float)(r.y >> 8) * (1.0f / 16777216.0f);           // [0, 1)
-    float rad = __builtin_sqrtf(-2.0f * 0.69314718055994531f * __builtin_amdgcn_logf(u1));
-    float tr = (b & 1) ? __builtin_amdgcn_sinf(u2) : __builtin_amdgcn_cosf(u2);  // sin/cos(2 pi u2)
-    return rad * tr;
+    return beam_normal_k(noise_key(seed, env), step, b);
 }
 
 // uniform u32 for (seed, env, episode) — autoreset spawn choice.

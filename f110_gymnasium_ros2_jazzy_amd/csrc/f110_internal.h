@@ -27,7 +27,8 @@ struct StepArgs {
     const f110_params *pa;                    // [A] RaceCar params (update_pose, ray_cast boxes)
     int32_t E, A, B, theta_dis, integrator, ego, autoreset, mode;  // mode 0 step, 1 reset
     int32_t ray_wpb;          // chunked ray kernel: waves (cars) per block, 1 or 4 (F110_RAY_WPB)
-    int32_t ray_kernel;       // 0: k_rays on the row-major EDT; 1: k_rays_tiled, flat ray order; 2: chunked
+    int32_t ray_kernel;       // 0: k_rays on the row-major EDT; 1: k_rays_tiled, flat ray order; 2: chunked;
+                              // 3: chunked k_rays_fx (fixed-point cell index, scalar per-car set-up)
     uint8_t chunk_order[kMaxChunks];  // beam-chunk dispatch order of the chunked ray kernel
     uint64_t *wtrace;         // diagnostic wave trace of the next ray launch (f110_debug_wave_trace) or null
     hipEvent_t gate_wait;     // f110_set_ray_gate: waited on before the ray launch, or null
@@ -114,7 +115,19 @@ struct RayArgs {
     const uint32_t *heavy_count;
     int32_t HB, nch;
     int32_t wpb;  // chunked: waves (cars) per block
+    // fixed-point cell index of k_rays_fx (see fx_cell in f110_kernels.hip):
+    // t = fma(x, inv_res, fx_cx) = 1.5*2^22 + column, on a 2^-30 grid
+    double fx_cx, fx_cy;
 };
+
+// k_rays_fx's magic offset: 1.5 * 2^22.  t = M + q for q in [0, 2^21) lies in
+// the binade [2^22, 2^23), whose ulp is 2^-30, so the low 30 mantissa bits of
+// t hold q's fraction and the next 21 its integer part.
+constexpr double kFxMagic = 6291456.0;
+// bits [61:30] of M: exponent[9:0] (0x015), mantissa bit 51, 21 zero bits
+constexpr uint32_t kFxU0 = 0x05600000u;
+// guard band of the fixed-point fraction, in units of 2^-30 (error budget < 2^-29)
+constexpr uint32_t kFxBand = 4u;
 
 struct ScanArgs {
     MapView map;

@@ -19,6 +19,8 @@
 //  f110_dynamics_batch).
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+
 #include "f110_internal.h"
 
 namespace f110 {
@@ -456,6 +458,201 @@ __global__ void __launch_bounds__(kBlock) k_rays_tiled(RayArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------
+// k_rays_fx: the chunked ray kernel with a fixed-point cell index (one-wave
+// blocks, axis-aligned maps; same results as k_rays_tiled, bit for bit).
+//
+// xy_2_rc's column is int(x_rot / res) with x_rot = x - orig_x
+// (laser_models.py:55-86).  Here one fma puts q = (x - orig_x) / res on a
+// 2^-30 fixed-point grid: t = fma(x, inv_res, M - orig_x * inv_res) with
+// M = 1.5 * 2^22, so t = M + q lies in [2^22, 2^23) for every on-map q and
+// bits [50:30] of t are int(q), bits [29:0] its fraction.  The column, the
+// row, the bounds test and a guard band then cost integer ops only, where the
+// fp64 form took 2 fp64 subtracts, 2 multiplies, 2 fract, 2 adds, a max, 5
+// compares and 2 conversions per lookup.
+//
+// Error budget (in units of q): the constant's rounding (2^-31), t's rounding
+// (2^-31), inv_res's rounding, the reference's own rounding of x - orig_x
+// and of x_rot / res (each <= q * 2^-53 <= 2^-32 for q < 2^21): < 2^-29 in
+// all.  A lane whose fraction lies within kFxBand * 2^-30 = 2^-28 of an
+// integer (either coordinate) takes the exact IEEE path of tiled_cell behind a
+// wave-uniform branch; every other lane has the reference's cell and the
+// reference's bounds verdict (x_rot >= 0 and x_rot < W * res are decided by
+// more than the budget).  Off-map: the sign / exponent test rejects any t
+// outside [2^22, 2^23) (NaN and inf included), the column test the rest.
+//
+// The loop test d > eps is the high word of d != 0: every EDT entry is 0 or
+// >= res > eps (checked at f110_create).  Per car, the set-up (beam-index run,
+// scan pose, speed, noise counter) is wave-uniform and read with scalar loads.
+template <class T>
+__device__ __forceinline__ T ld_const(const T *p) {  // read-only for the kernel: a scalar load when uniform
+    return *reinterpret_cast<const __attribute__((address_space(4))) T *>(reinterpret_cast<uintptr_t>(p));
+}
+
+__device__ __forceinline__ uint32_t dhi(double v) { return (uint32_t)(__double_as_longlong(v) >> 32); }
+__device__ __forceinline__ uint32_t dlo(double v) { return (uint32_t)__double_as_longlong(v); }
+
+// tiled_cell's IEEE path as a byte offset (the fixed-point path's fallback)
+__device__ __forceinline__ uint32_t exact_offset(const TiledMapView &m, double x, double y, uint32_t oob8) {
+    const double xr = x - m.ox, yr = y - m.oy;
+    const bool inb = (xr >= 0) & (xr < m.wres) & (yr >= 0) & (yr < m.hres);  // false for NaN
+    if (!inb) return oob8;
+    int32_t c = (int32_t)(xr / m.res);
+    int32_t r = (int32_t)(yr / m.res);
+    if (c >= m.W) {  // dt[r, W] is dt[r+1, 0] in the reference's row-major read
+        c = 0;
+        ++r;
+    }
+    return r >= m.H ? oob8 : tiled_offset_u24(m.wt, r, c);
+}
+
+// tiled_offset_u24 in 6 integer ops: with R4 = row & ~3 and C4 = col & ~3,
+//   ((row >> 2) * wt + (col >> 2)) * 128 + (row & 3) * 32 + (col & 3) * 8
+//     = R4 * (32 wt - 32) + C4 * 24 + row * 32 + col * 8
+// (24-bit multiplies: row, col < 2^21 and wt < 2^19 on the fixed-point path;
+// off-map lanes compute garbage that the caller's select discards)
+__device__ __forceinline__ uint32_t fx_offset(uint32_t k1, uint32_t row, uint32_t col) {
+    const uint32_t rc = (row << 5) + (col << 3);
+    return __umul24(row & ~3u, k1) + __umul24(col & ~3u, 24u) + rc;
+}
+
+template <bool MASK, bool HANDOFF>
+__global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
+    int g, k;
+    if ((int)blockIdx.x < a.HB) {  // heavy-first blocks: the listed waves
+        const uint32_t item = blockIdx.x;
+        if (item >= ld_const(a.heavy_count)) return;
+        const uint32_t v = ld_const(a.heavy_list + item);
+        g = (int)(v >> 8);
+        k = (int)(v & 255u);
+    } else {
+        const int blk = (int)blockIdx.x - a.HB;
+        const int slot = blk / a.G4;
+        g = blk - slot * a.G4;
+        k = (int)a.order[slot];
+        if (g >= a.EA) return;
+        if (a.HB && ((ld_const(a.heavy_mask + g) >> k) & 1u)) return;  // ran in a heavy block
+    }
+    const int lane = (int)threadIdx.x;
+    const int B = a.B;
+    const int b0 = k * 64;
+    const int b = b0 + lane;
+    const int e = HANDOFF ? g / a.A : g;
+    const bool has = b < B && (!MASK || ld_const(a.reset_mask + e));
+    const int64_t r = (int64_t)g * B + b;
+
+    // ---- per-car set-up (wave-uniform: scalar loads) ----
+    // get_scan's beam index (laser_models.py:167-184) from the car's runs:
+    // the run holding b0 by a scalar binary search, then the (few) runs that
+    // start inside this wave's 64 beams
+    const BeamRun *R = a.runs + (size_t)g * kMaxSeg;
+    const int n = ld_const(a.nruns + g);
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (ld_const(&R[mid].start) <= b0) lo = mid;
+        else hi = mid - 1;
+    }
+    int rs = ld_const(&R[lo].start);
+    double t0 = ld_const(&R[lo].t0), dl = ld_const(&R[lo].delta);
+    for (int j = lo + 1; j < n; ++j) {
+        const int s2 = ld_const(&R[j].start);
+        if (s2 > b0 + 63) break;
+        if (b >= s2) {
+            rs = s2;
+            t0 = ld_const(&R[j].t0);
+            dl = ld_const(&R[j].delta);
+        }
+    }
+    const double x00 = ld_const(a.ray0 + g), y00 = ld_const(a.ray0 + a.EA + g);
+    const double d00 = ld_const(a.ray0 + 2 * a.EA + g);  // :129
+    const double v = ld_const(a.vel + g);
+    // every lane runs the set-up (lanes past the last beam on beam B-1, their
+    // results unused): no divergent branch, no zero-initialised copies
+    const int bc = b < B ? b : B - 1;
+    const double t = t0 + (double)(bc - rs) * dl;
+    int ti = (int)t;  // int(theta_index), laser_models.py:124
+    if (ti >= a.theta_dis) ti = 0;
+    const double c = a.cosines[ti], s = a.sines[ti];
+    const double bcos = a.beam_cos[bc], side = a.side[bc];
+    double x = x00, y = y00, d = has ? d00 : 0.0;
+    double noise = 0.0;
+    {
+        const RayArgs &K = *kernarg_rays();
+        if (K.noise_ext)
+            noise = K.noise_ext[(size_t)e * B + bc];
+        else if (K.noise_std > 0.0)
+            noise = K.noise_std *
+                    (double)beam_normal_k(noise_key(K.seed, (uint64_t)(K.env_offset + e)), ld_const(K.noise_step + e), bc);
+    }
+
+    // ---- trace_ray's loop (laser_models.py:133-141) ----
+    uint32_t oobv;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(oobv) : "s"((uint32_t)a.m.oob << 3));
+    const TiledMapView &m = a.m;
+    const double cxk = a.fx_cx, cyk = a.fx_cy, mr = a.max_range;
+    // inv_res in a VGPR pair for the whole trace: the fma's other operand is an
+    // SGPR constant, and a VOP3 reads one SGPR (an opaque copy, as oobv)
+    double ir;
+    asm volatile("v_mov_b64 %0, %1" : "=v"(ir) : "s"(m.inv_res));
+    const uint32_t W = (uint32_t)m.W, H = (uint32_t)m.H;
+    const uint32_t k1 = (uint32_t)m.wt * 32u - 32u;  // tile-row stride of fx_offset
+    double tot = d;  // :130 (lanes without a ray: d = 0, never traced)
+    uint32_t iters = 0, lane_iters = 0;
+    for (;;) {
+        const uint64_t mk = __builtin_amdgcn_ballot_w64(dhi(d) != 0u) & __builtin_amdgcn_ballot_w64(tot <= mr);
+        if (!mk) break;
+        ++iters;
+        lane_iters += (uint32_t)__popcll(mk);
+        if ((dhi(d) != 0u) & (tot <= mr)) {
+            x += d * c;  // :135
+            y += d * s;  // :136
+            // v_fma_f64 with the constant from its SGPR pair (the compiler's
+            // v_fmac form would first copy it into the accumulator, 2 v_movs per fma)
+            double tx, ty;
+            asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tx) : "v"(x), "v"(ir), "s"(cxk));
+            asm("v_fma_f64 %0, %1, %2, %3" : "=v"(ty) : "v"(y), "v"(ir), "s"(cyk));
+            const uint32_t hx = dhi(tx), lx = dlo(tx), hy = dhi(ty), ly = dlo(ty);
+            const uint32_t col = __builtin_amdgcn_alignbit(hx, lx, 30) - kFxU0;
+            const uint32_t row = __builtin_amdgcn_alignbit(hy, ly, 30) - kFxU0;
+            const bool inb = (col < W) & (row < H) & ((int32_t)hx >= 0x40000000) & ((int32_t)hy >= 0x40000000);
+            const bool near = ((lx << 2) + 4u * kFxBand < 8u * kFxBand) | ((ly << 2) + 4u * kFxBand < 8u * kFxBand);
+            const uint32_t fast = fx_offset(k1, row, col);
+            const uint32_t sel = 0u - (uint32_t)inb;
+            uint32_t off = (fast & sel) | (oobv & ~sel);
+            if (__builtin_amdgcn_ballot_w64(near)) {  // wave-uniform, rare
+                if (near) off = exact_offset(m, x, y, oobv);
+            }
+            d = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(m.dt) + off);
+            tot += d;  // :141
+        }
+    }
+
+    // ---- epilogue (as trace_wave) ----
+    const uint32_t lanes = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(has));
+    if (has) {
+        const RayArgs &K = *kernarg_rays();
+        double range = tot > mr ? mr : tot;  // :143-144
+        if (K.noise_ext || K.noise_std > 0.0) range += noise;  // noise after the clamp (laser_models.py:450-452)
+        if (v != 0.0 && ttc_fires(range, side, v * bcos, K.ttc_thresh)) K.ttc_hit[g] = 1;
+        if (K.obs && g == e * a.A) K.obs[(size_t)e * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
+        if (K.scans_f32) K.scans_f32[r] = (float)range;
+        if (K.scans_f64) K.scans_f64[r] = range;
+        if (HANDOFF) K.scan[r] = range;
+    }
+    if (lane == 0) {
+        const RayArgs &K = *kernarg_rays();
+        if (lanes) {  // one (lookups, rays) atomic pair per wave; the first lookup came from k_agents
+            unsigned long long *slot = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+            atomicAdd(slot, (unsigned long long)(lanes + lane_iters));
+            atomicAdd(slot + 1, (unsigned long long)lanes);
+        }
+        if (K.wcost) {  // this wave's cost, the next step's heavy-first prediction
+            const uint32_t mx = lanes ? 1u + iters : 0u;
+            K.wcost[(size_t)g * a.nch + k] = (uint8_t)(mx < 255u ? mx : 255u);
+        }
+    }
+}
 
 // F110Env.step's time + _check_done (f110_env.py:404-406, :310-352) and the
 // env's autoreset / episode / noise bookkeeping, for env e.  Split in two so
@@ -954,7 +1151,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         ra.scans_f64 = a.out.scans_f64;
         const bool rot = !(a.tmap.os == 0.0 && a.tmap.oc == 1.0);
         const bool mask = ra.reset_mask != nullptr;
-        const bool ch = a.ray_kernel == 2;
+        const bool ch = a.ray_kernel >= 2;
         dim3 g2 = grid;
         if (ch) {
             ra.wpb = a.ray_wpb;
@@ -990,7 +1187,19 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
             reinterpret_cast<const void *>(&k_rays_tiled<true, true, true, true>)};
         void *args[] = {&ra};
         const void *f = fn[v];
-        if (a.wtrace && ch && !rot && !mask)  // diagnostic wave trace (f110_debug_wave_trace)
+        // k_rays_fx (ray_kernel 3; f110_create checked its preconditions: axis-aligned
+        // map, one-wave blocks, W, H < 2^21, |origin / res| < 2^20, EDT entries 0 or > eps)
+        const bool fx = a.ray_kernel == 3 && !rot && ra.wpb == 1;
+        if (fx) {
+            ra.fx_cx = std::fma(-a.tmap.ox, a.tmap.inv_res, kFxMagic);
+            ra.fx_cy = std::fma(-a.tmap.oy, a.tmap.inv_res, kFxMagic);
+            const void *fx_fn[4] = {reinterpret_cast<const void *>(&k_rays_fx<false, false>),
+                                    reinterpret_cast<const void *>(&k_rays_fx<false, true>),
+                                    reinterpret_cast<const void *>(&k_rays_fx<true, false>),
+                                    reinterpret_cast<const void *>(&k_rays_fx<true, true>)};
+            f = fx_fn[(mask ? 2 : 0) + (single ? 0 : 1)];
+        }
+        if (a.wtrace && ch && !rot && !mask && !fx)  // diagnostic wave trace (f110_debug_wave_trace)
             f = single ? reinterpret_cast<const void *>(&k_rays_tiled<false, false, false, true, true>)
                        : reinterpret_cast<const void *>(&k_rays_tiled<false, false, true, true, true>);
         ra.wtrace = a.wtrace;

@@ -236,6 +236,11 @@ class BatchSim:
         k = max(n.value, 1)
         return {"steps": n.value, "k_agents_ms": ms[0] / k, "k_rays_ms": ms[1] / k, "k_post_ms": ms[2] / k}
 
+    @property
+    def ray_kernel(self) -> int:
+        """The ray kernel this context launches (f110_ray_kernel: 3 = k_rays_fx)."""
+        return _lib.check(self.L.f110_ray_kernel(self.ctx), "f110_ray_kernel")
+
     def close(self):
         if getattr(self, "ctx", None):
             torch.cuda.synchronize(self.device)

@@ -236,6 +236,13 @@ F110_API int f110_set_ray_gate(f110_ctx *ctx, void *wait_event, void *record_eve
  * Scheduling only: results are unchanged. */
 F110_API int f110_disable_heavy_first(f110_ctx *ctx);
 
+/* The ray kernel this context launches (>= 0), or a negative error code:
+ * 0 row-major k_rays, 1 tiled flat ray order, 2 tiled chunked, 3 chunked
+ * k_rays_fx (fixed-point cell index; the default where its preconditions
+ * hold: axis-aligned map, one-wave blocks, EDT entries 0 or > eps).
+ * Selected at f110_create (env F110_RAY_KERNEL overrides the default). */
+F110_API int f110_ray_kernel(const f110_ctx *ctx);
+
 /* ---- opponent policy -------------------------------------------------------
  * Replaces gap_follow_action (rl_training/utils/gap_follow.py:3-58), the
  * rule-based opponent train_ddpg.py:168 computes on the host each step from

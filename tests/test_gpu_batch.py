@@ -122,10 +122,11 @@ def test_full_size_properties(tracks, gpu):
 
 @pytest.mark.parametrize("A", [1, 2])
 def test_ray_kernel_dispatch_variants_identical(tracks, gpu, monkeypatch, A):
-    """The three ray-kernel dispatches (F110_RAY_KERNEL: 0 row-major EDT +
+    """The ray-kernel dispatches (F110_RAY_KERNEL: 0 row-major EDT +
     k_post, 1 tiled flat ray order, 2 tiled chunked in descending chunk
-    order -- the default, in one-wave blocks; and the same with 4-car
-    blocks, F110_RAY_WPB=4) give bit-identical steps: scans, obs, collisions,
+    order in one-wave blocks, the same with 4-car blocks (F110_RAY_WPB=4),
+    3 chunked k_rays_fx -- the default, fixed-point cell index) give
+    bit-identical steps: scans, obs, collisions,
     states, with noise, autoreset and a masked reset."""
     E = 300  # not a multiple of 4 cars per chunked block
     sp = _spawns(A)
@@ -134,7 +135,7 @@ def test_ray_kernel_dispatch_variants_identical(tracks, gpu, monkeypatch, A):
     acts = np.stack([rng.uniform(-0.4189, 0.4189, (30, E, A)), rng.uniform(0, 20, (30, E, A))], -1).astype(np.float32)
     mask = rng.random(E) < 0.5
     outs = []
-    for k, wpb in (("0", "1"), ("1", "1"), ("2", "1"), ("2", "4")):
+    for k, wpb in (("0", "1"), ("1", "1"), ("2", "1"), ("2", "4"), ("3", "1")):
         monkeypatch.setenv("F110_RAY_KERNEL", k)
         monkeypatch.setenv("F110_RAY_WPB", wpb)
         sim = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=4,

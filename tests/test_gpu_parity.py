@@ -77,7 +77,7 @@ def test_step_rotated_origin_vs_oracle(rotated, gpu, oracle_mod, monkeypatch, A)
     poses[:, 1:, 0] += 0.8  # the other car 0.8 m along x
     acts = np.stack([rng.uniform(-0.4189, 0.4189, (6, E, A)), rng.uniform(0, 8, (6, E, A))], -1).astype(np.float32)
     outs = []
-    for k in ("0", "1", "2"):
+    for k in ("0", "1", "2", "3"):  # 3 (k_rays_fx) falls back to 2 on a rotated map
         monkeypatch.setenv("F110_RAY_KERNEL", k)
         sim = BatchSim(tm, n_envs=E, n_agents=A, device=gpu, noise_std=0.0, keep_f64_scans=True)
         sim.reset(poses.reshape(E, A, 3))
@@ -286,3 +286,67 @@ def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A):
         ref.state[:] = sim.agent_states().cpu().numpy().reshape(E * A, 7)
         sim.step(act)
         rs, rc = ref.step(act)
+
+
+@pytest.mark.parametrize("kernel", ["2", "3"])
+def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanners, monkeypatch, kernel):
+    """k_rays_fx's fixed-point cell index (F110_RAY_KERNEL=3, the default)
+    against the oracle's IEEE xy_2_rc (laser_models.py:55-104) where it is
+    hardest: scan origins exactly on cell edges and corners with the beam
+    whose table direction is exactly (1, 0) (every lookup of that ray then
+    sits on a row edge: the guard-band path), origins just inside / outside
+    the map edges looking out, and origins far off the map (dt[-1, -1]
+    steps).  Scans must be bit-exact; kernels 2 and 3 must agree."""
+    from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
+    monkeypatch.setenv("F110_RAY_KERNEL", kernel)
+    tm = tracks("Spielberg_map")
+    ox, oy, _ = tm.origin
+    res = tm.resolution
+    H, W = tm.free_mask.shape
+    rng = np.random.default_rng(11)
+    sp = _spawns_for(tm)
+    fov, td = 4.7, 2000
+    yaw_x = fov / 2 + 0.5 * 2 * np.pi / td   # beam 0 has theta index 0.5 -> (cos, sin) = (1, 0) exactly
+    poses = []
+    for i in range(96):  # on-track origins snapped to a row edge / a column edge / a corner
+        x, y, _ = sp[rng.integers(0, sp.shape[0])]
+        r = np.floor((y - oy) / res)
+        c = np.floor((x - ox) / res)
+        if i % 3 == 0:
+            y = oy + r * res
+        elif i % 3 == 1:
+            x = ox + c * res
+        else:
+            x, y = ox + c * res, oy + r * res
+        poses.append((x, y, yaw_x + (0.0 if i % 2 == 0 else rng.normal(0, 1e-3))))
+    for i in range(32):  # near the four map edges, looking out
+        side = i % 4
+        t = rng.uniform(0.1, 0.9)
+        eps = [0.0, 1e-12, 1e-9, 1e-6][(i // 4) % 4] * (1 if i % 8 < 4 else -1)
+        if side == 0:
+            poses.append((ox + eps, oy + t * H * res, np.pi))
+        elif side == 1:
+            poses.append((ox + W * res + eps, oy + t * H * res, 0.0))
+        elif side == 2:
+            poses.append((ox + t * W * res, oy + eps, -np.pi / 2))
+        else:
+            poses.append((ox + t * W * res, oy + H * res + eps, np.pi / 2))
+    for i in range(16):  # far off the map
+        poses.append((ox - 5.0 - 100.0 * i, oy + rng.uniform(-50, 150), rng.uniform(-np.pi, np.pi)))
+    poses = np.asarray(poses, np.float64)
+    E = poses.shape[0]
+    sim = BatchSim(tm, n_envs=E, n_agents=1, device=gpu, noise_std=0.0, keep_f64_scans=True)
+    assert sim.ray_kernel == int(kernel)  # no silent fallback on this axis-aligned map
+    out = sim.reset(poses[:, None, :])
+    torch.cuda.synchronize()
+    st = sim.agent_states().cpu().numpy().reshape(E, 7)
+    got = out.scans_f64.cpu().numpy().reshape(E, -1)
+    ref = oracle_scanners("Spielberg_map").scan(np.stack([st[:, 0], st[:, 1], st[:, 4]], 1))
+    sim.close()
+    bad = np.flatnonzero(~np.all(got == ref, axis=1))
+    assert bad.size == 0, f"poses {bad[:8]} differ from the oracle"
+
+
+def _spawns_for(tm):
+    from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns
+    return centerline_spawns("Spielberg", 1)[:, 0]
