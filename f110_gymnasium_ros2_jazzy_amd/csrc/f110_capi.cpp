@@ -80,6 +80,17 @@ struct f110_ctx {
     int32_t heavy_cap = 0, heavy_T = 16, nch = 0;  // F110_HEAVY_T (with one-wave blocks and a 1/6 list: 16 best)
     uint64_t launch_n = 0;
     int ray_wpb = 1;  // F110_RAY_WPB: 1 (one-wave blocks, default) or 4
+    // k_rays_fx straggler hand-off (opt-in, F110_EVICT=1; F110_EVICT_T / _K tune it).  Measured
+    // (DESIGN §3.2): the hand-off cuts the main pass's wave-iterations by a third but not its
+    // L1 accesses, which set its time (-4.5 %), and the tail's longest residual ray chains
+    // (~0.27 ms at 65536 envs) run after it: off by default
+    bool evict = false;
+    double *ev = nullptr;
+    int32_t *ev_gb = nullptr;
+    uint32_t *ev_ctr = nullptr;
+    uint32_t ev_cap = 0, ev_capp = 0;
+    int32_t ev_P = 1;
+    int32_t ev_T = 16, ev_K = 8;
     int64_t wtrace_n = 0;
     bool wtrace_armed = false;
 
@@ -467,6 +478,23 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (const char *v = std::getenv("F110_RAY_WPB")) c->ray_wpb = std::atoi(v) == 1 ? 1 : 4;
     if (const char *v = std::getenv("F110_HEAVY_T")) c->heavy_T = std::atoi(v);  // 0: no heavy-first dispatch
     if (c->ray_kernel == 3 && !fx_eligible(H, W, resolution, origin, C.eps, edt_k, c->ray_wpb)) c->ray_kernel = 2;
+    if (const char *v = std::getenv("F110_EVICT")) c->evict = std::atoi(v) != 0;
+    if (const char *v = std::getenv("F110_EVICT_T")) c->ev_T = std::max(0, std::min(63, std::atoi(v)));
+    if (const char *v = std::getenv("F110_EVICT_K")) c->ev_K = std::max(0, std::atoi(v));
+    if (c->ray_kernel == 3 && c->evict) {
+        // records for 1/8 of the rays (measured: ~5 % are handed off at T = 16, K = 8);
+        // a wave whose hand-off would overflow keeps tracing its rays itself
+        const size_t rays = EA * (size_t)C.n_beams;
+        const size_t cap = std::min<size_t>(std::max<size_t>(4096, rays / 8), (size_t)1 << 30);
+        c->ev_P = (int32_t)std::max<size_t>(1, std::min<size_t>(kEvMaxParts, cap / 4096));
+        c->ev_capp = (uint32_t)(cap / (size_t)c->ev_P);
+        c->ev_cap = c->ev_capp * (uint32_t)c->ev_P;
+        ALLOC(c->ev, 7 * (size_t)c->ev_cap);
+        ALLOC(c->ev_gb, 2 * (size_t)c->ev_cap);
+        ALLOC(c->ev_ctr, (size_t)kEvMaxParts * kEvStride);
+        // the hand-off absorbs the long waves' tails: heavy-first is off unless asked for
+        if (!std::getenv("F110_HEAVY_T")) c->heavy_T = 0;
+    }
     if (c->ray_kernel >= 2 && c->heavy_T > 0) {
         // up to 1/8 of the waves, in blocks of 4 (measured: ~7% of the waves
         // have a ray longer than 40 lookups and carry ~46% of the wave-iterations)
@@ -590,6 +618,16 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
         a.heavy_count = c->heavy_count;
         a.heavy_cap = c->heavy_cap;
         a.heavy_T = c->heavy_T;
+    }
+    if (c->ev) {
+        a.ev = c->ev;
+        a.ev_gb = c->ev_gb;
+        a.ev_ctr = c->ev_ctr;
+        a.ev_cap = c->ev_cap;
+        a.ev_capp = c->ev_capp;
+        a.ev_P = c->ev_P;
+        a.ev_T = c->ev_T;
+        a.ev_K = c->ev_K;
     }
     a.gate_wait = c->gate_wait;
     a.gate_record = c->gate_record;

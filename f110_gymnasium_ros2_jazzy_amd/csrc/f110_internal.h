@@ -39,6 +39,13 @@ struct StepArgs {
     uint32_t *heavy_list;     // [2][heavy_cap] (car << 8 | chunk), by step parity
     uint32_t *heavy_mask;     // [EA] chunks of the car that are in the heavy list
     uint32_t *heavy_count;    // [2] list lengths, by step parity
+    // k_rays_fx straggler hand-off (see RayArgs::ev); null = off
+    double *ev;
+    int32_t *ev_gb;
+    uint32_t *ev_ctr;
+    uint32_t ev_cap, ev_capp;
+    int32_t ev_P;
+    int32_t ev_T, ev_K;
     int32_t heavy_cap, heavy_T, heavy_build, heavy_use, parity, ray_nch;
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
     uint64_t seed;
@@ -118,7 +125,22 @@ struct RayArgs {
     // fixed-point cell index of k_rays_fx (see fx_cell in f110_kernels.hip):
     // t = fma(x, inv_res, fx_cx) = 1.5*2^22 + column, on a 2^-30 grid
     double fx_cx, fx_cy;
+    // straggler hand-off of k_rays_fx (EVICT) -> k_rays_fx_tail: SoA records
+    // ev[7][ev_cap] = x, y, d, tot, cos, sin, noise; ev_gb[2][ev_cap] = car, beam.
+    // The queue is split in ev_P partitions of ev_capp records (partition p =
+    // records [p*ev_capp, (p+1)*ev_capp)), each with its own counters on a
+    // 128-B line: ev_ctr[p*kEvStride] records written, [p*kEvStride+1] taken.
+    // (~10^6 waves appending to ONE counter serialise at the memory side.)
+    double *ev;
+    int32_t *ev_gb;
+    uint32_t *ev_ctr;
+    uint32_t ev_cap, ev_capp;
+    int32_t ev_P;
+    int32_t ev_T, ev_K;  // evict a wave's active rays once <= ev_T remain after >= ev_K iterations
 };
+
+constexpr int kEvStride = 32;    // u32 per hand-off partition counter line (128 B)
+constexpr int kEvMaxParts = 256;
 
 // k_rays_fx's magic offset: 1.5 * 2^22.  t = M + q for q in [0, 2^21) lies in
 // the binade [2^22, 2^23), whose ulp is 2^-30, so the low 30 mantissa bits of

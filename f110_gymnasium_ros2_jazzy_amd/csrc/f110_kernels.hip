@@ -19,6 +19,7 @@
 //  f110_dynamics_batch).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "f110_internal.h"
@@ -137,6 +138,12 @@ __device__ __forceinline__ void reset_next_heavy(const StepArgs &a) {
 
 __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
     const int g = blockIdx.x * 64 + threadIdx.x;
+    if (a.ev_ctr && blockIdx.x == 0) {  // this step's straggler queue starts empty (k_rays_fx / k_rays_fx_tail)
+        for (int p = threadIdx.x; p < a.ev_P; p += 64) {
+            a.ev_ctr[p * kEvStride] = 0u;
+            a.ev_ctr[p * kEvStride + 1] = 0u;
+        }
+    }
     const int EA = a.E * a.A;
     const bool valid = g < EA;
     const int A = a.A;
@@ -516,7 +523,83 @@ __device__ __forceinline__ uint32_t fx_offset(uint32_t k1, uint32_t row, uint32_
     return __umul24(row & ~3u, k1) + __umul24(col & ~3u, 24u) + rc;
 }
 
-template <bool MASK, bool HANDOFF>
+// Loop-invariant state of the fixed-point sphere trace.
+struct FxLoop {
+    double cxk, cyk, ir, mr;
+    uint32_t oobv, W, H, k1;
+};
+
+__device__ __forceinline__ FxLoop fx_loop(const RayArgs &a) {
+    FxLoop L;
+    // the off-map offset and inv_res in VGPRs for the whole trace (opaque
+    // copies: the select cannot read an SGPR beside its VCC condition, and the
+    // fma's other operand is an SGPR constant, a VOP3 reads one SGPR)
+    asm volatile("v_mov_b32 %0, %1" : "=v"(L.oobv) : "s"((uint32_t)a.m.oob << 3));
+    asm volatile("v_mov_b64 %0, %1" : "=v"(L.ir) : "s"(a.m.inv_res));
+    L.cxk = a.fx_cx;
+    L.cyk = a.fx_cy;
+    L.mr = a.max_range;
+    L.W = (uint32_t)a.m.W;
+    L.H = (uint32_t)a.m.H;
+    L.k1 = (uint32_t)a.m.wt * 32u - 32u;  // tile-row stride of fx_offset
+    return L;
+}
+
+// One iteration of trace_ray's loop (laser_models.py:135-141) for an active
+// lane: step, fixed-point cell, EDT lookup.
+__device__ __forceinline__ void fx_step(const TiledMapView &m, const FxLoop &L, double &x, double &y, double &d,
+                                        double &tot, double c, double s) {
+    x += d * c;  // :135
+    y += d * s;  // :136
+    // v_fma_f64 with the constant from its SGPR pair (the compiler's v_fmac
+    // form would first copy it into the accumulator, 2 v_movs per fma)
+    double tx, ty;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tx) : "v"(x), "v"(L.ir), "s"(L.cxk));
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(ty) : "v"(y), "v"(L.ir), "s"(L.cyk));
+    const uint32_t hx = dhi(tx), lx = dlo(tx), hy = dhi(ty), ly = dlo(ty);
+    const uint32_t col = __builtin_amdgcn_alignbit(hx, lx, 30) - kFxU0;
+    const uint32_t row = __builtin_amdgcn_alignbit(hy, ly, 30) - kFxU0;
+    const bool inb = (col < L.W) & (row < L.H) & ((int32_t)hx >= 0x40000000) & ((int32_t)hy >= 0x40000000);
+    const bool near = ((lx << 2) + 4u * kFxBand < 8u * kFxBand) | ((ly << 2) + 4u * kFxBand < 8u * kFxBand);
+    const uint32_t fast = fx_offset(L.k1, row, col);
+    const uint32_t sel = 0u - (uint32_t)inb;
+    uint32_t off = (fast & sel) | (L.oobv & ~sel);
+    if (__builtin_amdgcn_ballot_w64(near)) {  // wave-uniform, rare
+        if (near) off = exact_offset(m, x, y, L.oobv);
+    }
+    d = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(m.dt) + off);
+    tot += d;  // :141
+}
+
+// The ray's outputs: clamp (:143-144), noise after the clamp
+// (laser_models.py:450-452), check_ttc_jit's beam test on the noisy scan
+// (laser_models.py:188-217), obs / scan entries (F110Env._pack_flat_obs);
+// with other cars in the env (HANDOFF) the f64 range also goes to
+// k_post_multi, whose agent ray_cast re-writes the entries it shortens.
+template <bool HANDOFF>
+__device__ __forceinline__ void fx_epilogue(const RayArgs &K, int g, int e, int b, double tot, double mr,
+                                            double noise, double v, double bcos, double side) {
+    const int64_t r = (int64_t)g * K.B + b;
+    double range = tot > mr ? mr : tot;
+    if (K.noise_ext || K.noise_std > 0.0) range += noise;
+    if (v != 0.0 && ttc_fires(range, side, v * bcos, K.ttc_thresh)) K.ttc_hit[g] = 1;
+    if (K.obs && g == e * K.A) K.obs[(size_t)e * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
+    if (K.scans_f32) K.scans_f32[r] = (float)range;
+    if (K.scans_f64) K.scans_f64[r] = range;
+    if (HANDOFF) K.scan[r] = range;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {  // set bits of mask below this lane
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// EVICT: straggler hand-off.  A wave's longest ray sets its length while
+// most lanes idle (SIMT efficiency 0.55).  Once <= ev_T of its
+// rays are still tracing after >= ev_K iterations, the wave writes their
+// state (x, y, d, tot, cos, sin, noise, car, beam: the whole loop state) to
+// the hand-off queue and ends; k_rays_fx_tail finishes them with lane refill.
+// The state is exact, so the results are those of the uninterrupted loop.
+template <bool MASK, bool HANDOFF, bool EVICT>
 __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
     int g, k;
     if ((int)blockIdx.x < a.HB) {  // heavy-first blocks: the listed waves
@@ -539,7 +622,6 @@ __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
     const int b = b0 + lane;
     const int e = HANDOFF ? g / a.A : g;
     const bool has = b < B && (!MASK || ld_const(a.reset_mask + e));
-    const int64_t r = (int64_t)g * B + b;
 
     // ---- per-car set-up (wave-uniform: scalar loads) ----
     // get_scan's beam index (laser_models.py:167-184) from the car's runs:
@@ -587,59 +669,47 @@ __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
     }
 
     // ---- trace_ray's loop (laser_models.py:133-141) ----
-    uint32_t oobv;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(oobv) : "s"((uint32_t)a.m.oob << 3));
-    const TiledMapView &m = a.m;
-    const double cxk = a.fx_cx, cyk = a.fx_cy, mr = a.max_range;
-    // inv_res in a VGPR pair for the whole trace: the fma's other operand is an
-    // SGPR constant, and a VOP3 reads one SGPR (an opaque copy, as oobv)
-    double ir;
-    asm volatile("v_mov_b64 %0, %1" : "=v"(ir) : "s"(m.inv_res));
-    const uint32_t W = (uint32_t)m.W, H = (uint32_t)m.H;
-    const uint32_t k1 = (uint32_t)m.wt * 32u - 32u;  // tile-row stride of fx_offset
+    const FxLoop L = fx_loop(a);
     double tot = d;  // :130 (lanes without a ray: d = 0, never traced)
     uint32_t iters = 0, lane_iters = 0;
+    bool evicted = false, can_evict = EVICT;
     for (;;) {
-        const uint64_t mk = __builtin_amdgcn_ballot_w64(dhi(d) != 0u) & __builtin_amdgcn_ballot_w64(tot <= mr);
+        const bool act = (dhi(d) != 0u) & (tot <= L.mr);
+        const uint64_t mk = __builtin_amdgcn_ballot_w64(dhi(d) != 0u) & __builtin_amdgcn_ballot_w64(tot <= L.mr);
         if (!mk) break;
+        if (EVICT && can_evict && iters >= (uint32_t)a.ev_K && (uint32_t)__popcll(mk) <= (uint32_t)a.ev_T) {
+            const RayArgs &K = *kernarg_rays();
+            const uint32_t cnt = (uint32_t)__popcll(mk);
+            const uint32_t part = blockIdx.x % (uint32_t)K.ev_P;
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(K.ev_ctr + part * kEvStride, cnt);
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (base + cnt <= K.ev_capp) {
+                if (act) {
+                    const size_t i = (size_t)part * K.ev_capp + base + lanes_below(mk), C = K.ev_cap;
+                    K.ev[i] = x;
+                    K.ev[C + i] = y;
+                    K.ev[2 * C + i] = d;
+                    K.ev[3 * C + i] = tot;
+                    K.ev[4 * C + i] = c;
+                    K.ev[5 * C + i] = s;
+                    K.ev[6 * C + i] = noise;
+                    K.ev_gb[i] = g;
+                    K.ev_gb[C + i] = b;
+                    evicted = true;
+                }
+                break;
+            }
+            can_evict = false;  // queue full: this wave finishes its rays itself
+        }
         ++iters;
         lane_iters += (uint32_t)__popcll(mk);
-        if ((dhi(d) != 0u) & (tot <= mr)) {
-            x += d * c;  // :135
-            y += d * s;  // :136
-            // v_fma_f64 with the constant from its SGPR pair (the compiler's
-            // v_fmac form would first copy it into the accumulator, 2 v_movs per fma)
-            double tx, ty;
-            asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tx) : "v"(x), "v"(ir), "s"(cxk));
-            asm("v_fma_f64 %0, %1, %2, %3" : "=v"(ty) : "v"(y), "v"(ir), "s"(cyk));
-            const uint32_t hx = dhi(tx), lx = dlo(tx), hy = dhi(ty), ly = dlo(ty);
-            const uint32_t col = __builtin_amdgcn_alignbit(hx, lx, 30) - kFxU0;
-            const uint32_t row = __builtin_amdgcn_alignbit(hy, ly, 30) - kFxU0;
-            const bool inb = (col < W) & (row < H) & ((int32_t)hx >= 0x40000000) & ((int32_t)hy >= 0x40000000);
-            const bool near = ((lx << 2) + 4u * kFxBand < 8u * kFxBand) | ((ly << 2) + 4u * kFxBand < 8u * kFxBand);
-            const uint32_t fast = fx_offset(k1, row, col);
-            const uint32_t sel = 0u - (uint32_t)inb;
-            uint32_t off = (fast & sel) | (oobv & ~sel);
-            if (__builtin_amdgcn_ballot_w64(near)) {  // wave-uniform, rare
-                if (near) off = exact_offset(m, x, y, oobv);
-            }
-            d = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(m.dt) + off);
-            tot += d;  // :141
-        }
+        if (act) fx_step(a.m, L, x, y, d, tot, c, s);
     }
 
-    // ---- epilogue (as trace_wave) ----
+    // ---- epilogue ----
     const uint32_t lanes = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(has));
-    if (has) {
-        const RayArgs &K = *kernarg_rays();
-        double range = tot > mr ? mr : tot;  // :143-144
-        if (K.noise_ext || K.noise_std > 0.0) range += noise;  // noise after the clamp (laser_models.py:450-452)
-        if (v != 0.0 && ttc_fires(range, side, v * bcos, K.ttc_thresh)) K.ttc_hit[g] = 1;
-        if (K.obs && g == e * a.A) K.obs[(size_t)e * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
-        if (K.scans_f32) K.scans_f32[r] = (float)range;
-        if (K.scans_f64) K.scans_f64[r] = range;
-        if (HANDOFF) K.scan[r] = range;
-    }
+    if (has && !evicted) fx_epilogue<HANDOFF>(*kernarg_rays(), g, e, b, tot, L.mr, noise, v, bcos, side);
     if (lane == 0) {
         const RayArgs &K = *kernarg_rays();
         if (lanes) {  // one (lookups, rays) atomic pair per wave; the first lookup came from k_agents
@@ -651,6 +721,86 @@ __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
             const uint32_t mx = lanes ? 1u + iters : 0u;
             K.wcost[(size_t)g * a.nch + k] = (uint8_t)(mx < 255u ? mx : 255u);
         }
+    }
+}
+
+// k_rays_fx_tail: the handed-off rays, traced to the end with lane refill.
+// Persistent waves take records from the queue (one atomic per refill);
+// whenever >= kTailRefill lanes are idle, the finished lanes write their
+// outputs and every idle lane takes the next record: the re-arm is the
+// record's 9 loads, so the lanes stay busy where a ray-per-lane wave would
+// wait on its longest ray.  Every wave exits once the queue is drained and
+// its lanes are done (the queue was filled by the previous launch: no wait).
+constexpr uint32_t kTailRefill = 16;
+constexpr int kTailWaves = 8192;  // 8 waves per SIMD on 256 CUs
+
+template <bool HANDOFF>
+__global__ void __launch_bounds__(64) k_rays_fx_tail(RayArgs a) {
+    // wave -> partition blockIdx % P (the waves of a partition share its counters)
+    const uint32_t part = blockIdx.x % (uint32_t)a.ev_P;
+    const uint32_t capp = a.ev_capp;
+    uint32_t nrec = ld_const(a.ev_ctr + part * kEvStride);
+    nrec = nrec < capp ? nrec : capp;  // reservations past the capacity were not written
+    if ((blockIdx.x / (uint32_t)a.ev_P) * 64u >= nrec) return;  // nothing left for this wave's first take
+    uint32_t *head = a.ev_ctr + part * kEvStride + 1;
+    const size_t pbase = (size_t)part * capp;
+    const size_t cap = a.ev_cap;
+    const int lane = (int)threadIdx.x;
+    const FxLoop L = fx_loop(a);
+    double x = 0.0, y = 0.0, d = 0.0, tot = 0.0, c = 0.0, s = 0.0, noise = 0.0, v = 0.0, bcos = 0.0, side = 0.0;
+    int g = 0, b = 0;
+    bool busy = false, exhausted = false;
+    uint32_t lane_iters = 0;
+    for (;;) {
+        bool tracing = busy & (dhi(d) != 0u) & (tot <= L.mr);
+        uint64_t tm = __builtin_amdgcn_ballot_w64(tracing);
+        const bool refill = !exhausted && (uint32_t)__popcll(tm) <= 64u - kTailRefill;
+        if (refill || exhausted) {
+            if (busy && !tracing) {  // finished: outputs, lane free
+                const RayArgs &K = *kernarg_rays();
+                fx_epilogue<HANDOFF>(K, g, HANDOFF ? g / K.A : g, b, tot, L.mr, noise, v, bcos, side);
+                busy = false;
+            }
+        }
+        if (refill) {
+            const uint64_t fm = __builtin_amdgcn_ballot_w64(!busy);
+            const uint32_t cnt = (uint32_t)__popcll(fm);
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(head, cnt);
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (base + cnt >= nrec) exhausted = true;
+            if (!busy) {
+                const uint32_t ip = base + lanes_below(fm);
+                if (ip < nrec) {
+                    const size_t C = cap, i = pbase + ip;
+                    x = a.ev[i];
+                    y = a.ev[C + i];
+                    d = a.ev[2 * C + i];
+                    tot = a.ev[3 * C + i];
+                    c = a.ev[4 * C + i];
+                    s = a.ev[5 * C + i];
+                    noise = a.ev[6 * C + i];
+                    g = a.ev_gb[i];
+                    b = a.ev_gb[C + i];
+                    v = a.vel[g];
+                    bcos = a.beam_cos[b];
+                    side = a.side[b];
+                    busy = true;
+                }
+            }
+            tracing = busy & (dhi(d) != 0u) & (tot <= L.mr);
+            tm = __builtin_amdgcn_ballot_w64(tracing);
+        }
+        if (!tm) {
+            if (exhausted) break;
+            continue;  // every lane idle, queue not drained: the next pass refills
+        }
+        lane_iters += (uint32_t)__popcll(tm);
+        if (tracing) fx_step(a.m, L, x, y, d, tot, c, s);
+    }
+    if (lane == 0 && lane_iters) {  // lookups only: the rays were counted by k_rays_fx
+        unsigned long long *slot = a.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+        atomicAdd(slot, (unsigned long long)lane_iters);
     }
 }
 
@@ -1193,11 +1343,23 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         if (fx) {
             ra.fx_cx = std::fma(-a.tmap.ox, a.tmap.inv_res, kFxMagic);
             ra.fx_cy = std::fma(-a.tmap.oy, a.tmap.inv_res, kFxMagic);
-            const void *fx_fn[4] = {reinterpret_cast<const void *>(&k_rays_fx<false, false>),
-                                    reinterpret_cast<const void *>(&k_rays_fx<false, true>),
-                                    reinterpret_cast<const void *>(&k_rays_fx<true, false>),
-                                    reinterpret_cast<const void *>(&k_rays_fx<true, true>)};
-            f = fx_fn[(mask ? 2 : 0) + (single ? 0 : 1)];
+            ra.ev = a.ev;
+            ra.ev_gb = a.ev_gb;
+            ra.ev_ctr = a.ev_ctr;
+            ra.ev_cap = a.ev_cap;
+            ra.ev_capp = a.ev_capp;
+            ra.ev_P = a.ev_P;
+            ra.ev_T = a.ev_T;
+            ra.ev_K = a.ev_K;
+            const void *fx_fn[8] = {reinterpret_cast<const void *>(&k_rays_fx<false, false, false>),
+                                    reinterpret_cast<const void *>(&k_rays_fx<false, true, false>),
+                                    reinterpret_cast<const void *>(&k_rays_fx<true, false, false>),
+                                    reinterpret_cast<const void *>(&k_rays_fx<true, true, false>),
+                                    reinterpret_cast<const void *>(&k_rays_fx<false, false, true>),
+                                    reinterpret_cast<const void *>(&k_rays_fx<false, true, true>),
+                                    reinterpret_cast<const void *>(&k_rays_fx<true, false, true>),
+                                    reinterpret_cast<const void *>(&k_rays_fx<true, true, true>)};
+            f = fx_fn[(a.ev ? 4 : 0) + (mask ? 2 : 0) + (single ? 0 : 1)];
         }
         if (a.wtrace && ch && !rot && !mask && !fx)  // diagnostic wave trace (f110_debug_wave_trace)
             f = single ? reinterpret_cast<const void *>(&k_rays_tiled<false, false, false, true, true>)
@@ -1205,6 +1367,13 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         ra.wtrace = a.wtrace;
         const unsigned bdim = ch ? 64u * (unsigned)ra.wpb : (unsigned)kBlock;
         if ((e = hipLaunchKernel(f, g2, dim3(bdim), args, 0, s)) != hipSuccess) return e;
+        if (fx && a.ev) {  // the handed-off stragglers (the queue is read on the device)
+            const unsigned tg = (unsigned)std::max<int64_t>(
+                a.ev_P, std::min<int64_t>(kTailWaves, ((int64_t)a.ev_cap + 63) / 64) / a.ev_P * a.ev_P);
+            const void *tf = single ? reinterpret_cast<const void *>(&k_rays_fx_tail<false>)
+                                    : reinterpret_cast<const void *>(&k_rays_fx_tail<true>);
+            if ((e = hipLaunchKernel(tf, dim3(tg), dim3(64), args, 0, s)) != hipSuccess) return e;
+        }
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (a.gate_record && (e = hipEventRecord(a.gate_record, s)) != hipSuccess) return e;

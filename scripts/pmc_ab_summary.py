@@ -3,14 +3,16 @@ import csv, glob, json, os, sys
 d = sys.argv[1]
 res = {}
 for path in sorted(glob.glob(os.path.join(d, "v*_g*", "**", "*counter_collection.csv"), recursive=True)):
-    var = os.path.relpath(path, d).split(os.sep)[0].split("_")[0]
+    var = os.path.relpath(path, d).split(os.sep)[0].rsplit("_g", 1)[0]
     vals = {}
     with open(path) as f:
         for row in csv.DictReader(f):
-            if "k_rays" in row.get("Kernel_Name", ""):
-                vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
-    for k, v in vals.items():
-        res.setdefault(var, {})[k] = sum(v) / len(v)
+            kn = row.get("Kernel_Name", "")
+            if "k_rays" in kn:
+                tag = "tail" if "tail" in kn else "main"
+                vals.setdefault((tag, row["Counter_Name"]), []).append(float(row["Counter_Value"]))
+    for (tag, k), v in vals.items():
+        res.setdefault(var + ("" if tag == "main" else "/tail"), {})[k] = sum(v) / len(v)
 for var, c in res.items():
     if "GRBM_GUI_ACTIVE" in c:
         cyc = c["GRBM_GUI_ACTIVE"] / 8.0

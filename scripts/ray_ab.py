@@ -16,7 +16,8 @@ import torch  # noqa: E402
 from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns, load_map  # noqa: E402
 from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim  # noqa: E402
 
-KNOBS = ("F110_RAY_KERNEL", "F110_CHUNK_ORDER", "F110_HEAVY_T", "F110_RAY_WPB", "F110_HEAVY_DIV")
+KNOBS = ("F110_RAY_KERNEL", "F110_CHUNK_ORDER", "F110_HEAVY_T", "F110_RAY_WPB", "F110_HEAVY_DIV", "F110_EVICT",
+         "F110_EVICT_T", "F110_EVICT_K")
 
 
 def parse_variants(spec):

@@ -125,7 +125,8 @@ def test_ray_kernel_dispatch_variants_identical(tracks, gpu, monkeypatch, A):
     """The ray-kernel dispatches (F110_RAY_KERNEL: 0 row-major EDT +
     k_post, 1 tiled flat ray order, 2 tiled chunked in descending chunk
     order in one-wave blocks, the same with 4-car blocks (F110_RAY_WPB=4),
-    3 chunked k_rays_fx -- the default, fixed-point cell index) give
+    3 chunked k_rays_fx -- the default, fixed-point cell index --, and 3 with
+    the straggler hand-off to the refill tail kernel, F110_EVICT=1) give
     bit-identical steps: scans, obs, collisions,
     states, with noise, autoreset and a masked reset."""
     E = 300  # not a multiple of 4 cars per chunked block
@@ -135,9 +136,11 @@ def test_ray_kernel_dispatch_variants_identical(tracks, gpu, monkeypatch, A):
     acts = np.stack([rng.uniform(-0.4189, 0.4189, (30, E, A)), rng.uniform(0, 20, (30, E, A))], -1).astype(np.float32)
     mask = rng.random(E) < 0.5
     outs = []
-    for k, wpb in (("0", "1"), ("1", "1"), ("2", "1"), ("2", "4"), ("3", "1")):
+    for k, wpb, evict in (("0", "1", "0"), ("1", "1", "0"), ("2", "1", "0"), ("2", "4", "0"), ("3", "1", "0"),
+                          ("3", "1", "1")):
         monkeypatch.setenv("F110_RAY_KERNEL", k)
         monkeypatch.setenv("F110_RAY_WPB", wpb)
+        monkeypatch.setenv("F110_EVICT", evict)  # 3 + 1: k_rays_fx with the straggler hand-off to k_rays_fx_tail
         sim = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=4,
                    keep_f64_scans=True)
         sim.reset(poses)
