@@ -62,7 +62,8 @@ EXPORTS = [
     "f110_host_window_ranges", "f110_track_create", "f110_track_destroy", "f110_track_arrays",
     "f110_default_reward_params", "f110_reward", "f110_replay_create", "f110_replay_destroy", "f110_replay_add",
     "f110_replay_sample", "f110_replay_update_priorities", "f110_replay_length", "f110_replay_arrays",
-    "f110_debug_wave_trace", "f110_set_ray_gate", "f110_disable_heavy_first", "f110_ray_kernel", "f110_adam_step", "f110_ddpg_scratch_floats", "f110_ddpg_actor_head",
+    "f110_debug_wave_trace", "f110_set_ray_gate", "f110_disable_heavy_first", "f110_ray_kernel",
+    "f110_dynamics_ks_batch", "f110_collision_batch", "f110_collision_multiple", "f110_adam_step", "f110_ddpg_scratch_floats", "f110_ddpg_actor_head",
     "f110_ddpg_actor_head_bwd", "f110_ddpg_td_target", "f110_ddpg_critic_loss", "f110_ddpg_critic_loss_bwd",
     "f110_ddpg_q_mean", "f110_ddpg_q_mean_bwd", "f110_ddpg_relu_bwd_scratch_floats", "f110_ddpg_relu_bwd", "f110_ddpg_linear_relu",
 ]
@@ -112,6 +113,9 @@ def load(build_if_missing: bool = True):
     L.f110_set_state.argtypes = [_P, _P, _P, _P, _P]
     L.f110_scan_batch.argtypes = [_P, _P, i64, _P, _P, _P, _P]
     L.f110_dynamics_batch.argtypes = [_P, _P, _P, _P, i64, _P]
+    L.f110_dynamics_ks_batch.argtypes = [_P, _P, _P, _P, i64, _P]
+    L.f110_collision_batch.argtypes = [_P, _P, i64, _P, _P]
+    L.f110_collision_multiple.argtypes = [_P, i64, ctypes.c_int32, _P, _P, _P]
     L.f110_read_counters.argtypes = [_P, ctypes.POINTER(u64), ctypes.POINTER(u64), _P]
     L.f110_reset_counters.argtypes = [_P, _P]
     L.f110_set_scan_noise.argtypes = [_P, _P]

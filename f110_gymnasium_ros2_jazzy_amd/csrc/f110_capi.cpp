@@ -742,6 +742,28 @@ extern "C" int f110_dynamics_batch(f110_ctx *ctx, const double *x, const double 
     return F110_OK;
 }
 
+extern "C" int f110_dynamics_ks_batch(f110_ctx *ctx, const double *x, const double *u, double *f, int64_t M,
+                                      void *stream) {
+    if (!ctx || !x || !u || !f || M < 0) return fail(F110_E_INVALID, "f110_dynamics_ks_batch: bad arguments");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    HIP_TRY(launch_dynamics_ks_batch(x, u, f, M, ctx->p, (hipStream_t)stream));
+    return F110_OK;
+}
+
+extern "C" int f110_collision_batch(const double *v1, const double *v2, int64_t M, uint8_t *out, void *stream) {
+    if (M < 0 || (M > 0 && (!v1 || !v2 || !out))) return fail(F110_E_INVALID, "f110_collision_batch: bad arguments");
+    HIP_TRY(launch_collision_batch(v1, v2, M, out, (hipStream_t)stream));
+    return F110_OK;
+}
+
+extern "C" int f110_collision_multiple(const double *verts, int64_t M, int32_t N, double *collisions, double *idx,
+                                       void *stream) {
+    if (M < 0 || N < 1 || N > kMaxMultiBodies || (M > 0 && (!verts || !collisions || !idx)))
+        return fail(F110_E_INVALID, "f110_collision_multiple: bad arguments (1 <= N <= 64)");
+    HIP_TRY(launch_collision_multiple(verts, M, N, collisions, idx, (hipStream_t)stream));
+    return F110_OK;
+}
+
 extern "C" int f110_read_counters(f110_ctx *ctx, uint64_t *lookups, uint64_t *rays, void *stream) {
     if (!ctx) return fail(F110_E_INVALID, "f110_read_counters: null context");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;

@@ -73,6 +73,20 @@ F110_HD double steering_constraint(double sa, double sv, double s_min, double s_
     return sv;
 }
 
+// vehicle_dynamics_ks, dynamic_models.py:90-121: the kinematic single-track
+// right-hand side of x[5] = (x, y, steer, v, yaw) under the constrained input.
+F110_HD void vehicle_dynamics_ks(const double x[5], double u0_in, double u1_in, const f110_params &p,
+                                 double f[5]) {
+    const double lwb = p.lf + p.lr;
+    const double u0 = steering_constraint(x[2], u0_in, p.s_min, p.s_max, p.sv_min, p.sv_max);
+    const double u1 = accl_constraints(x[3], u1_in, p.v_switch, p.a_max, p.v_min, p.v_max);
+    f[0] = x[3] * cos(x[4]);
+    f[1] = x[3] * sin(x[4]);
+    f[2] = u0;
+    f[3] = u1;
+    f[4] = x[3] / lwb * tan(x[2]);
+}
+
 // vehicle_dynamics_st, dynamic_models.py:123-176 (KS branch :152-160 via
 // vehicle_dynamics_ks :90-121).  Python's left-to-right order kept.
 F110_HD void vehicle_dynamics_st(const double x[7], double u0_in, double u1_in, const f110_params &p,

@@ -15,6 +15,7 @@ namespace f110 {
 constexpr int kCtrSlots = 256;
 constexpr int kCtrStride = 16;  // u64 per slot (128 B)
 constexpr int kRayBlock = 256; // threads per block of the ray kernels
+constexpr int kMaxMultiBodies = 64;  // f110_collision_multiple: bodies per set
 constexpr int kMaxChunks = 32;  // 64-beam chunks per scan (n_beams <= 2048) for the chunked ray dispatch
 
 // Everything one launch of the fused env-step kernel needs, passed by value.
@@ -282,6 +283,11 @@ hipError_t launch_scan_batch(const ScanArgs &a, hipStream_t s);
 hipError_t launch_gap_follow(const GapFollowArgs &a, hipStream_t s);
 hipError_t launch_reward(const RewardArgs &a, hipStream_t s);
 size_t gap_follow_lds_bytes(int B);
+hipError_t launch_dynamics_ks_batch(const double *x, const double *u, double *f, int64_t M, const f110_params &p,
+                                    hipStream_t s);
+hipError_t launch_collision_batch(const double *v1, const double *v2, int64_t M, uint8_t *out, hipStream_t s);
+hipError_t launch_collision_multiple(const double *verts, int64_t M, int32_t N, double *collisions, double *idx,
+                                     hipStream_t s);
 hipError_t launch_dynamics_batch(const double *x, const double *u, double *f, int64_t M, const f110_params &p,
                                  hipStream_t s);
 

@@ -1467,4 +1467,91 @@ hipError_t launch_dynamics_batch(const double *x, const double *u, double *f, in
     return hipGetLastError();
 }
 
+// vehicle_dynamics_ks over M kinematic states [M][5] (f110_dynamics_ks_batch).
+__global__ void __launch_bounds__(kBlock) k_dynamics_ks(const double *__restrict__ x, const double *__restrict__ u,
+                                                        double *__restrict__ f, int64_t M, f110_params p) {
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= M) return;
+    double xs[5], fs[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) xs[k] = x[5 * i + k];
+    vehicle_dynamics_ks(xs, u[2 * i], u[2 * i + 1], p, fs);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) f[5 * i + k] = fs[k];
+}
+
+hipError_t launch_dynamics_ks_batch(const double *x, const double *u, double *f, int64_t M, const f110_params &p,
+                                    hipStream_t s) {
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_dynamics_ks, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, x, u, f, M, p);
+    return hipGetLastError();
+}
+
+// collision (collision_models.py:113-182, GJK) for M vertex pairs: one thread
+// per pair, the pair's 2 x 8 doubles in registers (f110_collision_batch).
+__global__ void __launch_bounds__(kBlock) k_collision_batch(const double *__restrict__ v1,
+                                                            const double *__restrict__ v2, int64_t M,
+                                                            uint8_t *__restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= M) return;
+    double a[8], b[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        a[k] = v1[8 * i + k];
+        b[k] = v2[8 * i + k];
+    }
+    out[i] = gjk_collision(a, b) ? 1 : 0;
+}
+
+hipError_t launch_collision_batch(const double *v1, const double *v2, int64_t M, uint8_t *out, hipStream_t s) {
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_collision_batch, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, v1, v2,
+                       M, out);
+    return hipGetLastError();
+}
+
+// collision_multiple (collision_models.py:184-212) for M independent sets of
+// N bodies: one wave per set, its N(N-1)/2 pairs spread over the lanes, then
+// lane 0 writes the flags and partner indices in the reference's (i, j)
+// order, so the last colliding pair of each body wins as in the reference.
+__global__ void __launch_bounds__(64) k_collision_multiple(const double *__restrict__ verts, int64_t M, int32_t N,
+                                                           double *__restrict__ collisions, double *__restrict__ idx) {
+    const int64_t m = blockIdx.x;
+    if (m >= M) return;
+    __shared__ uint8_t hit[kMaxMultiBodies * kMaxMultiBodies];
+    const double *v = verts + (size_t)m * N * 8;
+    const int P = N * (N - 1) / 2;
+    for (int q = threadIdx.x; q < P; q += 64) {
+        int i = 0, r = q;  // pair q -> (i, j), i < j, in the reference's loop order
+        while (r >= N - 1 - i) {
+            r -= N - 1 - i;
+            ++i;
+        }
+        const int j = i + 1 + r;
+        hit[i * N + j] = gjk_collision(v + 8 * i, v + 8 * j) ? 1 : 0;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    double *c = collisions + (size_t)m * N, *ix = idx + (size_t)m * N;
+    for (int i = 0; i < N; ++i) {
+        c[i] = 0.0;
+        ix[i] = -1.0;
+    }
+    for (int i = 0; i < N - 1; ++i)
+        for (int j = i + 1; j < N; ++j)
+            if (hit[i * N + j]) {
+                c[i] = 1.0;
+                c[j] = 1.0;
+                ix[i] = (double)j;
+                ix[j] = (double)i;
+            }
+}
+
+hipError_t launch_collision_multiple(const double *verts, int64_t M, int32_t N, double *collisions, double *idx,
+                                     hipStream_t s) {
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_collision_multiple, dim3((unsigned)M), dim3(64), 0, s, verts, M, N, collisions, idx);
+    return hipGetLastError();
+}
+
 }  // namespace f110

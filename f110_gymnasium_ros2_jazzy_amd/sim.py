@@ -216,6 +216,15 @@ class BatchSim:
                    "f110_dynamics_batch")
         return f
 
+    def dynamics_ks_batch(self, x, u) -> torch.Tensor:
+        """vehicle_dynamics_ks (dynamic_models.py:90-121) for kinematic states [M, 5]."""
+        x = torch.as_tensor(x, dtype=torch.float64, device=self.device).reshape(-1, 5).contiguous()
+        u = torch.as_tensor(u, dtype=torch.float64, device=self.device).reshape(-1, 2).contiguous()
+        f = torch.empty_like(x)
+        _lib.check(self.L.f110_dynamics_ks_batch(self.ctx, _ptr(x), _ptr(u), _ptr(f), x.shape[0], self._stream()),
+                   "f110_dynamics_ks_batch")
+        return f
+
     def read_counters(self):
         lk, rays = ctypes.c_uint64(), ctypes.c_uint64()
         _lib.check(self.L.f110_read_counters(self.ctx, ctypes.byref(lk), ctypes.byref(rays), self._stream()),

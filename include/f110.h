@@ -193,6 +193,28 @@ F110_API int f110_scan_batch(f110_ctx *ctx, const double *poses, int64_t M, doub
  * x [M][7], u [M][2] (steer velocity, acceleration) -> f [M][7]. */
 F110_API int f110_dynamics_batch(f110_ctx *ctx, const double *x, const double *u, double *f, int64_t M, void *stream);
 
+/* vehicle_dynamics_ks (dynamic_models.py:90-121) for M kinematic states:
+ * x[M][5] = (x, y, steer, v, yaw), u[M][2] = (steer velocity, accel) ->
+ * f[M][5], under the context's params (the KS model of the reference's
+ * DynamicsTest KATs; the ST model's |v| < 0.5 branch uses the same terms).
+ * Device pointers, async on `stream`.  Replaces: a loop of
+ * vehicle_dynamics_ks calls. */
+F110_API int f110_dynamics_ks_batch(f110_ctx *ctx, const double *x, const double *u, double *f, int64_t M,
+                                    void *stream);
+
+/* ---- collision building blocks (no context) --------------------------------
+ * f110_collision_batch: collision(vertices1, vertices2) (collision_models.py:
+ * 113-182, 2-D GJK, <= 1000 iterations) for M pairs: v1[M][4][2], v2[M][4][2]
+ * -> out[M] (1 = overlap).  Replaces: a Python loop over collision().
+ * f110_collision_multiple: collision_multiple(vertices) (collision_models.py:
+ * 184-212) for M independent sets of N bodies: verts[M][N][4][2] ->
+ * collisions[M][N] (0./1.) and idx[M][N] (partner index, -1. if none; the
+ * last colliding pair in the reference's i < j loop order wins), 1 <= N <= 64.
+ * Device pointers, async on `stream`. */
+F110_API int f110_collision_batch(const double *v1, const double *v2, int64_t M, uint8_t *out, void *stream);
+F110_API int f110_collision_multiple(const double *verts, int64_t M, int32_t N, double *collisions, double *idx,
+                                     void *stream);
+
 /* ---- counters -------------------------------------------------------------
  * EDT lookups and rays traced by f110_step/f110_reset/f110_scan_batch since
  * the last reset of the counters (device-side accumulation; reading syncs

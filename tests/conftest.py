@@ -1,5 +1,6 @@
 """Shared fixtures.  `-m "not gpu"` runs on CPU (oracle vs golden vectors,
 host-side library logic, gloo multi-process); `-m gpu` needs an MI355X."""
+import json
 import os
 import sys
 
@@ -62,3 +63,39 @@ def tracks():
             cache[map_name] = t
         return cache[map_name]
     return get
+
+
+# ---- per-fixture budgets of non-bit-exact entries ---------------------------
+# Only the agent ray_cast's re-cast beams (laser_models.py:318-346: exact
+# cos/sin/atan2, ocml vs glibc differ by an ulp, amplified near-parallel) may
+# differ from the reference.  Each fixture's count of non-bit-exact entries was
+# recorded once on an MI355X (F110_RECORD_NONEXACT=1 writes
+# gpurun_out/nonexact_beams.json) into tests/golden/nonexact_beams.json and is
+# asserted as an upper bound: a drift in the ray_cast shows up red instead of
+# hiding under a ">95 % bit-exact" bar.
+_BUDGET_FILE = os.path.join(GOLDEN, "nonexact_beams.json")
+_RECORDED: dict = {}
+
+
+@pytest.fixture(scope="session")
+def nonexact_budget():
+    budget = {}
+    if os.path.exists(_BUDGET_FILE):
+        with open(_BUDGET_FILE) as f:
+            budget = json.load(f)
+    record = os.environ.get("F110_RECORD_NONEXACT") == "1"
+
+    def check(key, count):
+        count = int(count)
+        _RECORDED[key] = count
+        if record:
+            return
+        assert key in budget, f"no recorded non-exact budget for {key} (count {count})"
+        assert count <= budget[key], f"{key}: {count} non-bit-exact entries > recorded {budget[key]}"
+
+    yield check
+    if record and _RECORDED:
+        out = os.path.join(REPO, "gpurun_out")
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "nonexact_beams.json"), "w") as f:
+            json.dump(dict(sorted(_RECORDED.items())), f, indent=1)

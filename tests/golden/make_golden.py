@@ -351,10 +351,11 @@ def gen_raycast_ttc(rng):
 
 
 # ------------------------------------------------------------- simulator ----
-def gen_sim(map_name, tag, poses, n_steps, rng, action_fn=None):
+def gen_sim(map_name, tag, poses, n_steps, rng, action_fn=None, integrator=None):
     bc.RaceCar.scan_simulator = None
     A = len(poses)
-    sim = bc.Simulator(DEFAULT_PARAMS, A, 12345, time_step=0.01, integrator=bc.Integrator.RK4)
+    sim = bc.Simulator(DEFAULT_PARAMS, A, 12345, time_step=0.01,
+                       integrator=bc.Integrator.RK4 if integrator is None else integrator)
     sim.set_map(os.path.join(MAPS, map_name + ".yaml"), ".png")
     sim.reset(np.asarray(poses, np.float64))
     for ag in sim.agents:
@@ -371,8 +372,59 @@ def gen_sim(map_name, tag, poses, n_steps, rng, action_fn=None):
         states.append(np.stack([ag.state.copy() for ag in sim.agents]))
         cols.append(np.asarray(obs['collisions'], np.float64).copy())
     save(f"sim_{tag}.npz", map_name=np.bytes_(map_name), poses=np.asarray(poses, np.float64),
+         integrator=np.int32(2 if integrator is bc.Integrator.Euler else 1),  # base_classes.Integrator value
          actions=np.asarray(acts), scans=np.asarray(scans), states=np.asarray(states),
          collisions=np.asarray(cols))
+
+
+def gen_euler(cl):
+    """Simulator.step traces with the Euler integrator (base_classes.py:376-396,
+    RaceCar's own default, :69): one agent on the track and a 2-agent pair."""
+    rng = np.random.default_rng(4242)
+
+    def ahead(i, d):
+        j = (i + 3) % cl.shape[0]
+        th = np.arctan2(cl[j, 1] - cl[i, 1], cl[j, 0] - cl[i, 0])
+        k = (i + d) % cl.shape[0]
+        return [cl[i, 0], cl[i, 1], th], [cl[k, 0], cl[k, 1], th]
+
+    gen_sim("Spielberg_map", "1agent_euler", [ahead(1500, 25)[0]], 80, rng, integrator=bc.Integrator.Euler)
+    gen_sim("Spielberg_map", "2agent_euler", list(ahead(2600, 20)), 60, rng, integrator=bc.Integrator.Euler)
+
+
+def gen_dynamics_kat():
+    """The reference's zero-initial-state KATs (DynamicsTest.test_zeroinit_*,
+    dynamic_models.py:281-423): DynamicsTest's vehicle params, the four inputs,
+    the ground-truth end states held in the reference test (data) and, as a
+    cross-check, scipy odeint's end states of the reference's func_ST /
+    func_KS exactly as the test integrates them (t = arange(0, 1, 1e-4))."""
+    from scipy.integrate import odeint
+    t = dm.DynamicsTest()
+    t.setUp()
+    P = (t.mu, t.C_Sf, t.C_Sr, t.lf, t.lr, t.h, t.m, t.I, t.s_min, t.s_max, t.sv_min, t.sv_max, t.v_switch,
+         t.a_max, t.v_min, t.v_max)
+    g = 9.81
+    names = ["roll", "dec", "acc", "rollleft"]
+    U = np.array([[0., 0.], [0., -0.7 * g], [0.15, 0.63 * g], [0.15, 0.]])
+    gt_st = np.array([[0.] * 7,
+                      [-3.4335000000000013, 0., 0., -6.8670000000000018, 0., 0., 0.],
+                      [3.0731976046859715, 0.2869835398304389, 0.1500000000000000, 6.1802999999999999,
+                       0.1097747074946325, 0.3248268063223301, 0.0697547542798040],
+                      [0., 0., 0.15, 0., 0., 0., 0.]])
+    gt_ks = np.array([[0.] * 5,
+                      [-3.4335000000000013, 0., 0., -6.8670000000000018, 0.],
+                      [3.0845676868494927, 0.1484249221523042, 0.1500000000000000, 6.1803000000000017,
+                       0.1203664469224163],
+                      [0., 0., 0.15, 0., 0.]])
+    tt = np.arange(0., 1., 1e-4)
+    end_st, end_ks = [], []
+    for u in U:
+        end_st.append(odeint(dm.func_ST, np.zeros(7), tt, args=(u,) + P)[-1])
+        end_ks.append(odeint(dm.func_KS, np.zeros(5), tt, args=(u,) + P)[-1])
+    end_st, end_ks = np.asarray(end_st), np.asarray(end_ks)
+    assert np.all(np.abs(end_st - gt_st) < 1e-2) and np.all(np.abs(end_ks - gt_ks) < 1e-2)
+    save("dynamics_kat.npz", names=np.array(names), params=np.array(P), u=U, t=tt[-1:], dt=np.float64(1e-4),
+         n_steps=np.int64(tt.size - 1), gt_st=gt_st, gt_ks=gt_ks, odeint_st=end_st, odeint_ks=end_ks)
 
 
 def gen_update_pose(rng, cl):
@@ -718,6 +770,8 @@ def main():
     gen_env_gapfollow(cl)
     gen_reward(cl)
     gen_scans_rotated(np.random.default_rng(35))
+    gen_euler(cl)
+    gen_dynamics_kat()
 
 
 if __name__ == "__main__":
@@ -726,7 +780,7 @@ if __name__ == "__main__":
         for name in sys.argv[1:]:
             {"env_noise": lambda c: gen_env_noise(c), "env_params": lambda c: gen_env_params(c),
              "gap_follow": lambda c: gen_gap_follow(), "env_gapfollow": gen_env_gapfollow,
-             "reward": gen_reward,
+             "reward": gen_reward, "euler": gen_euler, "dyn_kat": lambda c: gen_dynamics_kat(),
              "scans_rot": lambda c: gen_scans_rotated(np.random.default_rng(35))}[name](_cl)
     else:
         main()

@@ -19,8 +19,9 @@ def env(gpu):
     e.close()
 
 
-def test_f110env_matches_reference_trace(env):
+def test_f110env_matches_reference_trace(env, nonexact_budget):
     d = golden("env_2agent.npz")
+    nonexact = 0
     obs, info = env.reset(options=d["reset_poses"])
     assert obs.dtype == np.float32 and obs.shape == (1088,)
     np.testing.assert_allclose(obs, d["obs"][0], rtol=1e-6, atol=1e-6)
@@ -28,7 +29,7 @@ def test_f110env_matches_reference_trace(env):
     for t in range(d["actions"].shape[0]):
         obs, r, term, trunc, info = env.step(d["actions"][t])
         np.testing.assert_allclose(obs, d["obs"][t + 1], rtol=1e-5, atol=1e-5)
-        assert np.mean(obs == d["obs"][t + 1]) > 0.99
+        nonexact += int(np.sum(obs != d["obs"][t + 1]))
         assert r == d["reward"][t] and term == d["terminated"][t] and trunc == d["truncated"][t]
         for k in ("poses_x", "poses_y", "poses_theta", "linear_vels_x", "linear_vels_y", "ang_vels_z"):
             np.testing.assert_allclose(info[k], d["info_" + k][t + 1], rtol=1e-5, atol=1e-5)
@@ -39,6 +40,7 @@ def test_f110env_matches_reference_trace(env):
         assert abs(info["time"] - d["info_time"][t + 1]) < 1e-12
         np.testing.assert_allclose(np.stack(info["scans"]), d["info_scans"][t + 1], rtol=1e-5, atol=1e-5)
     assert env.unwrapped.timestep == 0.01
+    nonexact_budget("env_2agent_obs", nonexact)
 
 
 def test_f110env_api_surface(env):
@@ -80,9 +82,11 @@ def test_vector_env_numpy_two_agents(gpu):
     venv.close()
 
 
-def _replay(env, d, obs_exact=0.99):
+def _replay(env, d):
     """Drive the facade through a recorded reference run (resets marked by
-    is_reset) and compare every call's outputs."""
+    is_reset) and compare every call's outputs; returns the number of obs
+    entries that are not bit-exact (ray_cast beams only)."""
+    nonexact = 0
     for t in range(d["obs"].shape[0]):
         if d["is_reset"][t]:
             obs, info = env.reset(options=d["reset_poses"])
@@ -90,15 +94,16 @@ def _replay(env, d, obs_exact=0.99):
             obs, r, term, trunc, info = env.step(d["actions"][t])
             assert r == d["reward"][t] and term == d["terminated"][t] and trunc == d["truncated"][t]
         np.testing.assert_allclose(obs, d["obs"][t], rtol=1e-5, atol=1e-5)
-        assert np.mean(obs == d["obs"][t]) >= obs_exact, t
+        nonexact += int(np.sum(obs != d["obs"][t]))
         for k in ("poses_x", "poses_y", "poses_theta", "linear_vels_x", "ang_vels_z"):
             np.testing.assert_allclose(info[k], d["info_" + k][t], rtol=1e-5, atol=1e-5)
         assert np.array_equal(info["collisions"], d["info_collisions"][t])
         assert np.array_equal(info["lap_counts"], d["info_lap_counts"][t])
         np.testing.assert_allclose(np.stack(info["scans"]), d["info_scans"][t], rtol=1e-5, atol=1e-5)
+    return nonexact
 
 
-def test_f110env_reference_noise_stream(gpu):
+def test_f110env_reference_noise_stream(gpu, nonexact_budget):
     """Noise on (the reference default): the facade replays the reference's
     per-car default_rng(seed) draws, so noisy scans match the reference run,
     including the generator restart at the second reset."""
@@ -106,12 +111,12 @@ def test_f110env_reference_noise_stream(gpu):
     d = golden("env_2agent_noise.npz")
     env = F110Env(map_dir=MAPS + os.sep, map="Spielberg_map", map_ext=".png", num_agents=2, seed=int(d["seed"]))
     try:
-        _replay(env, d)
+        nonexact_budget("env_2agent_noise_obs", _replay(env, d))
     finally:
         env.close()
 
 
-def test_f110env_update_params_per_agent(gpu):
+def test_f110env_update_params_per_agent(gpu, nonexact_budget):
     """update_params(p, index=0) before reset: agent 0's dynamics and the box
     it ray-casts agent 1 with use p; GJK keeps the construction params."""
     from f110_gym.envs import F110Env
@@ -122,7 +127,7 @@ def test_f110env_update_params_per_agent(gpu):
         with pytest.raises(IndexError):
             env.update_params(p1, index=2)
         env.update_params(p1, index=0)
-        _replay(env, d)
+        nonexact_budget("env_2agent_params_obs", _replay(env, d))
     finally:
         env.close()
 

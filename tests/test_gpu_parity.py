@@ -131,7 +131,7 @@ def _resync_trace(sim, d):
     T = d["actions"].shape[0]
     st0 = np.zeros((A, 7))
     st0[:, 0], st0[:, 1], st0[:, 4] = d["poses"][:, 0], d["poses"][:, 1], d["poses"][:, 2]
-    worst_state, scan_exact = 0.0, 0
+    worst_state, scan_exact, nonexact = 0.0, 0, 0
     for t in range(T):
         prev = st0 if t == 0 else d["states"][t - 1]
         buf = np.zeros((2, A))
@@ -152,20 +152,25 @@ def _resync_trace(sim, d):
             # (ocml vs glibc, 1 ulp) amplified by near-parallel beam/edge
             # intersections; bound well inside the north star's 1e-5
             np.testing.assert_allclose(scans, d["scans"][t], rtol=1e-9, atol=1e-9)
-            assert np.mean(scans == d["scans"][t]) > 0.95
+            nonexact += int(np.sum(scans != d["scans"][t]))
         assert np.array_equal(out.collisions.cpu().numpy()[0], d["collisions"][t].astype(np.uint8)), t
-    return worst_state, scan_exact, T
+    return worst_state, scan_exact, T, nonexact
 
 
-@pytest.mark.parametrize("tag", ["1agent", "1agent_crash", "2agent", "2agent_overlap", "3agent", "corridor"])
-def test_simulator_traces(sims, tag):
+@pytest.mark.parametrize("tag", ["1agent", "1agent_crash", "2agent", "2agent_overlap", "3agent", "corridor",
+                                 "1agent_euler", "2agent_euler"])
+def test_simulator_traces(sims, tag, nonexact_budget):
+    """Reference Simulator.step traces, RK4 and (the *_euler fixtures) the
+    Euler integrator of update_pose (base_classes.py:376-396)."""
     d = golden(f"sim_{tag}.npz")
     A = d["poses"].shape[0]
-    sim = sims(d["map_name"].item().decode(), 1, A)
-    worst, exact, T = _resync_trace(sim, d)
+    kw = {"integrator": int(d["integrator"])} if "integrator" in d and int(d["integrator"]) != 1 else {}
+    sim = sims(d["map_name"].item().decode(), 1, A, **kw)
+    worst, exact, T, nonexact = _resync_trace(sim, d)
     assert worst < 1e-12, worst
     if A == 1:
         assert exact == T, f"only {exact}/{T} steps bit-exact"
+    nonexact_budget(f"sim_trace/{tag}", nonexact)
 
 
 def test_free_running_trace_matches(sims):
@@ -182,7 +187,7 @@ def test_free_running_trace_matches(sims):
         assert np.array_equal(out.collisions.cpu().numpy()[0], d["collisions"][t].astype(np.uint8))
 
 
-def test_batch_matches_oracle_multi_env(sims, oracle_scanners):
+def test_batch_matches_oracle_multi_env(sims, oracle_scanners, nonexact_budget):
     """64 envs x 2 agents, random actions, 20 steps vs the oracle (F110Env
     reset semantics: reset + one zero-action step)."""
     from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns
@@ -197,6 +202,7 @@ def test_batch_matches_oracle_multi_env(sims, oracle_scanners):
     ref.reset(poses)
     rs, rc = ref.step(np.zeros((E, A, 2)))
     np.testing.assert_allclose(sim.out.scans_f64.cpu().numpy(), rs, rtol=1e-9, atol=1e-9)
+    nonexact = int(np.sum(sim.out.scans_f64.cpu().numpy() != rs))
     for t in range(20):
         act = np.stack([rng.uniform(-0.4189, 0.4189, (E, A)), rng.uniform(0, 20, (E, A))], -1).astype(np.float32)
         out = sim.step(act)
@@ -205,10 +211,10 @@ def test_batch_matches_oracle_multi_env(sims, oracle_scanners):
         np.testing.assert_allclose(st, ref.state, rtol=1e-10, atol=1e-10)
         g = out.scans_f64.cpu().numpy()
         np.testing.assert_allclose(g, rs, rtol=1e-9, atol=1e-9)
-        frac_exact = np.mean(g == rs)
-        assert frac_exact > 0.98, (t, frac_exact)
+        nonexact += int(np.sum(g != rs))
         ref.state[:] = st      # keep the two in lock-step (ulp-level trig differences)
         np.testing.assert_array_equal(out.collisions.cpu().numpy(), rc.astype(np.uint8))
+    nonexact_budget("multi_env_64x2_20steps", nonexact)
 
 
 def test_obs_packing(sims):
@@ -263,7 +269,7 @@ def _adversarial_poses(rng, E, A, sp):
 
 
 @pytest.mark.parametrize("A", [2, 3])
-def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A):
+def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A, nonexact_budget):
     """Agent ray_cast (base_classes.py:206-227, laser_models.py:318-346) with
     opponents behind / beside / touching / on edge-line extensions: the device
     beam-window filter must not change a single range."""
@@ -277,15 +283,17 @@ def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A):
     sim.reset(poses)
     ref.reset(poses)
     rs, rc = ref.step(np.zeros((E, A, 2)))
+    nonexact = 0
     for t in range(4):
         g = sim.out.scans_f64.cpu().numpy()
         np.testing.assert_allclose(g, rs, rtol=1e-9, atol=1e-9)
-        assert np.mean(g == rs) > 0.99, t
+        nonexact += int(np.sum(g != rs))
         np.testing.assert_array_equal(sim.out.collisions.cpu().numpy(), rc.astype(np.uint8))
         act = np.stack([rng.uniform(-0.2, 0.2, (E, A)), rng.uniform(0, 3, (E, A))], -1)
         ref.state[:] = sim.agent_states().cpu().numpy().reshape(E * A, 7)
         sim.step(act)
         rs, rc = ref.step(act)
+    nonexact_budget(f"ray_cast_adversarial_A{A}", nonexact)
 
 
 @pytest.mark.parametrize("kernel", ["2", "3"])
@@ -350,3 +358,65 @@ def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanne
 def _spawns_for(tm):
     from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns
     return centerline_spawns("Spielberg", 1)[:, 0]
+
+
+def _rk4_device(f, x, dt, n):
+    for _ in range(n):
+        k1 = f(x)
+        k2 = f(x + dt * (k1 / 2))
+        k3 = f(x + dt * (k2 / 2))
+        k4 = f(x + dt * k3)
+        x = x + dt * (1 / 6) * (k1 + 2 * k2 + 2 * k3 + k4)
+    return x
+
+
+def test_dynamics_zeroinit_kats(gpu, tracks):
+    """The reference's DynamicsTest.test_zeroinit_{roll,dec,acc,rollleft}
+    (dynamic_models.py:281-423) through the device right-hand sides
+    (f110_dynamics_batch: vehicle_dynamics_st, f110_dynamics_ks_batch:
+    vehicle_dynamics_ks) with DynamicsTest's vehicle params: zero initial
+    state, the four inputs integrated together (4 rows) for 1 s at dt 1e-4
+    (RK4; the reference uses odeint on the same time grid).  End states within
+    the reference's 1e-2 of its ground truth; the rolling car stays exactly
+    at rest, as the reference asserts with == (:310-311)."""
+    from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
+    d = golden("dynamics_kat.npz")
+    sim = BatchSim(tracks("Spielberg_map"), n_envs=1, n_agents=1, device=gpu, noise_std=0.0,
+                   params=dict(zip(PKEYS, d["params"])))
+    u = torch.as_tensor(d["u"], device=gpu)
+    n, dt = int(d["n_steps"]), float(d["dt"])
+    st = _rk4_device(lambda x: sim.dynamics_batch(x, u), torch.zeros(4, 7, dtype=torch.float64, device=gpu), dt, n)
+    ks = _rk4_device(lambda x: sim.dynamics_ks_batch(x, u), torch.zeros(4, 5, dtype=torch.float64, device=gpu), dt, n)
+    st, ks = st.cpu().numpy(), ks.cpu().numpy()
+    sim.close()
+    assert np.all(np.abs(st - d["gt_st"]) < 1e-2), st
+    assert np.all(np.abs(ks - d["gt_ks"]) < 1e-2), ks
+    # and against scipy odeint on the reference's own func_ST / func_KS (the fixture's cross-check)
+    assert np.all(np.abs(st - d["odeint_st"]) < 1e-3) and np.all(np.abs(ks - d["odeint_ks"]) < 1e-3)
+    roll = list(d["names"]).index("roll")
+    assert np.all(st[roll] == 0.0) and np.all(ks[roll] == 0.0)
+
+
+def test_collision_batch_golden(gpu):
+    """f110_collision_batch (collision_models.py:113, GJK) on 3000 car-box
+    pairs of the reference fixture (coincident centres and equal headings
+    included), and f110_collision_multiple (collision_models.py:184-212) on
+    the reference's own KAT CollisionTests.test_multiple_collisions (:313-324,
+    7 perturbed bodies: collisions [1,1,1,1,1,1,0], idx [5,5,5,5,5,4,-1]) and
+    on 200 clustered sets of 2..6 cars."""
+    from f110_gymnasium_ros2_jazzy_amd.collision import collision_batch, collision_multiple
+    d = golden("collision.npz")
+    got = collision_batch(d["verts_a"], d["verts_b"], device=gpu).cpu().numpy()
+    assert np.array_equal(got, d["overlap"])
+    c, i = collision_multiple(d["kat_vertices"], device=gpu)
+    assert np.array_equal(c.cpu().numpy(), d["kat_expected_collisions"])
+    assert np.array_equal(i.cpu().numpy(), d["kat_expected_idx"])
+    assert np.array_equal(c.cpu().numpy(), d["kat_collisions"]) and np.array_equal(i.cpu().numpy(), d["kat_idx"])
+    counts = d["mb_count"]
+    for k in np.unique(counts):
+        sel = np.flatnonzero(counts == k)
+        cc, ii = collision_multiple(d["mb_vertices"][sel, :k], device=gpu)
+        assert np.array_equal(cc.cpu().numpy(), d["mb_collisions"][sel, :k])
+        assert np.array_equal(ii.cpu().numpy(), d["mb_idx"][sel, :k])
+    # empty batch is a no-op
+    assert collision_batch(np.zeros((0, 4, 2)), np.zeros((0, 4, 2)), device=gpu).numel() == 0

@@ -133,12 +133,15 @@ def test_update_pose(oracle_mod):
             st = u["states"][k, t + 1].copy()   # re-sync: compare single steps
 
 
-@pytest.mark.parametrize("tag", ["1agent", "1agent_crash", "2agent", "2agent_overlap", "3agent", "corridor"])
+@pytest.mark.parametrize("tag", ["1agent", "1agent_crash", "2agent", "2agent_overlap", "3agent", "corridor",
+                                 "1agent_euler", "2agent_euler"])
 def test_simulator_traces(oracle_mod, oracle_scanners, tag):
+    """Simulator.step traces (base_classes.py:566-625), RK4 and -- the *_euler
+    fixtures -- the Euler integrator (base_classes.py:376-396)."""
     d = golden(f"sim_{tag}.npz")
     sc = oracle_scanners(d["map_name"].item().decode())
     A = d["poses"].shape[0]
-    sim = oracle_mod.OracleSim(sc, 1, A)
+    sim = oracle_mod.OracleSim(sc, 1, A, integrator=int(d["integrator"]) if "integrator" in d else 1)
     sim.reset(d["poses"])
     for t in range(d["actions"].shape[0]):
         scans, cols = sim.step(d["actions"][t])
@@ -201,3 +204,31 @@ def test_track_arrays_match_reference():
         assert np.array_equal(getattr(t, arr), d["track_" + arr]), arr
     assert t.L == float(d["track_L"])
     t.close()
+
+
+def _rk4(f, x, dt, n):
+    for _ in range(n):
+        k1 = f(x)
+        k2 = f(x + dt * (k1 / 2))
+        k3 = f(x + dt * (k2 / 2))
+        k4 = f(x + dt * k3)
+        x = x + dt * (1 / 6) * (k1 + 2 * k2 + 2 * k3 + k4)
+    return x
+
+
+def test_dynamics_zeroinit_kats_oracle(oracle_mod):
+    """DynamicsTest.test_zeroinit_{roll,dec,acc,rollleft} (dynamic_models.py:
+    281-423): zero initial state, 1 s at dt 1e-4 (RK4 here, odeint in the
+    reference), end state within the reference's 1e-2 of its ground truth;
+    the roll case exactly at rest, as the reference asserts (:310-311)."""
+    d = golden("dynamics_kat.npz")
+    P = oracle_mod.make_params(dict(zip(["mu", "C_Sf", "C_Sr", "lf", "lr", "h", "m", "I", "s_min", "s_max",
+                                         "sv_min", "sv_max", "v_switch", "a_max", "v_min", "v_max"], d["params"])))
+    n, dt = int(d["n_steps"]), float(d["dt"])
+    for k, u in enumerate(d["u"]):
+        st = _rk4(lambda x: oracle_mod.vehicle_dynamics_st(x, u, P), np.zeros(7), dt, n)
+        ks = _rk4(lambda x: oracle_mod.vehicle_dynamics_ks(x, u, P), np.zeros(5), dt, n)
+        assert np.all(np.abs(st - d["gt_st"][k]) < 1e-2), (d["names"][k], st)
+        assert np.all(np.abs(ks - d["gt_ks"][k]) < 1e-2), (d["names"][k], ks)
+        if d["names"][k] == "roll":
+            assert np.all(st == 0.0) and np.all(ks == 0.0)
