@@ -72,6 +72,7 @@ struct f110_ctx {
     const double *noise_ext = nullptr;  // f110_set_scan_noise (caller-owned)
     uint64_t *wtrace = nullptr;         // f110_debug_wave_trace buffer (diagnostics)
     bool heavy_off = false;             // f110_disable_heavy_first
+    bool reset_f32 = false;             // f110_set_reset_dtype
     hipEvent_t gate_wait = nullptr;     // f110_set_ray_gate (caller-owned events)
     hipEvent_t gate_record = nullptr;
     // heavy-first ray dispatch (chunked kernel)
@@ -629,6 +630,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
         a.ev_T = c->ev_T;
         a.ev_K = c->ev_K;
     }
+    a.reset_f32 = c->reset_f32 ? 1 : 0;
     a.gate_wait = c->gate_wait;
     a.gate_record = c->gate_record;
     if (c->wtrace_armed) {  // one traced ray launch
@@ -667,6 +669,17 @@ extern "C" int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dty
     return F110_OK;
 }
 
+extern "C" int f110_set_reset_dtype(f110_ctx *ctx, int32_t dtype) {
+    if (!ctx || (dtype != F110_F32 && dtype != F110_F64))
+        return fail(F110_E_INVALID, "f110_set_reset_dtype: null context or dtype not F110_F32 / F110_F64");
+    ctx->reset_f32 = dtype == F110_F32;
+    return F110_OK;
+}
+
+extern "C" void f110_host_np_sincosf(const float *x, int64_t n, int32_t cos_op, float *out) {
+    for (int64_t i = 0; i < n; ++i) out[i] = np_sincosf(x[i], cos_op != 0);
+}
+
 extern "C" int f110_ray_kernel(const f110_ctx *ctx) {
     if (!ctx) return fail(F110_E_INVALID, "f110_ray_kernel: null context");
     return ctx->ray_kernel;
@@ -693,6 +706,16 @@ extern "C" int f110_get_state(f110_ctx *ctx, double *state, double *steer_buf, i
     if (state) HIP_TRY(hipMemcpyAsync(state, ctx->st, 7 * EA * sizeof(double), hipMemcpyDeviceToDevice, s));
     if (steer_buf) HIP_TRY(hipMemcpyAsync(steer_buf, ctx->sb, 2 * EA * sizeof(double), hipMemcpyDeviceToDevice, s));
     if (steer_cnt) HIP_TRY(hipMemcpyAsync(steer_cnt, ctx->scnt, EA * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    return F110_OK;
+}
+
+extern "C" int f110_get_lap_state(f110_ctx *ctx, double *start_rot, int32_t *toggles, void *stream) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_get_lap_state: null context");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    const size_t E = (size_t)ctx->cfg.n_envs, EA = E * ctx->cfg.n_agents;
+    hipStream_t s = (hipStream_t)stream;
+    if (start_rot) HIP_TRY(hipMemcpyAsync(start_rot, ctx->start_rot, 2 * E * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (toggles) HIP_TRY(hipMemcpyAsync(toggles, ctx->toggles, EA * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
     return F110_OK;
 }
 

@@ -732,6 +732,42 @@ F110_HD double u01_open(uint32_t hi, uint32_t lo) {  // (0, 1], 53 bits
     return ((double)v + 1.0) * (1.0 / 9007199254740992.0);
 }
 
+// ---------------------------------------------------- NumPy float32 trig --
+// np.cos / np.sin on float32 (NumPy 2.2, the x86 SIMD loop of
+// umath/loops_trigonometric: Cody-Waite reduction by pi/2 in three fma steps,
+// degree-8 cosine / degree-9 sine minimax polynomials on [-pi/4, pi/4],
+// quadrant select; |x| beyond 71476.0625 (cos) / 117435.992 (sin) goes to
+// libm, here the correctly rounded float of the f64 function).  F110Env.reset
+// evaluates start_rot this way when its options are float32
+// (f110_env.py:448-451, train_ddpg's dtype).  Bit-exact against the installed
+// NumPy on [-pi, pi] and beyond (tests/test_host_lib.py).
+F110_HD float np_sincosf(float x, bool cos_op) {
+    if (x != x) return x;
+    const float ax = x < 0.0f ? -x : x;
+    if (ax > (cos_op ? 71476.0625f : 117435.992f)) return (float)(cos_op ? cos((double)x) : sin((double)x));
+    const float magic = 0x1.800000p+23f;
+    float q = fmaf(x, 0x1.45f306p-1f, magic);  // x * 2/pi, rounded to the nearest integer (one fma)
+    q = q - magic;
+    float r = fmaf(q, -0x1.921fb0p+00f, x);
+    r = fmaf(q, -0x1.5110b4p-22f, r);
+    r = fmaf(q, -0x1.846988p-48f, r);
+    const float r2 = r * r;
+    float c = fmaf(0x1.98e616p-16f, r2, -0x1.6c06dcp-10f);
+    c = fmaf(c, r2, 0x1.55553cp-05f);
+    c = fmaf(c, r2, -0x1.000000p-01f);
+    c = fmaf(c, r2, 0x1.000000p+00f);
+    float sn = fmaf(0x1.7d3bbcp-19f, r2, -0x1.a06bbap-13f);
+    sn = fmaf(sn, r2, 0x1.11119ap-07f);
+    sn = fmaf(sn, r2, -0x1.555556p-03f);
+    sn = fmaf(sn, r2, 0.0f);
+    sn = fmaf(sn, r, r);
+    int iq = (int)q;  // q is integral
+    if (cos_op) iq += 1;
+    float v = (iq & 1) == 0 ? sn : c;
+    if ((iq & 2) == 2) v = 0.0f - v;
+    return v;
+}
+
 // Philox2x32-10 (Salmon et al., SC'11; passes BigCrush): one 32x32->64
 // multiply and one xor3 per round, half the work of Philox4x32 for the 48
 // random bits one normal needs.

@@ -27,6 +27,7 @@ struct StepArgs {
     f110_params p;                            // Simulator / F110Env params (GJK boxes, lidar_max)
     const f110_params *pa;                    // [A] RaceCar params (update_pose, ray_cast boxes)
     int32_t E, A, B, theta_dis, integrator, ego, autoreset, mode;  // mode 0 step, 1 reset
+    int32_t reset_f32;        // resets follow F110Env.reset(options=float32 poses) (f110_set_reset_dtype)
     int32_t ray_wpb;          // chunked ray kernel: waves (cars) per block, 1 or 4 (F110_RAY_WPB)
     int32_t ray_kernel;       // 0: k_rays on the row-major EDT; 1: k_rays_tiled, flat ray order; 2: chunked;
                               // 3: chunked k_rays_fx (fixed-point cell index, scalar per-car set-up)

@@ -196,21 +196,35 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
             uint32_t k = spawn_draw(a.seed, genv, episode) % (uint32_t)a.n_spawn;
             pz = a.spawn + ((size_t)k * A + ag) * 3;
         }
+        // float32 options (train_ddpg's dtype): the poses are float32 values
+        // and start_rot is NumPy's float32 cos / sin of the float32 yaw
+        double px = pz[0], py = pz[1], pth = pz[2];
+        if (a.reset_f32) {
+            px = (double)(float)px;
+            py = (double)(float)py;
+            pth = (double)(float)pth;
+        }
 #pragma unroll
         for (int k = 0; k < 7; ++k) s[k] = 0.0;
-        s[0] = pz[0];
-        s[1] = pz[1];
-        s[4] = pz[2];
+        s[0] = px;
+        s[1] = py;
+        s[4] = pth;
         b0 = b1 = 0.0;
         cnt = 0;
         raw_steer = 0.0;
         vel = 0.0;
-        a.start[g] = pz[0];
-        a.start[EA + g] = pz[1];
-        a.start[2 * EA + g] = pz[2];
-        if (ag == a.ego) {  // F110Env.reset's start_rot (f110_env.py:450-451), once per episode
-            a.start_rot[e] = cos(-pz[2]);
-            a.start_rot[a.E + e] = sin(-pz[2]);
+        a.start[g] = px;
+        a.start[EA + g] = py;
+        a.start[2 * EA + g] = pth;
+        if (ag == a.ego) {  // F110Env.reset's start_rot (f110_env.py:448-451), once per episode
+            if (a.reset_f32) {
+                const float nt = -(float)pth;
+                a.start_rot[e] = (double)np_sincosf(nt, true);
+                a.start_rot[a.E + e] = (double)np_sincosf(nt, false);
+            } else {
+                a.start_rot[e] = cos(-pth);
+                a.start_rot[a.E + e] = sin(-pth);
+            }
         }
         a.toggles[g] = 0;
         a.near_start[g] = 1;
@@ -852,8 +866,12 @@ __device__ void env_epilogue(const StepArgs &a, int e, const double *stl, int st
         const EpiCar &c = cars[i];
         double px = stl[i * stride] - c.sx;
         double py = stl[i * stride + 1] - c.sy;
-        double dx = r00 * px + r01 * py;
-        double dy = r10 * px + r11 * py;
+        // np.dot(start_rot, [dx; dy]) (f110_env.py:330) is a BLAS dgemm: on
+        // the reference's host each row is fma(r_i1, py, r_i0 * px)
+        // (measured, tests/golden/env_lap_f32.npz; the float32 start_rot is
+        // widened to f64 first)
+        double dx = fma(r01, py, r00 * px);
+        double dy = fma(r11, py, r10 * px);
         double ty;
         if (dy > 2.0) ty = dy - 2.0;
         else if (dy < -2.0) ty = -2.0 - dy;

@@ -89,6 +89,7 @@ class BatchSim:
                                       k.ctypes.data, track.height, track.width, track.resolution, origin,
                                       spawn.ctypes.data if spawn is not None else None, n_spawn), "f110_create")
         self.ctx = ctx
+        self.reset_dtype = np.float64  # f110_set_reset_dtype: the context's default
         E, A, B = self.E, self.A, self.B
         kw = dict(device=dev)
         self.out = StepOut(
@@ -184,6 +185,14 @@ class BatchSim:
         _lib.check(self.L.f110_get_state(self.ctx, _ptr(st), _ptr(sb), _ptr(sc), self._stream()), "f110_get_state")
         return st, sb, sc
 
+    def lap_state(self):
+        """(start_rot [2, E] f64, toggles [E, A] i32): F110Env's start_rot and
+        toggle_list as the device holds them (f110_get_lap_state)."""
+        rot = torch.empty(2, self.E, dtype=torch.float64, device=self.device)
+        tog = torch.empty(self.E * self.A, dtype=torch.int32, device=self.device)
+        _lib.check(self.L.f110_get_lap_state(self.ctx, _ptr(rot), _ptr(tog), self._stream()), "f110_get_lap_state")
+        return rot, tog.reshape(self.E, self.A)
+
     def set_state(self, state=None, steer_buf=None, steer_cnt=None):
         EA = self.E * self.A
         st = None if state is None else torch.as_tensor(state, dtype=torch.float64, device=self.device).reshape(7, EA).contiguous()
@@ -244,6 +253,14 @@ class BatchSim:
         _lib.check(self.L.f110_profile_end(self.ctx, ms, ctypes.byref(n)), "f110_profile_end")
         k = max(n.value, 1)
         return {"steps": n.value, "k_agents_ms": ms[0] / k, "k_rays_ms": ms[1] / k, "k_post_ms": ms[2] / k}
+
+    def set_reset_dtype(self, dtype):
+        """F110Env.reset semantics for the following resets and autoresets
+        (f110_set_reset_dtype): float32 options round the poses to float32
+        and give start_rot NumPy's float32 cos / sin (f110_env.py:448-451)."""
+        f32 = np.dtype(str(dtype).replace("torch.", "")) == np.float32
+        _lib.check(self.L.f110_set_reset_dtype(self.ctx, _lib.F32 if f32 else _lib.F64), "f110_set_reset_dtype")
+        self.reset_dtype = np.float32 if f32 else np.float64
 
     @property
     def ray_kernel(self) -> int:

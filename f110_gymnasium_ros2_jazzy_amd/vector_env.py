@@ -44,7 +44,7 @@ class F110VectorEnv:
                  params: dict | None = None, seed: int = 42, timestep: float = 0.01, device=0,
                  spawn_poses: np.ndarray | None = None, noise_std: float = 0.01, env_offset: int = 0,
                  ego_idx: int = 0, as_numpy: bool = False, autoreset: bool = True, opponent: str | None = None,
-                 opponent_idx: int = 1, reward_fn=None, infos: str = "full", **kwargs):
+                 opponent_idx: int = 1, reward_fn=None, infos: str = "full", options_dtype=np.float32, **kwargs):
         self.num_envs = int(num_envs)
         self.num_agents = int(num_agents)
         self.params = dict(params or DEFAULT_PARAMS)
@@ -58,6 +58,12 @@ class F110VectorEnv:
                             device=device, seed=seed, timestep=timestep, ego_idx=ego_idx, noise_std=noise_std,
                             autoreset=autoreset, spawn_poses=self.spawn_poses, env_offset=env_offset, **kwargs)
         self.device = self.sim.device
+        # F110Env.reset computes start_rot in the dtype of its options
+        # (f110_env.py:448-451): autoresets and option-less resets follow
+        # options_dtype (train_ddpg passes float32 poses); an explicit
+        # reset(options=...) follows that array's dtype
+        self.options_dtype = np.dtype(options_dtype)
+        self.sim.set_reset_dtype(self.options_dtype)
         B, A = self.sim.B, self.num_agents
         x_min, x_max, y_min, y_max = self.track.bounds
         self.single_observation_space = _box(
@@ -124,8 +130,11 @@ class F110VectorEnv:
             self._rng = np.random.default_rng(seed)
         if options is None:
             idx = self._rng.integers(0, self.spawn_poses.shape[0], self.num_envs)
-            options = self.spawn_poses[idx]
+            options = self.spawn_poses[idx].astype(self.options_dtype)
+        dt = options.dtype if hasattr(options, "dtype") else np.asarray(options).dtype
+        self.sim.set_reset_dtype(dt)
         out = self.sim.reset(options)
+        self.sim.set_reset_dtype(self.options_dtype)  # the device autoresets
         self._opponent_next(out)
         if self.reward_fn is not None:
             self.reward_fn.reset()

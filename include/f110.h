@@ -178,6 +178,11 @@ F110_API int f110_set_scan_noise(f110_ctx *ctx, const double *noise);
  * steer_buf: device [2][n_envs*n_agents] f64 ([newest, older]); steer_cnt:
  * device [n_envs*n_agents] i32 — RaceCar.steer_buffer (base_classes.py:108-109). */
 F110_API int f110_get_state(f110_ctx *ctx, double *state, double *steer_buf, int32_t *steer_cnt, void *stream);
+/* F110Env's lap bookkeeping as the device holds it (f110_env.py:310-352,
+ * 441-451): start_rot[2][E] = cos(-th), sin(-th) of each env's ego reset
+ * yaw (float64, or float32 values under F110_F32 resets) and toggles[E*A]
+ * (toggle_list).  Device pointers (either may be NULL), async on `stream`. */
+F110_API int f110_get_lap_state(f110_ctx *ctx, double *start_rot, int32_t *toggles, void *stream);
 F110_API int f110_set_state(f110_ctx *ctx, const double *state, const double *steer_buf, const int32_t *steer_cnt,
                    void *stream);
 
@@ -265,6 +270,14 @@ F110_API int f110_disable_heavy_first(f110_ctx *ctx);
  * Selected at f110_create (env F110_RAY_KERNEL overrides the default). */
 F110_API int f110_ray_kernel(const f110_ctx *ctx);
 
+/* The dtype of the reset poses whose F110Env.reset semantics the following
+ * resets follow (f110_env.py:441-451): F110_F32 (train_ddpg passes float32
+ * options) rounds the reset / autoreset poses to float32 and evaluates the lap
+ * logic's start_rot as NumPy's float32 cos / sin of the float32 yaw;
+ * F110_F64 (the default) keeps float64.  Replaces: the dtype the consumer's
+ * `options` array carries into F110Env.reset. */
+F110_API int f110_set_reset_dtype(f110_ctx *ctx, int32_t dtype);
+
 /* ---- opponent policy -------------------------------------------------------
  * Replaces gap_follow_action (rl_training/utils/gap_follow.py:3-58), the
  * rule-based opponent train_ddpg.py:168 computes on the host each step from
@@ -306,6 +319,9 @@ F110_API int f110_host_cell_index(int32_t H, int32_t W, double resolution, const
  * ray_cast visits for an opponent box whose angular window at the scan
  * origin is center +- half (world frame), for a car at yaw.  Host only; the
  * CPU tests check they contain every beam inside the window. */
+/* NumPy's float32 np.cos (cos_op != 0) / np.sin over n values, as the
+ * device evaluates F110Env.reset's float32 start_rot (test hook). */
+F110_API void f110_host_np_sincosf(const float *x, int64_t n, int32_t cos_op, float *out);
 F110_API void f110_host_window_ranges(double yaw, double fov, int32_t n_beams, double center, double half,
                                       int32_t ranges_out[4]);
 

@@ -535,6 +535,57 @@ def _track_poses(cl, i, gap):
     return np.array([[cl[i, 0], cl[i, 1], th], [cl[k, 0], cl[k, 1], th]], np.float32)
 
 
+def gen_env_lap_f32(cl, max_steps=1500):
+    """F110Env (2 agents, noise off) reset with float32 options -- train_ddpg's
+    dtype -- whose cars each drive full-lock circles (radius ~0.74 m) in an
+    open free area of the Spielberg map (> 12 m from any wall) through their
+    start zones: the lap toggles (_check_done, f110_env.py:310-352, with the
+    float32 start_rot of f110_env.py:448-451) count past 4 for both cars and
+    the episode terminates on laps.  Records toggles, lap counts / times,
+    terminated and collisions per step."""
+    sys.path.insert(0, REPO)
+    from f110_gymnasium_ros2_jazzy_amd.maps import load_map
+    tm = load_map("Spielberg_map")
+    tm.ensure_edt()
+    dt = tm.resolution * np.sqrt(tm.edt_k.astype(np.float64))
+    rr, cc = np.nonzero(dt > 12.0)
+    k = int(np.random.default_rng(0).integers(0, rr.size))
+    x = tm.origin[0] + (cc[k] + 0.5) * tm.resolution
+    y = tm.origin[1] + (rr[k] + 0.5) * tm.resolution
+    poses = np.array([[x, y, 0.3], [x, y - 3.0, 0.3]], np.float32)
+    f110_env = _refload.load_env()
+    bc.RaceCar.scan_simulator = None
+    orig_reset = bc.RaceCar.reset
+
+    def reset_no_noise(self, pose):
+        orig_reset(self, pose)
+        self.scan_rng = None
+
+    bc.RaceCar.reset = reset_no_noise
+    try:
+        env = f110_env.F110Env(map_dir=MAPS + "/", map="Spielberg_map", map_ext=".png", num_agents=2)
+        obs, info = env.reset(options=poses)
+        acts = np.array([[0.4189, 1.5], [0.4189, 1.3]], np.float32)
+        tog, laps, times, term, cols = [env.toggle_list.copy()], [np.asarray(info["lap_counts"]).copy()], \
+            [np.asarray(info["lap_times"]).copy()], [False], [np.asarray(info["collisions"]).copy()]
+        start_rot = env.start_rot.copy()
+        for t in range(max_steps):
+            o, r, te, tr, inf = env.step(acts)
+            tog.append(env.toggle_list.copy())
+            laps.append(np.asarray(inf["lap_counts"]).copy())
+            times.append(np.asarray(inf["lap_times"]).copy())
+            term.append(bool(te))
+            cols.append(np.asarray(inf["collisions"]).copy())
+            if te:
+                break
+        assert term[-1] and not np.any(np.asarray(cols)) and np.all(tog[-1] >= 4)
+        save("env_lap_f32.npz", reset_poses=poses, actions=acts, start_rot=start_rot,
+             toggles=np.asarray(tog), lap_counts=np.asarray(laps), lap_times=np.asarray(times),
+             terminated=np.asarray(term), collisions=np.asarray(cols))
+    finally:
+        bc.RaceCar.reset = orig_reset
+
+
 def gen_env_noise(cl):
     """F110Env (2 agents) with the reference's own scan noise: every RaceCar
     re-creates default_rng(seed) at reset (base_classes.py:204) and scan adds
@@ -772,6 +823,7 @@ def main():
     gen_scans_rotated(np.random.default_rng(35))
     gen_euler(cl)
     gen_dynamics_kat()
+    gen_env_lap_f32(cl)
 
 
 if __name__ == "__main__":
@@ -780,7 +832,7 @@ if __name__ == "__main__":
         for name in sys.argv[1:]:
             {"env_noise": lambda c: gen_env_noise(c), "env_params": lambda c: gen_env_params(c),
              "gap_follow": lambda c: gen_gap_follow(), "env_gapfollow": gen_env_gapfollow,
-             "reward": gen_reward, "euler": gen_euler, "dyn_kat": lambda c: gen_dynamics_kat(),
+             "reward": gen_reward, "euler": gen_euler, "lap_f32": gen_env_lap_f32, "dyn_kat": lambda c: gen_dynamics_kat(),
              "scans_rot": lambda c: gen_scans_rotated(np.random.default_rng(35))}[name](_cl)
     else:
         main()

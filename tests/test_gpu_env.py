@@ -148,3 +148,37 @@ def test_f110env_update_map_keeps_state(gpu):
         assert not np.array_equal(obs2[:1080], obs[:1080])   # new walls
     finally:
         env.close()
+
+
+@pytest.mark.parametrize("options_dtype", ["float32", "auto"])
+def test_vector_env_float32_lap_boundary(gpu, options_dtype):
+    """The batched VectorEnv's device lap logic with float32 reset options
+    (train_ddpg's dtype) against a reference F110Env episode
+    (tests/golden/env_lap_f32.npz): both cars circle through their start
+    zones, the toggles pass 4 and the episode terminates on laps.  start_rot
+    is NumPy's float32 cos / sin of the float32 yaw and np.dot's fma rows
+    (f110_env.py:330, 448-451): lap counts, lap times, collisions and
+    terminated equal the reference at every step.  "auto": the dtype comes
+    from the options array itself; "float32": the env's options_dtype."""
+    from f110_gymnasium_ros2_jazzy_amd.vector_env import F110VectorEnv
+    d = golden("env_lap_f32.npz")
+    kw = {"options_dtype": np.float64} if options_dtype == "auto" else {}
+    env = F110VectorEnv(1, num_agents=2, noise_std=0.0, autoreset=False, device=gpu, **kw)
+    try:
+        obs, info = env.reset(options=d["reset_poses"][None])
+        rot, _ = env.sim.lap_state()
+        sr = d["start_rot"].astype(np.float64)   # the reference's float32 matrix
+        assert np.array_equal(rot[:, 0].cpu().numpy(), [sr[0, 0], sr[1, 0]])
+        T = d["terminated"].shape[0]
+        for t in range(T):
+            if t:
+                obs, r, term, trunc, info = env.step(d["actions"][None])
+                assert bool(term[0]) == bool(d["terminated"][t]), t
+            _, tog = env.sim.lap_state()
+            assert np.array_equal(tog[0].cpu().numpy(), d["toggles"][t].astype(np.int32)), t
+            assert np.array_equal(info["lap_counts"][0].cpu().numpy(), d["lap_counts"][t].astype(np.float32)), t
+            assert np.array_equal(info["lap_times"][0].cpu().numpy(), d["lap_times"][t].astype(np.float32)), t
+            assert np.array_equal(info["collisions"][0].cpu().numpy(), d["collisions"][t].astype(np.int8)), t
+        assert bool(term[0]) and d["lap_counts"][-1].min() >= 2
+    finally:
+        env.close()

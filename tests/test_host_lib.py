@@ -241,3 +241,24 @@ def test_window_ranges_contain_window_beams():
             inside = np.nonzero(np.abs(d) <= half)[0]
             covered = ((inside >= out[0]) & (inside <= out[1])) | ((inside >= out[2]) & (inside <= out[3]))
             assert covered.all(), (fov, B, yaw, center, half, out, inside[~covered])
+
+
+def test_np_float32_sincos_matches_numpy():
+    """The device's float32 start_rot trig (f110_device.h np_sincosf,
+    F110Env.reset with float32 options, f110_env.py:448-451) against the
+    installed NumPy's float32 np.cos / np.sin, bit for bit: yaw range, wider
+    arguments, quadrant boundaries, signed zeros, NaN."""
+    import ctypes
+    from f110_gymnasium_ros2_jazzy_amd import _lib
+    L = _lib.load()
+    rng = np.random.default_rng(3)
+    xs = [rng.uniform(-np.pi, np.pi, 400_000), rng.uniform(-200, 200, 200_000),
+          (np.arange(-64, 65) * np.pi / 4), np.array([0.0, -0.0, np.pi, -np.pi, 1e-30, -1e-30])]
+    x = np.concatenate(xs).astype(np.float32)
+    x = np.concatenate([x, np.nextafter(x[-129 - 6:-6], np.float32(np.inf)), np.array([np.nan], np.float32)])
+    for op, ref in ((1, np.cos), (0, np.sin)):
+        out = np.empty_like(x)
+        L.f110_host_np_sincosf(x.ctypes.data_as(ctypes.c_void_p), x.size, op, out.ctypes.data_as(ctypes.c_void_p))
+        want = ref(x)
+        same = (out == want) | (np.isnan(out) & np.isnan(want))
+        assert same.all(), (op, x[~same][:5], out[~same][:5], want[~same][:5])
