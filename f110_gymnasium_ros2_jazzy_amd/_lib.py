@@ -34,7 +34,8 @@ class F110Config(ctypes.Structure):
 
 class F110Outputs(ctypes.Structure):
     _fields_ = [("obs", _P), ("scans", _P), ("scans_f64", _P), ("collisions", _P), ("terminated", _P),
-                ("was_reset", _P), ("lap_times", _P), ("lap_counts", _P), ("sim_time", _P)]
+                ("was_reset", _P), ("lap_times", _P), ("lap_counts", _P), ("sim_time", _P),
+                ("obs_stride", ctypes.c_int64)]
 
 
 class F110RewardParams(ctypes.Structure):

@@ -644,6 +644,8 @@ extern "C" int f110_reset(f110_ctx *ctx, const double *poses, const uint8_t *env
                           void *stream) {
     if (!ctx || !poses) return fail(F110_E_INVALID, "f110_reset: null argument");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    if (out && out->obs_stride && out->obs_stride < (int64_t)ctx->cfg.n_beams + 4 * ctx->cfg.n_agents)
+        return fail(F110_E_INVALID, "f110_reset: obs_stride < n_beams + 4*n_agents");
     StepArgs a = make_step_args(ctx, out);
     a.mode = 1;
     a.reset_poses = poses;
@@ -658,6 +660,8 @@ extern "C" int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dty
     if (actions_dtype != F110_F32 && actions_dtype != F110_F64)
         return fail(F110_E_INVALID, "f110_step: actions_dtype must be F110_F32 or F110_F64");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    if (out && out->obs_stride && out->obs_stride < (int64_t)ctx->cfg.n_beams + 4 * ctx->cfg.n_agents)
+        return fail(F110_E_INVALID, "f110_step: obs_stride < n_beams + 4*n_agents");
     StepArgs a = make_step_args(ctx, out);
     a.mode = 0;
     a.heavy_build = a.heavy_use = (a.wcost && a.ray_kernel >= 2 && !ctx->heavy_off) ? 1 : 0;  // not on resets

@@ -48,6 +48,11 @@ __device__ __forceinline__ void count_rays(unsigned long long *ctr, uint32_t n, 
     }
 }
 
+// floats between obs rows: f110_outputs.obs_stride, or packed B + 4A
+__host__ __device__ __forceinline__ int64_t obs_row(const StepArgs &a) {
+    return a.out.obs_stride ? a.out.obs_stride : (int64_t)a.B + 4 * a.A;
+}
+
 // F110Env._pack_flat_obs's scan entry (f110_env.py:557-560): f32, NaN ->
 // lidar_max, +-inf -> lidar_max / 0, clip, / lidar_max in f32.
 __device__ __forceinline__ float obs_scan_value(double r, float lmax) {
@@ -1022,9 +1027,8 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
     }
 
     // ---- outputs --------------------------------------------------------
-    const int obs_len = B + 4 * A;
     if (a.out.obs) {  // F110Env._pack_flat_obs, f110_env.py:552-584 (scan of agent 0, e = 0)
-        float *o = a.out.obs + (size_t)e * obs_len;
+        float *o = a.out.obs + (size_t)e * obs_row(a);
         const float lmax = (float)a.p.lidar_max;
         for (int b = tid; b < B; b += kBlock) o[b] = obs_scan_value(scan[b], lmax);
         if (tid < A) {
@@ -1070,7 +1074,7 @@ __global__ void __launch_bounds__(64) k_post_single(StepArgs a) {
         yaw = 0.0;
     }
     if (a.out.obs) {
-        float *o = a.out.obs + (size_t)e * (a.B + 4) + a.B;
+        float *o = a.out.obs + (size_t)e * obs_row(a) + a.B;
         o[0] = (float)stl[0];
         o[1] = (float)stl[1];
         o[2] = (float)wrap_angle(yaw);
@@ -1241,7 +1245,7 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
                 const size_t o = ((size_t)e * A + i) * B + b;
                 if (a.out.scans) a.out.scans[o] = (float)cur;
                 if (a.out.scans_f64) a.out.scans_f64[o] = cur;
-                if (i == 0 && a.out.obs) a.out.obs[(size_t)e * (B + 4 * A) + b] = obs_scan_value(cur, (float)a.p.lidar_max);
+                if (i == 0 && a.out.obs) a.out.obs[(size_t)e * obs_row(a) + b] = obs_scan_value(cur, (float)a.p.lidar_max);
             }
         }
         __syncthreads();
@@ -1250,7 +1254,7 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
     // ---- outputs --------------------------------------------------------
     // the scan entries were written by the ray pass (and patched above)
     if (a.out.obs && tid < A) {  // F110Env._pack_flat_obs, f110_env.py:552-584: pose entries
-        float *o = a.out.obs + (size_t)e * (B + 4 * A) + B + 4 * tid;
+        float *o = a.out.obs + (size_t)e * obs_row(a) + B + 4 * tid;
         o[0] = (float)sh.stl[tid][0];
         o[1] = (float)sh.stl[tid][1];
         o[2] = (float)wrap_angle(sh.stl[tid][4]);
@@ -1313,7 +1317,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         ra.ttc_thresh = a.ttc_thresh;
         ra.ttc_hit = a.ttc_hit;
         ra.obs = a.out.obs;
-        ra.obs_len = a.B + 4 * a.A;
+        ra.obs_len = (int32_t)obs_row(a);
         ra.lidar_max = (float)a.p.lidar_max;
         ra.scans_f32 = a.out.scans;
         ra.scans_f64 = a.out.scans_f64;

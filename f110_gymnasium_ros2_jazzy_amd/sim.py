@@ -92,8 +92,13 @@ class BatchSim:
         self.reset_dtype = np.float64  # f110_set_reset_dtype: the context's default
         E, A, B = self.E, self.A, self.B
         kw = dict(device=dev)
+        # obs rows padded to a 128-B multiple (1088 floats for A = 1, packed
+        # 1088 already for A = 2): the ray kernel's 64-beam obs stores then
+        # cover whole cache lines; out.obs is the [E, B + 4A] view
+        self.obs_stride = (B + 4 * A + 31) // 32 * 32
+        self._obs_buf = torch.empty(E, self.obs_stride, dtype=torch.float32, **kw)
         self.out = StepOut(
-            obs=torch.empty(E, B + 4 * A, dtype=torch.float32, **kw),
+            obs=self._obs_buf[:, :B + 4 * A],
             scans=torch.empty(E, A, B, dtype=torch.float32, **kw),
             collisions=torch.zeros(E, A, dtype=torch.uint8, **kw),
             terminated=torch.zeros(E, dtype=torch.uint8, **kw),
@@ -108,10 +113,11 @@ class BatchSim:
             scans_f64=self.out.scans_f64.data_ptr() if keep_f64_scans else None,
             collisions=self.out.collisions.data_ptr(), terminated=self.out.terminated.data_ptr(),
             was_reset=self.out.was_reset.data_ptr(), lap_times=self.out.lap_times.data_ptr(),
-            lap_counts=self.out.lap_counts.data_ptr(), sim_time=self.out.sim_time.data_ptr())
+            lap_counts=self.out.lap_counts.data_ptr(), sim_time=self.out.sim_time.data_ptr(),
+            obs_stride=self.obs_stride)
         self._outs_min = _lib.F110Outputs(
             obs=self.out.obs.data_ptr(), collisions=self.out.collisions.data_ptr(),
-            terminated=self.out.terminated.data_ptr())
+            terminated=self.out.terminated.data_ptr(), obs_stride=self.obs_stride)
 
     # ------------------------------------------------------------------
     def _stream(self):

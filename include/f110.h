@@ -100,6 +100,9 @@ typedef struct f110_outputs {
     float *lap_times;    /* [n_envs][n_agents] */
     float *lap_counts;   /* [n_envs][n_agents] */
     double *sim_time;    /* [n_envs] F110Env.current_time */
+    int64_t obs_stride;  /* floats from one obs row to the next (>= n_beams + 4*n_agents); 0 = packed.
+                            A 128-B multiple (1088 for A = 1) keeps every 64-beam chunk of a row on
+                            whole cache lines: the ray kernel's obs stores are not split. */
 } f110_outputs;
 
 typedef struct f110_ctx f110_ctx;

@@ -51,7 +51,7 @@ class f110_config(ctypes.Structure):
 
 class f110_outputs(ctypes.Structure):
     _fields_ = [(k, _P) for k in ("obs", "scans", "scans_f64", "collisions", "terminated", "was_reset",
-                                  "lap_times", "lap_counts", "sim_time")]
+                                  "lap_times", "lap_counts", "sim_time")] + [("obs_stride", _i64)]
 
 
 _lib = None
