@@ -231,7 +231,9 @@ def scan_check(O, scanner, runner, act, threads):
     poses = np.concatenate(poses)
     ref = scanner.scan(poses, threads=threads)
     diff = g - ref
-    return {"kernel": "k_rays_tiled (the timed runner, one extra step)", "cars": int(poses.shape[0]),
+    names = {0: "k_rays", 1: "k_rays_tiled (flat)", 2: "k_rays_tiled (chunked)", 3: "k_rays_fx"}
+    kern = names.get(sims[0].ray_kernel, str(sims[0].ray_kernel))
+    return {"kernel": f"{kern} (the timed runner, one extra step)", "cars": int(poses.shape[0]),
             "cars_skipped_ttc": skipped, "rays": int(diff.size),
             "l2": float(np.sqrt(np.sum(diff * diff))), "max_abs": float(np.max(np.abs(diff))),
             "bit_exact_fraction": float(np.mean(diff == 0.0))}

@@ -22,14 +22,18 @@ STEPS, WARM = 200, 20
 BENCH = [sys.executable, os.path.join(REPO, "bench.py"), "--workload", "ddpg", "--steps", str(STEPS),
          "--warmup", str(WARM)]
 
-with open(os.path.join(OUT, "bench.json"), "w") as f:
-    subprocess.run(["timeout", "-k", "10", "300"] + BENCH, cwd=REPO, env=env, stdout=f, check=True)
+SUMMARIZE_ONLY = "--summarize" in sys.argv  # re-summarise a merged kernel_stats.csv (no GPU)
 d = os.path.join(OUT, "trace")
-with open(os.path.join(OUT, "trace.log"), "w") as log:
-    subprocess.run(["timeout", "-k", "10", "400", "rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv",
-                    "-d", d, "-o", "run", "--"] + BENCH, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT,
-                   check=True)
-stats = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)[0]
+if not SUMMARIZE_ONLY:
+    with open(os.path.join(OUT, "bench.json"), "w") as f:
+        subprocess.run(["timeout", "-k", "10", "300"] + BENCH, cwd=REPO, env=env, stdout=f, check=True)
+    with open(os.path.join(OUT, "trace.log"), "w") as log:
+        subprocess.run(["timeout", "-k", "10", "400", "rocprofv3", "--kernel-trace", "--stats", "--output-format",
+                        "csv", "-d", d, "-o", "run", "--"] + BENCH, cwd="/tmp", env=env, stdout=log,
+                       stderr=subprocess.STDOUT, check=True)
+    stats = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)[0]
+else:
+    stats = os.path.join(OUT, "kernel_stats.csv")
 
 
 REPLAY = ("k_add_copy", "k_add_scan", "k_count", "k_finish", "k_gather", "k_hist", "k_keys", "k_place",
@@ -41,7 +45,7 @@ HEADS = ("k_colsum_finish", "k_head_bwd_rows", "k_head_fwd", "k_head_wgrad", "k_
 def stage(name):
     n = name
     if "f110::" in n:
-        k = n.split("f110::", 1)[1].split("(")[0].split("<")[0]
+        k = n.split("(f110::")[0].split("(float")[0].split("(int")[0].split("<")[0].split("::")[-1]
         if k in ("k_agents", "k_rays", "k_rays_fx", "k_rays_fx_tail", "k_rays_tiled", "k_post", "k_post_multi",
                  "k_post_single"):
             return "env_step"
@@ -82,6 +86,7 @@ summary = {
             "are hipBLASLt (Cijk*), heads / ReLU backward / Adam are libf110 kernels",
 }
 import shutil  # noqa: E402
-shutil.copy(stats, os.path.join(OUT, "kernel_stats.csv"))
+if not SUMMARIZE_ONLY:
+    shutil.copy(stats, os.path.join(OUT, "kernel_stats.csv"))
 json.dump(summary, open(os.path.join(OUT, "summary.json"), "w"), indent=1)
 print(json.dumps(summary["kernel_ms_per_step_by_stage"]))
