@@ -496,6 +496,9 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
         // the hand-off absorbs the long waves' tails: heavy-first is off unless asked for
         if (!std::getenv("F110_HEAVY_T")) c->heavy_T = 0;
     }
+    // heavy-first pays where one ray grid is a few rounds of waves deep (8192 cars: 0.175 vs 0.181 ms)
+    // and costs where it is deep (65536 cars: 1.288 vs 1.251 ms without; profiles/r02_ray_ab/ab_heavy.json)
+    if (!std::getenv("F110_HEAVY_T") && EA > 32768) c->heavy_T = 0;
     if (c->ray_kernel >= 2 && c->heavy_T > 0) {
         // up to 1/8 of the waves, in blocks of 4 (measured: ~7% of the waves
         // have a ray longer than 40 lookups and carry ~46% of the wave-iterations)
@@ -619,6 +622,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
         a.heavy_count = c->heavy_count;
         a.heavy_cap = c->heavy_cap;
         a.heavy_T = c->heavy_T;
+        a.heavy_on = c->heavy_off ? 0 : 1;
     }
     if (c->ev) {
         a.ev = c->ev;

@@ -49,6 +49,7 @@ struct StepArgs {
     int32_t ev_P;
     int32_t ev_T, ev_K;
     int32_t heavy_cap, heavy_T, heavy_build, heavy_use, parity, ray_nch;
+    int32_t heavy_on;         // heavy-first enabled for this context (wcost is written for the next step)
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
     uint64_t seed;
     int64_t env_offset;

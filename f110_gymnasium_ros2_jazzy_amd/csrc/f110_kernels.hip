@@ -1330,7 +1330,9 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
             ra.G4 = (EA + ra.wpb - 1) / ra.wpb;
             ra.nch = (a.B + 63) / 64;
             for (int i = 0; i < kMaxChunks; ++i) ra.order[i] = a.chunk_order[i];
-            ra.wcost = a.wcost;
+            // the per-wave cost bytes feed the next step's heavy-first list only:
+            // not written when heavy-first is off (the stream sub-shard runner)
+            ra.wcost = a.heavy_on ? a.wcost : nullptr;
             if (a.heavy_use && !mask) {
                 ra.HB = (a.heavy_cap + ra.wpb - 1) / ra.wpb;
                 ra.heavy_list = a.heavy_list + (size_t)a.parity * a.heavy_cap;

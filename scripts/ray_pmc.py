@@ -1,5 +1,7 @@
-"""Counter-collection target: 100 f110_step launches at 8192 envs (bench
-workload), nothing else on the GPU.  Used with rocprofv3 --pmc."""
+"""Counter-collection target: 100 f110_step launches at MB_ENVS envs (bench
+workload), nothing else on the GPU.  Used with rocprofv3 --pmc.  Heavy-first
+dispatch is off unless MB_HEAVY=1, as in the bench's timed runner
+(streams.StreamShards turns it off)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
@@ -9,6 +11,9 @@ E = int(os.environ.get("MB_ENVS", 8192))
 A = int(os.environ.get("MB_AGENTS", 1))
 sp = centerline_spawns("Spielberg", A)
 sim = BatchSim(load_map("Spielberg_map"), n_envs=E, n_agents=A, autoreset=True, spawn_poses=sp)
+if os.environ.get("MB_HEAVY", "0") != "1":
+    from f110_gymnasium_ros2_jazzy_amd import _lib
+    _lib.check(sim.L.f110_disable_heavy_first(sim.ctx), "f110_disable_heavy_first")
 rng = np.random.default_rng(0)
 sim.reset(sp[rng.integers(0, sp.shape[0], E)])
 g = torch.Generator(device="cuda"); g.manual_seed(0)
