@@ -211,7 +211,7 @@ def scan_check(O, scanner, runner, act, threads):
     import torch
     sims = getattr(runner, "sims", [runner])
     if sims[0].A != 1:
-        return {"skipped": "multi-agent: the agent ray_cast edits scans after the trace"}
+        return scan_check_multi(O, scanner, runner, act, threads)
     for sm in sims:
         sm.set_scan_noise(torch.zeros(sm.E, sm.B, dtype=torch.float64, device=sm.device))
     runner.step(act, minimal_outputs=False)
@@ -237,6 +237,45 @@ def scan_check(O, scanner, runner, act, threads):
             "cars_skipped_ttc": skipped, "rays": int(diff.size),
             "l2": float(np.sqrt(np.sum(diff * diff))), "max_abs": float(np.max(np.abs(diff))),
             "bit_exact_fraction": float(np.mean(diff == 0.0))}
+
+
+def scan_check_multi(O, scanner, runner, act, threads, S=256):
+    """Multi-agent scan check of the timed kernel: the agent ray_cast edits
+    the traced scans, so the oracle steps a sample of S envs in lock-step
+    instead (Simulator.step, base_classes.py:566-625): the oracle takes the
+    device's pre-step state (state, steer buffer and count) and the same
+    actions, noise zeroed on both sides; envs the step autoreset are skipped.
+    Ray_cast beams may differ in the last ulps (ocml vs glibc trig); the
+    count of non-bit-exact beams is reported."""
+    import numpy as np
+    import torch
+    sm = runner.sims[0] if hasattr(runner, "sims") else runner
+    A, B = sm.A, sm.B
+    S = min(S, sm.E)
+    st, sb, sc = sm.get_state()
+    ref = O.OracleSim(scanner, S, A)
+    ref.state[:] = st[:, :S * A].t().cpu().numpy()
+    ref.buf[:] = sb[:, :S * A].t().cpu().numpy()
+    ref.cnt[:] = sc[:S * A].cpu().numpy()
+    sims = getattr(runner, "sims", [runner])
+    for m in sims:
+        m.set_scan_noise(torch.zeros(m.E, m.B, dtype=torch.float64, device=m.device))
+    runner.step(act, minimal_outputs=False)
+    if hasattr(runner, "join"):
+        runner.join()
+    torch.cuda.synchronize()
+    a = act[:S] if act.shape[0] >= S else act
+    rs, _ = ref.step(a.double().cpu().numpy().reshape(S, A, 2), threads=threads)
+    g = sm.out.scans_f64[:S].cpu().numpy()
+    keep = sm.out.was_reset[:S].cpu().numpy() == 0
+    for m in sims:
+        m.set_scan_noise(None)
+    diff = (g - rs)[keep]
+    return {"kernel": "k_rays_fx + k_post_multi (the timed runner, one extra step), oracle in lock-step",
+            "envs": int(keep.sum()), "agents": A, "rays": int(diff.size),
+            "l2": float(np.sqrt(np.sum(diff * diff))), "max_abs": float(np.max(np.abs(diff))) if diff.size else 0.0,
+            "bit_exact_fraction": float(np.mean(diff == 0.0)) if diff.size else 1.0,
+            "non_bit_exact_beams": int(np.sum(diff != 0.0))}
 
 
 def main():

@@ -36,10 +36,13 @@ def parse_variants(spec):
 
 
 def make(tm, sp, E, A, env, **kw):
+    env = dict(env)
     for k in KNOBS:
         os.environ.pop(k, None)
-    os.environ.update(env)
-    return BatchSim(tm, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=7,
+    os.environ.update({k: v for k, v in env.items() if k != "NOISE"})
+    noise = float(env.pop("NOISE", os.environ.get("AB_NOISE", "0.01"))) if "NOISE" in env else \
+        float(os.environ.get("AB_NOISE", "0.01"))
+    return BatchSim(tm, n_envs=E, n_agents=A, noise_std=noise, autoreset=True, spawn_poses=sp, seed=7,
                     keep_f64_scans=True, **kw)
 
 
