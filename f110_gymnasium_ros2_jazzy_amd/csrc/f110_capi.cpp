@@ -348,7 +348,7 @@ static TiledMapView make_tiled_view(const MapView &m, const double *dt_tiled) {
 static bool fx_eligible(int32_t H, int32_t W, double res, const double origin[3], double eps, const uint32_t *edt_k,
                         int32_t wpb) {
     if (origin[2] != 0.0 || wpb != 1) return false;
-    if (H >= (1 << 21) || W >= (1 << 21)) return false;
+    if (H >= (1 << 21) || W >= (1 << 19)) return false;  // fx_offset's 24-bit multiply by wt * 128
     const double ir = 1.0 / res;
     if (!(std::fabs(origin[0] * ir) < 1048576.0) || !(std::fabs(origin[1] * ir) < 1048576.0)) return false;
     uint32_t kmin = 0;
@@ -375,6 +375,8 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
         return fail(F110_E_INVALID, "f110_create: n_envs must be > 0 and 1 <= n_agents <= 8");
     if (C.n_beams < 2 || C.theta_dis < 2 || H <= 0 || W <= 0 || !(resolution > 0))
         return fail(F110_E_INVALID, "f110_create: bad sensor/map dimensions");
+    if ((uint64_t)(H + 3) * (uint64_t)(W + 3) * 8u >= (1ull << 32))
+        return fail(F110_E_INVALID, "f110_create: map too large (the EDT tables are addressed by 32-bit byte offsets)");
     if (!(C.fov > 0) || !(C.fov < 2 * kPi))
         return fail(F110_E_INVALID, "f110_create: fov must be in (0, 2*pi) (one index wrap per scan)");
     if (C.ego_idx < 0 || C.ego_idx >= C.n_agents) return fail(F110_E_INVALID, "f110_create: bad ego_idx");
@@ -915,9 +917,9 @@ extern "C" int f110_host_cell_index(int32_t H, int32_t W, double resolution, con
         lin_out[3 * i] = cell_index(m, x, y);
         lin_out[3 * i + 1] = cell_index_fast(m, x, y);
         const int32_t q = rot ? tiled_cell<true>(t, x, y) : tiled_cell<false>(t, x, y);
-        const int32_t tile = q >> 4, within = q & 15;
-        const int64_t r = (int64_t)(tile / t.wt) * 4 + (within >> 2);
-        const int64_t c = (int64_t)(tile % t.wt) * 4 + (within & 3);
+        const int32_t tile = q >> 4, within = q & 15;  // column-major within the tile (tiled_index)
+        const int64_t r = (int64_t)(tile / t.wt) * 4 + (within & 3);
+        const int64_t c = (int64_t)(tile % t.wt) * 4 + (within >> 2);
         lin_out[3 * i + 2] = r * W + c;
     }
     return F110_OK;

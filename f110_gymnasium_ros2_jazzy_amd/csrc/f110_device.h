@@ -260,8 +260,11 @@ struct TiledMapView {
     double res, inv_res, ox, oy, oc, os, wres, hres;
 };
 
+// Cells are column-major inside a tile: index = tile * 16 + (c & 3) * 4 +
+// (r & 3), so (c >> 2) * 16 + (c & 3) * 4 == c * 4 and the index is
+// (r >> 2) * wt * 16 + c * 4 + (r & 3) -- one multiply-add (k_rays_fx).
 F110_HD int32_t tiled_index(int32_t wt, int32_t r, int32_t c) {
-    return (((r >> 2) * wt + (c >> 2)) << 4) + ((r & 3) << 2) + (c & 3);
+    return (r >> 2) * wt * 16 + c * 4 + (r & 3);
 }
 
 // xy_2_rc + distance_transform (laser_models.py:55-104) on the tiled EDT.
@@ -308,16 +311,12 @@ F110_HD int32_t tiled_cell(const TiledMapView &m, double x, double y) {
 // common iteration carries no exec-mask juggling), and the EDT read as a
 // 32-bit byte offset from the table base (SGPR-base global load).
 __device__ __forceinline__ uint32_t tiled_index_u24(int32_t wt, int32_t r, int32_t c) {
-    return ((__umul24((uint32_t)r >> 2, (uint32_t)wt) + ((uint32_t)c >> 2)) << 4) | (((uint32_t)r & 3u) << 2) |
-           ((uint32_t)c & 3u);
+    return __umul24((uint32_t)r >> 2, (uint32_t)wt << 4) + (((uint32_t)c << 2) | ((uint32_t)r & 3u));
 }
 
-// the same cell as a byte offset into the f64 table (the << 3 folded into
-// the bit assembly)
+// the same cell as a byte offset into the f64 table
 __device__ __forceinline__ uint32_t tiled_offset_u24(int32_t wt, int32_t r, int32_t c) {
-    const uint32_t tile = (__umul24((uint32_t)r >> 2, (uint32_t)wt) + ((uint32_t)c >> 2)) << 7;
-    const uint32_t rc = (((uint32_t)r & 3u) << 2) | ((uint32_t)c & 3u);  // 4-bit cell within the tile
-    return tile | (rc << 3);
+    return (__umul24((uint32_t)r >> 2, (uint32_t)wt) << 7) + (((uint32_t)c << 5) | (((uint32_t)r & 3u) << 3));
 }
 
 // oob8: the byte offset of m.oob (m.oob << 3), passed by the caller so that a

@@ -532,14 +532,12 @@ __device__ __forceinline__ uint32_t exact_offset(const TiledMapView &m, double x
     return r >= m.H ? oob8 : tiled_offset_u24(m.wt, r, c);
 }
 
-// tiled_offset_u24 in 6 integer ops: with R4 = row & ~3 and C4 = col & ~3,
-//   ((row >> 2) * wt + (col >> 2)) * 128 + (row & 3) * 32 + (col & 3) * 8
-//     = R4 * (32 wt - 32) + C4 * 24 + row * 32 + col * 8
-// (24-bit multiplies: row, col < 2^21 and wt < 2^19 on the fixed-point path;
-// off-map lanes compute garbage that the caller's select discards)
+// tiled_offset_u24 with the tile-row stride k1 = wt * 128 in an SGPR:
+// (row >> 2) * k1 + (col << 5 | (row & 3) << 3) -- 5 integer ops (24-bit
+// multiply: row >> 2 < 2^19 and k1 < 2^24 on the fixed-point path; off-map
+// lanes compute garbage that the caller's select discards)
 __device__ __forceinline__ uint32_t fx_offset(uint32_t k1, uint32_t row, uint32_t col) {
-    const uint32_t rc = (row << 5) + (col << 3);
-    return __umul24(row & ~3u, k1) + __umul24(col & ~3u, 24u) + rc;
+    return __umul24(row >> 2, k1) + ((col << 5) | ((row & 3u) << 3));
 }
 
 // Loop-invariant state of the fixed-point sphere trace.
@@ -560,7 +558,7 @@ __device__ __forceinline__ FxLoop fx_loop(const RayArgs &a) {
     L.mr = a.max_range;
     L.W = (uint32_t)a.m.W;
     L.H = (uint32_t)a.m.H;
-    L.k1 = (uint32_t)a.m.wt * 32u - 32u;  // tile-row stride of fx_offset
+    L.k1 = (uint32_t)a.m.wt * 128u;  // tile-row stride of fx_offset (bytes)
     return L;
 }
 
