@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=1000)
     ap.add_argument("--cpu-warmup", type=int, default=100)
     ap.add_argument("--seed", type=int, default=12345)
+    ap.add_argument("--ramp-s", type=float, default=1.0,
+                    help="untimed steps for at least this long before the W warm-up steps (the idle GPU "
+                         "clocks down; DVFS ramp), reported as config.ramp")
     ap.add_argument("--streams", type=int, default=2,
                     help="sub-shards of the GPU's envs on concurrent dedicated-queue streams "
                          "(streams.StreamShards); 1 = one context on the current stream")
@@ -330,9 +333,24 @@ def main():
             return StreamShards(track, n_envs=n_envs, n_streams=s, env_offset=offset, **kw)
         return BatchSim(track, n_envs=n_envs, env_offset=offset, **kw)
 
+    ramp = {"seconds": args.ramp_s, "steps": 0}
+
     def timed(r, p0, a, minimal=True):
-        """W untimed steps, then K steps between barrier + synchronize (max over ranks)."""
+        """W untimed steps, then K steps between barrier + synchronize (max over ranks).
+        Before them, untimed steps for >= ramp_s seconds bring the clocks up
+        (the timed region is unchanged: exactly K full steps)."""
         r.reset(p0)
+        t_end = time.perf_counter() + args.ramp_s
+        n = 0
+        while time.perf_counter() < t_end:
+            r.step(a[n % max(W, 1)], minimal_outputs=minimal)
+            n += 1
+            if n % 16 == 0:
+                torch.cuda.synchronize(dev)
+        ramp["steps"] = max(ramp["steps"], n)
+        if n:
+            torch.cuda.synchronize(dev)
+            r.reset(p0)
         for w in range(W):
             r.step(a[w], minimal_outputs=minimal)
         torch.cuda.synchronize(dev)
@@ -428,6 +446,7 @@ def main():
             "integrator": "RK4", "scan_noise": not args.no_noise, "autoreset": True,
             "parallelism": f"env-shard x{world} (no collectives)",
             "streams_per_gpu": S if not isinstance(runner, BatchSim) else 1,
+            "ramp": ramp,
             "runner": ("StreamShards: S unjoined stream sub-shards, actions resident in HBM" if S > 1 else
                        "one BatchSim context") + "; minimal outputs (obs, collisions, terminated): no f32 "
                        "info['scans'] copy, lap_times/counts, sim_time, was_reset",
