@@ -94,6 +94,15 @@ struct f110_ctx {
     int32_t ev_T = 16, ev_K = 8;
     int64_t wtrace_n = 0;
     bool wtrace_armed = false;
+    // the fixed-point ray kernel's row-major EDT (see StepArgs::rm)
+    double *rm = nullptr;
+    int32_t rm_w = 0;
+    uint32_t rm_oob = 0, rm_zero = 0;
+    int fx_ilp = 1;         // rays per lane (F110_FX_ILP; default by car count)
+    bool fx_tiled = false;  // F110_FX_TABLE=tiled: A/B of the 4x4-tiled EDT
+    uint32_t fx_lds = 0;  // F110_FX_LDS: diagnostic occupancy cap of the ray kernel
+    bool fx_nolean = false;
+  // F110_FX_LEAN=0: A/B of the round-2 ray loop
 
     hipEvent_t *next_prof_events() {
         if (prof_n >= prof_max) return nullptr;
@@ -498,6 +507,18 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
         // the hand-off absorbs the long waves' tails: heavy-first is off unless asked for
         if (!std::getenv("F110_HEAVY_T")) c->heavy_T = 0;
     }
+    if (c->ray_kernel == 3) {
+        // the row-major table's byte offsets (one padding column / row, a zero cell) stay 32-bit
+        const uint64_t rm_bytes = ((uint64_t)W + 16) / 16 * 16 * ((uint64_t)H + 1) * 8 + 128;
+        if (const char *v = std::getenv("F110_FX_TABLE")) c->fx_tiled = std::string(v) == "tiled";
+        if (rm_bytes >= (1ull << 32)) c->fx_tiled = true;
+        // rays per lane: N > 1 keeps N gathers in flight per lane where the grid
+        // is deep enough (measured); the evicting kernel is single-ray
+        c->fx_ilp = EA >= 32768 ? 2 : 1;
+        if (const char *v = std::getenv("F110_FX_ILP")) c->fx_ilp = std::max(1, std::min(4, std::atoi(v)));
+        if (c->evict || c->fx_tiled) c->fx_ilp = 1;
+        if (c->fx_ilp > 1 && !std::getenv("F110_HEAVY_T")) c->heavy_T = 0;  // k_rays_fxn has no heavy-first prefix
+    }
     // heavy-first pays where one ray grid is a few rounds of waves deep (8192 cars: 0.175 vs 0.181 ms)
     // and costs where it is deep (65536 cars: 1.288 vs 1.251 ms without; profiles/r02_ray_ab/ab_heavy.json)
     if (!std::getenv("F110_HEAVY_T") && EA > 32768) c->heavy_T = 0;
@@ -537,6 +558,25 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (e == hipSuccess && c->spawn)
         e = hipMemcpy(c->spawn, spawn_poses, (size_t)n_spawn * C.n_agents * 3 * sizeof(double),
                       hipMemcpyHostToDevice);
+    if (const char *v = std::getenv("F110_FX_LEAN")) c->fx_nolean = std::atoi(v) == 0;
+    if (const char *v = std::getenv("F110_FX_LDS")) c->fx_lds = (uint32_t)std::max(0, std::min(65536, std::atoi(v)));
+    if (c->ray_kernel == 3 && !c->fx_tiled && e == hipSuccess) {
+        // k_rays_fx / k_rays_fxn's row-major EDT: rows of rm_w cells (128-B
+        // aligned), the padding columns and row H hold dt[-1,-1] (a clamped
+        // index then reads the reference's off-map value), and a 0.0 after the
+        // last row is the zero cell of rays that have ended
+        const size_t Wp = ((size_t)W + 1 + 15) / 16 * 16, Hp = (size_t)H + 1;
+        const double oobv = dt[(size_t)H * W - 1];
+        std::vector<double> rm(Wp * Hp + 16, oobv);
+        for (int r = 0; r < H; ++r)
+            for (int q = 0; q < W; ++q) rm[(size_t)r * Wp + q] = dt[(size_t)r * W + q];
+        rm[Wp * Hp] = 0.0;
+        if ((e = c->alloc(&c->rm, rm.size())) == hipSuccess)
+            e = hipMemcpy(c->rm, rm.data(), rm.size() * sizeof(double), hipMemcpyHostToDevice);
+        c->rm_w = (int32_t)Wp;
+        c->rm_oob = (uint32_t)(((size_t)(H - 1) * Wp + (W - 1)) * 8);
+        c->rm_zero = (uint32_t)(Wp * Hp * 8);
+    }
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) return cleanup(F110_E_HIP, std::string("f110_create upload: ") + hipGetErrorString(e));
     size_t lds = step_lds_bytes(C.n_agents, C.n_beams);
@@ -637,6 +677,14 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
         a.ev_K = c->ev_K;
     }
     a.reset_f32 = c->reset_f32 ? 1 : 0;
+    a.rm = c->rm;
+    a.rm_w = c->rm_w;
+    a.rm_oob = c->rm_oob;
+    a.rm_zero = c->rm_zero;
+    a.fx_tiled = c->fx_tiled ? 1 : 0;
+    a.fx_lds = c->fx_lds;
+    a.fx_nolean = c->fx_nolean ? 1 : 0;
+    a.fx_ilp = c->fx_ilp;
     a.gate_wait = c->gate_wait;
     a.gate_record = c->gate_record;
     if (c->wtrace_armed) {  // one traced ray launch

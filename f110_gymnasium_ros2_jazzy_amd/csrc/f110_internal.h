@@ -50,6 +50,16 @@ struct StepArgs {
     int32_t ev_T, ev_K;
     int32_t heavy_cap, heavy_T, heavy_build, heavy_use, parity, ray_nch;
     int32_t heavy_on;         // heavy-first enabled for this context (wcost is written for the next step)
+    // k_rays_fx / k_rays_fxn's row-major EDT: rows of rm_w cells (128-B
+    // aligned), columns W..rm_w-1 and row H hold dt[-1,-1], a 0.0 at byte
+    // rm_zero past the end; rm_oob = byte offset of dt[H-1][W-1]
+    const double *rm;
+    int32_t rm_w;
+    uint32_t rm_oob, rm_zero;
+    int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2..4: k_rays_fxn)
+    int32_t fx_tiled;   // F110_FX_TABLE=tiled (A/B): k_rays_fx on the 4x4-tiled EDT
+    int32_t fx_nolean;  // F110_FX_LEAN=0 (A/B): the ballot-per-iteration loop of round 2
+    uint32_t fx_lds;  // F110_FX_LDS (diagnostic): unused dynamic LDS per k_rays_fx block (occupancy cap)
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
     uint64_t seed;
     int64_t env_offset;
@@ -128,6 +138,9 @@ struct RayArgs {
     // fixed-point cell index of k_rays_fx (see fx_cell in f110_kernels.hip):
     // t = fma(x, inv_res, fx_cx) = 1.5*2^22 + column, on a 2^-30 grid
     double fx_cx, fx_cy;
+    // |q| bound of a scan origin whose rays stay in t's binade: 2^21 - 32 - max_range / res
+    double fx_lim;
+    uint32_t fx_zero;  // byte offset of the row-major table's zero cell (k_rays_fxn)
     // straggler hand-off of k_rays_fx (EVICT) -> k_rays_fx_tail: SoA records
     // ev[7][ev_cap] = x, y, d, tot, cos, sin, noise; ev_gb[2][ev_cap] = car, beam.
     // The queue is split in ev_P partitions of ev_capp records (partition p =

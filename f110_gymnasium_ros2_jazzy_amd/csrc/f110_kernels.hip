@@ -518,7 +518,32 @@ __device__ __forceinline__ T ld_const(const T *p) {  // read-only for the kernel
 __device__ __forceinline__ uint32_t dhi(double v) { return (uint32_t)(__double_as_longlong(v) >> 32); }
 __device__ __forceinline__ uint32_t dlo(double v) { return (uint32_t)__double_as_longlong(v); }
 
+// The fixed-point loop's EDT layouts.  FMT 0: the 4x4-tiled table shared
+// with the other ray kernels: fx_offset<0> is tiled_offset_u24 with the
+// tile-row stride k1 = wt * 128 in an SGPR, (row >> 2) * k1 + (col << 5 |
+// (row & 3) << 3) -- 5 integer ops (24-bit multiply: row >> 2 < 2^19 and
+// k1 < 2^24 on the fixed-point path; off-map lanes compute garbage that the
+// caller's select discards).  FMT 3: the row-major table of k_rays_fx /
+// k_rays_fxn (StepArgs::rm), rows of k1 = wt * 8 bytes: row * k1 + col * 8,
+// and off-map indices are clamped into the padding, which holds dt[-1,-1],
+// instead of selected.  Measured at 65536 envs: FMT 3 1.184 vs
+// FMT 0 1.210 ms; an inexact f32 8x4-tiled or u16 8x8-tiled table (4x the
+// cells per cache line) gained only 2-3 %: the gathers' line footprint is not
+// what bounds the loop.
+template <int FMT>
+__device__ __forceinline__ uint32_t fx_offset(uint32_t k1, uint32_t row, uint32_t col) {
+    static_assert(FMT == 0 || FMT == 3, "EDT layout");
+    if (FMT == 0) return __umul24(row >> 2, k1) + ((col << 5) | ((row & 3u) << 3));
+    return __umul24(row, k1) + (col << 3);
+}
+
+template <int FMT>
+__device__ __forceinline__ double fx_load(const void *base, uint32_t off) {
+    return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(base) + off);
+}
+
 // tiled_cell's IEEE path as a byte offset (the fixed-point path's fallback)
+template <int FMT>
 __device__ __forceinline__ uint32_t exact_offset(const TiledMapView &m, double x, double y, uint32_t oob8) {
     const double xr = x - m.ox, yr = y - m.oy;
     const bool inb = (xr >= 0) & (xr < m.wres) & (yr >= 0) & (yr < m.hres);  // false for NaN
@@ -529,15 +554,7 @@ __device__ __forceinline__ uint32_t exact_offset(const TiledMapView &m, double x
         c = 0;
         ++r;
     }
-    return r >= m.H ? oob8 : tiled_offset_u24(m.wt, r, c);
-}
-
-// tiled_offset_u24 with the tile-row stride k1 = wt * 128 in an SGPR:
-// (row >> 2) * k1 + (col << 5 | (row & 3) << 3) -- 5 integer ops (24-bit
-// multiply: row >> 2 < 2^19 and k1 < 2^24 on the fixed-point path; off-map
-// lanes compute garbage that the caller's select discards)
-__device__ __forceinline__ uint32_t fx_offset(uint32_t k1, uint32_t row, uint32_t col) {
-    return __umul24(row >> 2, k1) + ((col << 5) | ((row & 3u) << 3));
+    return r >= m.H ? oob8 : fx_offset<FMT>((uint32_t)m.wt * (FMT == 3 ? 8u : 128u), (uint32_t)r, (uint32_t)c);
 }
 
 // Loop-invariant state of the fixed-point sphere trace.
@@ -546,12 +563,14 @@ struct FxLoop {
     uint32_t oobv, W, H, k1;
 };
 
+template <int FMT = 0>
 __device__ __forceinline__ FxLoop fx_loop(const RayArgs &a) {
     FxLoop L;
     // the off-map offset and inv_res in VGPRs for the whole trace (opaque
     // copies: the select cannot read an SGPR beside its VCC condition, and the
-    // fma's other operand is an SGPR constant, a VOP3 reads one SGPR)
-    asm volatile("v_mov_b32 %0, %1" : "=v"(L.oobv) : "s"((uint32_t)a.m.oob << 3));
+    // fma's other operand is an SGPR constant, a VOP3 reads one SGPR); the
+    // row-major layout carries the off-map byte offset itself in m.oob
+    asm volatile("v_mov_b32 %0, %1" : "=v"(L.oobv) : "s"(FMT == 0 ? (uint32_t)a.m.oob << 3 : (uint32_t)a.m.oob));
     asm volatile("v_mov_b64 %0, %1" : "=v"(L.ir) : "s"(a.m.inv_res));
     L.cxk = a.fx_cx;
     L.cyk = a.fx_cy;
@@ -559,11 +578,16 @@ __device__ __forceinline__ FxLoop fx_loop(const RayArgs &a) {
     L.W = (uint32_t)a.m.W;
     L.H = (uint32_t)a.m.H;
     L.k1 = (uint32_t)a.m.wt * 128u;  // tile-row stride of fx_offset (bytes)
+    if (FMT == 3) {  // row-major rows of m.wt cells; columns W .. wt-1 and row H hold dt[-1,-1]
+        L.W = (uint32_t)a.m.wt - 1u;
+        L.k1 = (uint32_t)a.m.wt * 8u;
+    }
     return L;
 }
 
 // One iteration of trace_ray's loop (laser_models.py:135-141) for an active
 // lane: step, fixed-point cell, EDT lookup.
+template <int FMT = 0>
 __device__ __forceinline__ void fx_step(const TiledMapView &m, const FxLoop &L, double &x, double &y, double &d,
                                         double &tot, double c, double s) {
     x += d * c;  // :135
@@ -578,14 +602,52 @@ __device__ __forceinline__ void fx_step(const TiledMapView &m, const FxLoop &L, 
     const uint32_t row = __builtin_amdgcn_alignbit(hy, ly, 30) - kFxU0;
     const bool inb = (col < L.W) & (row < L.H) & ((int32_t)hx >= 0x40000000) & ((int32_t)hy >= 0x40000000);
     const bool near = ((lx << 2) + 4u * kFxBand < 8u * kFxBand) | ((ly << 2) + 4u * kFxBand < 8u * kFxBand);
-    const uint32_t fast = fx_offset(L.k1, row, col);
+    const uint32_t fast = fx_offset<FMT>(L.k1, row, col);
     const uint32_t sel = 0u - (uint32_t)inb;
     uint32_t off = (fast & sel) | (L.oobv & ~sel);
     if (__builtin_amdgcn_ballot_w64(near)) {  // wave-uniform, rare
-        if (near) off = exact_offset(m, x, y, L.oobv);
+        if (near) off = exact_offset<FMT>(m, x, y, L.oobv);
     }
-    d = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(m.dt) + off);
+    d = fx_load<FMT>(m.dt, off);
     tot += d;  // :141
+}
+
+// fx_step for a car whose rays cannot leave t's binade (SAFE: the scan
+// origin lies within 2^21 - 16 cells of the map origin, less the max range;
+// every lookup of a ray is within max_range of its origin, since the loop
+// steps only while tot <= max_range): the sign / exponent tests drop out and
+// the column and row tests are one unsigned compare each.
+template <int FMT>
+__device__ __forceinline__ void fx_step_safe(const TiledMapView &m, const FxLoop &L, double &x, double &y, double &d,
+                                             double &tot, double c, double s) {
+    x += d * c;  // :135
+    y += d * s;  // :136
+    double tx, ty;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tx) : "v"(x), "v"(L.ir), "s"(L.cxk));
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(ty) : "v"(y), "v"(L.ir), "s"(L.cyk));
+    const uint32_t lx = dlo(tx), ly = dlo(ty);
+    const uint32_t col = __builtin_amdgcn_alignbit(dhi(tx), lx, 30) - kFxU0;
+    const uint32_t row = __builtin_amdgcn_alignbit(dhi(ty), ly, 30) - kFxU0;
+    const bool near = ((lx << 2) + 4u * kFxBand < 8u * kFxBand) | ((ly << 2) + 4u * kFxBand < 8u * kFxBand);
+    uint32_t off;
+    if (FMT == 3) {  // clamped into the padding, which holds dt[-1,-1]: no bounds select
+        off = fx_offset<3>(L.k1, min(row, L.H), min(col, L.W));
+    } else {
+        const bool inb = (col < L.W) & (row < L.H);
+        const uint32_t sel = 0u - (uint32_t)inb;  // a select, not an exec-mask branch
+        off = (fx_offset<FMT>(L.k1, row, col) & sel) | (L.oobv & ~sel);
+    }
+    if (__builtin_amdgcn_ballot_w64(near)) {  // wave-uniform, rare
+        if (near) off = exact_offset<FMT>(m, x, y, L.oobv);
+    }
+    d = fx_load<FMT>(m.dt, off);
+    tot += d;  // :141
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
 }
 
 // The ray's outputs: clamp (:143-144), noise after the clamp
@@ -616,7 +678,14 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {  // set bits of
 // state (x, y, d, tot, cos, sin, noise, car, beam: the whole loop state) to
 // the hand-off queue and ends; k_rays_fx_tail finishes them with lane refill.
 // The state is exact, so the results are those of the uninterrupted loop.
-template <bool MASK, bool HANDOFF, bool EVICT>
+//
+// LEAN (every launch but the EVICT and A/B ones): lanes whose ray has ended
+// leave the loop (exec mask) instead of a ballot + select per iteration,
+// each lane counts its own lookups (summed once per wave), and cars whose
+// rays stay in t's binade take fx_step_safe: ~36 instead of ~59 instructions
+// per iteration on the wave's serial path (the kernel is latency-bound: at
+// 6 / 4 / 2 waves per SIMD it takes 1.31x / 1.62x / 2.9x as long).
+template <bool MASK, bool HANDOFF, bool EVICT, int FMT = 0, bool LEAN = !EVICT>
 __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
     int g, k;
     if ((int)blockIdx.x < a.HB) {  // heavy-first blocks: the listed waves
@@ -686,11 +755,29 @@ __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
     }
 
     // ---- trace_ray's loop (laser_models.py:133-141) ----
-    const FxLoop L = fx_loop(a);
+    const FxLoop L = fx_loop<FMT>(a);
     double tot = d;  // :130 (lanes without a ray: d = 0, never traced)
     uint32_t iters = 0, lane_iters = 0;
     bool evicted = false, can_evict = EVICT;
-    for (;;) {
+    if (LEAN) {
+        uint32_t cnt = 0;
+        const double qx = fma(x00, L.ir, L.cxk) - kFxMagic, qy = fma(y00, L.ir, L.cyk) - kFxMagic;
+        __builtin_amdgcn_s_waitcnt(0);  // the set-up loads (c, s) land before the loop, not in it
+        if (fabs(qx) < a.fx_lim && fabs(qy) < a.fx_lim) {  // wave-uniform (false for NaN)
+            while ((dhi(d) != 0u) & (tot <= L.mr)) {
+                fx_step_safe<FMT>(a.m, L, x, y, d, tot, c, s);
+                ++cnt;
+            }
+        } else {
+            while ((dhi(d) != 0u) & (tot <= L.mr)) {
+                fx_step<FMT>(a.m, L, x, y, d, tot, c, s);
+                ++cnt;
+            }
+        }
+        lane_iters = wave_sum(cnt);
+        if (a.wcost) iters = wave_max(cnt);
+    }
+    for (; !LEAN;) {
         const bool act = (dhi(d) != 0u) & (tot <= L.mr);
         const uint64_t mk = __builtin_amdgcn_ballot_w64(dhi(d) != 0u) & __builtin_amdgcn_ballot_w64(tot <= L.mr);
         if (!mk) break;
@@ -721,7 +808,7 @@ __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
         }
         ++iters;
         lane_iters += (uint32_t)__popcll(mk);
-        if (act) fx_step(a.m, L, x, y, d, tot, c, s);
+        if (act) fx_step<FMT>(a.m, L, x, y, d, tot, c, s);
     }
 
     // ---- epilogue ----
@@ -738,6 +825,176 @@ __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
             const uint32_t mx = lanes ? 1u + iters : 0u;
             K.wcost[(size_t)g * a.nch + k] = (uint8_t)(mx < 255u ? mx : 255u);
         }
+    }
+}
+
+// One fixed-point step of ray r of an ILP lane (k_rays_fxn, row-major table):
+// the cell's byte offset for an active ray, the zero cell's (a 0.0 past the
+// table's end, which no clamped index reaches) for a ray that has ended, so
+// that its load returns d = 0 and leaves its total, x and y as they are.
+__device__ __forceinline__ uint32_t fxn_offset(const TiledMapView &m, const FxLoop &L, double &x, double &y,
+                                               double d, double c, double s, bool act, uint64_t amask,
+                                               uint32_t zero) {
+    x += d * c;  // :135
+    y += d * s;  // :136
+    double tx, ty;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tx) : "v"(x), "v"(L.ir), "s"(L.cxk));
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(ty) : "v"(y), "v"(L.ir), "s"(L.cyk));
+    const uint32_t lx = dlo(tx), ly = dlo(ty);
+    const uint32_t col = __builtin_amdgcn_alignbit(dhi(tx), lx, 30) - kFxU0;
+    const uint32_t row = __builtin_amdgcn_alignbit(dhi(ty), ly, 30) - kFxU0;
+    // ballots of bare compares are their lane masks; a ballot of a combined
+    // bool would first be materialised in a VGPR (2 more VALU per ballot)
+    const uint32_t band = min((lx << 2) + 4u * kFxBand, (ly << 2) + 4u * kFxBand);
+    uint32_t fast = fx_offset<3>(L.k1, min(row, L.H), min(col, L.W));
+    asm volatile("" : "+v"(fast));  // computed for every lane, then selected (no exec-mask branch)
+    uint32_t off = act ? fast : zero;
+    if (__builtin_amdgcn_ballot_w64(band < 8u * kFxBand) & amask) {  // wave-uniform, rare
+        if (act & (band < 8u * kFxBand)) off = exact_offset<3>(m, x, y, L.oobv);
+    }
+    return off;
+}
+
+// k_rays_fxn: N rays per lane (beams b0 + 64 r + lane, r < N, of one car: N
+// adjacent 64-beam chunks), traced in one loop so that each lane keeps N
+// independent EDT gathers in flight.  The single-ray kernel is bound by the
+// latency of its dependent gather chain, not by issue (at 6 / 4
+// / 2 waves per SIMD it takes 1.31x / 1.62x / 2.9x as long).  A ray that has
+// ended reads the zero cell (d = 0); a chunk whose rays have all ended skips
+// its step (wave-uniform); the active-ray masks are ballots, so the lookup
+// count is a scalar popcount.  Cars whose rays could leave t's binade trace
+// their N rays one after the other with fx_step.  Row-major EDT with
+// dt[-1,-1] in the padding column / row (FMT 3).  Bit-identical to k_rays_fx.
+template <int N, bool MASK, bool HANDOFF>
+__global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
+    const int blk = (int)blockIdx.x;
+    const int slot = blk / a.G4;
+    const int g = blk - slot * a.G4;
+    if (g >= a.EA) return;
+    const int ng = (a.nch + N - 1) / N;
+    const int grp = ng - 1 - slot;  // descending, as the chunk order of k_rays_fx
+    const int lane = (int)threadIdx.x;
+    const int B = a.B;
+    const int b0 = grp * 64 * N;
+    const int e = HANDOFF ? g / a.A : g;
+    const bool live = !MASK || ld_const(a.reset_mask + e);
+
+    // ---- per-car set-up (wave-uniform: scalar loads), as in k_rays_fx ----
+    const BeamRun *R = a.runs + (size_t)g * kMaxSeg;
+    const int n = ld_const(a.nruns + g);
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (ld_const(&R[mid].start) <= b0) lo = mid;
+        else hi = mid - 1;
+    }
+    int rs[N];
+    double t0[N], dl[N];
+    {
+        const int s0 = ld_const(&R[lo].start);
+        const double u0 = ld_const(&R[lo].t0), w0 = ld_const(&R[lo].delta);
+#pragma unroll
+        for (int r = 0; r < N; ++r) {
+            rs[r] = s0;
+            t0[r] = u0;
+            dl[r] = w0;
+        }
+    }
+    for (int j = lo + 1; j < n; ++j) {
+        const int s2 = ld_const(&R[j].start);
+        if (s2 > b0 + 64 * N - 1) break;
+        const double tj = ld_const(&R[j].t0), dj = ld_const(&R[j].delta);
+#pragma unroll
+        for (int r = 0; r < N; ++r)
+            if (b0 + 64 * r + lane >= s2) {
+                rs[r] = s2;
+                t0[r] = tj;
+                dl[r] = dj;
+            }
+    }
+    const double x00 = ld_const(a.ray0 + g), y00 = ld_const(a.ray0 + a.EA + g);
+    const double d00 = ld_const(a.ray0 + 2 * a.EA + g);  // :129
+    double x[N], y[N], d[N], tot[N], c[N], sn[N];
+    int bc[N];
+    bool has[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+        const int b = b0 + 64 * r + lane;
+        has[r] = live && b < B;
+        bc[r] = b < B ? b : B - 1;
+        int ti = (int)(t0[r] + (double)(bc[r] - rs[r]) * dl[r]);  // int(theta_index), :124
+        if (ti >= a.theta_dis) ti = 0;
+        c[r] = a.cosines[ti];
+        sn[r] = a.sines[ti];
+        x[r] = x00;
+        y[r] = y00;
+        d[r] = has[r] ? d00 : 0.0;
+        tot[r] = d[r];  // :130
+    }
+
+    // ---- trace_ray's loop (laser_models.py:133-141), N rays per lane ----
+    const FxLoop L = fx_loop<3>(a);
+    const uint32_t zero = a.fx_zero;
+    uint32_t lane_iters = 0;
+    const double qx = fma(x00, L.ir, L.cxk) - kFxMagic, qy = fma(y00, L.ir, L.cyk) - kFxMagic;
+    __builtin_amdgcn_s_waitcnt(0);  // the set-up loads land before the loop, not in it
+    if (fabs(qx) < a.fx_lim && fabs(qy) < a.fx_lim) {  // wave-uniform (false for NaN)
+        // no per-ray flag is carried across iterations (an i1 array would be
+        // packed into a VGPR): activity is recomputed from d and the total
+        for (;;) {
+            uint64_t m[N], any = 0;
+#pragma unroll
+            for (int r = 0; r < N; ++r) {
+                m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+                any |= m[r];
+                lane_iters += (uint32_t)__popcll(m[r]);
+            }
+            if (!any) break;
+            uint32_t off[N];
+#pragma unroll
+            for (int r = 0; r < N; ++r) {
+                off[r] = zero;
+                if (m[r]) {
+                    const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+                    off[r] = fxn_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < N; ++r) d[r] = fx_load<3>(a.m.dt, off[r]);
+#pragma unroll
+            for (int r = 0; r < N; ++r) tot[r] += d[r];  // :141
+        }
+    } else {
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int r = 0; r < N; ++r)
+            while ((dhi(d[r]) != 0u) & (tot[r] <= L.mr)) {
+                fx_step<3>(a.m, L, x[r], y[r], d[r], tot[r], c[r], sn[r]);
+                ++cnt;
+            }
+        lane_iters = wave_sum(cnt);
+    }
+
+    // ---- epilogue ----
+    const RayArgs &K = *kernarg_rays();
+    const double v = ld_const(a.vel + g);
+    uint32_t lanes = 0;
+    const bool noise_on = K.noise_ext || K.noise_std > 0.0;
+    const uint32_t key = noise_key(K.seed, (uint64_t)(K.env_offset + e));
+    const uint64_t step = noise_on && !K.noise_ext ? ld_const(K.noise_step + e) : 0;
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+        double nz = 0.0;
+        if (K.noise_ext) nz = K.noise_ext[(size_t)e * B + bc[r]];
+        else if (K.noise_std > 0.0) nz = K.noise_std * (double)beam_normal_k(key, step, bc[r]);
+        if (has[r])
+            fx_epilogue<HANDOFF>(K, g, e, b0 + 64 * r + lane, tot[r], L.mr, nz, v, a.beam_cos[bc[r]], a.side[bc[r]]);
+        lanes += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(has[r]));
+    }
+    if (lane == 0 && lanes) {  // one (lookups, rays) atomic pair per wave; the first lookup came from k_agents
+        unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+        atomicAdd(cs, (unsigned long long)(lanes + lane_iters));
+        atomicAdd(cs + 1, (unsigned long long)lanes);
     }
 }
 
@@ -1365,6 +1622,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         if (fx) {
             ra.fx_cx = std::fma(-a.tmap.ox, a.tmap.inv_res, kFxMagic);
             ra.fx_cy = std::fma(-a.tmap.oy, a.tmap.inv_res, kFxMagic);
+            ra.fx_lim = 2097152.0 - 32.0 - a.max_range * a.tmap.inv_res;
             ra.ev = a.ev;
             ra.ev_gb = a.ev_gb;
             ra.ev_ctr = a.ev_ctr;
@@ -1382,13 +1640,51 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                                     reinterpret_cast<const void *>(&k_rays_fx<true, false, true>),
                                     reinterpret_cast<const void *>(&k_rays_fx<true, true, true>)};
             f = fx_fn[(a.ev ? 4 : 0) + (mask ? 2 : 0) + (single ? 0 : 1)];
+            if (!a.ev && a.rm && !a.fx_tiled) {
+                // the row-major EDT (dt[-1,-1] in the padding column / row, a
+                // zero cell past the end): N rays per lane (k_rays_fxn) or the
+                // single-ray loop (k_rays_fx<.., 3>, heavy-first capable)
+                ra.m.dt = a.rm;
+                ra.m.wt = a.rm_w;
+                ra.m.oob = (int32_t)a.rm_oob;
+                ra.fx_zero = a.rm_zero;
+                const int N = a.fx_ilp;
+                const int v2 = (mask ? 2 : 0) + (single ? 0 : 1);
+                if (N >= 2 && N <= 4) {
+                    const void *fn_n[3][4] = {
+                        {reinterpret_cast<const void *>(&k_rays_fxn<2, false, false>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<2, false, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<2, true, false>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<2, true, true>)},
+                        {reinterpret_cast<const void *>(&k_rays_fxn<3, false, false>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<3, false, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<3, true, false>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<3, true, true>)},
+                        {reinterpret_cast<const void *>(&k_rays_fxn<4, false, false>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<4, false, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<4, true, false>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<4, true, true>)}};
+                    ra.HB = 0;
+                    ra.wcost = nullptr;
+                    g2 = dim3((unsigned)(ra.G4 * ((ra.nch + N - 1) / N)));
+                    f = fn_n[N - 2][v2];
+                } else {
+                    const void *fn_1[4] = {reinterpret_cast<const void *>(&k_rays_fx<false, false, false, 3>),
+                                           reinterpret_cast<const void *>(&k_rays_fx<false, true, false, 3>),
+                                           reinterpret_cast<const void *>(&k_rays_fx<true, false, false, 3>),
+                                           reinterpret_cast<const void *>(&k_rays_fx<true, true, false, 3>)};
+                    f = fn_1[v2];
+                }
+            }
+            if (a.fx_nolean && single && !mask && !a.ev)  // A/B: the round-2 loop (tiled EDT)
+                f = reinterpret_cast<const void *>(&k_rays_fx<false, false, false, 0, false>);
         }
         if (a.wtrace && ch && !rot && !mask && !fx)  // diagnostic wave trace (f110_debug_wave_trace)
             f = single ? reinterpret_cast<const void *>(&k_rays_tiled<false, false, false, true, true>)
                        : reinterpret_cast<const void *>(&k_rays_tiled<false, false, true, true, true>);
         ra.wtrace = a.wtrace;
         const unsigned bdim = ch ? 64u * (unsigned)ra.wpb : (unsigned)kBlock;
-        if ((e = hipLaunchKernel(f, g2, dim3(bdim), args, 0, s)) != hipSuccess) return e;
+        if ((e = hipLaunchKernel(f, g2, dim3(bdim), args, fx ? a.fx_lds : 0u, s)) != hipSuccess) return e;
         if (fx && a.ev) {  // the handed-off stragglers (the queue is read on the device)
             const unsigned tg = (unsigned)std::max<int64_t>(
                 a.ev_P, std::min<int64_t>(kTailWaves, ((int64_t)a.ev_cap + 63) / 64) / a.ev_P * a.ev_P);

@@ -296,17 +296,22 @@ def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A, nonexact
     nonexact_budget(f"ray_cast_adversarial_A{A}", nonexact)
 
 
-@pytest.mark.parametrize("kernel", ["2", "3"])
-def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanners, monkeypatch, kernel):
-    """k_rays_fx's fixed-point cell index (F110_RAY_KERNEL=3, the default)
-    against the oracle's IEEE xy_2_rc (laser_models.py:55-104) where it is
-    hardest: scan origins exactly on cell edges and corners with the beam
-    whose table direction is exactly (1, 0) (every lookup of that ray then
-    sits on a row edge: the guard-band path), origins just inside / outside
-    the map edges looking out, and origins far off the map (dt[-1, -1]
-    steps).  Scans must be bit-exact; kernels 2 and 3 must agree."""
+@pytest.mark.parametrize("kernel,ilp,table", [("2", "1", "rm"), ("3", "1", "rm"), ("3", "2", "rm"), ("3", "1", "tiled")])
+def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanners, monkeypatch, kernel, ilp, table):
+    """k_rays_fx's fixed-point cell index (F110_RAY_KERNEL=3, the default;
+    on the row-major EDT with 1 or 2 rays per lane, k_rays_fxn for 2, and on
+    the 4x4-tiled EDT) against the oracle's IEEE xy_2_rc
+    (laser_models.py:55-104) where it is hardest: scan origins exactly on
+    cell edges and corners with the beam whose table direction is exactly
+    (1, 0) (every lookup of that ray then sits on a row edge: the guard-band
+    path), origins just inside / outside the map edges looking out (clamped
+    into the row-major padding), and origins far off the map (dt[-1, -1]
+    steps; the cars whose rays could leave t's binade take fx_step).  Scans
+    must be bit-exact; every kernel must agree."""
     from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
     monkeypatch.setenv("F110_RAY_KERNEL", kernel)
+    monkeypatch.setenv("F110_FX_ILP", ilp)
+    monkeypatch.setenv("F110_FX_TABLE", table)
     tm = tracks("Spielberg_map")
     ox, oy, _ = tm.origin
     res = tm.resolution
@@ -341,6 +346,9 @@ def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanne
             poses.append((ox + t * W * res, oy + H * res + eps, np.pi / 2))
     for i in range(16):  # far off the map
         poses.append((ox - 5.0 - 100.0 * i, oy + rng.uniform(-50, 150), rng.uniform(-np.pi, np.pi)))
+    for i in range(8):  # beyond 2^21 cells: t leaves its binade (the per-car check sends these to fx_step)
+        far = (2.0e5, -2.0e5, 1.0e7, -3.0e8)[i % 4]
+        poses.append((ox + far if i < 4 else ox + 10.0, oy + (far if i >= 4 else 10.0), rng.uniform(-np.pi, np.pi)))
     poses = np.asarray(poses, np.float64)
     E = poses.shape[0]
     sim = BatchSim(tm, n_envs=E, n_agents=1, device=gpu, noise_std=0.0, keep_f64_scans=True)
