@@ -236,6 +236,8 @@ def scan_check(O, scanner, runner, act, threads):
     diff = g - ref
     names = {0: "k_rays", 1: "k_rays_tiled (flat)", 2: "k_rays_tiled (chunked)", 3: "k_rays_fx"}
     kern = names.get(sims[0].ray_kernel, str(sims[0].ray_kernel))
+    if sims[0].ray_kernel == 3 and sims[0].ray_lanes > 1:
+        kern = f"k_rays_fxn ({sims[0].ray_lanes} rays per lane)"
     return {"kernel": f"{kern} (the timed runner, one extra step)", "cars": int(poses.shape[0]),
             "cars_skipped_ttc": skipped, "rays": int(diff.size),
             "l2": float(np.sqrt(np.sum(diff * diff))), "max_abs": float(np.max(np.abs(diff))),
@@ -406,7 +408,11 @@ def main():
     busy = load_profile("pmc_busy", E, A)
     traffic = pmc.get("bytes_per_launch") if pmc else None
     roof = {
-        "kernel": "k_rays", "bound": "gather-latency/VALU-issue (HBM is not the limit: see hbm_traffic_frac)",
+        "kernel": "k_rays", "bound": ("latency of the dependent EDT gather chain (HBM is not the limit: see "
+                                      "hbm_traffic_frac; capping occupancy at 6/4/2 waves per SIMD costs "
+                                      "1.31x/1.62x/2.9x, DESIGN.md 3.2)"),
+        "ray_kernel": ("k_rays_fxn, %d rays per lane" % sim.ray_lanes) if sim.ray_kernel == 3 and sim.ray_lanes > 1
+        else "k_rays_fx" if sim.ray_kernel == 3 else "ray kernel %d" % sim.ray_kernel,
         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
         "traffic": traffic, "kernel_ms": k_ms, "algorithmic_bytes_per_launch": rays_bytes_launch,
         "mean_lookups_per_ray": mean_look,

@@ -514,10 +514,11 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
         if (rm_bytes >= (1ull << 32)) c->fx_tiled = true;
         // rays per lane: N > 1 keeps N gathers in flight per lane where the grid
         // is deep enough (measured); the evicting kernel is single-ray
-        c->fx_ilp = EA >= 32768 ? 2 : 1;
+        // (k_rays ms, 1 vs 2 rays per lane: 4096 cars 0.107 / 0.124, 8192 0.165 / 0.175,
+        // 16384 0.304 / 0.284, 32768 0.637 / 0.547, 65536 1.190 / 1.054; profiles/r02_ray_ab/)
+        c->fx_ilp = EA >= 12288 ? 2 : 1;
         if (const char *v = std::getenv("F110_FX_ILP")) c->fx_ilp = std::max(1, std::min(4, std::atoi(v)));
         if (c->evict || c->fx_tiled) c->fx_ilp = 1;
-        if (c->fx_ilp > 1 && !std::getenv("F110_HEAVY_T")) c->heavy_T = 0;  // k_rays_fxn has no heavy-first prefix
     }
     // heavy-first pays where one ray grid is a few rounds of waves deep (8192 cars: 0.175 vs 0.181 ms)
     // and costs where it is deep (65536 cars: 1.288 vs 1.251 ms without; profiles/r02_ray_ab/ab_heavy.json)
@@ -655,7 +656,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.n_spawn = c->n_spawn;
     if (out) a.out = *out;
     a.ctr = c->ctr;
-    a.ray_nch = c->nch;
+    a.ray_nch = c->fx_ilp > 1 ? (c->nch + c->fx_ilp - 1) / c->fx_ilp : c->nch;  // k_rays_fxn: chunk groups
     a.parity = (int32_t)(c->launch_n++ & 1);
     if (c->wcost) {
         a.wcost = c->wcost;
@@ -741,6 +742,11 @@ extern "C" void f110_host_np_sincosf(const float *x, int64_t n, int32_t cos_op, 
 extern "C" int f110_ray_kernel(const f110_ctx *ctx) {
     if (!ctx) return fail(F110_E_INVALID, "f110_ray_kernel: null context");
     return ctx->ray_kernel;
+}
+
+extern "C" int f110_ray_lanes(const f110_ctx *ctx) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_ray_lanes: null context");
+    return ctx->ray_kernel == 3 ? ctx->fx_ilp : 1;
 }
 
 extern "C" int f110_disable_heavy_first(f110_ctx *ctx) {

@@ -865,14 +865,28 @@ __device__ __forceinline__ uint32_t fxn_offset(const TiledMapView &m, const FxLo
 // count is a scalar popcount.  Cars whose rays could leave t's binade trace
 // their N rays one after the other with fx_step.  Row-major EDT with
 // dt[-1,-1] in the padding column / row (FMT 3).  Bit-identical to k_rays_fx.
+//
+// Heavy-first (as k_rays_fx, with a chunk group in place of a chunk: a.nch is
+// the number of groups per car here): HB leading blocks run the groups whose
+// longest ray took >= heavy_T lookups in the previous launch.
 template <int N, bool MASK, bool HANDOFF>
 __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
-    const int blk = (int)blockIdx.x;
-    const int slot = blk / a.G4;
-    const int g = blk - slot * a.G4;
-    if (g >= a.EA) return;
-    const int ng = (a.nch + N - 1) / N;
-    const int grp = ng - 1 - slot;  // descending, as the chunk order of k_rays_fx
+    const int ng = a.nch;  // chunk groups of N chunks per car
+    int g, grp;
+    if ((int)blockIdx.x < a.HB) {  // heavy-first blocks: the listed groups
+        const uint32_t item = blockIdx.x;
+        if (item >= ld_const(a.heavy_count)) return;
+        const uint32_t hv = ld_const(a.heavy_list + item);
+        g = (int)(hv >> 8);
+        grp = (int)(hv & 255u);
+    } else {
+        const int blk = (int)blockIdx.x - a.HB;
+        const int slot = blk / a.G4;
+        g = blk - slot * a.G4;
+        if (g >= a.EA) return;
+        grp = ng - 1 - slot;  // descending, as the chunk order of k_rays_fx
+        if (a.HB && ((ld_const(a.heavy_mask + g) >> grp) & 1u)) return;  // ran in a heavy block
+    }
     const int lane = (int)threadIdx.x;
     const int B = a.B;
     const int b0 = grp * 64 * N;
@@ -935,7 +949,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
     // ---- trace_ray's loop (laser_models.py:133-141), N rays per lane ----
     const FxLoop L = fx_loop<3>(a);
     const uint32_t zero = a.fx_zero;
-    uint32_t lane_iters = 0;
+    uint32_t lane_iters = 0, iters = 0;
     const double qx = fma(x00, L.ir, L.cxk) - kFxMagic, qy = fma(y00, L.ir, L.cyk) - kFxMagic;
     __builtin_amdgcn_s_waitcnt(0);  // the set-up loads land before the loop, not in it
     if (fabs(qx) < a.fx_lim && fabs(qy) < a.fx_lim) {  // wave-uniform (false for NaN)
@@ -950,6 +964,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
                 lane_iters += (uint32_t)__popcll(m[r]);
             }
             if (!any) break;
+            ++iters;
             uint32_t off[N];
 #pragma unroll
             for (int r = 0; r < N; ++r) {
@@ -973,6 +988,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
                 ++cnt;
             }
         lane_iters = wave_sum(cnt);
+        iters = wave_max(cnt);
     }
 
     // ---- epilogue ----
@@ -991,10 +1007,16 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
             fx_epilogue<HANDOFF>(K, g, e, b0 + 64 * r + lane, tot[r], L.mr, nz, v, a.beam_cos[bc[r]], a.side[bc[r]]);
         lanes += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(has[r]));
     }
-    if (lane == 0 && lanes) {  // one (lookups, rays) atomic pair per wave; the first lookup came from k_agents
-        unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
-        atomicAdd(cs, (unsigned long long)(lanes + lane_iters));
-        atomicAdd(cs + 1, (unsigned long long)lanes);
+    if (lane == 0) {
+        if (lanes) {  // one (lookups, rays) atomic pair per wave; the first lookup came from k_agents
+            unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+            atomicAdd(cs, (unsigned long long)(lanes + lane_iters));
+            atomicAdd(cs + 1, (unsigned long long)lanes);
+        }
+        if (K.wcost) {  // this group's cost, the next step's heavy-first prediction
+            const uint32_t mx = lanes ? 1u + iters : 0u;
+            K.wcost[(size_t)g * ng + grp] = (uint8_t)(mx < 255u ? mx : 255u);
+        }
     }
 }
 
@@ -1664,9 +1686,8 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                          reinterpret_cast<const void *>(&k_rays_fxn<4, false, true>),
                          reinterpret_cast<const void *>(&k_rays_fxn<4, true, false>),
                          reinterpret_cast<const void *>(&k_rays_fxn<4, true, true>)}};
-                    ra.HB = 0;
-                    ra.wcost = nullptr;
-                    g2 = dim3((unsigned)(ra.G4 * ((ra.nch + N - 1) / N)));
+                    ra.nch = (ra.nch + N - 1) / N;  // chunk groups per car (heavy list / wcost units)
+                    g2 = dim3((unsigned)(ra.HB + ra.G4 * ra.nch));
                     f = fn_n[N - 2][v2];
                 } else {
                     const void *fn_1[4] = {reinterpret_cast<const void *>(&k_rays_fx<false, false, false, 3>),

@@ -273,6 +273,11 @@ class BatchSim:
         """The ray kernel this context launches (f110_ray_kernel: 3 = k_rays_fx)."""
         return _lib.check(self.L.f110_ray_kernel(self.ctx), "f110_ray_kernel")
 
+    @property
+    def ray_lanes(self) -> int:
+        """Rays per lane of the fixed-point ray kernel (f110_ray_lanes: 1 = k_rays_fx, 2 = k_rays_fxn)."""
+        return _lib.check(self.L.f110_ray_lanes(self.ctx), "f110_ray_lanes")
+
     def close(self):
         if getattr(self, "ctx", None):
             torch.cuda.synchronize(self.device)

@@ -273,6 +273,11 @@ F110_API int f110_disable_heavy_first(f110_ctx *ctx);
  * Selected at f110_create (env F110_RAY_KERNEL overrides the default). */
 F110_API int f110_ray_kernel(const f110_ctx *ctx);
 
+/* Rays traced per lane by the fixed-point ray kernel (1: k_rays_fx, 2..4:
+ * k_rays_fxn; F110_FX_ILP overrides the size-based default); 1 for the
+ * other ray kernels.  Diagnostic, no reference counterpart. */
+F110_API int f110_ray_lanes(const f110_ctx *ctx);
+
 /* The dtype of the reset poses whose F110Env.reset semantics the following
  * resets follow (f110_env.py:441-451): F110_F32 (train_ddpg passes float32
  * options) rounds the reset / autoreset poses to float32 and evaluates the lap

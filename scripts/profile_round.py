@@ -128,6 +128,7 @@ try:
     cyc = busy["GRBM_GUI_ACTIVE"] / 8.0
     busy["valu_busy"] = busy["SQ_ACTIVE_INST_VALU"] * 4.0 / (simds * cyc)
     busy["waves_per_simd"] = busy["SQ_WAVE_CYCLES"] * 4.0 / (simds * cyc)
+    busy["wait_frac"] = busy["SQ_WAIT_ANY"] / max(1.0, busy["SQ_WAVE_CYCLES"])  # share of wave time in s_waitcnt
     busy["note"] = ("valu_busy = SQ_ACTIVE_INST_VALU*4 / (1024 SIMDs * GRBM_GUI_ACTIVE/8); waves_per_simd = "
                     "SQ_WAVE_CYCLES*4 / (1024 * GRBM_GUI_ACTIVE/8); mean per k_rays dispatch, scripts/ray_pmc.py (minimal outputs)")
 except Exception as exc:
