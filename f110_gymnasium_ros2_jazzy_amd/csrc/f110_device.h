@@ -791,18 +791,30 @@ F110_HD uint32_t noise_key(uint64_t seed, uint64_t env) {
            ((uint32_t)(env >> 32) * 0xC2B2AE35u);
 }
 
-// N(0,1) for beam b of the env's stream at `step`: one Philox2x32 block per
-// beam (counter (step, b | step_hi << 16), key noise_key(seed, env)),
-// Box-Muller on 24-bit uniforms in fp32 hardware transcendentals (v_log,
-// v_sqrt, v_cos: the noise is a statistical quantity, its ~1e-7 relative
-// precision is far below the 0.01 m std it scales; tails are cut at 5.8
-// sigma).  The key is per env: wave-uniform in the chunked ray kernels.
-F110_D float beam_normal_k(uint32_t key, uint64_t step, int b) {
-    const U2 r = philox2x32((uint32_t)step, (uint32_t)b | ((uint32_t)(step >> 32) << 16), key);
+// N(0,1) noise of the env's stream at `step`: beams b and b + 64 of each
+// 128-beam block share one Philox2x32 block (counter (step, p | step_hi <<
+// 16) with p = (b >> 7) * 64 + (b & 63), key noise_key(seed, env)) and take
+// the two outputs of one Box-Muller transform, rad * cos and rad * sin
+// (independent N(0,1)), on 24-bit uniforms in fp32 hardware transcendentals
+// (v_log, v_sqrt, v_cos, v_sin: the noise is a statistical quantity, its ~1e-7
+// relative precision is far below the 0.01 m std it scales; tails are cut at
+// 5.8 sigma).  A lane tracing both beams (k_rays_fxn<2>) draws once for two.
+// The key is per env: wave-uniform in the chunked ray kernels.
+F110_D void beam_normal_pair_k(uint32_t key, uint64_t step, int p, float &n_lo, float &n_hi) {
+    const U2 r = philox2x32((uint32_t)step, (uint32_t)p | ((uint32_t)(step >> 32) << 16), key);
     const float u1 = ((float)(r.x >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
     const float u2 = (float)(r.y >> 8) * (1.0f / 16777216.0f);           // [0, 1)
     const float rad = __builtin_amdgcn_sqrtf(-2.0f * 0.69314718055994531f * __builtin_amdgcn_logf(u1));
-    return rad * __builtin_amdgcn_cosf(u2);  // cos(2 pi u2)
+    n_lo = rad * __builtin_amdgcn_cosf(u2);  // cos(2 pi u2): beam (b & ~64)
+    n_hi = rad * __builtin_amdgcn_sinf(u2);  // sin(2 pi u2): beam (b | 64)
+}
+
+F110_D int beam_noise_pair(int b) { return ((b >> 7) << 6) | (b & 63); }
+
+F110_D float beam_normal_k(uint32_t key, uint64_t step, int b) {
+    float lo, hi;
+    beam_normal_pair_k(key, step, beam_noise_pair(b), lo, hi);
+    return (b & 64) ? hi : lo;
 }
 
 F110_D float beam_normal(uint64_t seed, uint64_t env, uint64_t step, int b) {

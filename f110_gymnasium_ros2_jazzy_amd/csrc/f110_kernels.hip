@@ -998,11 +998,20 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
     const bool noise_on = K.noise_ext || K.noise_std > 0.0;
     const uint32_t key = noise_key(K.seed, (uint64_t)(K.env_offset + e));
     const uint64_t step = noise_on && !K.noise_ext ? ld_const(K.noise_step + e) : 0;
+    float pn[N];  // device-stream normals: with N = 2 the lane's beams b and b + 64 share one draw
+    if (!K.noise_ext && K.noise_std > 0.0) {
+        if (N == 2) {
+            beam_normal_pair_k(key, step, beam_noise_pair(b0 + lane), pn[0], pn[1]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < N; ++r) pn[r] = beam_normal_k(key, step, bc[r]);
+        }
+    }
 #pragma unroll
     for (int r = 0; r < N; ++r) {
         double nz = 0.0;
         if (K.noise_ext) nz = K.noise_ext[(size_t)e * B + bc[r]];
-        else if (K.noise_std > 0.0) nz = K.noise_std * (double)beam_normal_k(key, step, bc[r]);
+        else if (K.noise_std > 0.0) nz = K.noise_std * (double)pn[r];
         if (has[r])
             fx_epilogue<HANDOFF>(K, g, e, b0 + 64 * r + lane, tot[r], L.mr, nz, v, a.beam_cos[bc[r]], a.side[bc[r]]);
         lanes += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(has[r]));

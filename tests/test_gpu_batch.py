@@ -52,6 +52,13 @@ def test_noise_statistics(tracks, gpu):
     same = np.abs(n1[:, 0] - n1[:, 1]) < 1e-12
     assert same.mean() > 0.9
     assert abs(n1.mean()) < 5e-4 and abs(n1.std() - 0.01) < 5e-4
+    # beams b and b + 64 of a 128-beam block take the two outputs of one Box-Muller draw: uncorrelated
+    blk = n1[:, 0, :1024].reshape(E, 8, 2, 64)
+    lo, hi = blk[:, :, 0].ravel(), blk[:, :, 1].ravel()
+    ok = (np.abs(lo) < 0.1) & (np.abs(hi) < 0.1)  # noise is cut at 5.8 sigma; drop occluded beams
+    assert ok.mean() > 0.95
+    assert abs(np.corrcoef(lo[ok], hi[ok])[0, 1]) < 0.05
+    assert abs(np.corrcoef(lo[ok] ** 2, hi[ok] ** 2)[0, 1]) < 0.05
     assert not np.allclose(n1[0, 0], n1[1, 0])     # different envs, different streams
     n2 = noisy.step(zero).scans_f64.cpu().numpy() - clean.step(zero).scans_f64.cpu().numpy()
     assert not np.allclose(n1[:, 0], n2[:, 0])     # next step, next draw
