@@ -178,13 +178,14 @@ def oracle_module():
     return O
 
 
-def auto_streams(envs):
+def auto_streams(envs, agents=1):
     """Stream sub-shards per GPU (measured 300-step bench lines):
     8192 envs 40.4 / 46.6 / 49.2 M env-steps/s at S = 1 / 2 / 4; 16384 55.2 /
     48.4 at S = 2 / 4; 32768 61.8 / 46.2; 65536 62.4 / 52.7.  Small shards
     leave CUs idle in k_agents / k_post and the grid tail, which more
-    concurrent sub-shards fill; large ones fill the GPU themselves."""
-    return 4 if envs <= 8192 else 2
+    concurrent sub-shards fill; large ones fill the GPU themselves.  Counted
+    in cars (envs x agents): C4's 8192 two-agent envs run S = 2."""
+    return 4 if envs * agents <= 8192 else 2
 
 
 def cpu_baseline(O, scanner, poses, acts_np, args):
@@ -316,7 +317,7 @@ def main():
     shard = D.shard_range(G, world, rank)
     E = shard.count
     K, W = args.steps, args.warmup
-    S = args.streams if args.streams > 0 else auto_streams(E)
+    S = args.streams if args.streams > 0 else auto_streams(E, A)
     noise = 0.0 if args.no_noise else 0.01
 
     track = load_map(args.map)
@@ -478,7 +479,7 @@ def main():
         for label, n in (("C3_shard_8192", 8192), ("C2_4096", 4096)):
             if n >= E:
                 continue
-            S2 = args.streams if args.streams > 0 else auto_streams(n)
+            S2 = args.streams if args.streams > 0 else auto_streams(n, A)
             r2 = make(n, 0, S2)
             el2, _ = timed(r2, spawn[rng.integers(0, spawn.shape[0], size=n)], actions(W + K, n, 0))
             line = {"envs": n, "value": n * K / el2, "ms_per_step": el2 / K * 1e3,
