@@ -44,6 +44,29 @@ FUSED = os.environ.get("F110_DDPG_FUSED", "1") != "0"
 MFMA_HIDDEN = os.environ.get("F110_DDPG_MFMA", "0") == "1"
 
 
+# The learner's GEMM choices at batch 4096 (torch TunableOp, tuned on MI355X
+# over hipBLASLt and rocBLAS solutions: tuning/tunableop_gfx950.csv, read-only).
+# At C5's batch the learner update went 0.545 -> 0.486 ms.
+# F110_TUNABLEOP=0 keeps torch's default heuristics.
+TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "tunableop_gfx950.csv")
+
+
+def enable_tuned_gemms(device: torch.device) -> bool:
+    """Switch on TunableOp with the shipped results (no tuning, no file writes).
+    TunableOp validates the file against this torch / HIP / hipBLASLt / arch and
+    ignores it on a mismatch; shapes not in the file keep the defaults."""
+    if os.environ.get("F110_TUNABLEOP", "1") == "0" or device.type != "cuda" or not os.path.exists(TUNED_GEMMS):
+        return False
+    import torch.cuda.tunable as tunable
+    if "gfx950" not in torch.cuda.get_device_properties(device).gcnArchName:
+        return False
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    tunable.record_untuned_enable(False)
+    tunable.set_filename(TUNED_GEMMS)
+    return bool(tunable.read_file(TUNED_GEMMS))
+
+
 def _fused(x: torch.Tensor) -> bool:
     return FUSED and x.is_cuda
 
@@ -272,6 +295,7 @@ class DDPGLearner:
                  seed: int = 42, device="cuda:0", replay="device", process_group=None, max_add: int | None = None,
                  check_finite: bool = False, path: str | None = None, graphs: bool = False):
         self.device = torch.device(device)
+        self.tuned_gemms = enable_tuned_gemms(self.device)
         self.obs_dim, self.act_dim = int(obs_dim), int(act_dim)
         self.action_low = np.asarray(action_low, dtype=np.float32)
         self.action_high = np.asarray(action_high, dtype=np.float32)
