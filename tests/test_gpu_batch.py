@@ -250,3 +250,35 @@ def test_stream_shards_broadcast_reset(tracks, gpu):
     full.reset(sp[100])
     assert torch.equal(sh.obs, full.out.obs)
     sh.close()
+
+
+@pytest.mark.parametrize("beams,A", [(64, 1), (333, 2), (2048, 1), (1080, 3)])
+def test_rays_per_lane_identical_across_beam_counts(tracks, gpu, monkeypatch, beams, A):
+    """k_rays_fxn (2 and 3 rays per lane) against k_rays_fx (1) for scan sizes
+    whose 64-beam chunks do not pair evenly (1, 6, 32 chunks; 17 with three
+    agents): scans, obs, collisions and states bit-identical over 25 noisy
+    steps with autoreset and a masked reset."""
+    E = 96
+    sp = _spawns(A)
+    rng = np.random.default_rng(beams)
+    poses = sp[rng.integers(0, sp.shape[0], E)]
+    acts = np.stack([rng.uniform(-0.4189, 0.4189, (25, E, A)), rng.uniform(0, 20, (25, E, A))], -1).astype(np.float32)
+    mask = rng.random(E) < 0.5
+    outs = []
+    for ilp in ("1", "2", "3"):
+        monkeypatch.setenv("F110_FX_ILP", ilp)
+        sim = _sim(tracks, gpu, n_envs=E, n_agents=A, num_beams=beams, noise_std=0.01, autoreset=True,
+                   spawn_poses=sp, seed=9, keep_f64_scans=True)
+        assert sim.ray_kernel == 3 and sim.ray_lanes == int(ilp)
+        sim.reset(poses)
+        rec = []
+        for t in range(25):
+            o = sim.reset(poses[::-1].copy(), env_mask=mask) if t == 12 else sim.step(acts[t])
+            rec.append((o.scans_f64.clone(), o.obs.clone(), o.collisions.clone(), sim.agent_states().clone()))
+        torch.cuda.synchronize()
+        outs.append(rec)
+        sim.close()
+    for rec in outs[1:]:
+        for t, (a, b) in enumerate(zip(outs[0], rec)):
+            for x, y in zip(a, b):
+                assert torch.equal(x, y), f"step {t}"
