@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -37,8 +38,11 @@ int fail(int code, const std::string &msg) {
 // shared with f110_replay_capi.cpp (one thread-local error string per library)
 int f110_set_error(int code, const std::string &msg) { return fail(code, msg); }
 
+struct MapTables;
+
 struct f110_ctx {
     int device = 0;
+    MapTables *maps = nullptr;  // the shared read-only EDT tables (dt, dt_tiled, rm)
     f110_config cfg{};
     f110_params p{};                 // Simulator-level params (fixed at create)
     std::vector<f110_params> agent_p;  // RaceCar params per agent (f110_set_params)
@@ -374,6 +378,124 @@ static int use_device(const f110_ctx *c) {
     return F110_OK;
 }
 
+// ------------------------------------------------------ shared map tables --
+// The EDT tables (row-major dt, the 4x4-tiled copy, the fixed-point kernel's
+// padded row-major table) are read-only after f110_create.  Contexts on one
+// device built from the same map (same H, W, resolution and EDT) share one
+// copy: S stream sub-shards of a GPU's envs (streams.StreamShards) then keep
+// one table's neighbourhood in each XCD's L2 instead of S (32 MB per copy of
+// the Spielberg table).  Refcounted; F110_SHARE_MAP=0 gives each context its
+// own copy (A/B).
+struct MapTables {
+    int device = 0;
+    int32_t H = 0, W = 0;
+    uint64_t res_bits = 0;
+    std::vector<uint32_t> k;  // the EDT the tables were built from (exact match, not a hash)
+    double *dt = nullptr, *dt_tiled = nullptr, *rm = nullptr;
+    int32_t rm_w = 0;
+    uint32_t rm_oob = 0, rm_zero = 0;
+    int refs = 0;
+    bool shared = true;
+};
+static std::mutex g_maps_mu;
+static std::vector<MapTables *> g_maps;
+
+static void free_map_tables(MapTables *t) {
+    (void)hipSetDevice(t->device);
+    if (t->dt) (void)hipFree(t->dt);
+    if (t->dt_tiled) (void)hipFree(t->dt_tiled);
+    if (t->rm) (void)hipFree(t->rm);
+    delete t;
+}
+
+static void release_map_tables(MapTables *t) {
+    if (!t) return;
+    std::lock_guard<std::mutex> g(g_maps_mu);
+    if (--t->refs > 0) return;
+    g_maps.erase(std::remove(g_maps.begin(), g_maps.end(), t), g_maps.end());
+    free_map_tables(t);
+}
+
+template <class T>
+static hipError_t upload(T **p, const std::vector<T> &h) {
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(p), std::max<size_t>(h.size() * sizeof(T), 16));
+    if (e == hipSuccess) e = hipMemcpy(*p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+    return e;
+}
+
+// The tables of (device, map), built and uploaded on first use; `want_rm`
+// adds the padded row-major table if the entry lacks it.  Called with the
+// device current.
+static hipError_t acquire_map_tables(int device, const uint32_t *edt_k, int32_t H, int32_t W, double res,
+                                     int32_t wt, int32_t tiles_h, bool want_rm, MapTables **out) {
+    std::lock_guard<std::mutex> g(g_maps_mu);
+    const size_t N = (size_t)H * W;
+    uint64_t rb;
+    std::memcpy(&rb, &res, 8);
+    bool share = true;
+    if (const char *v = std::getenv("F110_SHARE_MAP")) share = std::atoi(v) != 0;
+    MapTables *t = nullptr;
+    if (share)
+        for (MapTables *q : g_maps)
+            if (q->shared && q->device == device && q->H == H && q->W == W && q->res_bits == rb &&
+                std::memcmp(q->k.data(), edt_k, N * sizeof(uint32_t)) == 0) {
+                t = q;
+                break;
+            }
+    const bool fresh = t == nullptr;
+    if (fresh) {
+        t = new MapTables();
+        t->device = device;
+        t->H = H;
+        t->W = W;
+        t->res_bits = rb;
+        t->shared = share;
+        t->k.assign(edt_k, edt_k + N);
+    }
+    hipError_t e = hipSuccess;
+    std::vector<double> dt;
+    auto dt_host = [&]() -> const std::vector<double> & {
+        if (dt.empty()) {  // dt = res * EDT (get_dt, laser_models.py:52) -- bit-exact from the integer k
+            dt.resize(N);
+            for (size_t i = 0; i < N; ++i) dt[i] = res * std::sqrt((double)edt_k[i]);
+        }
+        return dt;
+    };
+    if (fresh) {
+        e = upload(&t->dt, dt_host());
+        if (e == hipSuccess) {
+            std::vector<double> dtt((size_t)wt * tiles_h * 16, 0.0);  // padding cells are never read
+            for (int r = 0; r < H; ++r)
+                for (int q = 0; q < W; ++q) dtt[(size_t)tiled_index(wt, r, q)] = dt[(size_t)r * W + q];
+            e = upload(&t->dt_tiled, dtt);
+        }
+    }
+    if (e == hipSuccess && want_rm && !t->rm) {
+        // k_rays_fx / k_rays_fxn's row-major EDT: rows of rm_w cells (128-B
+        // aligned), the padding columns and row H hold dt[-1,-1] (a clamped
+        // index then reads the reference's off-map value), and a 0.0 after the
+        // last row is the zero cell of rays that have ended
+        const std::vector<double> &d = dt_host();
+        const size_t Wp = ((size_t)W + 1 + 15) / 16 * 16, Hp = (size_t)H + 1;
+        std::vector<double> rm(Wp * Hp + 16, d[N - 1]);
+        for (int r = 0; r < H; ++r)
+            for (int q = 0; q < W; ++q) rm[(size_t)r * Wp + q] = d[(size_t)r * W + q];
+        rm[Wp * Hp] = 0.0;
+        e = upload(&t->rm, rm);
+        t->rm_w = (int32_t)Wp;
+        t->rm_oob = (uint32_t)(((size_t)(H - 1) * Wp + (W - 1)) * 8);
+        t->rm_zero = (uint32_t)(Wp * Hp * 8);
+    }
+    if (e != hipSuccess) {
+        if (fresh) free_map_tables(t);
+        return e;
+    }
+    if (fresh) g_maps.push_back(t);
+    ++t->refs;
+    *out = t;
+    return hipSuccess;
+}
+
 extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cfg, const f110_params *params,
                            const uint32_t *edt_k, int32_t H, int32_t W, double resolution, const double origin[3],
                            const double *spawn_poses, int32_t n_spawn) {
@@ -445,6 +567,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
 
     auto cleanup = [&](int code, const std::string &msg) {
         for (void *q : c->allocs) (void)hipFree(q);
+        release_map_tables(c->maps);
         delete c;
         return fail(code, msg);
     };
@@ -454,11 +577,8 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
         if (e_ != hipSuccess) return cleanup(F110_E_ALLOC, std::string("hipMalloc " #ptr ": ") + hipGetErrorString(e_)); \
     } while (0)
 
-    const size_t N = (size_t)H * W;
-    ALLOC(c->dt, N);
     c->wt = (W + 3) / 4;
     c->tiles_h = (H + 3) / 4;
-    ALLOC(c->dt_tiled, (size_t)c->wt * c->tiles_h * 16);
     ALLOC(c->sines, (size_t)C.theta_dis);
     ALLOC(c->cosines, (size_t)C.theta_dis);
     ALLOC(c->angles, (size_t)C.n_beams);
@@ -536,18 +656,9 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     }
 #undef ALLOC
 
-    // dt = res * EDT (get_dt, laser_models.py:52) — bit-exact from the integer k.
-    std::vector<double> dt(N);
-    for (size_t i = 0; i < N; ++i) dt[i] = resolution * std::sqrt((double)edt_k[i]);
-    std::vector<double> dtt((size_t)c->wt * c->tiles_h * 16, 0.0);  // padding cells are never read
-    for (int r = 0; r < H; ++r)
-        for (int q = 0; q < W; ++q) dtt[(size_t)tiled_index(c->wt, r, q)] = dt[(size_t)r * W + q];
     std::vector<double> s(C.theta_dis), co(C.theta_dis), an(C.n_beams), bc(C.n_beams), sd(C.n_beams);
     f110_host_tables(C.theta_dis, C.n_beams, C.fov, params, s.data(), co.data(), an.data(), bc.data(), sd.data());
     hipError_t e = hipSuccess;
-    if (e == hipSuccess) e = hipMemcpy(c->dt, dt.data(), N * sizeof(double), hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = hipMemcpy(c->dt_tiled, dtt.data(), dtt.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->sines, s.data(), s.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->cosines, co.data(), co.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->angles, an.data(), an.size() * sizeof(double), hipMemcpyHostToDevice);
@@ -561,22 +672,18 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
                       hipMemcpyHostToDevice);
     if (const char *v = std::getenv("F110_FX_LEAN")) c->fx_nolean = std::atoi(v) == 0;
     if (const char *v = std::getenv("F110_FX_LDS")) c->fx_lds = (uint32_t)std::max(0, std::min(65536, std::atoi(v)));
-    if (c->ray_kernel == 3 && !c->fx_tiled && e == hipSuccess) {
-        // k_rays_fx / k_rays_fxn's row-major EDT: rows of rm_w cells (128-B
-        // aligned), the padding columns and row H hold dt[-1,-1] (a clamped
-        // index then reads the reference's off-map value), and a 0.0 after the
-        // last row is the zero cell of rays that have ended
-        const size_t Wp = ((size_t)W + 1 + 15) / 16 * 16, Hp = (size_t)H + 1;
-        const double oobv = dt[(size_t)H * W - 1];
-        std::vector<double> rm(Wp * Hp + 16, oobv);
-        for (int r = 0; r < H; ++r)
-            for (int q = 0; q < W; ++q) rm[(size_t)r * Wp + q] = dt[(size_t)r * W + q];
-        rm[Wp * Hp] = 0.0;
-        if ((e = c->alloc(&c->rm, rm.size())) == hipSuccess)
-            e = hipMemcpy(c->rm, rm.data(), rm.size() * sizeof(double), hipMemcpyHostToDevice);
-        c->rm_w = (int32_t)Wp;
-        c->rm_oob = (uint32_t)(((size_t)(H - 1) * Wp + (W - 1)) * 8);
-        c->rm_zero = (uint32_t)(Wp * Hp * 8);
+    if (e == hipSuccess)
+        e = acquire_map_tables(device, edt_k, H, W, resolution, c->wt, c->tiles_h, c->ray_kernel == 3 && !c->fx_tiled,
+                               &c->maps);
+    if (e == hipSuccess) {
+        c->dt = c->maps->dt;
+        c->dt_tiled = c->maps->dt_tiled;
+        if (c->ray_kernel == 3 && !c->fx_tiled) {
+            c->rm = c->maps->rm;
+            c->rm_w = c->maps->rm_w;
+            c->rm_oob = c->maps->rm_oob;
+            c->rm_zero = c->maps->rm_zero;
+        }
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) return cleanup(F110_E_HIP, std::string("f110_create upload: ") + hipGetErrorString(e));
@@ -593,6 +700,7 @@ extern "C" int f110_destroy(f110_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     ctx->free_prof();
     for (void *q : ctx->allocs) (void)hipFree(q);
+    release_map_tables(ctx->maps);
     delete ctx;
     return F110_OK;
 }
