@@ -863,6 +863,17 @@ extern "C" int f110_disable_heavy_first(f110_ctx *ctx) {
     return F110_OK;
 }
 
+extern "C" int f110_set_ray_lanes(f110_ctx *ctx, int32_t n) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_lanes: null context");
+    if (n < 1 || n > 4) return fail(F110_E_INVALID, "f110_set_ray_lanes: n must be in 1..4");
+    if (ctx->launch_n != 0)
+        return fail(F110_E_INVALID, "f110_set_ray_lanes: call before the first reset/step (heavy-first state is per group)");
+    const bool fx = ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled;
+    if (!fx && n != 1) return fail(F110_E_INVALID, "f110_set_ray_lanes: this context's ray kernel traces one ray per lane");
+    if (fx && !std::getenv("F110_FX_ILP")) ctx->fx_ilp = n;  // the env override still wins (A/B runs)
+    return F110_OK;
+}
+
 extern "C" int f110_set_ray_gate(f110_ctx *ctx, void *wait_event, void *record_event) {
     if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_gate: null context");
     ctx->gate_wait = static_cast<hipEvent_t>(wait_event);

@@ -64,7 +64,7 @@ class StreamShards:
     for all of them (do that before reading `obs`)."""
 
     def __init__(self, track, n_envs: int, n_streams: int = 2, env_offset: int = 0, heavy_first: bool = False,
-                 **kw):
+                 ray_lanes: int | None = None, **kw):
         if n_streams < 1 or n_envs % n_streams:
             raise ValueError(f"n_envs ({n_envs}) must split evenly into n_streams ({n_streams})")
         self.S = n_streams
@@ -84,6 +84,12 @@ class StreamShards:
         self.device = dev
         self.n_agents = int(kw.get("n_agents", 2))
         self.streams = [dedicated_stream(self.device) for _ in range(self.S)]
+        if ray_lanes is None:
+            # f110_create's rule (2 rays per lane from 12288 cars up) applied to the cars the GPU
+            # traces at once, not to one sub-shard's: 16384 envs as 2 x 8192 59.9 vs 56.0 M
+            # env-steps/s, 8192 as 4 x 2048 53.1 vs 47.6 M (profiles/r02_share_map/)
+            ray_lanes = 2 if n_envs * self.n_agents >= 12288 else 1
+        self.ray_lanes = ray_lanes
         for s in range(self.S):
             with torch.cuda.stream(self.streams[s]):
                 sm = BatchSim(track, n_envs=self.Es, env_offset=env_offset + s * self.Es, device=self.device, **kw)
@@ -91,6 +97,8 @@ class StreamShards:
                     # the other sub-shard's ray pass fills this one's tail; heavy-first's list
                     # upkeep then costs more than it saves (42.5 vs 41.8 M env-steps/s)
                     _lib.check(sm.L.f110_disable_heavy_first(sm.ctx), "f110_disable_heavy_first")
+                if sm.ray_kernel == 3:  # the fixed-point kernel (the others trace one ray per lane)
+                    _lib.check(sm.L.f110_set_ray_lanes(sm.ctx, int(ray_lanes)), "f110_set_ray_lanes")
                 self.sims.append(sm)
         self._sl = [slice(s * self.Es, (s + 1) * self.Es) for s in range(self.S)]
         self._fork()

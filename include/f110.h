@@ -278,6 +278,14 @@ F110_API int f110_ray_kernel(const f110_ctx *ctx);
  * other ray kernels.  Diagnostic, no reference counterpart. */
 F110_API int f110_ray_lanes(const f110_ctx *ctx);
 
+/* Sets the rays per lane of the fixed-point ray kernel (1..4) before the
+ * context's first reset/step.  The size-based default looks at this
+ * context's cars only; a caller stepping S contexts concurrently on one GPU
+ * (streams.StreamShards) knows the GPU's total and passes the choice for
+ * that.  Scheduling only: results are unchanged.  F110_FX_ILP
+ * still overrides.  Diagnostic / tuning, no reference counterpart. */
+F110_API int f110_set_ray_lanes(f110_ctx *ctx, int32_t n);
+
 /* The dtype of the reset poses whose F110Env.reset semantics the following
  * resets follow (f110_env.py:441-451): F110_F32 (train_ddpg passes float32
  * options) rounds the reset / autoreset poses to float32 and evaluates the lap

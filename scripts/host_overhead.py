@@ -33,7 +33,7 @@ for E, S in cases:
         step = lambda a: sim.step(a, minimal_outputs=True)
         reset = sim.reset
     else:
-        sim = StreamShards(tm, E, n_streams=S, **kw)
+        sim = StreamShards(tm, E, n_streams=S, heavy_first=os.environ.get("HF", "0") == "1", **kw)
         step = lambda a: sim.step(a, minimal_outputs=True)
         reset = sim.reset
     reset(p0)
