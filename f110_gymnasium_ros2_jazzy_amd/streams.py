@@ -101,6 +101,7 @@ class StreamShards:
                     _lib.check(sm.L.f110_set_ray_lanes(sm.ctx, int(ray_lanes)), "f110_set_ray_lanes")
                 self.sims.append(sm)
         self._sl = [slice(s * self.Es, (s + 1) * self.Es) for s in range(self.S)]
+        self._handles = [ctypes.c_void_p(st.cuda_stream) for st in self.streams]
         self._fork()
 
     def _caller(self):
@@ -163,12 +164,28 @@ class StreamShards:
         """Launch every sub-shard's step on its stream (not joined).  The
         sub-streams first wait for the caller's stream: actions produced there
         (a policy, torch.rand) and any reads of the previous obs queued there
-        (`obs`, a torch.cat) are ordered before this step's kernels."""
+        (`obs`, a torch.cat) are ordered before this step's kernels.
+
+        Sub-shard s reads its rows of the contiguous action tensor by pointer
+        offset, and f110_step is called with that sub-shard's stream handle
+        directly (no per-sub-shard tensor views or stream switches: at 4096
+        envs x 4 sub-shards the submission loop was 80 of the 111 us of a
+        step)."""
         a = torch.as_tensor(actions, device=self.device)
+        if a.dtype not in (torch.float32, torch.float64):
+            a = a.to(torch.float32)
+        if tuple(a.shape) != (self.E, self.n_agents, 2):
+            raise ValueError(f"actions must be [{self.E}, {self.n_agents}, 2]; got {tuple(a.shape)}")
+        a = a.contiguous()
         self._fork()
-        for s in range(self.S):
-            with torch.cuda.stream(self.streams[s]):
-                self.sims[s].step(a[self._sl[s]], minimal_outputs=minimal_outputs)
+        dt = _lib.F64 if a.dtype == torch.float64 else _lib.F32
+        base, stride = a.data_ptr(), self.Es * self.n_agents * 2 * a.element_size()
+        for s, sm in enumerate(self.sims):
+            sm._keep_a = a
+            outs = sm._outs_min if minimal_outputs else sm._outs
+            rc = sm.L.f110_step(sm.ctx, ctypes.c_void_p(base + s * stride), dt, ctypes.byref(outs), self._handles[s])
+            if rc < 0:
+                _lib.check(rc, "f110_step")
         self._hold(a)
 
     def join(self):
