@@ -102,6 +102,10 @@ struct f110_ctx {
     double *rm = nullptr;
     int32_t rm_w = 0;
     uint32_t rm_oob = 0, rm_zero = 0;
+    const double *rmp = nullptr;  // k_rays_fxn's padded table (shared, see MapTables)
+    int32_t rmp_w = 0, rmp_P = 0;
+    uint32_t rmp_zero = 0;
+    bool fx_pad = false;    // F110_FX_PAD (default on): k_rays_fxn on the padded table
     int fx_ilp = 1;         // rays per lane (F110_FX_ILP; default by car count)
     bool fx_tiled = false;  // F110_FX_TABLE=tiled: A/B of the 4x4-tiled EDT
     uint32_t fx_lds = 0;  // F110_FX_LDS: diagnostic occupancy cap of the ray kernel
@@ -391,9 +395,9 @@ struct MapTables {
     int32_t H = 0, W = 0;
     uint64_t res_bits = 0;
     std::vector<uint32_t> k;  // the EDT the tables were built from (exact match, not a hash)
-    double *dt = nullptr, *dt_tiled = nullptr, *rm = nullptr;
-    int32_t rm_w = 0;
-    uint32_t rm_oob = 0, rm_zero = 0;
+    double *dt = nullptr, *dt_tiled = nullptr, *rm = nullptr, *rmp = nullptr;
+    int32_t rm_w = 0, rmp_w = 0, rmp_P = 0;
+    uint32_t rm_oob = 0, rm_zero = 0, rmp_zero = 0;
     int refs = 0;
     bool shared = true;
 };
@@ -405,6 +409,7 @@ static void free_map_tables(MapTables *t) {
     if (t->dt) (void)hipFree(t->dt);
     if (t->dt_tiled) (void)hipFree(t->dt_tiled);
     if (t->rm) (void)hipFree(t->rm);
+    if (t->rmp) (void)hipFree(t->rmp);
     delete t;
 }
 
@@ -424,10 +429,11 @@ static hipError_t upload(T **p, const std::vector<T> &h) {
 }
 
 // The tables of (device, map), built and uploaded on first use; `want_rm`
-// adds the padded row-major table if the entry lacks it.  Called with the
-// device current.
+// adds the row-major table if the entry lacks it, `pad` > 0 the table padded
+// by `pad` cells on every side (an entry keeps the padding it was built with:
+// the kernel's per-car test reads the entry's).  Called with the device current.
 static hipError_t acquire_map_tables(int device, const uint32_t *edt_k, int32_t H, int32_t W, double res,
-                                     int32_t wt, int32_t tiles_h, bool want_rm, MapTables **out) {
+                                     int32_t wt, int32_t tiles_h, bool want_rm, int32_t pad, MapTables **out) {
     std::lock_guard<std::mutex> g(g_maps_mu);
     const size_t N = (size_t)H * W;
     uint64_t rb;
@@ -485,6 +491,25 @@ static hipError_t acquire_map_tables(int device, const uint32_t *edt_k, int32_t 
         t->rm_w = (int32_t)Wp;
         t->rm_oob = (uint32_t)(((size_t)(H - 1) * Wp + (W - 1)) * 8);
         t->rm_zero = (uint32_t)(Wp * Hp * 8);
+    }
+    if (e == hipSuccess && pad > 0 && !t->rmp) {
+        // k_rays_fxn's padded table (PAD, see kFxpBase): cell (r, c) at row
+        // r + P, column c + P; every other cell holds dt[-1,-1] (the
+        // reference's off-map read), and a 0.0 after the last row is the zero
+        // cell.  Built only where its byte offsets stay 32-bit and a row
+        // stride stays a 24-bit multiplier.
+        const size_t P = (size_t)pad, Wp = ((size_t)W + 2 * P + 15) / 16 * 16, Hp = (size_t)H + 2 * P;
+        if ((Wp * Hp + 16) * 8 < (1ull << 32) && Wp * 8 < (1u << 24)) {
+            const std::vector<double> &d = dt_host();
+            std::vector<double> rmp(Wp * Hp + 16, d[N - 1]);
+            for (int r = 0; r < H; ++r)
+                for (int q = 0; q < W; ++q) rmp[((size_t)r + P) * Wp + q + P] = d[(size_t)r * W + q];
+            rmp[Wp * Hp] = 0.0;
+            e = upload(&t->rmp, rmp);
+            t->rmp_w = (int32_t)Wp;
+            t->rmp_P = (int32_t)P;
+            t->rmp_zero = (uint32_t)(Wp * Hp * 8);
+        }
     }
     if (e != hipSuccess) {
         if (fresh) free_map_tables(t);
@@ -671,10 +696,15 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
         e = hipMemcpy(c->spawn, spawn_poses, (size_t)n_spawn * C.n_agents * 3 * sizeof(double),
                       hipMemcpyHostToDevice);
     if (const char *v = std::getenv("F110_FX_LEAN")) c->fx_nolean = std::atoi(v) == 0;
+    // PAD: k_rays_fxn's clamp-free loop on a table padded by the max range (+ 8 cells of margin)
+    c->fx_pad = c->ray_kernel == 3 && !c->fx_tiled && !c->evict;
+    if (const char *v = std::getenv("F110_FX_PAD")) c->fx_pad = c->fx_pad && std::atoi(v) != 0;
+    const double pad_q = std::ceil(C.max_range / resolution) + 8.0;
+    const int32_t fx_pad_cells = pad_q > 0.0 && pad_q < 65536.0 ? (int32_t)pad_q : 0;  // else no padded table
     if (const char *v = std::getenv("F110_FX_LDS")) c->fx_lds = (uint32_t)std::max(0, std::min(65536, std::atoi(v)));
     if (e == hipSuccess)
         e = acquire_map_tables(device, edt_k, H, W, resolution, c->wt, c->tiles_h, c->ray_kernel == 3 && !c->fx_tiled,
-                               &c->maps);
+                               c->fx_pad ? fx_pad_cells : 0, &c->maps);
     if (e == hipSuccess) {
         c->dt = c->maps->dt;
         c->dt_tiled = c->maps->dt_tiled;
@@ -683,6 +713,12 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
             c->rm_w = c->maps->rm_w;
             c->rm_oob = c->maps->rm_oob;
             c->rm_zero = c->maps->rm_zero;
+            if (c->fx_pad && c->maps->rmp) {
+                c->rmp = c->maps->rmp;
+                c->rmp_w = c->maps->rmp_w;
+                c->rmp_P = c->maps->rmp_P;
+                c->rmp_zero = c->maps->rmp_zero;
+            }
         }
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -790,6 +826,11 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.rm_w = c->rm_w;
     a.rm_oob = c->rm_oob;
     a.rm_zero = c->rm_zero;
+    a.rmp = c->rmp;
+    a.rmp_w = c->rmp_w;
+    a.rmp_P = c->rmp_P;
+    a.rmp_zero = c->rmp_zero;
+    a.fx_pad = c->rmp ? 1 : 0;
     a.fx_tiled = c->fx_tiled ? 1 : 0;
     a.fx_lds = c->fx_lds;
     a.fx_nolean = c->fx_nolean ? 1 : 0;

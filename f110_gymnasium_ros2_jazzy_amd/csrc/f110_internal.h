@@ -56,6 +56,13 @@ struct StepArgs {
     const double *rm;
     int32_t rm_w;
     uint32_t rm_oob, rm_zero;
+    // k_rays_fxn's padded row-major EDT (PAD): rows of rmp_w cells, rmp_P
+    // cells of dt[-1,-1] on every side (cell (r, c) at row r + P, column
+    // c + P), a 0.0 at byte rmp_zero past the end; null = not built
+    const double *rmp;
+    int32_t rmp_w, rmp_P;
+    uint32_t rmp_zero;
+    int32_t fx_pad;     // F110_FX_PAD: k_rays_fxn on the padded table
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2..4: k_rays_fxn)
     int32_t fx_tiled;   // F110_FX_TABLE=tiled (A/B): k_rays_fx on the 4x4-tiled EDT
     int32_t fx_nolean;  // F110_FX_LEAN=0 (A/B): the ballot-per-iteration loop of round 2
@@ -141,6 +148,12 @@ struct RayArgs {
     // |q| bound of a scan origin whose rays stay in t's binade: 2^21 - 32 - max_range / res
     double fx_lim;
     uint32_t fx_zero;  // byte offset of the row-major table's zero cell (k_rays_fxn)
+    // PAD (k_rays_fxn on the padded table): fx_cx / fx_cy = 2^24 + P - origin /
+    // res, and a car takes the clamp-free loop when its scan origin's q lies in
+    // [fxp_lo, fxp_hx) x [fxp_lo, fxp_hy): every lookup of its rays then lands
+    // inside the padded table (see fxp_offset)
+    double fxp_lo, fxp_hx, fxp_hy;
+    int32_t fxp_P;
     // straggler hand-off of k_rays_fx (EVICT) -> k_rays_fx_tail: SoA records
     // ev[7][ev_cap] = x, y, d, tot, cos, sin, noise; ev_gb[2][ev_cap] = car, beam.
     // The queue is split in ev_P partitions of ev_capp records (partition p =
@@ -166,6 +179,16 @@ constexpr double kFxMagic = 6291456.0;
 constexpr uint32_t kFxU0 = 0x05600000u;
 // guard band of the fixed-point fraction, in units of 2^-30 (error budget < 2^-29)
 constexpr uint32_t kFxBand = 4u;
+// PAD: t = fma(x, inv_res, 2^24 + P - origin / res) lies in [2^24, 2^25),
+// ulp 2^-28.  Bits [51:28] of t (one v_alignbit by 28) hold int(t) - 2^24 =
+// floor(q) + P in their low 24 bits -- exactly the operand a 24-bit multiply
+// reads, so the padded table's byte offset is two u24 multiply(-add)s with no
+// bias subtraction and no clamp.  Error budget (units of q): the constant's
+// and t's roundings (2^-29 each), inv_res's (< 2^-31 for |x / res| < 2^21)
+// and the reference's own (< 2^-31): < 2^-27.4; the guard band is kFxpBand *
+// 2^-28 = 2^-26.
+constexpr double kFxpBase = 16777216.0;
+constexpr uint32_t kFxpBand = 4u;
 
 struct ScanArgs {
     MapView map;

@@ -855,6 +855,53 @@ __device__ __forceinline__ uint32_t fxn_offset(const TiledMapView &m, const FxLo
     return off;
 }
 
+// PAD (k_rays_fxn on the padded row-major table, kFxpBase): the IEEE path of
+// tiled_cell as a byte offset of the padded table; off-map reads go to cell
+// (-P, -P), which holds dt[-1,-1] like every padding cell.
+__device__ __forceinline__ uint32_t exact_offset_pad(const TiledMapView &m, double x, double y, uint32_t P) {
+    const double xr = x - m.ox, yr = y - m.oy;
+    const bool inb = (xr >= 0) & (xr < m.wres) & (yr >= 0) & (yr < m.hres);  // false for NaN
+    if (!inb) return 0u;
+    int32_t c = (int32_t)(xr / m.res);
+    int32_t r = (int32_t)(yr / m.res);
+    if (c >= m.W) {  // dt[r, W] is dt[r+1, 0] in the reference's row-major read
+        c = 0;
+        ++r;
+    }
+    return r >= m.H ? 0u : ((uint32_t)(r + (int32_t)P) * (uint32_t)m.wt + (uint32_t)(c + (int32_t)P)) * 8u;
+}
+
+// One step of ray r of a PAD lane whose car passed the origin test (every
+// lookup of its rays lies inside the padded table, fxp_lo / fxp_hx / fxp_hy):
+// t = fma(x, inv_res, 2^24 + P - origin / res); one v_alignbit by 28 puts
+// floor(q) + P in the low 24 bits, which the u24 multiplies read directly --
+// no bias subtraction, no bounds test, no clamp (~15 instead of ~20 VALU per
+// ray and iteration in fxn_offset).  Ended rays read the zero cell, lanes
+// within kFxpBand * 2^-28 of a cell edge take the IEEE path.
+__device__ __forceinline__ uint32_t fxp_offset(const TiledMapView &m, const FxLoop &L, double &x, double &y,
+                                               double d, double c, double s, bool act, uint64_t amask,
+                                               uint32_t zero_v, uint32_t P) {
+    x += d * c;  // :135
+    y += d * s;  // :136
+    double tx, ty;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tx) : "v"(x), "v"(L.ir), "s"(L.cxk));
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(ty) : "v"(y), "v"(L.ir), "s"(L.cyk));
+    const uint32_t lx = dlo(tx), ly = dlo(ty);
+    const uint32_t col = __builtin_amdgcn_alignbit(dhi(tx), lx, 28);
+    const uint32_t row = __builtin_amdgcn_alignbit(dhi(ty), ly, 28);
+    const uint32_t band = min((lx << 4) + 16u * kFxpBand, (ly << 4) + 16u * kFxpBand);
+    // (row & 0xffffff) * k1 + (col & 0xffffff) * 8: v_mul_u32_u24 + v_mad_u32_u24 (the compiler's
+    // form of the second multiply is a shift and a mask, one more VALU)
+    const uint32_t prow = __umul24(row, L.k1);
+    uint32_t fast;
+    asm volatile("v_mad_u32_u24 %0, %1, 8, %2" : "=v"(fast) : "v"(col), "v"(prow));
+    uint32_t off = act ? fast : zero_v;
+    if (__builtin_amdgcn_ballot_w64(band < 32u * kFxpBand) & amask) {  // wave-uniform, rare
+        if (act & (band < 32u * kFxpBand)) off = exact_offset_pad(m, x, y, P);
+    }
+    return off;
+}
+
 // k_rays_fxn: N rays per lane (beams b0 + 64 r + lane, r < N, of one car: N
 // adjacent 64-beam chunks), traced in one loop so that each lane keeps N
 // independent EDT gathers in flight.  The single-ray kernel is bound by the
@@ -869,7 +916,7 @@ __device__ __forceinline__ uint32_t fxn_offset(const TiledMapView &m, const FxLo
 // Heavy-first (as k_rays_fx, with a chunk group in place of a chunk: a.nch is
 // the number of groups per car here): HB leading blocks run the groups whose
 // longest ray took >= heavy_T lookups in the previous launch.
-template <int N, bool MASK, bool HANDOFF>
+template <int N, bool MASK, bool HANDOFF, bool PAD = false>
 __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
     const int ng = a.nch;  // chunk groups of N chunks per car
     int g, grp;
@@ -949,10 +996,20 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
     // ---- trace_ray's loop (laser_models.py:133-141), N rays per lane ----
     const FxLoop L = fx_loop<3>(a);
     const uint32_t zero = a.fx_zero;
+    uint32_t zero_v;  // in a VGPR for the whole trace (the select's other operand is its SGPR mask)
+    asm volatile("v_mov_b32 %0, %1" : "=v"(zero_v) : "s"(zero));
+    const uint32_t P = (uint32_t)a.fxp_P;
     uint32_t lane_iters = 0, iters = 0;
-    const double qx = fma(x00, L.ir, L.cxk) - kFxMagic, qy = fma(y00, L.ir, L.cyk) - kFxMagic;
+    bool fast_car;
+    if (PAD) {  // q + P of the scan origin inside [fxp_lo, fxp_h*): its rays stay in the padded table
+        const double ux = fma(x00, L.ir, L.cxk) - kFxpBase, uy = fma(y00, L.ir, L.cyk) - kFxpBase;
+        fast_car = (ux >= a.fxp_lo) & (ux < a.fxp_hx) & (uy >= a.fxp_lo) & (uy < a.fxp_hy);  // false for NaN
+    } else {
+        const double qx = fma(x00, L.ir, L.cxk) - kFxMagic, qy = fma(y00, L.ir, L.cyk) - kFxMagic;
+        fast_car = fabs(qx) < a.fx_lim && fabs(qy) < a.fx_lim;
+    }
     __builtin_amdgcn_s_waitcnt(0);  // the set-up loads land before the loop, not in it
-    if (fabs(qx) < a.fx_lim && fabs(qy) < a.fx_lim) {  // wave-uniform (false for NaN)
+    if (fast_car) {  // wave-uniform (false for NaN)
         // no per-ray flag is carried across iterations (an i1 array would be
         // packed into a VGPR): activity is recomputed from d and the total
         for (;;) {
@@ -971,7 +1028,8 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
                 off[r] = zero;
                 if (m[r]) {
                     const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
-                    off[r] = fxn_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero);
+                    off[r] = PAD ? fxp_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero_v, P)
+                                 : fxn_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero);
                 }
             }
 #pragma unroll
@@ -984,7 +1042,14 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
 #pragma unroll
         for (int r = 0; r < N; ++r)
             while ((dhi(d[r]) != 0u) & (tot[r] <= L.mr)) {
-                fx_step<3>(a.m, L, x[r], y[r], d[r], tot[r], c[r], sn[r]);
+                if (PAD) {  // a car whose origin is off the map: the IEEE cell of every lookup
+                    x[r] += d[r] * c[r];  // :135
+                    y[r] += d[r] * sn[r];  // :136
+                    d[r] = fx_load<3>(a.m.dt, exact_offset_pad(a.m, x[r], y[r], P));
+                    tot[r] += d[r];  // :141
+                } else {
+                    fx_step<3>(a.m, L, x[r], y[r], d[r], tot[r], c[r], sn[r]);
+                }
                 ++cnt;
             }
         lane_iters = wave_sum(cnt);
@@ -1695,9 +1760,39 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                          reinterpret_cast<const void *>(&k_rays_fxn<4, false, true>),
                          reinterpret_cast<const void *>(&k_rays_fxn<4, true, false>),
                          reinterpret_cast<const void *>(&k_rays_fxn<4, true, true>)}};
+                    const void *fn_p[3][4] = {
+                        {reinterpret_cast<const void *>(&k_rays_fxn<2, false, false, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<2, false, true, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<2, true, false, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<2, true, true, true>)},
+                        {reinterpret_cast<const void *>(&k_rays_fxn<3, false, false, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<3, false, true, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<3, true, false, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<3, true, true, true>)},
+                        {reinterpret_cast<const void *>(&k_rays_fxn<4, false, false, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<4, false, true, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<4, true, false, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxn<4, true, true, true>)}};
                     ra.nch = (ra.nch + N - 1) / N;  // chunk groups per car (heavy list / wcost units)
                     g2 = dim3((unsigned)(ra.HB + ra.G4 * ra.nch));
                     f = fn_n[N - 2][v2];
+                    if (a.fx_pad && a.rmp) {
+                        // the padded table (PAD): t = x / res + 2^24 + P; a car's rays stay in
+                        // the table when its origin's q + P lies in [Rn, W or H + 2P - Rn),
+                        // Rn = max_range / res + 2 cells (each lookup is within max_range of it)
+                        const double P = (double)a.rmp_P, Rn = std::ceil(a.max_range * a.tmap.inv_res) + 2.0;
+                        ra.m.dt = a.rmp;
+                        ra.m.wt = a.rmp_w;
+                        ra.m.oob = 0;
+                        ra.fx_zero = a.rmp_zero;
+                        ra.fxp_P = a.rmp_P;
+                        ra.fx_cx = std::fma(-a.tmap.ox, a.tmap.inv_res, kFxpBase + P);
+                        ra.fx_cy = std::fma(-a.tmap.oy, a.tmap.inv_res, kFxpBase + P);
+                        ra.fxp_lo = Rn;
+                        ra.fxp_hx = (double)a.tmap.W + 2.0 * P - Rn;
+                        ra.fxp_hy = (double)a.tmap.H + 2.0 * P - Rn;
+                        f = fn_p[N - 2][v2];
+                    }
                 } else {
                     const void *fn_1[4] = {reinterpret_cast<const void *>(&k_rays_fx<false, false, false, 3>),
                                            reinterpret_cast<const void *>(&k_rays_fx<false, true, false, 3>),

@@ -134,7 +134,8 @@ def test_ray_kernel_dispatch_variants_identical(tracks, gpu, monkeypatch, A):
     order in one-wave blocks, the same with 4-car blocks (F110_RAY_WPB=4),
     3 chunked k_rays_fx -- the default, fixed-point cell index -- on the
     row-major EDT with 1, 2 and 3 rays per lane (F110_FX_ILP; k_rays_fxn for
-    2 and 3), on the 4x4-tiled EDT (F110_FX_TABLE=tiled), and with the
+    2 and 3, on the padded table or, F110_FX_PAD=0, the clamped one), on
+    the 4x4-tiled EDT (F110_FX_TABLE=tiled), and with the
     straggler hand-off to the refill tail kernel, F110_EVICT=1) give
     bit-identical steps: scans, obs, collisions,
     states, with noise, autoreset and a masked reset."""
@@ -145,15 +146,18 @@ def test_ray_kernel_dispatch_variants_identical(tracks, gpu, monkeypatch, A):
     acts = np.stack([rng.uniform(-0.4189, 0.4189, (30, E, A)), rng.uniform(0, 20, (30, E, A))], -1).astype(np.float32)
     mask = rng.random(E) < 0.5
     outs = []
-    for k, wpb, evict, ilp, table in (("0", "1", "0", "1", "rm"), ("1", "1", "0", "1", "rm"), ("2", "1", "0", "1", "rm"),
-                                      ("2", "4", "0", "1", "rm"), ("3", "1", "0", "1", "rm"), ("3", "1", "0", "2", "rm"),
-                                      ("3", "1", "0", "3", "rm"), ("3", "1", "0", "1", "tiled"),
-                                      ("3", "1", "1", "1", "rm")):
+    for k, wpb, evict, ilp, table, pad in (("0", "1", "0", "1", "rm", "1"), ("1", "1", "0", "1", "rm", "1"),
+                                           ("2", "1", "0", "1", "rm", "1"), ("2", "4", "0", "1", "rm", "1"),
+                                           ("3", "1", "0", "1", "rm", "1"), ("3", "1", "0", "2", "rm", "1"),
+                                           ("3", "1", "0", "2", "rm", "0"), ("3", "1", "0", "3", "rm", "1"),
+                                           ("3", "1", "0", "3", "rm", "0"), ("3", "1", "0", "1", "tiled", "1"),
+                                           ("3", "1", "1", "1", "rm", "1")):
         monkeypatch.setenv("F110_RAY_KERNEL", k)
         monkeypatch.setenv("F110_RAY_WPB", wpb)
         monkeypatch.setenv("F110_EVICT", evict)  # 3 + 1: k_rays_fx with the straggler hand-off to k_rays_fx_tail
         monkeypatch.setenv("F110_FX_ILP", ilp)
         monkeypatch.setenv("F110_FX_TABLE", table)
+        monkeypatch.setenv("F110_FX_PAD", pad)  # k_rays_fxn on the padded table (1) or the clamped one (0)
         sim = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=4,
                    keep_f64_scans=True)
         sim.reset(poses)

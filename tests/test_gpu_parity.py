@@ -296,8 +296,10 @@ def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A, nonexact
     nonexact_budget(f"ray_cast_adversarial_A{A}", nonexact)
 
 
-@pytest.mark.parametrize("kernel,ilp,table", [("2", "1", "rm"), ("3", "1", "rm"), ("3", "2", "rm"), ("3", "1", "tiled")])
-def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanners, monkeypatch, kernel, ilp, table):
+@pytest.mark.parametrize("kernel,ilp,table,pad", [("2", "1", "rm", "1"), ("3", "1", "rm", "1"), ("3", "2", "rm", "0"),
+                                                   ("3", "2", "rm", "1"), ("3", "3", "rm", "1"), ("3", "1", "tiled", "1")])
+def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanners, monkeypatch, kernel, ilp, table,
+                                                      pad):
     """k_rays_fx's fixed-point cell index (F110_RAY_KERNEL=3, the default;
     on the row-major EDT with 1 or 2 rays per lane, k_rays_fxn for 2, and on
     the 4x4-tiled EDT) against the oracle's IEEE xy_2_rc
@@ -307,11 +309,16 @@ def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanne
     path), origins just inside / outside the map edges looking out (clamped
     into the row-major padding), and origins far off the map (dt[-1, -1]
     steps; the cars whose rays could leave t's binade take fx_step).  Scans
-    must be bit-exact; every kernel must agree."""
+    must be bit-exact; every kernel must agree.  With 2 or 3 rays per lane
+    k_rays_fxn runs on the padded table (F110_FX_PAD=1, the default: 2^24
+    binade, u24 offsets, no clamp) or the clamped one (0); origins 1-20
+    cells outside the map edges straddle its per-car test (fast loop up to
+    6 cells out, the IEEE loop beyond)."""
     from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
     monkeypatch.setenv("F110_RAY_KERNEL", kernel)
     monkeypatch.setenv("F110_FX_ILP", ilp)
     monkeypatch.setenv("F110_FX_TABLE", table)
+    monkeypatch.setenv("F110_FX_PAD", pad)
     tm = tracks("Spielberg_map")
     ox, oy, _ = tm.origin
     res = tm.resolution
@@ -346,6 +353,12 @@ def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanne
             poses.append((ox + t * W * res, oy + H * res + eps, np.pi / 2))
     for i in range(16):  # far off the map
         poses.append((ox - 5.0 - 100.0 * i, oy + rng.uniform(-50, 150), rng.uniform(-np.pi, np.pi)))
+    for k in (1, 5, 6, 7, 8, 20):  # k cells outside each edge, looking in and along (the padded loop's per-car test)
+        t = rng.uniform(0.2, 0.8)
+        poses.append((ox - k * res + 1e-7, oy + t * H * res, rng.uniform(-1.0, 1.0)))
+        poses.append((ox + (W + k) * res - 1e-7, oy + t * H * res, np.pi + rng.uniform(-1.0, 1.0)))
+        poses.append((ox + t * W * res, oy - k * res + 1e-7, np.pi / 2 + rng.uniform(-1.0, 1.0)))
+        poses.append((ox + t * W * res, oy + (H + k) * res - 1e-7, -np.pi / 2 + rng.uniform(-1.0, 1.0)))
     for i in range(8):  # beyond 2^21 cells: t leaves its binade (the per-car check sends these to fx_step)
         far = (2.0e5, -2.0e5, 1.0e7, -3.0e8)[i % 4]
         poses.append((ox + far if i < 4 else ox + 10.0, oy + (far if i >= 4 else 10.0), rng.uniform(-np.pi, np.pi)))
