@@ -403,10 +403,12 @@ def main():
 
     # second, separate pass: per-kernel HIP-event timing on the one-context run (not part of `value`)
     KP = min(K, 300)
+    sim.reset_counters()
     sim.profile_begin(KP)
     for k in range(KP):
         sim.step(acts[W + (k % K)], minimal_outputs=True)
     per_kernel = sim.profile_end()
+    loop_lookups, lane_slots = sim.read_simt()  # SIMT efficiency of the ray loop over the same launches
 
     B = sim.B
     # k_rays (the dominant kernel): per ray 4 B per EDT lookup (exact uint32 k
@@ -429,6 +431,8 @@ def main():
         "mean_lookups_per_ray": mean_look,
         "step_kernels_ms": {"k_agents": per_kernel["k_agents_ms"], "k_rays": k_ms, "k_post": per_kernel["k_post_ms"]},
         "step_algorithmic_bytes_per_env": algorithmic_bytes_per_env_step(B, A, mean_look),
+        # lookups made in the loop / (loop trips x 64 lanes x rays per lane), from the kernel's own counters
+        "simt_efficiency": loop_lookups / lane_slots if lane_slots else None,
     }
     if pmc and traffic:
         roof["hbm_traffic_gbs"] = traffic / (k_ms * 1e-3) / 1e9
@@ -438,7 +442,7 @@ def main():
         roof["l2_hit_rate"] = pmc.get("l2_hit_rate")
         roof["traffic_source"] = pmc["file"]
     if busy:
-        for k in ("valu_busy", "waves_per_simd", "simt_efficiency"):
+        for k in ("valu_busy", "waves_per_simd"):
             if k in busy:
                 roof[k] = busy[k]
         roof["busy_source"] = busy["file"]

@@ -1028,6 +1028,24 @@ extern "C" int f110_read_counters(f110_ctx *ctx, uint64_t *lookups, uint64_t *ra
     return F110_OK;
 }
 
+extern "C" int f110_read_simt(f110_ctx *ctx, uint64_t *loop_lookups, uint64_t *lane_slots, void *stream) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_read_simt: null context");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    std::vector<unsigned long long> h((size_t)kCtrSlots * kCtrStride);
+    HIP_TRY(hipMemcpyAsync(h.data(), ctx->ctr, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           (hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    unsigned long long lk = 0, ry = 0, sl = 0;
+    for (int i = 0; i < kCtrSlots; ++i) {
+        lk += h[(size_t)i * kCtrStride];
+        ry += h[(size_t)i * kCtrStride + 1];
+        sl += h[(size_t)i * kCtrStride + 2];
+    }
+    if (loop_lookups) *loop_lookups = lk - ry;  // the first lookup of every ray is k_agents'
+    if (lane_slots) *lane_slots = sl;
+    return F110_OK;
+}
+
 extern "C" int f110_set_params(f110_ctx *ctx, const f110_params *params, int32_t agent_idx, void *stream) {
     if (!ctx || !params) return fail(F110_E_INVALID, "f110_set_params: null argument");
     if (agent_idx >= ctx->cfg.n_agents)  // Simulator.update_params raises IndexError (base_classes.py:544-546)

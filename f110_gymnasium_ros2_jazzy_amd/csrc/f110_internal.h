@@ -101,7 +101,7 @@ struct StepArgs {
     const double *reset_poses;  // [E][A][3]
     const uint8_t *reset_mask;  // [E] or null
     f110_outputs out;
-    unsigned long long *ctr;    // [kCtrSlots][16]: [0] lookups, [1] rays (see count_rays)
+    unsigned long long *ctr;    // [kCtrSlots][16]: [0] lookups, [1] rays (see count_rays), [2] lane slots of the fixed-point loops
 };
 
 // k_rays_tiled's own argument block: only what the ray loop and its epilogue

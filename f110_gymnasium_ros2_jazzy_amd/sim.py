@@ -246,6 +246,15 @@ class BatchSim:
                    "f110_read_counters")
         return lk.value, rays.value
 
+    def read_simt(self):
+        """(loop lookups, lane slots) of the fixed-point ray loops since the
+        last counter reset (f110_read_simt); their ratio is the loop's SIMT
+        efficiency, None when the ray kernel keeps no lane-slot count."""
+        lk, sl = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.check(self.L.f110_read_simt(self.ctx, ctypes.byref(lk), ctypes.byref(sl), self._stream()),
+                   "f110_read_simt")
+        return lk.value, sl.value
+
     def reset_counters(self):
         _lib.check(self.L.f110_reset_counters(self.ctx, self._stream()), "f110_reset_counters")
 

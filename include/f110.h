@@ -229,6 +229,13 @@ F110_API int f110_collision_multiple(const double *verts, int64_t M, int32_t N, 
  * `stream`).  Used for the measured mean lookups per ray (roofline). */
 F110_API int f110_read_counters(f110_ctx *ctx, uint64_t *lookups, uint64_t *rays, void *stream);
 F110_API int f110_reset_counters(f110_ctx *ctx, void *stream);
+/* SIMT efficiency of the fixed-point ray loops (k_rays_fx / k_rays_fxn, the
+ * default kernels) since the last counter reset: loop_lookups = lookups made
+ * inside the loop (all lookups less the first one per ray, which k_agents
+ * makes), lane_slots = the loop's trip counts x 64 lanes x rays per lane,
+ * summed over waves; efficiency = loop_lookups / lane_slots.  Other ray
+ * kernels leave lane_slots at 0.  Diagnostic (no reference counterpart). */
+F110_API int f110_read_simt(f110_ctx *ctx, uint64_t *loop_lookups, uint64_t *lane_slots, void *stream);
 
 /* ---- per-kernel timing ----------------------------------------------------
  * Records HIP events around each of the three launches of the next

@@ -292,3 +292,27 @@ def test_rays_per_lane_identical_across_beam_counts(tracks, gpu, monkeypatch, be
         for t, (a, b) in enumerate(zip(outs[0], rec)):
             for x, y in zip(a, b):
                 assert torch.equal(x, y), f"step {t}"
+
+
+@pytest.mark.parametrize("ilp", ["1", "2"])
+def test_simt_counters(tracks, gpu, monkeypatch, ilp):
+    """f110_read_simt: the fixed-point loops count the lane slots they issue
+    (trip count x 64 x rays per lane); loop lookups = all lookups less the
+    first lookup of each ray (k_agents'), and never exceed the slots."""
+    monkeypatch.setenv("F110_FX_ILP", ilp)
+    E, A = 512, 1
+    sp = _spawns(A)
+    rng = np.random.default_rng(3)
+    sim = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=2)
+    assert sim.ray_kernel == 3 and sim.ray_lanes == int(ilp)
+    sim.reset(sp[rng.integers(0, sp.shape[0], E)])
+    sim.reset_counters()
+    for t in range(5):
+        sim.step(np.stack([rng.uniform(-0.4, 0.4, (E, A)), rng.uniform(0, 20, (E, A))], -1).astype(np.float32))
+    lookups, rays = sim.read_counters()
+    loop, slots = sim.read_simt()
+    assert rays == 5 * E * A * sim.B
+    assert loop == lookups - rays
+    assert 0 < loop <= slots
+    assert 0.2 < loop / slots <= 1.0
+    sim.close()
