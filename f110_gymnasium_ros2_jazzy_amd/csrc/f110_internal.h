@@ -63,6 +63,7 @@ struct StepArgs {
     int32_t rmp_w, rmp_P;
     uint32_t rmp_zero;
     int32_t fx_pad;     // F110_FX_PAD: k_rays_fxn on the padded table
+    int32_t count_slots;  // F110_SIMT (default 1): lane-slot counter of the fixed-point loops
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2..4: k_rays_fxn)
     int32_t fx_tiled;   // F110_FX_TABLE=tiled (A/B): k_rays_fx on the 4x4-tiled EDT
     int32_t fx_nolean;  // F110_FX_LEAN=0 (A/B): the ballot-per-iteration loop of round 2
@@ -154,6 +155,7 @@ struct RayArgs {
     // inside the padded table (see fxp_offset)
     double fxp_lo, fxp_hx, fxp_hy;
     int32_t fxp_P;
+    int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_read_simt; F110_SIMT)
     // straggler hand-off of k_rays_fx (EVICT) -> k_rays_fx_tail: SoA records
     // ev[7][ev_cap] = x, y, d, tot, cos, sin, noise; ev_gb[2][ev_cap] = car, beam.
     // The queue is split in ev_P partitions of ev_capp records (partition p =

@@ -775,7 +775,7 @@ __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
             }
         }
         lane_iters = wave_sum(cnt);
-        iters = wave_max(cnt);  // the wave's trip count (heavy-first cost, SIMT counter)
+        if (a.wcost || a.count_slots) iters = wave_max(cnt);  // the wave's trip count (heavy-first cost, SIMT counter)
     }
     for (; !LEAN;) {
         const bool act = (dhi(d) != 0u) & (tot <= L.mr);
@@ -820,7 +820,7 @@ __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
             unsigned long long *slot = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
             atomicAdd(slot, (unsigned long long)(lanes + lane_iters));
             atomicAdd(slot + 1, (unsigned long long)lanes);
-            atomicAdd(slot + 2, (unsigned long long)iters * 64ull);  // lane slots the loop issued (SIMT)
+            if (K.count_slots) atomicAdd(slot + 2, (unsigned long long)iters * 64ull);  // lane slots the loop issued (SIMT)
         }
         if (K.wcost) {  // this wave's cost, the next step's heavy-first prediction
             const uint32_t mx = lanes ? 1u + iters : 0u;
@@ -1086,9 +1086,10 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
         if (lanes) {  // one (lookups, rays) atomic pair per wave; the first lookup came from k_agents
             unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
             atomicAdd(cs, (unsigned long long)(lanes + lane_iters));
+            atomicAdd(cs + 1, (unsigned long long)lanes);
             // lane slots the loop issued: trip count x 64 lanes x N rays (the serial
             // IEEE loop of an off-map car counts its longest lane's total, a lower bound)
-            atomicAdd(cs + 2, (unsigned long long)iters * (fast_car ? 64ull * N : 64ull));
+            if (K.count_slots) atomicAdd(cs + 2, (unsigned long long)iters * (fast_car ? 64ull * N : 64ull));
         }
         if (K.wcost) {  // this group's cost, the next step's heavy-first prediction
             const uint32_t mx = lanes ? 1u + iters : 0u;
@@ -1656,6 +1657,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         ra.noise_ext = a.noise_ext;
         ra.noise_step = a.noise_step;
         ra.ctr = a.ctr;
+        ra.count_slots = a.count_slots;
         ra.eps = a.eps;
         ra.max_range = a.max_range;
         ra.noise_std = a.noise_std;

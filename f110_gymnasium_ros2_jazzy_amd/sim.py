@@ -246,6 +246,10 @@ class BatchSim:
                    "f110_read_counters")
         return lk.value, rays.value
 
+    def set_simt(self, on: bool = True):
+        """Count the fixed-point ray loops' lane slots (f110_set_simt; off by default)."""
+        _lib.check(self.L.f110_set_simt(self.ctx, int(bool(on))), "f110_set_simt")
+
     def read_simt(self):
         """(loop lookups, lane slots) of the fixed-point ray loops since the
         last counter reset (f110_read_simt); their ratio is the loop's SIMT

@@ -234,7 +234,11 @@ F110_API int f110_reset_counters(f110_ctx *ctx, void *stream);
  * inside the loop (all lookups less the first one per ray, which k_agents
  * makes), lane_slots = the loop's trip counts x 64 lanes x rays per lane,
  * summed over waves; efficiency = loop_lookups / lane_slots.  Other ray
- * kernels leave lane_slots at 0.  Diagnostic (no reference counterpart). */
+ * kernels, and launches made while the count is off, leave lane_slots as
+ * they are.  f110_set_simt(ctx, 1) turns the count on (off by default: its
+ * extra atomic per wave costs ~2 % of k_rays).  Diagnostics (no reference
+ * counterpart). */
+F110_API int f110_set_simt(f110_ctx *ctx, int32_t on);
 F110_API int f110_read_simt(f110_ctx *ctx, uint64_t *loop_lookups, uint64_t *lane_slots, void *stream);
 
 /* ---- per-kernel timing ----------------------------------------------------

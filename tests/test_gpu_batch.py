@@ -296,7 +296,7 @@ def test_rays_per_lane_identical_across_beam_counts(tracks, gpu, monkeypatch, be
 
 @pytest.mark.parametrize("ilp", ["1", "2"])
 def test_simt_counters(tracks, gpu, monkeypatch, ilp):
-    """f110_read_simt: the fixed-point loops count the lane slots they issue
+    """f110_set_simt / f110_read_simt: the fixed-point loops count the lane slots they issue
     (trip count x 64 x rays per lane); loop lookups = all lookups less the
     first lookup of each ray (k_agents'), and never exceed the slots."""
     monkeypatch.setenv("F110_FX_ILP", ilp)
@@ -306,6 +306,7 @@ def test_simt_counters(tracks, gpu, monkeypatch, ilp):
     sim = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=2)
     assert sim.ray_kernel == 3 and sim.ray_lanes == int(ilp)
     sim.reset(sp[rng.integers(0, sp.shape[0], E)])
+    sim.set_simt(True)
     sim.reset_counters()
     for t in range(5):
         sim.step(np.stack([rng.uniform(-0.4, 0.4, (E, A)), rng.uniform(0, 20, (E, A))], -1).astype(np.float32))
@@ -315,4 +316,7 @@ def test_simt_counters(tracks, gpu, monkeypatch, ilp):
     assert loop == lookups - rays
     assert 0 < loop <= slots
     assert 0.2 < loop / slots <= 1.0
+    sim.set_simt(False)
+    sim.step(np.zeros((E, A, 2), np.float32))
+    assert sim.read_simt()[1] == slots  # off: no lane slots added
     sim.close()

@@ -310,8 +310,8 @@ def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanne
     into the row-major padding), and origins far off the map (dt[-1, -1]
     steps; the cars whose rays could leave t's binade take fx_step).  Scans
     must be bit-exact; every kernel must agree.  With 2 or 3 rays per lane
-    k_rays_fxn runs on the padded table (F110_FX_PAD=1, the default: 2^24
-    binade, u24 offsets, no clamp) or the clamped one (0); origins 1-20
+    k_rays_fxn runs on the padded table (F110_FX_PAD=1, opt-in: 2^24
+    binade, u24 offsets, no clamp) or the clamped one (0, the default); origins 1-20
     cells outside the map edges straddle its per-car test (fast loop up to
     6 cells out, the IEEE loop beyond)."""
     from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
