@@ -245,14 +245,17 @@ def scan_check(O, scanner, runner, act, threads):
     poses = np.concatenate(poses)
     ref = scanner.scan(poses, threads=threads)
     diff = g - ref
-    names = {0: "k_rays", 1: "k_rays_tiled (flat)", 2: "k_rays_tiled (chunked)", 3: "k_rays_fx"}
-    kern = names.get(sims[0].ray_kernel, str(sims[0].ray_kernel))
-    if sims[0].ray_kernel == 3 and sims[0].ray_lanes > 1:
-        kern = f"k_rays_fxn ({sims[0].ray_lanes} rays per lane)"
-    return {"kernel": f"{kern} (the timed runner, one extra step)", "cars": int(poses.shape[0]),
+    return {"kernel": f"{ray_kernel_name(sims[0])} (the timed runner, one extra step)", "cars": int(poses.shape[0]),
             "cars_skipped_ttc": skipped, "rays": int(diff.size),
             "l2": float(np.sqrt(np.sum(diff * diff))), "max_abs": float(np.max(np.abs(diff))),
             "bit_exact_fraction": float(np.mean(diff == 0.0))}
+
+
+def ray_kernel_name(sm):
+    names = {0: "k_rays", 1: "k_rays_tiled (flat)", 2: "k_rays_tiled (chunked)", 3: "k_rays_fx"}
+    if sm.ray_kernel == 3 and sm.ray_lanes > 1:
+        return f"k_rays_fxn ({sm.ray_lanes} rays per lane)"
+    return names.get(sm.ray_kernel, str(sm.ray_kernel))
 
 
 def scan_check_multi(O, scanner, runner, act, threads, S=256):
@@ -287,7 +290,7 @@ def scan_check_multi(O, scanner, runner, act, threads, S=256):
     for m in sims:
         m.set_scan_noise(None)
     diff = (g - rs)[keep]
-    return {"kernel": "k_rays_fx + k_post_multi (the timed runner, one extra step), oracle in lock-step",
+    return {"kernel": f"{ray_kernel_name(sm)} + k_post_multi (the timed runner, one extra step), oracle in lock-step",
             "envs": int(keep.sum()), "agents": A, "rays": int(diff.size),
             "l2": float(np.sqrt(np.sum(diff * diff))), "max_abs": float(np.max(np.abs(diff))) if diff.size else 0.0,
             "bit_exact_fraction": float(np.mean(diff == 0.0)) if diff.size else 1.0,
