@@ -1098,6 +1098,152 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
     }
 }
 
+// k_rays_fxr (F110_FX_REFILL): one wave per car, whose 64-beam chunks are
+// traced two at a time with refill.  k_rays_fxn pairs adjacent chunks, and
+// a pair costs the longer chunk's trip count while the other slot idles; here
+// a slot whose chunk has ended writes that chunk's outputs and takes the
+// car's next chunk at once, so both slots keep gathers in flight until the
+// car's last chunk.  Offline model over oracle trip counts
+// (scripts/pair_model.py): 146.7k wave-iterations for adjacent pairs vs
+// 109.1k (116.5k with one iteration of re-arm per chunk).  Same per-ray
+// arithmetic as k_rays_fxn, so bit-identical.  No heavy-first (one wave per
+// car), no masked reset; cars whose rays could leave t's binade trace their
+// chunks one after the other with fx_step.
+__device__ __forceinline__ double beam_theta(const BeamRun *R, int n, int b0, int bc) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (ld_const(&R[mid].start) <= b0) lo = mid;
+        else hi = mid - 1;
+    }
+    int rs = ld_const(&R[lo].start);
+    double t0 = ld_const(&R[lo].t0), dl = ld_const(&R[lo].delta);
+    for (int j = lo + 1; j < n; ++j) {
+        const int s2 = ld_const(&R[j].start);
+        if (s2 > b0 + 63) break;
+        if (bc >= s2) {
+            rs = s2;
+            t0 = ld_const(&R[j].t0);
+            dl = ld_const(&R[j].delta);
+        }
+    }
+    return t0 + (double)(bc - rs) * dl;  // get_scan's theta_index (laser_models.py:167-184)
+}
+
+template <bool HANDOFF>
+__global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
+    // a.G4 waves per car: wave j takes the car's chunks nch-1-j, nch-1-j-G4, ... (car-minor
+    // block order: car g's waves run on XCD g % 8 when EA % 8 == 0)
+    const int wj = (int)blockIdx.x / a.EA;
+    const int g = (int)blockIdx.x - wj * a.EA;
+    const int lane = (int)threadIdx.x;
+    const int B = a.B;
+    const int e = HANDOFF ? g / a.A : g;
+    const int nch = (B + 63) >> 6;
+    const int wstride = a.G4;
+    const BeamRun *R = a.runs + (size_t)g * kMaxSeg;
+    const int n = ld_const(a.nruns + g);
+    const double x00 = ld_const(a.ray0 + g), y00 = ld_const(a.ray0 + a.EA + g);
+    const double d00 = ld_const(a.ray0 + 2 * a.EA + g);  // :129
+    const RayArgs &K = *kernarg_rays();
+    const FxLoop L = fx_loop<3>(a);
+    const uint32_t zero = a.fx_zero;
+
+    // slot r traces chunk kk[r] (-1: empty); lane l owns beam kk[r] * 64 + l
+    double x[2], y[2], d[2], tot[2], c[2], sn[2];
+    int kk[2];
+    int next = nch - 1 - wj;  // this wave's chunks, taken in descending order
+    auto arm = [&](int r) {
+        const int k = next;
+        next -= wstride;
+        kk[r] = k;
+        const int b = k * 64 + lane, bc = b < B ? b : B - 1;
+        int ti = (int)beam_theta(R, n, k * 64, bc);  // int(theta_index), :124
+        if (ti >= a.theta_dis) ti = 0;
+        c[r] = a.cosines[ti];
+        sn[r] = a.sines[ti];
+        x[r] = x00;
+        y[r] = y00;
+        d[r] = b < B ? d00 : 0.0;
+        tot[r] = d[r];  // :130
+    };
+    uint32_t lanes = 0;
+    auto finish = [&](int r) {  // the ended chunk's outputs (fx_epilogue, noise after the clamp)
+        const int b = kk[r] * 64 + lane, bc = b < B ? b : B - 1;
+        double nz = 0.0;
+        if (K.noise_ext) {
+            nz = K.noise_ext[(size_t)e * B + bc];
+        } else if (K.noise_std > 0.0) {
+            const uint32_t key = noise_key(K.seed, (uint64_t)(K.env_offset + e));
+            nz = K.noise_std * (double)beam_normal_k(key, ld_const(K.noise_step + e), bc);
+        }
+        if (b < B)
+            fx_epilogue<HANDOFF>(K, g, e, b, tot[r], L.mr, nz, ld_const(a.vel + g), a.beam_cos[bc], a.side[bc]);
+        lanes += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(b < B));
+    };
+
+    uint32_t lane_iters = 0, iters = 0;
+    const double qx = fma(x00, L.ir, L.cxk) - kFxMagic, qy = fma(y00, L.ir, L.cyk) - kFxMagic;
+    const bool fast_car = fabs(qx) < a.fx_lim && fabs(qy) < a.fx_lim;  // wave-uniform (false for NaN)
+    if (fast_car) {
+        kk[0] = kk[1] = -1;
+        d[0] = d[1] = tot[0] = tot[1] = x[0] = x[1] = y[0] = y[1] = c[0] = c[1] = sn[0] = sn[1] = 0.0;
+        if (next >= 0) arm(0);
+        if (next >= 0) arm(1);
+        __builtin_amdgcn_s_waitcnt(0);
+        for (;;) {
+            uint64_t m[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+            // the running slots' gathers go out first, so that they are in flight while
+            // an ended slot writes its chunk and re-arms (scalar run search, table loads)
+            double dn[2] = {0.0, 0.0};
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                if (m[r]) {
+                    const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+                    dn[r] = fx_load<3>(a.m.dt, fxn_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero));
+                }
+            const bool any = (m[0] | m[1]) != 0;
+            iters += any ? 1u : 0u;
+            lane_iters += (uint32_t)(__popcll(m[0]) + __popcll(m[1]));
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                if (kk[r] >= 0 && !m[r]) {  // wave-uniform: the chunk has ended; refill the slot
+                    finish(r);
+                    if (next >= 0) arm(r);
+                    else kk[r] = -1;
+                }
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                if (m[r]) {
+                    d[r] = dn[r];
+                    tot[r] += d[r];  // :141
+                }
+            if (!any && kk[0] < 0 && kk[1] < 0) break;
+        }
+    } else {
+        uint32_t cnt = 0;
+        while (next >= 0) {
+            arm(0);
+            while ((dhi(d[0]) != 0u) & (tot[0] <= L.mr)) {
+                fx_step<3>(a.m, L, x[0], y[0], d[0], tot[0], c[0], sn[0]);
+                ++cnt;
+            }
+            finish(0);
+        }
+        lane_iters = wave_sum(cnt);
+        iters = wave_max(cnt);
+    }
+    if (lane == 0) {
+        unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+        atomicAdd(cs, (unsigned long long)(lanes + lane_iters));  // the first lookup came from k_agents
+        atomicAdd(cs + 1, (unsigned long long)lanes);
+        if (K.count_slots) atomicAdd(cs + 2, (unsigned long long)iters * (fast_car ? 128ull : 64ull));
+    }
+}
+
 // k_rays_fx_tail: the handed-off rays, traced to the end with lane refill.
 // Persistent waves take records from the queue (one atomic per refill);
 // whenever >= kTailRefill lanes are idle, the finished lanes write their
@@ -1781,7 +1927,13 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                     ra.nch = (ra.nch + N - 1) / N;  // chunk groups per car (heavy list / wcost units)
                     g2 = dim3((unsigned)(ra.HB + ra.G4 * ra.nch));
                     f = fn_n[N - 2][v2];
-                    if (a.fx_pad && a.rmp) {
+                    if (a.fx_refill && N == 2 && !mask && ra.HB == 0 && !ra.wcost) {
+                        // one wave per car, two chunk slots with refill (k_rays_fxr; no heavy-first)
+                        f = single ? reinterpret_cast<const void *>(&k_rays_fxr<false>)
+                                   : reinterpret_cast<const void *>(&k_rays_fxr<true>);
+                        ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
+                        g2 = dim3((unsigned)(ra.EA * ra.G4));
+                    } else if (a.fx_pad && a.rmp) {
                         // the padded table (PAD): t = x / res + 2^24 + P; a car's rays stay in
                         // the table when its origin's q + P lies in [Rn, W or H + 2P - Rn),
                         // Rn = max_range / res + 2 cells (each lookup is within max_range of it)

@@ -320,3 +320,41 @@ def test_simt_counters(tracks, gpu, monkeypatch, ilp):
     sim.step(np.zeros((E, A, 2), np.float32))
     assert sim.read_simt()[1] == slots  # off: no lane slots added
     sim.close()
+
+
+@pytest.mark.parametrize("A,beams", [(1, 1080), (2, 1080), (1, 333), (1, 64)])
+def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
+    """k_rays_fxr (F110_FX_REFILL=1: one wave per car, two chunk slots, a
+    slot refilled with the car's next chunk as soon as its chunk ends)
+    against k_rays_fxn's adjacent pairs: scans, obs, collisions and states
+    bit-identical over 25 noisy steps with autoreset and a masked reset
+    (which runs k_rays_fxn), for 17, 6 and 1 chunks per car; its counters
+    (lookups, rays) equal k_rays_fxn's."""
+    E = 200
+    sp = _spawns(A)
+    rng = np.random.default_rng(beams + A)
+    poses = sp[rng.integers(0, sp.shape[0], E)]
+    acts = np.stack([rng.uniform(-0.4189, 0.4189, (25, E, A)), rng.uniform(0, 20, (25, E, A))], -1).astype(np.float32)
+    mask = rng.random(E) < 0.5
+    monkeypatch.setenv("F110_FX_ILP", "2")
+    monkeypatch.setenv("F110_HEAVY_T", "0")  # k_rays_fxr has no heavy-first dispatch
+    outs, ctrs = [], []
+    for refill in ("0", "1", "3"):  # off; one wave per car; three waves per car
+        monkeypatch.setenv("F110_FX_REFILL", refill)
+        sim = _sim(tracks, gpu, n_envs=E, n_agents=A, num_beams=beams, noise_std=0.01, autoreset=True,
+                   spawn_poses=sp, seed=6, keep_f64_scans=True)
+        sim.reset(poses)
+        sim.reset_counters()
+        rec = []
+        for t in range(25):
+            o = sim.reset(poses[::-1].copy(), env_mask=mask) if t == 12 else sim.step(acts[t])
+            rec.append((o.scans_f64.clone(), o.obs.clone(), o.collisions.clone(), sim.agent_states().clone()))
+        torch.cuda.synchronize()
+        outs.append(rec)
+        ctrs.append(sim.read_counters())
+        sim.close()
+    for k in (1, 2):
+        assert ctrs[0] == ctrs[k]
+        for t, (a, b) in enumerate(zip(outs[0], outs[k])):
+            for x, y in zip(a, b):
+                assert torch.equal(x, y), f"step {t}"
