@@ -253,6 +253,8 @@ def scan_check(O, scanner, runner, act, threads):
 
 def ray_kernel_name(sm):
     names = {0: "k_rays", 1: "k_rays_tiled (flat)", 2: "k_rays_tiled (chunked)", 3: "k_rays_fx"}
+    if sm.ray_kernel == 3 and sm.ray_refill > 0:
+        return f"k_rays_fxr ({sm.ray_refill} wave(s) per car, 2 chunk slots with refill)"
     if sm.ray_kernel == 3 and sm.ray_lanes > 1:
         return f"k_rays_fxn ({sm.ray_lanes} rays per lane)"
     return names.get(sm.ray_kernel, str(sm.ray_kernel))
@@ -433,8 +435,7 @@ def main():
         "kernel": "k_rays", "bound": ("latency of the dependent EDT gather chain (HBM is not the limit: see "
                                       "hbm_traffic_frac; capping occupancy at 6/4/2 waves per SIMD costs "
                                       "1.31x/1.62x/2.9x, DESIGN.md 3.2)"),
-        "ray_kernel": ("k_rays_fxn, %d rays per lane" % sim.ray_lanes) if sim.ray_kernel == 3 and sim.ray_lanes > 1
-        else "k_rays_fx" if sim.ray_kernel == 3 else "ray kernel %d" % sim.ray_kernel,
+        "ray_kernel": ray_kernel_name(sim),
         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
         "traffic": traffic, "kernel_ms": k_ms, "algorithmic_bytes_per_launch": rays_bytes_launch,
         "mean_lookups_per_ray": mean_look,

@@ -106,7 +106,7 @@ struct f110_ctx {
     int32_t rmp_w = 0, rmp_P = 0;
     uint32_t rmp_zero = 0;
     bool fx_pad = false;    // F110_FX_PAD (default on): k_rays_fxn on the padded table
-    int32_t fx_refill = 0;   // F110_FX_REFILL = waves per car of k_rays_fxr (A/B; 0 = off)
+    int32_t fx_refill = 0;   // waves per car of k_rays_fxr (0 = k_rays_fxn; F110_FX_REFILL overrides)
     bool count_slots = false;  // f110_set_simt / F110_SIMT: lane-slot counter of the fixed-point loops (f110_read_simt)
     int fx_ilp = 1;         // rays per lane (F110_FX_ILP; default by car count)
     bool fx_tiled = false;  // F110_FX_TABLE=tiled: A/B of the 4x4-tiled EDT
@@ -704,6 +704,10 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (const char *v = std::getenv("F110_FX_PAD"))
         c->fx_pad = c->ray_kernel == 3 && !c->fx_tiled && !c->evict && std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_SIMT")) c->count_slots = std::atoi(v) != 0;
+    // k_rays_fxr (one wave per car, two chunk slots with refill) where the grid is deep:
+    // 65536 envs as 2 x 32768 67.1 vs 63.0 M env-steps/s; at 16384 cars its long waves
+    // leave a tail (0.324 vs 0.289 ms); it runs only without heavy-first and masks
+    c->fx_refill = EA >= 32768 ? 1 : 0;
     if (const char *v = std::getenv("F110_FX_REFILL")) c->fx_refill = std::max(0, std::min(16, std::atoi(v)));
     const double pad_q = std::ceil(C.max_range / resolution) + 8.0;
     const int32_t fx_pad_cells = pad_q > 0.0 && pad_q < 65536.0 ? (int32_t)pad_q : 0;  // else no padded table
@@ -904,6 +908,13 @@ extern "C" int f110_ray_kernel(const f110_ctx *ctx) {
 extern "C" int f110_ray_lanes(const f110_ctx *ctx) {
     if (!ctx) return fail(F110_E_INVALID, "f110_ray_lanes: null context");
     return ctx->ray_kernel == 3 ? ctx->fx_ilp : 1;
+}
+
+extern "C" int f110_ray_refill(const f110_ctx *ctx) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_ray_refill: null context");
+    const bool fx = ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled && ctx->fx_ilp == 2;
+    const int waves = std::min<int>(ctx->fx_refill, (ctx->cfg.n_beams + 63) / 64);  // as the launch clamps it
+    return fx && waves > 0 && (ctx->heavy_off || !ctx->wcost) ? waves : 0;
 }
 
 extern "C" int f110_disable_heavy_first(f110_ctx *ctx) {

@@ -1109,13 +1109,8 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
 // arithmetic as k_rays_fxn, so bit-identical.  No heavy-first (one wave per
 // car), no masked reset; cars whose rays could leave t's binade trace their
 // chunks one after the other with fx_step.
-__device__ __forceinline__ double beam_theta(const BeamRun *R, int n, int b0, int bc) {
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (ld_const(&R[mid].start) <= b0) lo = mid;
-        else hi = mid - 1;
-    }
+__device__ __forceinline__ double beam_theta(const BeamRun *R, int n, int lo, int b0, int bc) {
+    // lo: the run holding beam b0 (found once per car for all its chunks, see k_rays_fxr)
     int rs = ld_const(&R[lo].start);
     double t0 = ld_const(&R[lo].t0), dl = ld_const(&R[lo].delta);
     for (int j = lo + 1; j < n; ++j) {
@@ -1153,12 +1148,25 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
     double x[2], y[2], d[2], tot[2], c[2], sn[2];
     int kk[2];
     int next = nch - 1 - wj;  // this wave's chunks, taken in descending order
+    // lane k < nch: the run holding beam 64 k (one divergent search per car instead of
+    // a dependent chain of scalar loads at every re-arm)
+    int vlo = 0;
+    if (lane < nch) {
+        int lo = 0, hi = n - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (R[mid].start <= lane * 64) lo = mid;
+            else hi = mid - 1;
+        }
+        vlo = lo;
+    }
     auto arm = [&](int r) {
         const int k = next;
         next -= wstride;
         kk[r] = k;
         const int b = k * 64 + lane, bc = b < B ? b : B - 1;
-        int ti = (int)beam_theta(R, n, k * 64, bc);  // int(theta_index), :124
+        const int lo = __builtin_amdgcn_readlane(vlo, k);
+        int ti = (int)beam_theta(R, n, lo, k * 64, bc);  // int(theta_index), :124
         if (ti >= a.theta_dis) ti = 0;
         c[r] = a.cosines[ti];
         sn[r] = a.sines[ti];

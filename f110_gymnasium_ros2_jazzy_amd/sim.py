@@ -291,6 +291,12 @@ class BatchSim:
         """Rays per lane of the fixed-point ray kernel (f110_ray_lanes: 1 = k_rays_fx, 2 = k_rays_fxn)."""
         return _lib.check(self.L.f110_ray_lanes(self.ctx), "f110_ray_lanes")
 
+    @property
+    def ray_refill(self) -> int:
+        """k_rays_fxr's waves per car for unmasked steps (f110_ray_refill), 0 when k_rays_fxn /
+        k_rays_fx trace this context's rays."""
+        return _lib.check(self.L.f110_ray_refill(self.ctx), "f110_ray_refill")
+
     def close(self):
         if getattr(self, "ctx", None):
             torch.cuda.synchronize(self.device)

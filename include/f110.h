@@ -288,6 +288,11 @@ F110_API int f110_ray_kernel(const f110_ctx *ctx);
  * k_rays_fxn; F110_FX_ILP overrides the size-based default); 1 for the
  * other ray kernels.  Diagnostic, no reference counterpart. */
 F110_API int f110_ray_lanes(const f110_ctx *ctx);
+/* k_rays_fxr's waves per car for unmasked steps (one wave per car traces the
+ * car's 64-beam chunks two at a time, refilling a slot as soon as its chunk
+ * ends), or 0 when the context steps with k_rays_fxn / k_rays_fx (heavy-first
+ * on, one ray per lane, or F110_FX_REFILL=0).  Default: 1 from 32768 cars. */
+F110_API int f110_ray_refill(const f110_ctx *ctx);
 
 /* Sets the rays per lane of the fixed-point ray kernel (1..4) before the
  * context's first reset/step.  The size-based default looks at this

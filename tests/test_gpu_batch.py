@@ -343,6 +343,7 @@ def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
         monkeypatch.setenv("F110_FX_REFILL", refill)
         sim = _sim(tracks, gpu, n_envs=E, n_agents=A, num_beams=beams, noise_std=0.01, autoreset=True,
                    spawn_poses=sp, seed=6, keep_f64_scans=True)
+        assert sim.ray_refill == min(int(refill), (beams + 63) // 64)
         sim.reset(poses)
         sim.reset_counters()
         rec = []
