@@ -105,7 +105,7 @@ struct f110_ctx {
     const double *rmp = nullptr;  // k_rays_fxn's padded table (shared, see MapTables)
     int32_t rmp_w = 0, rmp_P = 0;
     uint32_t rmp_zero = 0;
-    bool fx_pad = false;    // F110_FX_PAD (default on): k_rays_fxn on the padded table
+    bool fx_pad = false;    // k_rays_fxn / k_rays_fxr on the padded table (default from 32768 cars; F110_FX_PAD)
     int32_t fx_refill = 0;   // waves per car of k_rays_fxr (0 = k_rays_fxn; F110_FX_REFILL overrides)
     bool count_slots = false;  // f110_set_simt / F110_SIMT: lane-slot counter of the fixed-point loops (f110_read_simt)
     int fx_ilp = 1;         // rays per lane (F110_FX_ILP; default by car count)
@@ -699,10 +699,12 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
                       hipMemcpyHostToDevice);
     if (const char *v = std::getenv("F110_FX_LEAN")) c->fx_nolean = std::atoi(v) == 0;
     // PAD: k_rays_fxn's clamp-free loop on a table padded by the max range (+ 8 cells of margin)
-    // (opt-in: 46 -> 36 VALU per two-ray iteration measured 1.029 vs 1.026 ms at 65536 envs)
-    c->fx_pad = false;
-    if (const char *v = std::getenv("F110_FX_PAD"))
-        c->fx_pad = c->ray_kernel == 3 && !c->fx_tiled && !c->evict && std::atoi(v) != 0;
+    // on where k_rays_fxr runs (from 32768 cars): there the loop is issue-bound (VALU busy 88 %) and
+    // the clamp-free offsets (46 -> 36 VALU per two-ray iteration) measured 0.999 -> 0.956 ms at 65536;
+    // k_rays_fxn, latency-bound, did not gain from them (1.029 vs 1.026 ms), DESIGN §3.3
+    const bool fx_ok = c->ray_kernel == 3 && !c->fx_tiled && !c->evict;
+    c->fx_pad = fx_ok && EA >= 32768;
+    if (const char *v = std::getenv("F110_FX_PAD")) c->fx_pad = fx_ok && std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_SIMT")) c->count_slots = std::atoi(v) != 0;
     // k_rays_fxr (one wave per car, two chunk slots with refill) where the grid is deep:
     // 65536 envs as 2 x 32768 67.1 vs 63.0 M env-steps/s; at 16384 cars its long waves

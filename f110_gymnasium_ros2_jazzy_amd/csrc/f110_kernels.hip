@@ -1125,7 +1125,7 @@ __device__ __forceinline__ double beam_theta(const BeamRun *R, int n, int lo, in
     return t0 + (double)(bc - rs) * dl;  // get_scan's theta_index (laser_models.py:167-184)
 }
 
-template <bool HANDOFF>
+template <bool HANDOFF, bool PAD = false>
 __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
     // a.G4 waves per car: wave j takes the car's chunks nch-1-j, nch-1-j-G4, ... (car-minor
     // block order: car g's waves run on XCD g % 8 when EA % 8 == 0)
@@ -1191,8 +1191,17 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
     };
 
     uint32_t lane_iters = 0, iters = 0;
-    const double qx = fma(x00, L.ir, L.cxk) - kFxMagic, qy = fma(y00, L.ir, L.cyk) - kFxMagic;
-    const bool fast_car = fabs(qx) < a.fx_lim && fabs(qy) < a.fx_lim;  // wave-uniform (false for NaN)
+    bool fast_car;  // wave-uniform (false for NaN)
+    if (PAD) {  // q + P of the scan origin inside [fxp_lo, fxp_h*): its rays stay in the padded table
+        const double ux = fma(x00, L.ir, L.cxk) - kFxpBase, uy = fma(y00, L.ir, L.cyk) - kFxpBase;
+        fast_car = (ux >= a.fxp_lo) & (ux < a.fxp_hx) & (uy >= a.fxp_lo) & (uy < a.fxp_hy);
+    } else {
+        const double qx = fma(x00, L.ir, L.cxk) - kFxMagic, qy = fma(y00, L.ir, L.cyk) - kFxMagic;
+        fast_car = fabs(qx) < a.fx_lim && fabs(qy) < a.fx_lim;
+    }
+    const uint32_t P = (uint32_t)a.fxp_P;
+    uint32_t zero_v = zero;  // PAD: in a VGPR for the whole trace (the select's other operand is its SGPR mask)
+    if (PAD) asm volatile("v_mov_b32 %0, %1" : "=v"(zero_v) : "s"(zero));
     if (fast_car) {
         kk[0] = kk[1] = -1;
         d[0] = d[1] = tot[0] = tot[1] = x[0] = x[1] = y[0] = y[1] = c[0] = c[1] = sn[0] = sn[1] = 0.0;
@@ -1211,7 +1220,9 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
             for (int r = 0; r < 2; ++r)
                 if (m[r]) {
                     const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
-                    dn[r] = fx_load<3>(a.m.dt, fxn_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero));
+                    const uint32_t off = PAD ? fxp_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero_v, P)
+                                             : fxn_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero);
+                    dn[r] = fx_load<3>(a.m.dt, off);
                 }
             const bool any = (m[0] | m[1]) != 0;
             iters += any ? 1u : 0u;
@@ -1236,7 +1247,14 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
         while (next >= 0) {
             arm(0);
             while ((dhi(d[0]) != 0u) & (tot[0] <= L.mr)) {
-                fx_step<3>(a.m, L, x[0], y[0], d[0], tot[0], c[0], sn[0]);
+                if (PAD) {  // an origin off the map: the IEEE cell of every lookup
+                    x[0] += d[0] * c[0];  // :135
+                    y[0] += d[0] * sn[0];  // :136
+                    d[0] = fx_load<3>(a.m.dt, exact_offset_pad(a.m, x[0], y[0], P));
+                    tot[0] += d[0];  // :141
+                } else {
+                    fx_step<3>(a.m, L, x[0], y[0], d[0], tot[0], c[0], sn[0]);
+                }
                 ++cnt;
             }
             finish(0);
@@ -1935,13 +1953,8 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                     ra.nch = (ra.nch + N - 1) / N;  // chunk groups per car (heavy list / wcost units)
                     g2 = dim3((unsigned)(ra.HB + ra.G4 * ra.nch));
                     f = fn_n[N - 2][v2];
-                    if (a.fx_refill && N == 2 && !mask && ra.HB == 0 && !ra.wcost) {
-                        // one wave per car, two chunk slots with refill (k_rays_fxr; no heavy-first)
-                        f = single ? reinterpret_cast<const void *>(&k_rays_fxr<false>)
-                                   : reinterpret_cast<const void *>(&k_rays_fxr<true>);
-                        ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
-                        g2 = dim3((unsigned)(ra.EA * ra.G4));
-                    } else if (a.fx_pad && a.rmp) {
+                    const bool pad = a.fx_pad && a.rmp;
+                    if (pad) {
                         // the padded table (PAD): t = x / res + 2^24 + P; a car's rays stay in
                         // the table when its origin's q + P lies in [Rn, W or H + 2P - Rn),
                         // Rn = max_range / res + 2 cells (each lookup is within max_range of it)
@@ -1957,6 +1970,16 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                         ra.fxp_hx = (double)a.tmap.W + 2.0 * P - Rn;
                         ra.fxp_hy = (double)a.tmap.H + 2.0 * P - Rn;
                         f = fn_p[N - 2][v2];
+                    }
+                    if (a.fx_refill && N == 2 && !mask && ra.HB == 0 && !ra.wcost) {
+                        // one wave per car, two chunk slots with refill (k_rays_fxr; no heavy-first)
+                        const void *fr[4] = {reinterpret_cast<const void *>(&k_rays_fxr<false, false>),
+                                             reinterpret_cast<const void *>(&k_rays_fxr<true, false>),
+                                             reinterpret_cast<const void *>(&k_rays_fxr<false, true>),
+                                             reinterpret_cast<const void *>(&k_rays_fxr<true, true>)};
+                        f = fr[(pad ? 2 : 0) + (single ? 0 : 1)];
+                        ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
+                        g2 = dim3((unsigned)(ra.EA * ra.G4));
                     }
                 } else {
                     const void *fn_1[4] = {reinterpret_cast<const void *>(&k_rays_fx<false, false, false, 3>),
