@@ -1176,14 +1176,32 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
         tot[r] = d[r];  // :130
     };
     uint32_t lanes = 0;
+    // device noise: chunks 2p and 2p + 1 (beams b and b + 64 of a 128-beam block) share one
+    // Philox draw (beam_normal_pair_k); the half a finished chunk does not use is kept for its
+    // partner in a two-entry cache indexed by p & 1 (the open pairs are p and p - 1: the
+    // slots take the car's chunks in descending order), so most pairs are drawn once
+    float cval[2] = {0.0f, 0.0f};
+    int ctag[2] = {-1, -1};
     auto finish = [&](int r) {  // the ended chunk's outputs (fx_epilogue, noise after the clamp)
         const int b = kk[r] * 64 + lane, bc = b < B ? b : B - 1;
         double nz = 0.0;
         if (K.noise_ext) {
             nz = K.noise_ext[(size_t)e * B + bc];
         } else if (K.noise_std > 0.0) {
-            const uint32_t key = noise_key(K.seed, (uint64_t)(K.env_offset + e));
-            nz = K.noise_std * (double)beam_normal_k(key, ld_const(K.noise_step + e), bc);
+            const int pp = kk[r] >> 1, ci = pp & 1;
+            float nv;
+            if (ctag[ci] == pp) {
+                nv = cval[ci];
+                ctag[ci] = -1;
+            } else {  // the pair index of the unclamped beam: its other half is the partner beam's
+                const uint32_t key = noise_key(K.seed, (uint64_t)(K.env_offset + e));
+                float lo, hi;
+                beam_normal_pair_k(key, ld_const(K.noise_step + e), beam_noise_pair(b), lo, hi);
+                nv = (kk[r] & 1) ? hi : lo;
+                cval[ci] = (kk[r] & 1) ? lo : hi;
+                ctag[ci] = pp;
+            }
+            nz = K.noise_std * (double)nv;
         }
         if (b < B)
             fx_epilogue<HANDOFF>(K, g, e, b, tot[r], L.mr, nz, ld_const(a.vel + g), a.beam_cos[bc], a.side[bc]);
