@@ -1233,7 +1233,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
                 m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
             // the running slots' gathers go out first, so that they are in flight while
             // an ended slot writes its chunk and re-arms (scalar run search, table loads)
-            double dn[2] = {0.0, 0.0};
+            double dn[2];  // read only where m[r] (no per-iteration zeroing)
 #pragma unroll
             for (int r = 0; r < 2; ++r)
                 if (m[r]) {
