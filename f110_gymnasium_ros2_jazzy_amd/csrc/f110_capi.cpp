@@ -430,6 +430,29 @@ static hipError_t upload(T **p, const std::vector<T> &h) {
     return e;
 }
 
+// k_rays_fxn / k_rays_fxr's padded table (PAD, see kFxpBase): cell (r, c) at
+// row r + P, column c + P; every other cell holds dt[-1,-1] (the reference's
+// off-map read), and a 0.0 after the last row is the zero cell.  Built only
+// where its byte offsets stay 32-bit and a row stride stays a 24-bit
+// multiplier (else t->rmp stays null and the clamped table is used).
+static hipError_t build_padded_table(MapTables *t, int32_t pad, const std::vector<double> &d) {
+    const int32_t H = t->H, W = t->W;
+    const size_t N = (size_t)H * W;
+    const size_t P = (size_t)pad, Wp = ((size_t)W + 2 * P + 15) / 16 * 16, Hp = (size_t)H + 2 * P;
+    if ((Wp * Hp + 16) * 8 >= (1ull << 32) || Wp * 8 >= (1u << 24)) return hipSuccess;
+    std::vector<double> rmp(Wp * Hp + 16, d[N - 1]);
+    for (int r = 0; r < H; ++r)
+        for (int q = 0; q < W; ++q) rmp[((size_t)r + P) * Wp + q + P] = d[(size_t)r * W + q];
+    rmp[Wp * Hp] = 0.0;
+    const hipError_t e = upload(&t->rmp, rmp);
+    if (e == hipSuccess) {
+        t->rmp_w = (int32_t)Wp;
+        t->rmp_P = (int32_t)P;
+        t->rmp_zero = (uint32_t)(Wp * Hp * 8);
+    }
+    return e;
+}
+
 // The tables of (device, map), built and uploaded on first use; `want_rm`
 // adds the row-major table if the entry lacks it, `pad` > 0 the table padded
 // by `pad` cells on every side (an entry keeps the padding it was built with:
@@ -494,25 +517,7 @@ static hipError_t acquire_map_tables(int device, const uint32_t *edt_k, int32_t 
         t->rm_oob = (uint32_t)(((size_t)(H - 1) * Wp + (W - 1)) * 8);
         t->rm_zero = (uint32_t)(Wp * Hp * 8);
     }
-    if (e == hipSuccess && pad > 0 && !t->rmp) {
-        // k_rays_fxn's padded table (PAD, see kFxpBase): cell (r, c) at row
-        // r + P, column c + P; every other cell holds dt[-1,-1] (the
-        // reference's off-map read), and a 0.0 after the last row is the zero
-        // cell.  Built only where its byte offsets stay 32-bit and a row
-        // stride stays a 24-bit multiplier.
-        const size_t P = (size_t)pad, Wp = ((size_t)W + 2 * P + 15) / 16 * 16, Hp = (size_t)H + 2 * P;
-        if ((Wp * Hp + 16) * 8 < (1ull << 32) && Wp * 8 < (1u << 24)) {
-            const std::vector<double> &d = dt_host();
-            std::vector<double> rmp(Wp * Hp + 16, d[N - 1]);
-            for (int r = 0; r < H; ++r)
-                for (int q = 0; q < W; ++q) rmp[((size_t)r + P) * Wp + q + P] = d[(size_t)r * W + q];
-            rmp[Wp * Hp] = 0.0;
-            e = upload(&t->rmp, rmp);
-            t->rmp_w = (int32_t)Wp;
-            t->rmp_P = (int32_t)P;
-            t->rmp_zero = (uint32_t)(Wp * Hp * 8);
-        }
-    }
+    if (e == hipSuccess && pad > 0 && !t->rmp) e = build_padded_table(t, pad, dt_host());
     if (e != hipSuccess) {
         if (fresh) free_map_tables(t);
         return e;
@@ -917,6 +922,37 @@ extern "C" int f110_ray_refill(const f110_ctx *ctx) {
     const bool fx = ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled && ctx->fx_ilp == 2;
     const int waves = std::min<int>(ctx->fx_refill, (ctx->cfg.n_beams + 63) / 64);  // as the launch clamps it
     return fx && waves > 0 && (ctx->heavy_off || !ctx->wcost) ? waves : 0;
+}
+
+extern "C" int f110_set_ray_refill(f110_ctx *ctx, int32_t waves) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_refill: null context");
+    if (waves < 0 || waves > 16) return fail(F110_E_INVALID, "f110_set_ray_refill: waves must be in 0..16");
+    const bool fx = ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled;
+    if (!fx && waves != 0) return fail(F110_E_INVALID, "f110_set_ray_refill: this context's ray kernel has no refill");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    ctx->fx_refill = waves;
+    if (waves > 0 && !ctx->rmp && ctx->maps) {  // the padded table goes with k_rays_fxr
+        const double pad_q = std::ceil(ctx->cfg.max_range / ctx->res) + 8.0;
+        if (pad_q > 0.0 && pad_q < 65536.0) {
+            std::lock_guard<std::mutex> g(g_maps_mu);
+            MapTables *t = ctx->maps;
+            if (!t->rmp) {
+                std::vector<double> d((size_t)t->H * t->W);
+                double res;
+                std::memcpy(&res, &t->res_bits, 8);
+                for (size_t i = 0; i < d.size(); ++i) d[i] = res * std::sqrt((double)t->k[i]);
+                HIP_TRY(build_padded_table(t, (int32_t)pad_q, d));
+            }
+        }
+        if (ctx->maps->rmp) {
+            ctx->fx_pad = true;
+            ctx->rmp = ctx->maps->rmp;
+            ctx->rmp_w = ctx->maps->rmp_w;
+            ctx->rmp_P = ctx->maps->rmp_P;
+            ctx->rmp_zero = ctx->maps->rmp_zero;
+        }
+    }
+    return F110_OK;
 }
 
 extern "C" int f110_disable_heavy_first(f110_ctx *ctx) {

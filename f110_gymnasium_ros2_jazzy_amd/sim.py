@@ -291,6 +291,10 @@ class BatchSim:
         """Rays per lane of the fixed-point ray kernel (f110_ray_lanes: 1 = k_rays_fx, 2 = k_rays_fxn)."""
         return _lib.check(self.L.f110_ray_lanes(self.ctx), "f110_ray_lanes")
 
+    def set_ray_refill(self, waves: int):
+        """k_rays_fxr's waves per car (0: k_rays_fxn), with the padded EDT (f110_set_ray_refill)."""
+        _lib.check(self.L.f110_set_ray_refill(self.ctx, int(waves)), "f110_set_ray_refill")
+
     @property
     def ray_refill(self) -> int:
         """k_rays_fxr's waves per car for unmasked steps (f110_ray_refill), 0 when k_rays_fxn /

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import collections
 import ctypes
+import os
 
 import torch
 
@@ -64,7 +65,7 @@ class StreamShards:
     for all of them (do that before reading `obs`)."""
 
     def __init__(self, track, n_envs: int, n_streams: int = 2, env_offset: int = 0, heavy_first: bool = False,
-                 ray_lanes: int | None = None, **kw):
+                 ray_lanes: int | None = None, refill: int | None = None, **kw):
         if n_streams < 1 or n_envs % n_streams:
             raise ValueError(f"n_envs ({n_envs}) must split evenly into n_streams ({n_streams})")
         self.S = n_streams
@@ -90,6 +91,12 @@ class StreamShards:
             # env-steps/s, 8192 as 4 x 2048 53.1 vs 47.6 M (profiles/r02_share_map/)
             ray_lanes = 2 if n_envs * self.n_agents >= 12288 else 1
         self.ray_lanes = ray_lanes
+        if refill is None:
+            # k_rays_fxr (one wave per car, refilled chunk slots, padded EDT) from 32768 cars on the
+            # GPU, as f110_create's rule for one context: 32768 envs as 2 x 16384 69.2 vs 62.6 M
+            # env-steps/s, 16384 as 2 x 8192 58.7 vs 61.5 M (profiles/r02_refill_sizes/)
+            refill = 1 if n_envs * self.n_agents >= 32768 and ray_lanes == 2 and not heavy_first else 0
+        self.refill = refill
         for s in range(self.S):
             with torch.cuda.stream(self.streams[s]):
                 sm = BatchSim(track, n_envs=self.Es, env_offset=env_offset + s * self.Es, device=self.device, **kw)
@@ -99,6 +106,8 @@ class StreamShards:
                     _lib.check(sm.L.f110_disable_heavy_first(sm.ctx), "f110_disable_heavy_first")
                 if sm.ray_kernel == 3:  # the fixed-point kernel (the others trace one ray per lane)
                     _lib.check(sm.L.f110_set_ray_lanes(sm.ctx, int(ray_lanes)), "f110_set_ray_lanes")
+                    if os.environ.get("F110_FX_REFILL") is None:  # the env knob still wins (A/B runs)
+                        _lib.check(sm.L.f110_set_ray_refill(sm.ctx, int(refill)), "f110_set_ray_refill")
                 self.sims.append(sm)
         self._sl = [slice(s * self.Es, (s + 1) * self.Es) for s in range(self.S)]
         self._handles = [ctypes.c_void_p(st.cuda_stream) for st in self.streams]

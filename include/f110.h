@@ -293,6 +293,11 @@ F110_API int f110_ray_lanes(const f110_ctx *ctx);
  * ends), or 0 when the context steps with k_rays_fxn / k_rays_fx (heavy-first
  * on, one ray per lane, or F110_FX_REFILL=0).  Default: 1 from 32768 cars. */
 F110_API int f110_ray_refill(const f110_ctx *ctx);
+/* Set k_rays_fxr's waves per car (0: k_rays_fxn) and, when on, switch the
+ * context to the padded EDT (built on first use).  For callers that split one
+ * GPU's cars over several contexts (streams.StreamShards): the size rule is
+ * about the cars the GPU traces at once, not one context's.  Any time. */
+F110_API int f110_set_ray_refill(f110_ctx *ctx, int32_t waves);
 
 /* Sets the rays per lane of the fixed-point ray kernel (1..4) before the
  * context's first reset/step.  The size-based default looks at this

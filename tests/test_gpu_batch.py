@@ -177,13 +177,14 @@ def test_ray_kernel_dispatch_variants_identical(tracks, gpu, monkeypatch, A):
                 assert torch.equal(x, y), f"step {t}"
 
 
-@pytest.mark.parametrize("lanes", [1, 2])
-def test_stream_shards_match_single_context(tracks, gpu, lanes):
+@pytest.mark.parametrize("lanes,refill", [(1, 0), (2, 0), (2, 1)])
+def test_stream_shards_match_single_context(tracks, gpu, lanes, refill):
     """streams.StreamShards (bench.py's default timed runner): 4 sub-shards on
     4 dedicated-queue streams, never joined between steps, end bit-identical
     to one context stepping all envs (noise and autoreset on; the actions are
     resident before the loop, as in the bench), with the sub-shards' map
-    tables shared and 1 or 2 rays per lane (f110_set_ray_lanes)."""
+    tables shared and 1 or 2 rays per lane (f110_set_ray_lanes), and with
+    k_rays_fxr switched on per sub-shard (f110_set_ray_refill)."""
     from f110_gymnasium_ros2_jazzy_amd import _lib
     from f110_gymnasium_ros2_jazzy_amd.streams import StreamShards
     E, A, T = 256, 1, 60
@@ -193,9 +194,10 @@ def test_stream_shards_match_single_context(tracks, gpu, lanes):
     acts = torch.tensor(np.stack([rng.uniform(-0.4189, 0.4189, (T, E, A)), rng.uniform(0, 20, (T, E, A))], -1),
                         dtype=torch.float32, device=gpu)
     full = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=9)
-    sh = StreamShards(tracks("Spielberg_map"), n_envs=E, n_streams=4, ray_lanes=lanes,
+    sh = StreamShards(tracks("Spielberg_map"), n_envs=E, n_streams=4, ray_lanes=lanes, refill=refill,
                       n_agents=A, device=gpu, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=9)
     assert all(sm.ray_lanes == lanes for sm in sh.sims)
+    assert all(sm.ray_refill == refill for sm in sh.sims)  # f110_set_ray_refill (k_rays_fxr + padded EDT)
     full.reset(poses)
     sh.reset(poses)
     with pytest.raises(RuntimeError, match="before the first"):
