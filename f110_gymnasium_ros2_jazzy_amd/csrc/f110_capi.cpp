@@ -106,6 +106,7 @@ struct f110_ctx {
     int32_t rmp_w = 0, rmp_P = 0;
     uint32_t rmp_zero = 0;
     bool fx_pad = false;    // k_rays_fxn / k_rays_fxr on the padded table (default from 32768 cars; F110_FX_PAD)
+    int32_t fx_slots = 2;    // F110_FX_SLOTS (A/B): chunk slots per k_rays_fxr wave
     int32_t fx_refill = 0;   // waves per car of k_rays_fxr (0 = k_rays_fxn; F110_FX_REFILL overrides)
     bool count_slots = false;  // f110_set_simt / F110_SIMT: lane-slot counter of the fixed-point loops (f110_read_simt)
     int fx_ilp = 1;         // rays per lane (F110_FX_ILP; default by car count)
@@ -716,6 +717,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     // leave a tail (0.324 vs 0.289 ms); it runs only without heavy-first and masks
     c->fx_refill = EA >= 32768 ? 1 : 0;
     if (const char *v = std::getenv("F110_FX_REFILL")) c->fx_refill = std::max(0, std::min(16, std::atoi(v)));
+    if (const char *v = std::getenv("F110_FX_SLOTS")) c->fx_slots = std::atoi(v) == 3 ? 3 : 2;
     const double pad_q = std::ceil(C.max_range / resolution) + 8.0;
     const int32_t fx_pad_cells = pad_q > 0.0 && pad_q < 65536.0 ? (int32_t)pad_q : 0;  // else no padded table
     if (const char *v = std::getenv("F110_FX_LDS")) c->fx_lds = (uint32_t)std::max(0, std::min(65536, std::atoi(v)));
@@ -850,6 +852,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.fx_pad = c->rmp ? 1 : 0;
     a.count_slots = c->count_slots ? 1 : 0;
     a.fx_refill = c->fx_refill;
+    a.fx_slots = c->fx_slots;
     a.fx_tiled = c->fx_tiled ? 1 : 0;
     a.fx_lds = c->fx_lds;
     a.fx_nolean = c->fx_nolean ? 1 : 0;

@@ -63,6 +63,7 @@ struct StepArgs {
     int32_t rmp_w, rmp_P;
     uint32_t rmp_zero;
     int32_t fx_pad;     // F110_FX_PAD: k_rays_fxn on the padded table
+    int32_t fx_slots;   // F110_FX_SLOTS (A/B): chunk slots per k_rays_fxr wave, 2 or 3
     int32_t fx_refill;  // F110_FX_REFILL: waves per car of k_rays_fxr (two chunk slots with refill; 0 = off)
     int32_t count_slots;  // F110_SIMT (default 1): lane-slot counter of the fixed-point loops
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2..4: k_rays_fxn)

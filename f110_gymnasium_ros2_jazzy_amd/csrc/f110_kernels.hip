@@ -1125,7 +1125,7 @@ __device__ __forceinline__ double beam_theta(const BeamRun *R, int n, int lo, in
     return t0 + (double)(bc - rs) * dl;  // get_scan's theta_index (laser_models.py:167-184)
 }
 
-template <bool HANDOFF, bool PAD = false>
+template <bool HANDOFF, bool PAD = false, int NS = 2>
 __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
     // a.G4 waves per car: wave j takes the car's chunks nch-1-j, nch-1-j-G4, ... (car-minor
     // block order: car g's waves run on XCD g % 8 when EA % 8 == 0)
@@ -1145,8 +1145,8 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
     const uint32_t zero = a.fx_zero;
 
     // slot r traces chunk kk[r] (-1: empty); lane l owns beam kk[r] * 64 + l
-    double x[2], y[2], d[2], tot[2], c[2], sn[2];
-    int kk[2];
+    double x[NS], y[NS], d[NS], tot[NS], c[NS], sn[NS];
+    int kk[NS];
     int next = nch - 1 - wj;  // this wave's chunks, taken in descending order
     // lane k < nch: the run holding beam 64 k (one divergent search per car instead of
     // a dependent chain of scalar loads at every re-arm)
@@ -1221,44 +1221,55 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
     uint32_t zero_v = zero;  // PAD: in a VGPR for the whole trace (the select's other operand is its SGPR mask)
     if (PAD) asm volatile("v_mov_b32 %0, %1" : "=v"(zero_v) : "s"(zero));
     if (fast_car) {
-        kk[0] = kk[1] = -1;
-        d[0] = d[1] = tot[0] = tot[1] = x[0] = x[1] = y[0] = y[1] = c[0] = c[1] = sn[0] = sn[1] = 0.0;
-        if (next >= 0) arm(0);
-        if (next >= 0) arm(1);
+#pragma unroll
+        for (int r = 0; r < NS; ++r) {
+            kk[r] = -1;
+            d[r] = tot[r] = x[r] = y[r] = c[r] = sn[r] = 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < NS; ++r)
+            if (next >= 0) arm(r);
         __builtin_amdgcn_s_waitcnt(0);
         for (;;) {
-            uint64_t m[2];
+            uint64_t m[NS], mall = 0;
 #pragma unroll
-            for (int r = 0; r < 2; ++r)
+            for (int r = 0; r < NS; ++r)
                 m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
             // the running slots' gathers go out first, so that they are in flight while
             // an ended slot writes its chunk and re-arms (scalar run search, table loads)
-            double dn[2];  // read only where m[r] (no per-iteration zeroing)
+            double dn[NS];  // read only where m[r] (no per-iteration zeroing)
 #pragma unroll
-            for (int r = 0; r < 2; ++r)
+            for (int r = 0; r < NS; ++r)
                 if (m[r]) {
                     const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
                     const uint32_t off = PAD ? fxp_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero_v, P)
                                              : fxn_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero);
                     dn[r] = fx_load<3>(a.m.dt, off);
                 }
-            const bool any = (m[0] | m[1]) != 0;
-            iters += any ? 1u : 0u;
-            lane_iters += (uint32_t)(__popcll(m[0]) + __popcll(m[1]));
 #pragma unroll
-            for (int r = 0; r < 2; ++r)
+            for (int r = 0; r < NS; ++r) {
+                mall |= m[r];
+                lane_iters += (uint32_t)__popcll(m[r]);
+            }
+            const bool any = mall != 0;
+            iters += any ? 1u : 0u;
+            bool open = false;
+#pragma unroll
+            for (int r = 0; r < NS; ++r)
                 if (kk[r] >= 0 && !m[r]) {  // wave-uniform: the chunk has ended; refill the slot
                     finish(r);
                     if (next >= 0) arm(r);
                     else kk[r] = -1;
                 }
 #pragma unroll
-            for (int r = 0; r < 2; ++r)
+            for (int r = 0; r < NS; ++r) {
                 if (m[r]) {
                     d[r] = dn[r];
                     tot[r] += d[r];  // :141
                 }
-            if (!any && kk[0] < 0 && kk[1] < 0) break;
+                open |= kk[r] >= 0;
+            }
+            if (!any && !open) break;
         }
     } else {
         uint32_t cnt = 0;
@@ -1284,7 +1295,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
         unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
         atomicAdd(cs, (unsigned long long)(lanes + lane_iters));  // the first lookup came from k_agents
         atomicAdd(cs + 1, (unsigned long long)lanes);
-        if (K.count_slots) atomicAdd(cs + 2, (unsigned long long)iters * (fast_car ? 128ull : 64ull));
+        if (K.count_slots) atomicAdd(cs + 2, (unsigned long long)iters * (fast_car ? 64ull * NS : 64ull));
     }
 }
 
@@ -1991,11 +2002,15 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                     }
                     if (a.fx_refill && N == 2 && !mask && ra.HB == 0 && !ra.wcost) {
                         // one wave per car, two chunk slots with refill (k_rays_fxr; no heavy-first)
-                        const void *fr[4] = {reinterpret_cast<const void *>(&k_rays_fxr<false, false>),
-                                             reinterpret_cast<const void *>(&k_rays_fxr<true, false>),
-                                             reinterpret_cast<const void *>(&k_rays_fxr<false, true>),
-                                             reinterpret_cast<const void *>(&k_rays_fxr<true, true>)};
-                        f = fr[(pad ? 2 : 0) + (single ? 0 : 1)];
+                        const void *fr[8] = {reinterpret_cast<const void *>(&k_rays_fxr<false, false, 2>),
+                                             reinterpret_cast<const void *>(&k_rays_fxr<true, false, 2>),
+                                             reinterpret_cast<const void *>(&k_rays_fxr<false, true, 2>),
+                                             reinterpret_cast<const void *>(&k_rays_fxr<true, true, 2>),
+                                             reinterpret_cast<const void *>(&k_rays_fxr<false, false, 3>),
+                                             reinterpret_cast<const void *>(&k_rays_fxr<true, false, 3>),
+                                             reinterpret_cast<const void *>(&k_rays_fxr<false, true, 3>),
+                                             reinterpret_cast<const void *>(&k_rays_fxr<true, true, 3>)};
+                        f = fr[(a.fx_slots == 3 ? 4 : 0) + (pad ? 2 : 0) + (single ? 0 : 1)];
                         ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
                         g2 = dim3((unsigned)(ra.EA * ra.G4));
                     }
