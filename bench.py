@@ -432,9 +432,11 @@ def main():
     busy = load_profile("pmc_busy", E, A)
     traffic = pmc.get("bytes_per_launch") if pmc else None
     roof = {
-        "kernel": "k_rays", "bound": ("latency of the dependent EDT gather chain (HBM is not the limit: see "
-                                      "hbm_traffic_frac; capping occupancy at 6/4/2 waves per SIMD costs "
-                                      "1.31x/1.62x/2.9x, DESIGN.md 3.2)"),
+        "kernel": "k_rays",
+        "bound": ("VALU issue of the sphere-trace loop (valu_busy; HBM is not the limit: see hbm_traffic_frac and "
+                  "l2_hit_rate; DESIGN.md 3.4)" if sim.ray_kernel == 3 and sim.ray_refill > 0 else
+                  "latency of the dependent EDT gather chain (HBM is not the limit: see hbm_traffic_frac; capping "
+                  "occupancy at 6/4/2 waves per SIMD costs 1.31x/1.62x/2.9x, DESIGN.md 3.2)"),
         "ray_kernel": ray_kernel_name(sim),
         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
         "traffic": traffic, "kernel_ms": k_ms, "algorithmic_bytes_per_launch": rays_bytes_launch,
