@@ -184,8 +184,10 @@ def auto_streams(envs, agents=1):
     48.4 at S = 2 / 4; 32768 61.8 / 46.2; 65536 62.4 / 52.7.  Small shards
     leave CUs idle in k_agents / k_post and the grid tail, which more
     concurrent sub-shards fill; large ones fill the GPU themselves.  Counted
-    in cars (envs x agents): C4's 8192 two-agent envs run S = 2."""
-    return 4 if envs * agents <= 8192 else 2
+    in cars (envs x agents).  Round 2, end (k_rays_fxn / k_rays_fxr): 16384 envs
+    61.3 / 63.1 M at S = 2 / 4 (fxn), 65.3 M at S = 4 with k_rays_fxr
+    (profiles/r02_refill_small/): S = 4 up to 16384 cars."""
+    return 4 if envs * agents <= 16384 else 2
 
 
 def cpu_baseline(O, scanner, poses, acts_np, args):

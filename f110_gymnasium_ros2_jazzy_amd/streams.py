@@ -95,7 +95,10 @@ class StreamShards:
             # k_rays_fxr (one wave per car, refilled chunk slots, padded EDT) from 32768 cars on the
             # GPU, as f110_create's rule for one context: 32768 envs as 2 x 16384 69.2 vs 62.6 M
             # env-steps/s, 16384 as 2 x 8192 58.7 vs 61.5 M (profiles/r02_refill_sizes/)
-            refill = 1 if n_envs * self.n_agents >= 32768 and ray_lanes == 2 and not heavy_first else 0
+            # (with 4 sub-shards from 16384 cars: 65.3 vs 63.1 M; with 2 it lost there, 58.3 vs 61.3 M)
+            cars = n_envs * self.n_agents
+            refill = 1 if ((cars >= 32768 or (cars >= 16384 and n_streams >= 4)) and ray_lanes == 2
+                           and not heavy_first) else 0
         self.refill = refill
         for s in range(self.S):
             with torch.cuda.stream(self.streams[s]):
