@@ -32,6 +32,16 @@ sys.path.insert(0, REPO)
 
 METRIC = "env-steps/sec at 65536 parallel envs, 1080-beam lidar; scan L2 vs CPU ref"
 GLOBAL_ENVS = 65536
+DIGEST_ENVS = 64  # trajectory_digest: obs rows of global envs 0, G/64, 2G/64, ...
+
+
+def metric_name(global_envs: int, agents: int) -> str:
+    """BASELINE.json's metric for the run's own workload (the headline is
+    65536 single-agent envs; other --global-envs / --agents runs name theirs)."""
+    if global_envs == GLOBAL_ENVS and agents == 1:
+        return METRIC
+    who = "parallel envs" if agents == 1 else f"parallel {agents}-agent envs"
+    return f"env-steps/sec at {global_envs} {who}, 1080-beam lidar; scan L2 vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -166,9 +176,20 @@ def load_profile(kind: str, E: int, A: int):
     return None
 
 
+def affinity_cpus() -> int:
+    """CPUs this process may run on (os.cpu_count() counts the whole machine)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def cpu_threads() -> int:
-    t = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
-    return max(1, min(t, os.cpu_count() or t))
+    """OMP_NUM_THREADS when the host sets it (the GPU box sets 16: one GPU's
+    share of a 256-thread machine), else every CPU of the affinity set."""
+    n = affinity_cpus()
+    t = int(os.environ.get("OMP_NUM_THREADS") or 0) or n
+    return max(1, min(t, n))
 
 
 def oracle_module():
@@ -207,8 +228,13 @@ def cpu_baseline(O, scanner, poses, acts_np, args):
     for k in range(args.cpu_steps):
         sim.step(acts_np[(args.cpu_warmup + k) % T, :E], threads=threads)
     dt = time.perf_counter() - t0
+    omp = os.environ.get("OMP_NUM_THREADS")
     return {
-        "value": E * args.cpu_steps / dt, "unit": "env-steps/s", "cores": threads, "nproc": os.cpu_count(),
+        "value": E * args.cpu_steps / dt, "unit": "env-steps/s", "cores": threads,
+        "affinity_cpus": affinity_cpus(), "nproc": os.cpu_count(), "omp_num_threads": omp,
+        "cores_note": ("OMP_NUM_THREADS caps the threads: the GPU host sets it to its per-GPU CPU share "
+                       "(the machine's CPUs are shared by its GPUs' jobs)" if omp and int(omp) < affinity_cpus()
+                       else "every CPU of the process's affinity set"),
         "kind": "port",
         "sample": f"{E} envs x {args.cpu_steps} steps after {args.cpu_warmup} warm-up ({A} agent, {args.map}, RK4, "
                   f"noise {'off' if args.no_noise else 'on'}, the GPU run's spawn poses and actions), C oracle "
@@ -335,15 +361,19 @@ def main():
     gidx = rng.integers(0, spawn.shape[0], size=G)[shard.offset:shard.offset + E]
     poses0 = spawn[gidx]
 
-    def actions(n_steps, n_envs, offset):
+    def actions(n_steps, n_envs, offset, n_global):
+        """Uniform random actions keyed by GLOBAL env id: the job's [T, n_global]
+        draw (one seed, one shape on every rank), then this rank's columns, so
+        an env steps the same actions whatever the GPU count."""
         gen = torch.Generator(device=dev)
-        gen.manual_seed(offset)
-        a = torch.rand(n_steps, n_envs, A, 2, device=dev, generator=gen, dtype=torch.float32)
+        gen.manual_seed(args.seed)
+        a = torch.rand(n_steps, n_global, A, 2, device=dev, generator=gen, dtype=torch.float32)
+        a = a[:, offset:offset + n_envs].contiguous()
         a[..., 0] = a[..., 0] * (2 * 0.4189) - 0.4189   # steer in [-0.4189, 0.4189]
         a[..., 1] = a[..., 1] * 20.0                   # speed in [0, 20] (ddpg_config.yaml:19-20)
         return a
 
-    acts = actions(W + K + 1, E, shard.offset)
+    acts = actions(W + K + 1, E, shard.offset, G)
     stream = torch.cuda.current_stream(dev)
 
     def make(n_envs, offset, s):
@@ -387,8 +417,26 @@ def main():
         D.barrier()
         return D.max_over_ranks(t1 - t0), r.read_counters()
 
+    def digest(r):
+        """trajectory_digest: sha256 over the obs rows (f32 bytes) of global envs
+        0, G/64, 2G/64, ... after the timed steps, gathered in global-id order
+        (each row hashed by its owning rank): equal for N = 1 and N > 1 runs of
+        the same K / W / seed."""
+        import hashlib
+        stride = max(1, G // DIGEST_ENVS)
+        ids = list(range(0, G, stride))[:DIGEST_ENVS]
+        obs = r.obs if hasattr(r, "sims") else r.out.obs
+        h = torch.zeros(len(ids), dtype=torch.int64)
+        for j, gid in enumerate(ids):
+            if shard.offset <= gid < shard.offset + E:
+                row = obs[gid - shard.offset].cpu().numpy().tobytes()
+                h[j] = int.from_bytes(hashlib.sha256(row).digest()[:7], "little") + 1
+        h = D.sum_tensor_over_ranks(h)
+        return {"sha256": hashlib.sha256(h.numpy().tobytes()).hexdigest()[:32], "envs": len(ids), "stride": stride}
+
     runner = make(E, shard.offset, S)
     elapsed, (lookups, rays) = timed(runner, poses0, acts)
+    traj = digest(runner)
     mean_look = lookups / max(rays, 1)
     total_env_steps = D.sum_over_ranks(E * K)
     sim = runner if isinstance(runner, BatchSim) else make(E, shard.offset, 1)
@@ -401,15 +449,17 @@ def main():
     full_outputs = {"value": total_env_steps / el_full, "ms_per_step": el_full / K * 1e3,
                     "runner": "one context, every output (f32 + f64 scans, laps, sim_time, was_reset)"}
 
-    O = scanner = None
-    checks = None
-    if rank == 0:
-        O = oracle_module()
-        scanner = O.OracleScanner(track.free_mask, track.resolution, track.origin)
-        checks = scan_check(O, scanner, runner, acts[W + K], cpu_threads())
-
-    # second, separate pass: per-kernel HIP-event timing on the one-context run (not part of `value`)
-    KP = min(K, 300)
+    # second, separate pass: per-kernel HIP-event timing on the one-context run (not part of `value`).
+    # It runs right after the timed passes, behind its own clock ramp and before the CPU-side scan
+    # check (an idle GPU clocks down), over >= 100 steps whatever --steps is.
+    KP = max(100, min(K, 300))
+    t_end = time.perf_counter() + args.ramp_s
+    n = 0
+    while time.perf_counter() < t_end:
+        sim.step(acts[W + (n % K)], minimal_outputs=True)
+        n += 1
+        if n % 16 == 0:
+            torch.cuda.synchronize(dev)
     sim.profile_begin(KP)
     for k in range(KP):
         sim.step(acts[W + (k % K)], minimal_outputs=True)
@@ -423,6 +473,13 @@ def main():
     loop_lookups, lane_slots = sim.read_simt()
     sim.set_simt(False)
 
+    O = scanner = None
+    checks = None
+    if rank == 0:
+        O = oracle_module()
+        scanner = O.OracleScanner(track.free_mask, track.resolution, track.origin)
+        checks = scan_check(O, scanner, runner, acts[W + K], cpu_threads())
+
     B = sim.B
     # k_rays (the dominant kernel): per ray 4 B per EDT lookup (exact uint32 k
     # cell) + 4 B of f32 range out; the 120 B/agent of state I/O
@@ -435,6 +492,7 @@ def main():
     traffic = pmc.get("bytes_per_launch") if pmc else None
     roof = {
         "kernel": "k_rays",
+        "profiled_steps": per_kernel["steps"],
         "bound": ("VALU issue of the sphere-trace loop (valu_busy; HBM is not the limit: see hbm_traffic_frac and "
                   "l2_hit_rate; DESIGN.md 3.4)" if sim.ray_kernel == 3 and sim.ray_refill > 0 else
                   "latency of the dependent EDT gather chain (HBM is not the limit: see hbm_traffic_frac; capping "
@@ -448,6 +506,9 @@ def main():
         # lookups made in the loop / (loop trips x 64 lanes x rays per lane), from the kernel's own counters
         "simt_efficiency": loop_lookups / lane_slots if lane_slots else None,
     }
+    # consistency: the ray kernel runs inside the one-context step it is timed in
+    step_ms = (single or {"ms_per_step": elapsed / K * 1e3})["ms_per_step"]
+    roof["kernel_le_step"] = {"ok": bool(k_ms <= step_ms), "kernel_ms": k_ms, "one_context_step_ms": step_ms}
     if pmc and traffic:
         roof["hbm_traffic_gbs"] = traffic / (k_ms * 1e-3) / 1e9
         roof["hbm_traffic_frac"] = roof["hbm_traffic_gbs"] / HBM_PEAK_GBS
@@ -462,7 +523,7 @@ def main():
         roof["busy_source"] = busy["file"]
 
     result = {
-        "metric": METRIC,
+        "metric": metric_name(G, A),
         "value": total_env_steps / elapsed,
         "unit": "env-steps/s",
         "n_gpus": world,
@@ -486,6 +547,7 @@ def main():
                        "one BatchSim context") + "; minimal outputs (obs, collisions, terminated): no f32 "
                        "info['scans'] copy, lap_times/counts, sim_time, was_reset",
         },
+        "trajectory_digest": traj,
         "single_stream": single,
         "single_stream_full_outputs": full_outputs,
         "scan_l2_vs_cpu": checks["l2"] if checks and "l2" in checks else None,
@@ -499,13 +561,13 @@ def main():
                 continue
             S2 = args.streams if args.streams > 0 else auto_streams(n, A)
             r2 = make(n, 0, S2)
-            el2, _ = timed(r2, spawn[rng.integers(0, spawn.shape[0], size=n)], actions(W + K, n, 0))
+            el2, _ = timed(r2, spawn[rng.integers(0, spawn.shape[0], size=n)], actions(W + K, n, 0, n))
             line = {"envs": n, "value": n * K / el2, "ms_per_step": el2 / K * 1e3,
                     "streams": S2 if not isinstance(r2, BatchSim) else 1}
             if not isinstance(r2, BatchSim):
                 r2.close()
                 r1 = make(n, 0, 1)
-                el1, _ = timed(r1, spawn[rng.integers(0, spawn.shape[0], size=n)], actions(W + K, n, 0))
+                el1, _ = timed(r1, spawn[rng.integers(0, spawn.shape[0], size=n)], actions(W + K, n, 0, n))
                 line["single_stream"] = {"value": n * K / el1, "ms_per_step": el1 / K * 1e3}
                 r1.close()
             else:
@@ -515,7 +577,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             T = args.cpu_warmup + args.cpu_steps
-            a_cpu = acts if acts.shape[0] >= T else actions(T, E, shard.offset)
+            a_cpu = acts if acts.shape[0] >= T else actions(T, E, shard.offset, G)
             n = min(args.cpu_envs, E)
             result["cpu_baseline"] = cpu_baseline(O, scanner, poses0[:n], a_cpu[:T, :n].cpu().numpy(), args)
         except Exception as exc:  # report, never hide

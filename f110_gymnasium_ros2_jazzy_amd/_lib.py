@@ -183,7 +183,7 @@ def load(build_if_missing: bool = True):
             getattr(L, name).restype = ctypes.c_int
     L.f110_ddpg_scratch_floats.restype = i64
     L.f110_ddpg_relu_bwd_scratch_floats.restype = i64
-    if L.f110_abi_version() != 1:
+    if L.f110_abi_version() != 2:
         raise F110Error("libf110.so ABI version mismatch")
     _lib = L
     return L

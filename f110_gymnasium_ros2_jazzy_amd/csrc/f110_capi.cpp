@@ -424,11 +424,20 @@ static void release_map_tables(MapTables *t) {
     free_map_tables(t);
 }
 
+// Uploads into a local buffer and publishes it to *p only once the copy has
+// succeeded (a failed upload frees it and leaves *p untouched): a map entry
+// shared by other contexts never points at an uninitialised table.
 template <class T>
 static hipError_t upload(T **p, const std::vector<T> &h) {
-    hipError_t e = hipMalloc(reinterpret_cast<void **>(p), std::max<size_t>(h.size() * sizeof(T), 16));
-    if (e == hipSuccess) e = hipMemcpy(*p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
-    return e;
+    T *d = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&d), std::max<size_t>(h.size() * sizeof(T), 16));
+    if (e == hipSuccess) e = hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (d) (void)hipFree(d);
+        return e;
+    }
+    *p = d;
+    return hipSuccess;
 }
 
 // k_rays_fxn / k_rays_fxr's padded table (PAD, see kFxpBase): cell (r, c) at
@@ -514,9 +523,11 @@ static hipError_t acquire_map_tables(int device, const uint32_t *edt_k, int32_t 
             for (int q = 0; q < W; ++q) rm[(size_t)r * Wp + q] = d[(size_t)r * W + q];
         rm[Wp * Hp] = 0.0;
         e = upload(&t->rm, rm);
-        t->rm_w = (int32_t)Wp;
-        t->rm_oob = (uint32_t)(((size_t)(H - 1) * Wp + (W - 1)) * 8);
-        t->rm_zero = (uint32_t)(Wp * Hp * 8);
+        if (e == hipSuccess) {  // the metadata only with the table it describes
+            t->rm_w = (int32_t)Wp;
+            t->rm_oob = (uint32_t)(((size_t)(H - 1) * Wp + (W - 1)) * 8);
+            t->rm_zero = (uint32_t)(Wp * Hp * 8);
+        }
     }
     if (e == hipSuccess && pad > 0 && !t->rmp) e = build_padded_table(t, pad, dt_host());
     if (e != hipSuccess) {
@@ -934,7 +945,9 @@ extern "C" int f110_set_ray_refill(f110_ctx *ctx, int32_t waves) {
     if (!fx && waves != 0) return fail(F110_E_INVALID, "f110_set_ray_refill: this context's ray kernel has no refill");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     ctx->fx_refill = waves;
-    if (waves > 0 && !ctx->rmp && ctx->maps) {  // the padded table goes with k_rays_fxr
+    bool pad = true;  // F110_FX_PAD=0 keeps the clamped table (A/B runs), as at f110_create
+    if (const char *v = std::getenv("F110_FX_PAD")) pad = std::atoi(v) != 0;
+    if (waves > 0 && pad && !ctx->rmp && ctx->maps) {  // the padded table goes with k_rays_fxr
         const double pad_q = std::ceil(ctx->cfg.max_range / ctx->res) + 8.0;
         if (pad_q > 0.0 && pad_q < 65536.0) {
             std::lock_guard<std::mutex> g(g_maps_mu);

@@ -1457,7 +1457,10 @@ __device__ void env_epilogue(const StepArgs &a, int e, const double *stl, int st
     if (a.out.was_reset) a.out.was_reset[e] = (uint8_t)do_reset;
     if (a.out.sim_time) a.out.sim_time[e] = tnow;
     a.pending[e] = (a.autoreset && term) ? 1 : 0;
-    if (do_reset && a.mode == 0) a.episode[e] = v.episode + 1;
+    // autoreset spawn draws count episodes from the env's last explicit reset, so a
+    // reset replays the same trajectory whatever ran before it (the bench's
+    // trajectory digest compares N = 1 and N > 1 runs after a clock ramp)
+    if (do_reset) a.episode[e] = a.mode == 0 ? v.episode + 1 : 0u;
     a.nstep[e] = v.nstep + 1;
 }
 

@@ -52,19 +52,47 @@ TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning",
 
 
 def enable_tuned_gemms(device: torch.device) -> bool:
-    """Switch on TunableOp with the shipped results (no tuning, no file writes).
+    """Load the shipped TunableOp results once (no tuning, no file writes).
     TunableOp validates the file against this torch / HIP / hipBLASLt / arch and
-    ignores it on a mismatch; shapes not in the file keep the defaults."""
+    ignores it on a mismatch; shapes not in the file keep the defaults.  The
+    process-wide switch stays as the caller had it: `TunedGemms` turns it on
+    only around the learner's own GEMMs."""
     if os.environ.get("F110_TUNABLEOP", "1") == "0" or device.type != "cuda" or not os.path.exists(TUNED_GEMMS):
         return False
     import torch.cuda.tunable as tunable
     if "gfx950" not in torch.cuda.get_device_properties(device).gcnArchName:
         return False
-    tunable.enable(True)
-    tunable.tuning_enable(False)
-    tunable.record_untuned_enable(False)
-    tunable.set_filename(TUNED_GEMMS)
-    return bool(tunable.read_file(TUNED_GEMMS))
+    with TunedGemms(True):
+        if hasattr(tunable, "record_untuned_enable"):
+            tunable.record_untuned_enable(False)
+        tunable.set_filename(TUNED_GEMMS)
+        return bool(tunable.read_file(TUNED_GEMMS))
+
+
+class TunedGemms:
+    """Context: TunableOp on (lookups only, tuning off) for the learner's
+    GEMMs, then the caller's previous state back, so other models in the
+    process keep their own GEMM dispatch."""
+
+    def __init__(self, on: bool):
+        self.on = bool(on)
+        self._prev = None
+
+    def __enter__(self):
+        if self.on:
+            import torch.cuda.tunable as tunable
+            self._prev = (tunable.is_enabled(), tunable.tuning_is_enabled())
+            tunable.enable(True)
+            tunable.tuning_enable(False)
+        return self
+
+    def __exit__(self, *exc):
+        if self._prev is not None:
+            import torch.cuda.tunable as tunable
+            tunable.tuning_enable(self._prev[1])
+            tunable.enable(self._prev[0])
+            self._prev = None
+        return False
 
 
 def _fused(x: torch.Tensor) -> bool:
@@ -442,11 +470,12 @@ class DDPGLearner:
         """The learning part of replay() (agent.py:302-343) on one batch:
         critic step, actor step, soft target update.  Returns device tensors
         (critic_loss, actor_loss, td [B])."""
-        critic_loss, td = self._phase_critic(states, actions, rewards, next_states, dones, weights)
-        self.critic_grads.all_reduce()
-        actor_loss = self._phase_actor(states)
-        self.actor_grads.all_reduce()
-        self._phase_finish()
+        with TunedGemms(self.tuned_gemms):
+            critic_loss, td = self._phase_critic(states, actions, rewards, next_states, dones, weights)
+            self.critic_grads.all_reduce()
+            actor_loss = self._phase_actor(states)
+            self.actor_grads.all_reduce()
+            self._phase_finish()
         self.global_step += 1
         return {"critic_loss": critic_loss, "actor_loss": actor_loss, "td": td}
 
@@ -464,9 +493,10 @@ class DDPGLearner:
             if len(self.memory) < self.batch_size:
                 return None
             self._ready = True
-        if self.graphs:
-            return self._replay_graphed()
-        return self._replay_eager()
+        with TunedGemms(self.tuned_gemms):
+            if self.graphs:
+                return self._replay_graphed()
+            return self._replay_eager()
 
     def _replay_eager(self):
         idxs, b, w = self.memory.sample(beta=self.beta)
@@ -532,7 +562,7 @@ class DDPGLearner:
         """agent.py:350-370 for obs [N, obs_dim] (or [obs_dim]): actor output,
         plus N(0, sigma^2) noise clipped to [low, high] when training; sigma
         decays once per call (GaussianActionNoise.__call__, :520-539)."""
-        with torch.no_grad():
+        with torch.no_grad(), TunedGemms(self.tuned_gemms):
             o = torch.as_tensor(obs, device=self.device, dtype=torch.float32)
             a = self.actor(o)
             if training:

@@ -83,6 +83,17 @@ def sum_over_ranks(x: float) -> float:
     return float(t.item())
 
 
+def sum_tensor_over_ranks(t: torch.Tensor) -> torch.Tensor:
+    """Element-wise sum of an int64 / float64 CPU tensor over the ranks (a
+    copy; the input itself when there is one rank)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return t
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    x = t.to(dev).clone()
+    dist.all_reduce(x, op=dist.ReduceOp.SUM)
+    return x.cpu()
+
+
 def shutdown():
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()

@@ -103,7 +103,7 @@ class StreamShards:
         for s in range(self.S):
             with torch.cuda.stream(self.streams[s]):
                 sm = BatchSim(track, n_envs=self.Es, env_offset=env_offset + s * self.Es, device=self.device, **kw)
-                if not heavy_first and n_streams > 1:
+                if not heavy_first and (n_streams > 1 or refill):
                     # the other sub-shard's ray pass fills this one's tail; heavy-first's list
                     # upkeep then costs more than it saves (42.5 vs 41.8 M env-steps/s)
                     _lib.check(sm.L.f110_disable_heavy_first(sm.ctx), "f110_disable_heavy_first")
@@ -112,6 +112,8 @@ class StreamShards:
                     if os.environ.get("F110_FX_REFILL") is None:  # the env knob still wins (A/B runs)
                         _lib.check(sm.L.f110_set_ray_refill(sm.ctx, int(refill)), "f110_set_ray_refill")
                 self.sims.append(sm)
+        # what the contexts actually run (the env knob or an unsupported map can override the request)
+        self.refill = self.sims[0].ray_refill
         self._sl = [slice(s * self.Es, (s + 1) * self.Es) for s in range(self.S)]
         self._handles = [ctypes.c_void_p(st.cuda_stream) for st in self.streams]
         self._fork()

@@ -43,7 +43,7 @@ extern "C" {
 #define F110_API
 #endif
 
-#define F110_ABI_VERSION 1
+#define F110_ABI_VERSION 2  /* 2: f110_outputs.obs_stride */
 
 #define F110_OK 0
 #define F110_E_INVALID (-1)  /* bad argument / shape */

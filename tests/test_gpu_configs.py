@@ -56,6 +56,57 @@ def test_c3_65536_single_agent(tracks, gpu, oracle_scanners):
     sim.close()
 
 
+def test_c2_4096_single_agent(tracks, gpu, oracle_scanners):
+    """C2: 4096 single-agent envs on one GPU, stepped by the bench's own runner
+    for that size (bench.auto_streams: StreamShards, 4 unjoined sub-shards)
+    AND by one context, 20 random-action steps with autoreset (noise off).
+    The two runners agree bit for bit (obs, f64 scans, states, lookup
+    counts); every range in [0, 30], mean lookups per ray in the measured
+    band; a 512-env sample of the last step's scans bit-exact against the
+    oracle scanner at the cars' post-step poses (TTC-fired cars skipped)."""
+    import bench
+    from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns
+    from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
+    from f110_gymnasium_ros2_jazzy_amd.streams import StreamShards
+    E, T = 4096, 20
+    S = bench.auto_streams(E, 1)
+    assert S == 4
+    sp = centerline_spawns("Spielberg", 1)
+    kw = dict(n_agents=1, device=gpu, noise_std=0.0, autoreset=True, spawn_poses=sp, keep_f64_scans=True)
+    shards = StreamShards(tracks("Spielberg_map"), n_envs=E, n_streams=S, **kw)
+    one = BatchSim(tracks("Spielberg_map"), n_envs=E, **kw)
+    rng = np.random.default_rng(4096)
+    p0 = sp[rng.integers(0, sp.shape[0], E)]
+    shards.reset(p0)
+    one.reset(p0)
+    shards.reset_counters()
+    one.reset_counters()
+    g = torch.Generator(device=gpu)
+    g.manual_seed(22)
+    acts = torch.stack([_actions(g, E, 1, gpu) for _ in range(T)])
+    for t in range(T):
+        shards.step(acts[t], minimal_outputs=False)
+        out = one.step(acts[t])
+    shards.join()
+    torch.cuda.synchronize()
+    assert torch.equal(shards.obs, out.obs)
+    assert torch.equal(torch.cat([sm.out.scans_f64 for sm in shards.sims]), out.scans_f64)
+    assert torch.equal(torch.cat([sm.agent_states() for sm in shards.sims]), one.agent_states())
+    lk, rays = one.read_counters()
+    assert shards.read_counters() == (lk, rays)
+    assert rays == T * E * 1080 and 4.0 < lk / rays < 15.0
+    s = out.scans_f64
+    assert bool(((s >= 0) & (s <= 30)).all()) and bool(torch.isfinite(out.obs).all())
+    idx = rng.choice(E, 512, replace=False)
+    ok = out.collisions[idx, 0].cpu().numpy() == 0
+    st = one.agent_states()[idx, 0].cpu().numpy()[ok]
+    ref = oracle_scanners("Spielberg_map").scan(np.stack([st[:, 0], st[:, 1], st[:, 4]], 1))
+    assert ok.sum() > 400
+    assert np.array_equal(s[idx, 0].cpu().numpy()[ok], ref)
+    shards.close()
+    one.close()
+
+
 def test_c4_8192x2_lockstep_sample(tracks, gpu, oracle_scanners, nonexact_budget):
     """C4: 8192 envs x 2 agents on one GPU, 20 random-action steps (noise
     off, no autoreset).  The first 256 envs are stepped by the oracle in
