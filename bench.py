@@ -281,6 +281,8 @@ def scan_check(O, scanner, runner, act, threads):
 
 def ray_kernel_name(sm):
     names = {0: "k_rays", 1: "k_rays_tiled (flat)", 2: "k_rays_tiled (chunked)", 3: "k_rays_fx"}
+    if sm.ray_kernel == 3 and getattr(sm, "ray_pool", 0) > 0:
+        return f"k_rays_fxp ({sm.ray_pool} car(s) per wave, two ray slots per lane with lane-level refill)"
     if sm.ray_kernel == 3 and sm.ray_refill > 0:
         return f"k_rays_fxr ({sm.ray_refill} wave(s) per car, 2 chunk slots with refill)"
     if sm.ray_kernel == 3 and sm.ray_lanes > 1:

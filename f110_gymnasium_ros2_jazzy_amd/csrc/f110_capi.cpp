@@ -108,6 +108,9 @@ struct f110_ctx {
     bool fx_pad = false;    // k_rays_fxn / k_rays_fxr on the padded table (default from 32768 cars; F110_FX_PAD)
     int32_t fx_slots = 2;    // F110_FX_SLOTS (A/B): chunk slots per k_rays_fxr wave
     int32_t fx_refill = 0;   // waves per car of k_rays_fxr (0 = k_rays_fxn; F110_FX_REFILL overrides)
+    int32_t fx_pool = 0;     // cars per k_rays_fxp wave (lane-level refill; 0 = off; F110_FX_POOL)
+    int32_t pool_T = 80;     // k_rays_fxp's refill threshold in ended slots (F110_FX_POOL_T)
+    uint8_t *pcost = nullptr;  // [EA][nch] k_rays_fxp's per-chunk costs (queue order of the next launch)
     bool count_slots = false;  // f110_set_simt / F110_SIMT: lane-slot counter of the fixed-point loops (f110_read_simt)
     int fx_ilp = 1;         // rays per lane (F110_FX_ILP; default by car count)
     bool fx_tiled = false;  // F110_FX_TABLE=tiled: A/B of the 4x4-tiled EDT
@@ -729,6 +732,13 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     c->fx_refill = EA >= 32768 ? 1 : 0;
     if (const char *v = std::getenv("F110_FX_REFILL")) c->fx_refill = std::max(0, std::min(16, std::atoi(v)));
     if (const char *v = std::getenv("F110_FX_SLOTS")) c->fx_slots = std::atoi(v) == 3 ? 3 : 2;
+    if (const char *v = std::getenv("F110_FX_POOL")) c->fx_pool = std::max(0, std::min(2, std::atoi(v)));
+    if (const char *v = std::getenv("F110_FX_POOL_T")) c->pool_T = std::max(1, std::min(128, std::atoi(v)));
+    if (fx_ok) {
+        hipError_t ep = c->alloc(&c->pcost, EA * (size_t)c->nch);
+        if (ep == hipSuccess) ep = hipMemset(c->pcost, 0, EA * (size_t)c->nch);
+        if (ep != hipSuccess) return cleanup(F110_E_ALLOC, std::string("hipMalloc pcost: ") + hipGetErrorString(ep));
+    }
     const double pad_q = std::ceil(C.max_range / resolution) + 8.0;
     const int32_t fx_pad_cells = pad_q > 0.0 && pad_q < 65536.0 ? (int32_t)pad_q : 0;  // else no padded table
     if (const char *v = std::getenv("F110_FX_LDS")) c->fx_lds = (uint32_t)std::max(0, std::min(65536, std::atoi(v)));
@@ -863,6 +873,9 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.fx_pad = c->rmp ? 1 : 0;
     a.count_slots = c->count_slots ? 1 : 0;
     a.fx_refill = c->fx_refill;
+    a.fx_pool = c->fx_pool;
+    a.pool_T = c->pool_T;
+    a.pcost = c->pcost;
     a.fx_slots = c->fx_slots;
     a.fx_tiled = c->fx_tiled ? 1 : 0;
     a.fx_lds = c->fx_lds;
@@ -917,6 +930,10 @@ extern "C" int f110_set_reset_dtype(f110_ctx *ctx, int32_t dtype) {
     return F110_OK;
 }
 
+extern "C" void f110_host_sincos(const double *x, int64_t n, double *sn, double *cs) {
+    for (int64_t i = 0; i < n; ++i) cr_sincos(x[i], sn[i], cs[i]);
+}
+
 extern "C" void f110_host_np_sincosf(const float *x, int64_t n, int32_t cos_op, float *out) {
     for (int64_t i = 0; i < n; ++i) out[i] = np_sincosf(x[i], cos_op != 0);
 }
@@ -931,11 +948,41 @@ extern "C" int f110_ray_lanes(const f110_ctx *ctx) {
     return ctx->ray_kernel == 3 ? ctx->fx_ilp : 1;
 }
 
+static int effective_pool(const f110_ctx *ctx);
+
 extern "C" int f110_ray_refill(const f110_ctx *ctx) {
     if (!ctx) return fail(F110_E_INVALID, "f110_ray_refill: null context");
     const bool fx = ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled && ctx->fx_ilp == 2;
     const int waves = std::min<int>(ctx->fx_refill, (ctx->cfg.n_beams + 63) / 64);  // as the launch clamps it
-    return fx && waves > 0 && (ctx->heavy_off || !ctx->wcost) ? waves : 0;
+    return fx && waves > 0 && (ctx->heavy_off || !ctx->wcost) && !effective_pool(ctx) ? waves : 0;
+}
+
+// The padded EDT of k_rays_fxr / k_rays_fxp (built on first use, shared with
+// the map entry): F110_FX_PAD=0 keeps the clamped table (A/B runs).
+static int ensure_padded_table(f110_ctx *ctx) {
+    bool pad = true;
+    if (const char *v = std::getenv("F110_FX_PAD")) pad = std::atoi(v) != 0;
+    if (!pad || ctx->rmp || !ctx->maps) return F110_OK;
+    const double pad_q = std::ceil(ctx->cfg.max_range / ctx->res) + 8.0;
+    if (pad_q > 0.0 && pad_q < 65536.0) {
+        std::lock_guard<std::mutex> g(g_maps_mu);
+        MapTables *t = ctx->maps;
+        if (!t->rmp) {
+            std::vector<double> d((size_t)t->H * t->W);
+            double res;
+            std::memcpy(&res, &t->res_bits, 8);
+            for (size_t i = 0; i < d.size(); ++i) d[i] = res * std::sqrt((double)t->k[i]);
+            HIP_TRY(build_padded_table(t, (int32_t)pad_q, d));
+        }
+    }
+    if (ctx->maps->rmp) {
+        ctx->fx_pad = true;
+        ctx->rmp = ctx->maps->rmp;
+        ctx->rmp_w = ctx->maps->rmp_w;
+        ctx->rmp_P = ctx->maps->rmp_P;
+        ctx->rmp_zero = ctx->maps->rmp_zero;
+    }
+    return F110_OK;
 }
 
 extern "C" int f110_set_ray_refill(f110_ctx *ctx, int32_t waves) {
@@ -945,29 +992,36 @@ extern "C" int f110_set_ray_refill(f110_ctx *ctx, int32_t waves) {
     if (!fx && waves != 0) return fail(F110_E_INVALID, "f110_set_ray_refill: this context's ray kernel has no refill");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     ctx->fx_refill = waves;
-    bool pad = true;  // F110_FX_PAD=0 keeps the clamped table (A/B runs), as at f110_create
-    if (const char *v = std::getenv("F110_FX_PAD")) pad = std::atoi(v) != 0;
-    if (waves > 0 && pad && !ctx->rmp && ctx->maps) {  // the padded table goes with k_rays_fxr
-        const double pad_q = std::ceil(ctx->cfg.max_range / ctx->res) + 8.0;
-        if (pad_q > 0.0 && pad_q < 65536.0) {
-            std::lock_guard<std::mutex> g(g_maps_mu);
-            MapTables *t = ctx->maps;
-            if (!t->rmp) {
-                std::vector<double> d((size_t)t->H * t->W);
-                double res;
-                std::memcpy(&res, &t->res_bits, 8);
-                for (size_t i = 0; i < d.size(); ++i) d[i] = res * std::sqrt((double)t->k[i]);
-                HIP_TRY(build_padded_table(t, (int32_t)pad_q, d));
-            }
-        }
-        if (ctx->maps->rmp) {
-            ctx->fx_pad = true;
-            ctx->rmp = ctx->maps->rmp;
-            ctx->rmp_w = ctx->maps->rmp_w;
-            ctx->rmp_P = ctx->maps->rmp_P;
-            ctx->rmp_zero = ctx->maps->rmp_zero;
-        }
-    }
+    if (waves > 0) return ensure_padded_table(ctx);  // the padded table goes with k_rays_fxr
+    return F110_OK;
+}
+
+// k_rays_fxp runs for unmasked steps of a fixed-point context with two rays per
+// lane, the padded table and no heavy-first list, when the pool's chunks fit one
+// wave's queue (cars x chunks <= 64)
+static int effective_pool(const f110_ctx *ctx) {
+    const int nch = (ctx->cfg.n_beams + 63) / 64;
+    const bool fx = ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled && ctx->fx_ilp == 2 && ctx->fx_pad &&
+                    ctx->rmp && ctx->pcost;
+    const int pool = ctx->fx_pool;
+    return fx && pool > 0 && pool * nch <= 64 && (ctx->heavy_off || !ctx->wcost) ? pool : 0;
+}
+
+extern "C" int f110_ray_pool(const f110_ctx *ctx) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_ray_pool: null context");
+    return effective_pool(ctx);
+}
+
+extern "C" int f110_set_ray_pool(f110_ctx *ctx, int32_t cars, int32_t threshold) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_pool: null context");
+    if (cars < 0 || cars > 2) return fail(F110_E_INVALID, "f110_set_ray_pool: cars per wave must be in 0..2");
+    if (threshold < 0 || threshold > 128) return fail(F110_E_INVALID, "f110_set_ray_pool: threshold must be in 0..128");
+    const bool fx = ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled && ctx->pcost;
+    if (!fx && cars != 0) return fail(F110_E_INVALID, "f110_set_ray_pool: this context's ray kernel has no pool");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    ctx->fx_pool = cars;
+    if (threshold > 0) ctx->pool_T = threshold;
+    if (cars > 0) return ensure_padded_table(ctx);
     return F110_OK;
 }
 
@@ -1098,6 +1152,19 @@ extern "C" int f110_read_counters(f110_ctx *ctx, uint64_t *lookups, uint64_t *ra
     }
     if (lookups) *lookups = lk;
     if (rays) *rays = ry;
+    return F110_OK;
+}
+
+extern "C" int f110_read_counter(f110_ctx *ctx, int32_t idx, uint64_t *value, void *stream) {
+    if (!ctx || !value || idx < 0 || idx >= kCtrStride) return fail(F110_E_INVALID, "f110_read_counter: bad argument");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    std::vector<unsigned long long> h((size_t)kCtrSlots * kCtrStride);
+    HIP_TRY(hipMemcpyAsync(h.data(), ctx->ctr, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           (hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    unsigned long long v = 0;
+    for (int i = 0; i < kCtrSlots; ++i) v += h[(size_t)i * kCtrStride + idx];
+    *value = v;
     return F110_OK;
 }
 

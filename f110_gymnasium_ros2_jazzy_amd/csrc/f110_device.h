@@ -47,6 +47,114 @@ F110_HD double pymod(double a, double b) {
 // F110Env._wrap_angle / update_pose yaw wrap: ((a + pi) % 2pi) - pi.
 F110_HD double wrap_angle(double a) { return pymod(a + kPi, kTwoPi) - kPi; }
 
+// ------------------------------------------------ correctly rounded sin/cos --
+// The reference's np.sin / np.cos (and Numba's libm calls) are glibc's, which
+// return the correctly rounded result but in very rare cases; ocml's differ by
+// an ulp on a few percent of arguments, which is what left agent ray_cast
+// ranges and box vertices inexact.  cr_sincos evaluates sin and cos of x in
+// double-double arithmetic and rounds once: the Cody-Waite reduction by a
+// three-part pi/2 (the first product exact by fma), then Taylor series of
+// sin / cos on |r| <= pi/4 with the terms through r^7 (sin) / r^6 (cos) in
+// double-double Horner steps and the rest in double.  The sum before the last
+// rounding is within ~2^-70 relative, so the result is the correctly rounded
+// value except where the true value lies within that of a rounding midpoint.
+// Host and device compute it with the same IEEE operations (no contraction,
+// explicit fma): tests/test_host_lib.py checks it against NumPy bit for bit.
+// |x| >= 2^20 (never a scan or box angle here) falls back to the library call.
+struct DD {
+    double h, l;
+};
+
+F110_HD DD dd_two_sum(double a, double b) {
+    const double s = a + b;
+    const double bb = s - a;
+    return {s, (a - (s - bb)) + (b - bb)};
+}
+
+F110_HD DD dd_fast(double a, double b) {  // |a| >= |b|
+    const double s = a + b;
+    return {s, b - (s - a)};
+}
+
+F110_HD DD dd_mul(DD a, DD b) {
+    const double p = a.h * b.h;
+    double e = fma(a.h, b.h, -p);
+    e += a.h * b.l + a.l * b.h;
+    return dd_fast(p, e);
+}
+
+F110_HD DD dd_add(DD a, DD b) {
+    const DD s = dd_two_sum(a.h, b.h);
+    return dd_fast(s.h, s.l + (a.l + b.l));
+}
+
+// acc = c + z * acc in double-double
+F110_HD DD dd_horner(DD c, DD z, DD acc) { return dd_add(c, dd_mul(z, acc)); }
+
+F110_HD void cr_sincos(double x, double &sn, double &cs) {
+    if (!(fabs(x) < 1048576.0)) {  // NaN, inf, or beyond the exact reduction
+        sn = sin(x);
+        cs = cos(x);
+        return;
+    }
+    if (x == 0.0) {  // +-0 (keeps the sign of sin(-0.0))
+        sn = x;
+        cs = 1.0;
+        return;
+    }
+    const double P1 = 0x1.921fb54442d18p+0, P2 = 0x1.1a62633145c07p-54, P3 = -0x1.f1976b7ed8fbcp-110;
+    const double k = rint(x * 0x1.45f306dc9c883p-1);  // x * 2/pi, nearest quadrant
+    const double r1 = fma(-k, P1, x);                 // exact: |x| >= pi/4 has ulp >= 2^-53
+    const double q2 = k * P2;
+    const double q2l = fma(k, P2, -q2);
+    const DD s1 = dd_two_sum(r1, -q2);
+    const DD r = dd_fast(s1.h, s1.l - q2l - k * P3);  // x - k pi/2, double-double
+    const DD z = dd_mul(r, r);
+    const double zh = z.h;
+    // sin(r) = r (1 - z/3! + z^2/5! - z^3/7! + z^4 ps(z)),  ps = 1/9! - z/11! + ... - z^5/19!
+    double ps = 0x1.952c77030ad4ap-49 - zh * 0x1.2f49b46814157p-57;  // 1/17! - z/19!
+    ps = 0x1.ae7f3e733b81fp-41 - zh * ps;                             // 1/15!
+    ps = 0x1.6124613a86d09p-33 - zh * ps;                             // 1/13!
+    ps = 0x1.ae64567f544e4p-26 - zh * ps;                             // 1/11!
+    ps = 0x1.71de3a556c734p-19 - zh * ps;                             // 1/9!
+    DD as = {ps, 0.0};
+    as = dd_horner({-0x1.a01a01a01a01ap-13, -0x1.a01a01a01a01ap-73}, z, as);  // -1/7!
+    as = dd_horner({0x1.1111111111111p-7, 0x1.1111111111111p-63}, z, as);    // 1/5!
+    as = dd_horner({-0x1.5555555555555p-3, -0x1.5555555555555p-57}, z, as);  // -1/3!
+    as = dd_horner({1.0, 0.0}, z, as);
+    const DD sr = dd_mul(r, as);
+    // cos(r) = 1 - z/2! + z^2/4! - z^3/6! + z^4 pc(z),  pc = 1/8! - z/10! + ... - z^5/18!
+    double pc = 0x1.ae7f3e733b81fp-45 - zh * 0x1.6827863b97d97p-53;  // 1/16! - z/18!
+    pc = 0x1.93974a8c07c9dp-37 - zh * pc;                            // 1/14!
+    pc = 0x1.1eed8eff8d898p-29 - zh * pc;                            // 1/12!
+    pc = 0x1.27e4fb7789f5cp-22 - zh * pc;                            // 1/10!
+    pc = 0x1.a01a01a01a01ap-16 - zh * pc;                            // 1/8!
+    DD ac = {pc, 0.0};
+    ac = dd_horner({-0x1.6c16c16c16c17p-10, 0x1.f49f49f49f49fp-65}, z, ac);  // -1/6!
+    ac = dd_horner({0x1.5555555555555p-5, 0x1.5555555555555p-59}, z, ac);    // 1/4!
+    ac = dd_horner({-0.5, 0.0}, z, ac);
+    ac = dd_horner({1.0, 0.0}, z, ac);
+    const double s = sr.h + sr.l, c = ac.h + ac.l;
+    switch ((int)((int64_t)k & 3)) {
+        case 0: sn = s; cs = c; break;
+        case 1: sn = c; cs = -s; break;
+        case 2: sn = -s; cs = -c; break;
+        default: sn = -c; cs = s; break;
+    }
+}
+
+F110_HD double cr_sin(double x) {
+    double s, c;
+    cr_sincos(x, s, c);
+    return s;
+}
+
+F110_HD double cr_cos(double x) {
+    double s, c;
+    cr_sincos(x, s, c);
+    return c;
+}
+
 // ------------------------------------------------------------- dynamics --
 // accl_constraints, dynamic_models.py:29-60
 F110_HD double accl_constraints(double vel, double accl, double v_switch, double a_max, double v_min,
@@ -80,8 +188,10 @@ F110_HD void vehicle_dynamics_ks(const double x[5], double u0_in, double u1_in, 
     const double lwb = p.lf + p.lr;
     const double u0 = steering_constraint(x[2], u0_in, p.s_min, p.s_max, p.sv_min, p.sv_max);
     const double u1 = accl_constraints(x[3], u1_in, p.v_switch, p.a_max, p.v_min, p.v_max);
-    f[0] = x[3] * cos(x[4]);
-    f[1] = x[3] * sin(x[4]);
+    double s4, c4;
+    cr_sincos(x[4], s4, c4);
+    f[0] = x[3] * c4;
+    f[1] = x[3] * s4;
     f[2] = u0;
     f[3] = u1;
     f[4] = x[3] / lwb * tan(x[2]);
@@ -100,9 +210,11 @@ F110_HD void vehicle_dynamics_st(const double x[7], double u0_in, double u1_in, 
         double k0 = steering_constraint(x[2], u0, p.s_min, p.s_max, p.sv_min, p.sv_max);
         double k1 = accl_constraints(x[3], u1, p.v_switch, p.a_max, p.v_min, p.v_max);
         double tn = tan(x[2]);
-        double c2 = cos(x[2]);
-        f[0] = x[3] * cos(x[4]);
-        f[1] = x[3] * sin(x[4]);
+        double c2 = cr_cos(x[2]);
+        double s4, c4;
+        cr_sincos(x[4], s4, c4);
+        f[0] = x[3] * c4;
+        f[1] = x[3] * s4;
         f[2] = k0;
         f[3] = k1;
         f[4] = x[3] / lwb * tn;
@@ -113,8 +225,10 @@ F110_HD void vehicle_dynamics_st(const double x[7], double u0_in, double u1_in, 
         const double glf_p = kG * lf + u1 * h;
         const double lrlf = lr + lf;
         const double a = x[6] + x[4];
-        f[0] = x[3] * cos(a);
-        f[1] = x[3] * sin(a);
+        double sa, ca;
+        cr_sincos(a, sa, ca);
+        f[0] = x[3] * ca;
+        f[1] = x[3] * sa;
         f[2] = u0;
         f[3] = u1;
         f[4] = x[5];
@@ -447,7 +561,8 @@ F110_HD double dot2(double a0, double a1, double b0, double b1) {  // ndarray.do
 
 // get_trmtx + get_vertices, collision_models.py:218-260 -> [rl, rr, fr, fl].
 F110_HD void get_vertices(double x, double y, double th, double length, double width, double v[8]) {
-    double c = cos(th), s = sin(th);
+    double s, c;
+    cr_sincos(th, s, c);
     const double px[4] = {-length / 2, -length / 2, length / 2, length / 2};
     const double py[4] = {width / 2, -width / 2, -width / 2, width / 2};
 #pragma unroll
@@ -574,7 +689,8 @@ F110_HD int blocked_vertex_beam(double px, double py, double ego, double vx0, do
 // get_blocked_view_indices, laser_models.py:282-315
 F110_HD void blocked_range(double px, double py, double pth, const double v[8], int B, double fov, double incr,
                            int &lo, int &hi) {
-    double ex = cos(pth), ey = sin(pth);
+    double ey, ex;
+    cr_sincos(pth, ey, ex);
     double ego = atan2(ey, ex);
     int mn = 0, mx = 0;
 #pragma unroll

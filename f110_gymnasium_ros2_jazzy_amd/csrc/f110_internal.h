@@ -65,6 +65,9 @@ struct StepArgs {
     int32_t fx_pad;     // F110_FX_PAD: k_rays_fxn on the padded table
     int32_t fx_slots;   // F110_FX_SLOTS (A/B): chunk slots per k_rays_fxr wave, 2 or 3
     int32_t fx_refill;  // F110_FX_REFILL: waves per car of k_rays_fxr (two chunk slots with refill; 0 = off)
+    int32_t fx_pool;    // F110_FX_POOL: cars per k_rays_fxp wave (lane-level refill; 0 = off)
+    int32_t pool_T;     // F110_FX_POOL_T: k_rays_fxp refills once this many slots have ended
+    uint8_t *pcost;     // [EA][nch] k_rays_fxp's per-chunk cost of the previous launch (its queue order)
     int32_t count_slots;  // F110_SIMT (default 1): lane-slot counter of the fixed-point loops
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2..4: k_rays_fxn)
     int32_t fx_tiled;   // F110_FX_TABLE=tiled (A/B): k_rays_fx on the 4x4-tiled EDT
@@ -170,6 +173,11 @@ struct RayArgs {
     uint32_t ev_cap, ev_capp;
     int32_t ev_P;
     int32_t ev_T, ev_K;  // evict a wave's active rays once <= ev_T remain after >= ev_K iterations
+    // k_rays_fxp (lane-level refill over a pool of cars): per (car, 64-beam chunk) the
+    // longest ray's lookups of the previous launch (min 255), read for the queue order and
+    // rewritten; refill once pool_T ray slots of a wave have ended
+    uint8_t *pcost;
+    int32_t pool_T;
 };
 
 constexpr int kEvStride = 32;    // u32 per hand-off partition counter line (128 B)

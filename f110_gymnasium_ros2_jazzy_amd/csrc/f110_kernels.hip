@@ -227,8 +227,10 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
                 a.start_rot[e] = (double)np_sincosf(nt, true);
                 a.start_rot[a.E + e] = (double)np_sincosf(nt, false);
             } else {
-                a.start_rot[e] = cos(-pth);
-                a.start_rot[a.E + e] = sin(-pth);
+                double sr, crr;
+                cr_sincos(-pth, sr, crr);
+                a.start_rot[e] = crr;
+                a.start_rot[a.E + e] = sr;
             }
         }
         a.toggles[g] = 0;
@@ -247,8 +249,10 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
     // finite yaw, so the transcendentals are skipped (a non-finite yaw keeps
     // the reference's NaN)
     const bool no_offset = a.lidar_dist == 0.0 && isfinite(s[4]);
-    const double sx = no_offset ? s[0] + 0.0 : s[0] + a.lidar_dist * cos(s[4]);
-    const double sy = no_offset ? s[1] + 0.0 : s[1] + a.lidar_dist * sin(s[4]);
+    double sy4 = 0.0, cy4 = 1.0;
+    if (!no_offset) cr_sincos(s[4], sy4, cy4);
+    const double sx = no_offset ? s[0] + 0.0 : s[0] + a.lidar_dist * cy4;
+    const double sy = no_offset ? s[1] + 0.0 : s[1] + a.lidar_dist * sy4;
     a.ray0[g] = sx;
     a.ray0[EA + g] = sy;
     a.ray0[2 * EA + g] = a.map.dt[cell_index(a.map, sx, sy)];  // first lookup (laser_models.py:129)
@@ -1299,6 +1303,270 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
     }
 }
 
+// ------------------------------------------------------------------------
+// k_rays_fxp (F110_FX_POOL = NCAR cars per wave): lane-level refill over a
+// pool of cars.  k_rays_fxr refills a slot only when its whole 64-beam chunk
+// has ended, and a wave of ONE car cannot end before that car's longest ray
+// (mean ~83 loop iterations against ~49 for the car's rays spread over 128
+// lane slots: scripts/lane_refill_model.py).  Here a wave owns NCAR cars; its
+// queue holds their 64-beam chunks sorted by the previous launch's per-chunk
+// cost (pcost: the long, grazing-beam chunks start first), every lane has two
+// ray slots, and a slot whose ray has ended takes the queue's next ray.  The
+// finish + re-arm pass is wave-wide work whatever the number of lanes in it,
+// so it runs once >= pool_T slots wait (or none is still tracing).
+//
+// Per ray the arithmetic is k_rays_fxn's on the padded EDT (fxp_offset), so
+// the outputs are bit-identical.  A ray's beam index comes from an LDS table
+// of the pool's theta indices (built once per car from its beam runs), its
+// noise is the pair draw of beam_normal_k (the half of the partner beam is
+// not cached: the pass costs the same for any number of lanes).  The model
+// (same poses, 2 cars per wave, pool_T 80): 65 instead of 105 wave-iterations
+// per car, SIMT 0.75 instead of 0.46.
+// The pool's per-car constants, in LDS (read per lane by the lane's car at
+// re-arm / finish: SGPR copies of NCAR cars' values would spill).
+struct PoolCar {
+    double x0, y0, d0, vel;  // scan origin, first EDT lookup (:129), speed (TTC)
+    uint64_t step;           // noise counter (steps since reset)
+    uint32_t key, pad_;      // noise key of the car's env
+};
+
+// The kernarg block behind an opaque copy of its pointer: loads through it
+// stay where they are written (in the refill pass) instead of being hoisted
+// out of the trace loop into SGPRs, which would spill there.
+__device__ __forceinline__ const RayArgs &kernarg_here() {
+    const RayArgs *p;
+    asm volatile("s_mov_b64 %0, %1" : "=s"(p) : "s"(kernarg_rays()));
+    return *p;
+}
+
+__device__ __forceinline__ bool lane_in(uint64_t mask) {
+    return (uint32_t)(mask >> (threadIdx.x & 63)) & 1u;
+}
+
+template <bool HANDOFF, int NCAR>
+__global__ void __launch_bounds__(64, 8) k_rays_fxp(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
+    extern __shared__ __attribute__((aligned(16))) unsigned char fxp_smem[];
+    const int lane = (int)threadIdx.x;
+    const int B = a.B;
+    const int nch = (B + 63) >> 6;
+    const int g0 = (int)blockIdx.x * NCAR;
+    const int ncar = min(NCAR, a.EA - g0);
+    PoolCar *s_car = reinterpret_cast<PoolCar *>(fxp_smem);                                  // [NCAR]
+    uint32_t *s_cost = reinterpret_cast<uint32_t *>(fxp_smem + NCAR * sizeof(PoolCar));     // [64]
+    uint16_t *s_ti = reinterpret_cast<uint16_t *>(fxp_smem + NCAR * sizeof(PoolCar) + 256);  // [NCAR][B]
+    const RayArgs &K = *kernarg_rays();
+    const FxLoop L = fx_loop<3>(a);
+    const uint32_t P = (uint32_t)a.fxp_P;
+    const bool dev_noise = !K.noise_ext && K.noise_std > 0.0;
+
+    // ---- per-car set-up: constants and the theta index of every beam into LDS ----
+    bool all_fast = true;
+    for (int ci = 0; ci < ncar; ++ci) {
+        const int g = g0 + ci;
+        const int e = HANDOFF ? g / a.A : g;
+        const double x0 = ld_const(a.ray0 + g), y0 = ld_const(a.ray0 + a.EA + g);
+        // q + P of the scan origin inside [fxp_lo, fxp_h*): its rays stay in the padded table
+        const double ux = fma(x0, L.ir, L.cxk) - kFxpBase, uy = fma(y0, L.ir, L.cyk) - kFxpBase;
+        all_fast = all_fast && (ux >= a.fxp_lo) & (ux < a.fxp_hx) & (uy >= a.fxp_lo) & (uy < a.fxp_hy);
+        if (lane == 0) {
+            PoolCar pc;
+            pc.x0 = x0;
+            pc.y0 = y0;
+            pc.d0 = ld_const(a.ray0 + 2 * a.EA + g);  // :129
+            pc.vel = ld_const(a.vel + g);
+            pc.step = dev_noise ? ld_const(K.noise_step + e) : 0ull;
+            pc.key = noise_key(K.seed, (uint64_t)(K.env_offset + e));
+            pc.pad_ = 0u;
+            s_car[ci] = pc;
+        }
+        const BeamRun *R = a.runs + (size_t)g * kMaxSeg;
+        const int n = ld_const(a.nruns + g);
+        int vlo = 0;  // lane k < nch: the run holding beam 64 k
+        if (lane < nch) {
+            int lo = 0, hi = n - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (R[mid].start <= lane * 64) lo = mid;
+                else hi = mid - 1;
+            }
+            vlo = lo;
+        }
+        for (int k = 0; k < nch; ++k) {
+            const int b = k * 64 + lane, bc = b < B ? b : B - 1;
+            int ti = (int)beam_theta(R, n, __builtin_amdgcn_readlane(vlo, k), k * 64, bc);  // int(theta_index), :124
+            if (ti >= a.theta_dis) ti = 0;
+            if (b < B) s_ti[ci * B + b] = (uint16_t)ti;
+        }
+    }
+
+    // ---- the queue: the pool's (car, chunk) units by predicted cost ----
+    const int NU = ncar * nch;  // <= 64 (checked by the launcher)
+    const uint32_t NQ = (uint32_t)NU * 64u;
+    uint32_t ucode = 0, ukey = 0;
+    if (lane < NU) {
+        const int ci = lane / nch, k = lane - ci * nch;
+        const uint32_t cost = a.pcost ? (uint32_t)a.pcost[(size_t)(g0 + ci) * nch + k] : 0u;
+        ucode = ((uint32_t)ci << 5) | (uint32_t)k;
+        // ties (first launch): descending chunks (the left edge first), cars interleaved
+        ukey = (cost << 16) | ((uint32_t)k << 8) | (255u - (uint32_t)ci);
+        s_cost[lane] = 0u;
+    }
+    uint32_t rank = lane < NU ? 0u : (uint32_t)lane;
+    for (int j = 0; j < NU; ++j) rank += (uint32_t)(__builtin_amdgcn_readlane(ukey, j) > ukey) & (lane < NU ? 1u : 0u);
+    const uint32_t sorted = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank << 2), (int)ucode);  // lane r: unit of rank r
+    __syncthreads();  // the LDS tables (one wave)
+
+    uint32_t rays = 0, lane_iters = 0, iters = 0, passes = 0, refills = 0;
+    if (all_fast) {
+        uint32_t zero_v;  // in a VGPR for the whole trace (the select's other operand is its SGPR mask)
+        asm volatile("v_mov_b32 %0, %1" : "=v"(zero_v) : "s"(a.fx_zero));
+        double x[2], y[2], d[2], tot[2], c[2], sn[2];
+        // per slot: (iteration armed << 14) | (car << 12) | beam; -1 empty
+        int32_t code[2] = {-1, -1};
+        uint64_t occ[2] = {0ull, 0ull};
+        uint32_t nxt = 0;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) x[r] = y[r] = d[r] = tot[r] = c[r] = sn[r] = 0.0;
+        // slot r of the lanes in `m` takes the queue's next rays (in lane order)
+        auto arm = [&](int r, uint64_t m) {
+            const uint32_t p = nxt + lanes_below(m);
+            const uint32_t su = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(p >> 6, 63u) << 2), (int)sorted);
+            const RayArgs &Ka = kernarg_here();  // in the wave-uniform part
+            const bool mine = lane_in(m) && p < NQ;
+            if (mine) {
+                const int ci = (int)(su >> 5), k = (int)(su & 31u);
+                const int b = (k << 6) | (int)(p & 63u);
+                const int ti = s_ti[ci * B + (b < B ? b : B - 1)];
+                c[r] = Ka.cosines[ti];
+                sn[r] = Ka.sines[ti];
+                const PoolCar &pc = s_car[ci];
+                x[r] = pc.x0;
+                y[r] = pc.y0;
+                d[r] = b < B ? pc.d0 : 0.0;  // past the last beam: a ray that has ended
+                tot[r] = d[r];  // :130
+                code[r] = (int32_t)((iters << 14) | ((uint32_t)ci << 12) | (uint32_t)b);
+            }
+            occ[r] |= __builtin_amdgcn_ballot_w64(mine);
+            nxt = min(nxt + (uint32_t)__popcll(m), NQ);
+        };
+        // the ended rays of slot r in `m`: outputs (fx_epilogue: noise after the clamp, TTC, obs / scans)
+        auto finish = [&](int r, uint64_t m) {
+            const uint32_t cd = (uint32_t)code[r];
+            const int ci = (int)((cd >> 12) & 3u), b = (int)(cd & 4095u);
+            const bool real = lane_in(m) && b < B;
+            const RayArgs &Kf = kernarg_here();  // in the wave-uniform part
+            if (real) {
+                const int g = g0 + ci;
+                const int e = HANDOFF ? g / Kf.A : g;
+                const PoolCar &pc = s_car[ci];
+                double nz = 0.0;
+                if (Kf.noise_ext) nz = Kf.noise_ext[(size_t)e * B + b];
+                else if (Kf.noise_std > 0.0) nz = Kf.noise_std * (double)beam_normal_k(pc.key, pc.step, b);
+                fx_epilogue<HANDOFF>(Kf, g, e, b, tot[r], L.mr, nz, pc.vel, Kf.beam_cos[b], Kf.side[b]);
+                atomicMax(s_cost + ci * nch + (b >> 6), iters - (cd >> 14) + 1u);
+            }
+            if (lane_in(m)) code[r] = -1;
+            rays += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(real));
+            occ[r] &= ~m;
+        };
+        arm(0, ~0ull);
+        arm(1, ~0ull);
+        const uint32_t T = (uint32_t)a.pool_T;
+        // one back-edge (the slots' registers are not copied between two latches): refill,
+        // then one step of every tracing ray
+        for (;;) {
+            uint64_t m[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+            const uint64_t e0 = occ[0] & ~m[0], e1 = occ[1] & ~m[1];
+            const uint32_t ne = (uint32_t)(__popcll(e0) + __popcll(e1));
+            bool tracing = (m[0] | m[1]) != 0ull;
+            if (!tracing && !ne) break;  // the queue is done
+            if (ne && (ne >= T || !tracing)) {  // wave-uniform: finish the ended rays, refill their slots
+                ++passes;
+                refills += (e0 ? 1u : 0u) + (e1 ? 1u : 0u);
+                if (e0) {
+                    finish(0, e0);
+                    if (nxt < NQ) arm(0, e0);
+                }
+                if (e1) {
+                    finish(1, e1);
+                    if (nxt < NQ) arm(1, e1);
+                }
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+                    m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+                tracing = (m[0] | m[1]) != 0ull;
+            }
+            if (tracing) {
+                ++iters;
+                lane_iters += (uint32_t)(__popcll(m[0]) + __popcll(m[1]));
+                // trace_ray's step (laser_models.py:135-141) for every tracing ray; ended /
+                // empty slots read the zero cell (d = 0: total, x and y stay)
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+                    if (m[r]) {
+                        const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+                        const uint32_t off = fxp_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero_v, P);
+                        d[r] = fx_load<3>(a.m.dt, off);
+                    }
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+                    if (m[r]) tot[r] += d[r];  // :141
+            }
+        }
+        __syncthreads();
+        if (a.pcost && lane < NU) {  // this launch's per-chunk cost: the next launch's order
+            const uint32_t cst = s_cost[lane];
+            const int ci = lane / nch, k = lane - ci * nch;
+            a.pcost[(size_t)(g0 + ci) * nch + k] = (uint8_t)(cst < 255u ? cst : 255u);
+        }
+    } else {
+        // a car of the pool has its scan origin off the map: every lookup takes the IEEE
+        // cell (exact_offset_pad), one ray per lane, car by car, chunk by chunk
+        uint32_t cnt = 0;
+        for (int ci = 0; ci < ncar; ++ci) {
+            const int g = g0 + ci;
+            const int e = HANDOFF ? g / a.A : g;
+            const PoolCar pc = s_car[ci];
+            for (int k = 0; k < nch; ++k) {
+                const int b = k * 64 + lane;
+                if (b < B) {
+                    const int ti = s_ti[ci * B + b];
+                    const double cc = a.cosines[ti], ss = a.sines[ti];
+                    double x = pc.x0, y = pc.y0, d = pc.d0;
+                    double tot = d;  // :130
+                    while ((dhi(d) != 0u) & (tot <= L.mr)) {
+                        x += d * cc;  // :135
+                        y += d * ss;  // :136
+                        d = fx_load<3>(a.m.dt, exact_offset_pad(a.m, x, y, P));
+                        tot += d;  // :141
+                        ++cnt;
+                    }
+                    double nz = 0.0;
+                    if (K.noise_ext) nz = K.noise_ext[(size_t)e * B + b];
+                    else if (dev_noise) nz = K.noise_std * (double)beam_normal_k(pc.key, pc.step, b);
+                    fx_epilogue<HANDOFF>(K, g, e, b, tot, L.mr, nz, pc.vel, a.beam_cos[b], a.side[b]);
+                }
+                rays += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(b < B));
+            }
+        }
+        lane_iters = wave_sum(cnt);
+        iters = wave_max(cnt);
+    }
+    if (lane == 0) {
+        unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+        atomicAdd(cs, (unsigned long long)(rays + lane_iters));  // the first lookup came from k_agents
+        atomicAdd(cs + 1, (unsigned long long)rays);
+        if (K.count_slots) {
+            atomicAdd(cs + 2, (unsigned long long)iters * (all_fast ? 128ull : 64ull));
+            atomicAdd(cs + 3, (unsigned long long)passes);
+            atomicAdd(cs + 4, (unsigned long long)refills);
+        }
+    }
+}
+
 // k_rays_fx_tail: the handed-off rays, traced to the end with lane refill.
 // Persistent waves take records from the queue (one atomic per refill);
 // whenever >= kTailRefill lanes are idle, the finished lanes write their
@@ -1571,7 +1839,8 @@ __global__ void __launch_bounds__(kBlock) k_post(StepArgs a) {
                 const double ang = beam_angle(b, a.fov, a.beam_incr);
                 if (!(fabs(wrap_pm_pi(oth + ang - wc)) <= wh)) continue;
                 double bt = oth + ang + kPi / 2.;
-                double v30 = cos(bt), v31 = sin(bt);
+                double v31, v30;
+                cr_sincos(bt, v31, v30);
                 double cur = scan[i * B + b];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -1737,7 +2006,11 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
             const f110_params &pi = a.pa[i];
             get_vertices(sh.pose0[j][0], sh.pose0[j][1], sh.pose0[j][2], pi.length, pi.width, sh.rv[pr]);
         }
-        if (lane < A) sh.ego[lane] = atan2(sin(sh.stl[lane][4]), cos(sh.stl[lane][4]));  // post-TTC yaw
+        if (lane < A) {  // atan2(sin, cos) of the post-TTC yaw
+            double ys, yc;
+            cr_sincos(sh.stl[lane][4], ys, yc);
+            sh.ego[lane] = atan2(ys, yc);
+        }
         wave_sync();
         for (int w = lane; w < 4 * NP; w += 64) {  // get_blocked_view_indices, one vertex per lane
             const int pr = w >> 2, q = w & 3;
@@ -1790,7 +2063,8 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
             const double ang = beam_angle(b, a.fov, a.beam_incr);
             if (!(fabs(wrap_pm_pi(oth + ang - sh.wcen[pr])) <= sh.whalf[pr])) continue;  // box_beam_window
             const double bt = oth + ang + kPi / 2.;
-            const double v30 = cos(bt), v31 = sin(bt);
+            double v31, v30;
+            cr_sincos(bt, v31, v30);
             double cur = scan[i * B + b];
             const double cur0 = cur;
 #pragma unroll
@@ -1902,6 +2176,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
             g2 = dim3((unsigned)(ra.HB + ra.G4 * ra.nch));
         }
         const int v = (ch ? 8 : 0) + (rot ? 4 : 0) + (mask ? 2 : 0) + (single ? 0 : 1);  // HANDOFF for A >= 2
+        unsigned lds_bytes = a.fx_lds;  // dynamic LDS of the fixed-point kernels (F110_FX_LDS: occupancy probe)
         const void *fn[16] = {
             reinterpret_cast<const void *>(&k_rays_tiled<false, false, false, false>),
             reinterpret_cast<const void *>(&k_rays_tiled<false, false, true, false>),
@@ -2003,7 +2278,21 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                         ra.fxp_hy = (double)a.tmap.H + 2.0 * P - Rn;
                         f = fn_p[N - 2][v2];
                     }
-                    if (a.fx_refill && N == 2 && !mask && ra.HB == 0 && !ra.wcost) {
+                    const int pool = a.fx_pool;
+                    if (pool > 0 && pool <= 2 && N == 2 && pad && !mask && ra.HB == 0 && !ra.wcost && a.pcost &&
+                        pool * ra.nch <= 64) {
+                        // k_rays_fxp: lane-level refill over a pool of cars per wave (F110_FX_POOL)
+                        const int NC = pool;
+                        const void *fp[2][2] = {{reinterpret_cast<const void *>(&k_rays_fxp<false, 1>),
+                                                 reinterpret_cast<const void *>(&k_rays_fxp<true, 1>)},
+                                                {reinterpret_cast<const void *>(&k_rays_fxp<false, 2>),
+                                                 reinterpret_cast<const void *>(&k_rays_fxp<true, 2>)}};
+                        f = fp[NC - 1][single ? 0 : 1];
+                        ra.pcost = a.pcost;
+                        ra.pool_T = a.pool_T;
+                        g2 = dim3((unsigned)((ra.EA + NC - 1) / NC));
+                        lds_bytes = (unsigned)(NC * sizeof(PoolCar) + 256 + NC * a.B * 2);
+                    } else if (a.fx_refill && N == 2 && !mask && ra.HB == 0 && !ra.wcost) {
                         // one wave per car, two chunk slots with refill (k_rays_fxr; no heavy-first)
                         const void *fr[8] = {reinterpret_cast<const void *>(&k_rays_fxr<false, false, 2>),
                                              reinterpret_cast<const void *>(&k_rays_fxr<true, false, 2>),
@@ -2033,7 +2322,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                        : reinterpret_cast<const void *>(&k_rays_tiled<false, false, true, true, true>);
         ra.wtrace = a.wtrace;
         const unsigned bdim = ch ? 64u * (unsigned)ra.wpb : (unsigned)kBlock;
-        if ((e = hipLaunchKernel(f, g2, dim3(bdim), args, fx ? a.fx_lds : 0u, s)) != hipSuccess) return e;
+        if ((e = hipLaunchKernel(f, g2, dim3(bdim), args, fx ? lds_bytes : 0u, s)) != hipSuccess) return e;
         if (fx && a.ev) {  // the handed-off stragglers (the queue is read on the device)
             const unsigned tg = (unsigned)std::max<int64_t>(
                 a.ev_P, std::min<int64_t>(kTailWaves, ((int64_t)a.ev_cap + 63) / 64) / a.ev_P * a.ev_P);

@@ -525,7 +525,8 @@ __global__ void __launch_bounds__(64 * kRwWaves) k_reward(RewardArgs a) {
         double r_flank = 0.0;
         {  // _rot_into_opp_frame + flank window (:64-70, :332-337)
             const double dx = ex - ox, dy = ey - oy;
-            const double c = cos(-oth), s = sin(-oth);
+            double s, c;
+            cr_sincos(-oth, s, c);
             const double x_rel = c * dx - s * dy;
             const double y_rel = s * dx + c * dy;
             if (0.2 <= x_rel && x_rel <= 1.8 && 0.25 <= fabs(y_rel) && fabs(y_rel) <= 0.8) {

@@ -259,6 +259,12 @@ class BatchSim:
                    "f110_read_simt")
         return lk.value, sl.value
 
+    def read_counter(self, idx: int) -> int:
+        """Diagnostic counter idx summed over its lines (f110_read_counter)."""
+        v = ctypes.c_uint64()
+        _lib.check(self.L.f110_read_counter(self.ctx, int(idx), ctypes.byref(v), self._stream()), "f110_read_counter")
+        return v.value
+
     def reset_counters(self):
         _lib.check(self.L.f110_reset_counters(self.ctx, self._stream()), "f110_reset_counters")
 
@@ -300,6 +306,16 @@ class BatchSim:
         """k_rays_fxr's waves per car for unmasked steps (f110_ray_refill), 0 when k_rays_fxn /
         k_rays_fx trace this context's rays."""
         return _lib.check(self.L.f110_ray_refill(self.ctx), "f110_ray_refill")
+
+    def set_ray_pool(self, cars: int, threshold: int = 0):
+        """k_rays_fxp's cars per wave (0: off) and refill threshold (0: keep), with the padded EDT
+        (f110_set_ray_pool)."""
+        _lib.check(self.L.f110_set_ray_pool(self.ctx, int(cars), int(threshold)), "f110_set_ray_pool")
+
+    @property
+    def ray_pool(self) -> int:
+        """k_rays_fxp's cars per wave for unmasked steps (f110_ray_pool), 0 when another ray kernel runs."""
+        return _lib.check(self.L.f110_ray_pool(self.ctx), "f110_ray_pool")
 
     def close(self):
         if getattr(self, "ctx", None):

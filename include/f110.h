@@ -229,6 +229,10 @@ F110_API int f110_collision_multiple(const double *verts, int64_t M, int32_t N, 
  * `stream`).  Used for the measured mean lookups per ray (roofline). */
 F110_API int f110_read_counters(f110_ctx *ctx, uint64_t *lookups, uint64_t *rays, void *stream);
 F110_API int f110_reset_counters(f110_ctx *ctx, void *stream);
+/* Diagnostic: the sum over the counter lines of counter idx (0..15): 0
+ * lookups, 1 rays, 2 lane slots (f110_read_simt), 3 / 4 k_rays_fxp's refill
+ * passes / slot refills (with f110_set_simt on). */
+F110_API int f110_read_counter(f110_ctx *ctx, int32_t idx, uint64_t *value, void *stream);
 /* SIMT efficiency of the fixed-point ray loops (k_rays_fx / k_rays_fxn, the
  * default kernels) since the last counter reset: loop_lookups = lookups made
  * inside the loop (all lookups less the first one per ray, which k_agents
@@ -298,6 +302,16 @@ F110_API int f110_ray_refill(const f110_ctx *ctx);
  * GPU's cars over several contexts (streams.StreamShards): the size rule is
  * about the cars the GPU traces at once, not one context's.  Any time. */
 F110_API int f110_set_ray_refill(f110_ctx *ctx, int32_t waves);
+/* Cars per wave of k_rays_fxp (lane-level refill over a pool of cars: every
+ * lane has two ray slots, a slot whose ray has ended takes the pool's next ray;
+ * the pool's 64-beam chunks are queued by the previous step's per-chunk cost),
+ * or 0 when the context steps with k_rays_fxr / k_rays_fxn / k_rays_fx.
+ * Scheduling only: results are bit-identical to the other ray kernels. */
+F110_API int f110_ray_pool(const f110_ctx *ctx);
+/* Set k_rays_fxp's cars per wave (0..2; 0 = off) and its refill threshold
+ * (ended slots, 1..128; 0 keeps the current one); switches the context to the
+ * padded EDT.  F110_FX_POOL / F110_FX_POOL_T set the defaults.  Any time. */
+F110_API int f110_set_ray_pool(f110_ctx *ctx, int32_t cars, int32_t threshold);
 
 /* Sets the rays per lane of the fixed-point ray kernel (1..4) before the
  * context's first reset/step.  The size-based default looks at this
@@ -356,6 +370,10 @@ F110_API int f110_host_cell_index(int32_t H, int32_t W, double resolution, const
  * ray_cast visits for an opponent box whose angular window at the scan
  * origin is center +- half (world frame), for a car at yaw.  Host only; the
  * CPU tests check they contain every beam inside the window. */
+/* Host copy of the device's cr_sincos (the ray_cast / box / dynamics sin and
+ * cos: double-double evaluation, one rounding; matches NumPy's (glibc's)
+ * np.sin / np.cos).  Test hook, no reference counterpart. */
+F110_API void f110_host_sincos(const double *x, int64_t n, double *sn, double *cs);
 /* NumPy's float32 np.cos (cos_op != 0) / np.sin over n values, as the
  * device evaluates F110Env.reset's float32 start_rot (test hook). */
 F110_API void f110_host_np_sincosf(const float *x, int64_t n, int32_t cos_op, float *out);

@@ -173,6 +173,127 @@ def sim_lane(L, NS=2, T=32, order="desc", pair=False):
     return iters, events, served, lane_iters
 
 
+def sim_queue(Q, NS=2, T=32):
+    """Lane refill over per-wave queues Q [n_waves, U] of ray iteration counts
+    (-1 = padding at the end).  Returns per-wave (iters, events, lane_iters)."""
+    n, U = Q.shape
+    qlen = (Q >= 0).sum(1)
+    rem = np.full((n, 64 * NS), -1, np.int64)
+    k0 = np.minimum(64 * NS, qlen)
+    for c in range(n):
+        rem[c, :k0[c]] = Q[c, :k0[c]]
+    nxt = k0.copy()
+    iters = np.zeros(n, np.int64)
+    events = np.zeros(n, np.int64)
+    lane_iters = np.zeros(n, np.int64)
+    while True:
+        ended = rem == 0
+        n_end = ended.sum(1)
+        tracing = (rem > 0).any(1)
+        ev = (n_end > 0) & ((n_end >= T) | ~tracing)
+        if not ev.any() and not tracing.any():
+            break
+        for c in np.flatnonzero(ev):
+            free = np.flatnonzero(ended[c])
+            events[c] += len(np.unique(free // 64))  # slot arrays (r = j // 64) the pass touches
+            k = min(free.size, qlen[c] - nxt[c])
+            if k > 0:
+                rem[c, free[:k]] = Q[c, nxt[c]:nxt[c] + k]
+                nxt[c] += k
+            rem[c, free[k:]] = -1
+        act = rem > 0
+        wa = act.any(1)
+        iters += wa
+        lane_iters += act.sum(1)
+        rem[act] -= 1
+    return iters, events, lane_iters
+
+
+def pooled_queues(need, C, order, pred=None):
+    """Queues of C consecutive cars per wave.  order: 'chunk' (descending chunk
+    index, the C cars' chunk k together), 'lpt' (rays sorted by their own
+    cost: an oracle bound), 'pred' (64-beam chunks sorted by the predicted
+    per-chunk max from `pred`, the previous step's counts)."""
+    n, B = need.shape
+    nch = -(-B // 64)
+    W = n // C
+    out = []
+    for w in range(W):
+        cars = need[w * C:(w + 1) * C]
+        if order == "lpt":
+            q = np.sort(cars.ravel())[::-1]
+        else:
+            pad = np.full((C, nch * 64), -1, np.int64)
+            pad[:, :B] = cars
+            ch = pad.reshape(C, nch, 64)
+            if order == "chunk":
+                q = ch[:, ::-1].transpose(1, 0, 2).reshape(-1)
+            else:
+                pp = np.zeros((C, nch * 64), np.int64)
+                pp[:, :B] = pred[w * C:(w + 1) * C]
+                cost = pp.reshape(C, nch, 64).max(2).ravel()
+                o = np.argsort(-cost, kind="stable")
+                q = ch.reshape(C * nch, 64)[o].reshape(-1)
+            q = q[q >= 0] if False else q
+        out.append(q)
+    Q = np.stack(out)
+    # move padding (-1) to the end, keep order
+    res = np.full_like(Q, -1)
+    for i in range(Q.shape[0]):
+        v = Q[i][Q[i] >= 0]
+        res[i, :v.size] = v
+    return res
+
+
+def consecutive_counts(n_envs=1024, steps=60, seed=1):
+    """Pairs of consecutive steps' counts (t-1, t) of a random-action rollout."""
+    tm = load_map("Spielberg_map")
+    sp = centerline_spawns("Spielberg", 1)[:, 0]
+    sc = O.OracleScanner(tm.free_mask, tm.resolution, tm.origin)
+    sim = O.OracleSim(sc, n_envs, 1)
+    rng = np.random.default_rng(seed)
+    sim.reset(sp[rng.integers(0, sp.shape[0], n_envs)])
+    prev = None
+    pairs = []
+    for t in range(1, steps + 1):
+        a = np.stack([rng.uniform(-0.4189, 0.4189, n_envs), rng.uniform(0, 20, n_envs)], 1)
+        _, col = sim.step(a[:, None, :], threads=8)
+        if t >= steps - 1:
+            p = np.stack([sim.state[:, 0], sim.state[:, 1], sim.state[:, 4]], 1)
+            _, L, _ = sc.scan(p, with_probe=True, threads=8)
+            if prev is not None:
+                pairs.append((prev, L.astype(np.int64)))
+            prev = L.astype(np.int64)
+        hit = np.flatnonzero(col[:, 0] > 0)
+        if hit.size:
+            st = sim.state.copy()
+            sim.reset(sp[rng.integers(0, sp.shape[0], n_envs)])
+            keep = np.ones(n_envs, bool)
+            keep[hit] = False
+            sim.state[keep] = st[keep]
+    return pairs[-1]
+
+
+def main_pool():
+    prev, cur = consecutive_counts(int(os.environ.get("LR_ENVS", 1024)))
+    need, pneed = cur - 1, prev - 1
+    n = need.shape[0]
+    w = need.sum()
+    for C in (1, 2, 3, 4):
+        for NS in (2,):
+            for order in ("chunk", "pred"):
+                for T in (32, 48, 64, 80, 96, 112):
+                    Q = pooled_queues(need, C, order, pneed)
+                    it, ev, li = sim_queue(Q, NS, T)
+                    print(json.dumps({"C": C, "NS": NS, "order": order, "T": T,
+                                      "iters_per_car": float(it.sum() / n), "events_per_car": float(ev.sum() / n),
+                                      "cost_per_car(40/it,70/ev)": float((40 * it.sum() + 70 * ev.sum()) / n),
+                                      "served_per_event": float(1080 * n / max(ev.sum(), 1)),
+                                      "simt": float(w / (it.sum() * 64 * NS)),
+                                      "wave_iters_p50_p90_max": [float(np.percentile(it, 50)), float(np.percentile(it, 90)), int(it.max())]}),
+                          flush=True)
+
+
 def main():
     N = int(os.environ.get("LR_ENVS", 1024))
     L = rollout_counts(n_envs=N)
@@ -201,4 +322,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if os.environ.get("LR_POOL"):
+        main_pool()
+    else:
+        main()

@@ -17,7 +17,7 @@ from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns, load_map  # no
 from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim  # noqa: E402
 
 KNOBS = ("F110_RAY_KERNEL", "F110_CHUNK_ORDER", "F110_HEAVY_T", "F110_RAY_WPB", "F110_HEAVY_DIV", "F110_EVICT",
-         "F110_EVICT_T", "F110_EVICT_K", "F110_FX_LDS", "F110_FX_LEAN", "F110_FX_ILP", "F110_FX_TABLE", "F110_FX_PAIR", "F110_FX_PAD", "F110_SIMT", "F110_FX_REFILL", "F110_FX_SLOTS")
+         "F110_EVICT_T", "F110_EVICT_K", "F110_FX_LDS", "F110_FX_LEAN", "F110_FX_ILP", "F110_FX_TABLE", "F110_FX_PAIR", "F110_FX_PAD", "F110_SIMT", "F110_FX_REFILL", "F110_FX_SLOTS", "F110_FX_POOL", "F110_FX_POOL_T")
 
 
 def parse_variants(spec):
@@ -92,6 +92,7 @@ def main():
         # timing: interleaved rounds, minimal outputs (the bench's timed mode)
         times = {n: [] for n in sims}
         look = {}
+        diag = {}
         for _ in range(rounds):
             for n, sm in sims.items():
                 sm.reset(p0)
@@ -105,8 +106,14 @@ def main():
                 pk = sm.profile_end()
                 lk, rays = sm.read_counters()
                 look[n] = lk / max(rays, 1)
+                if os.environ.get("F110_SIMT") == "1" or "F110_SIMT" in variants[n]:
+                    cars = E * A * steps
+                    diag[n] = {"simt": (lk - rays) / max(sm.read_counter(2), 1),
+                               "slot_iters_per_car": sm.read_counter(2) / cars,
+                               "passes_per_car": sm.read_counter(3) / cars,
+                               "refills_per_car": sm.read_counter(4) / cars}
                 times[n].append(pk)
-        line = {"identical": ident, "mean_lookups": look}
+        line = {"identical": ident, "mean_lookups": look, "diag": diag}
         for n, ts in times.items():
             line[n] = {key: float(np.median([t[key] for t in ts])) for key in ts[0]}
         res["by_envs"][str(E)] = line

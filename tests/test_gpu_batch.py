@@ -362,3 +362,46 @@ def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
         for t, (a, b) in enumerate(zip(outs[0], outs[k])):
             for x, y in zip(a, b):
                 assert torch.equal(x, y), f"step {t}"
+
+
+@pytest.mark.parametrize("A,beams", [(1, 1080), (2, 1080), (1, 333), (1, 64)])
+def test_pool_kernel_identical(tracks, gpu, monkeypatch, A, beams):
+    """k_rays_fxp (F110_FX_POOL = 1 or 2 cars per wave: two ray slots per
+    lane, a slot whose ray has ended takes the pool's next ray, the pool's
+    chunks queued by the previous step's per-chunk cost) against k_rays_fxn:
+    scans, obs, collisions and states bit-identical over 25 noisy steps with
+    autoreset and a masked reset (which runs k_rays_fxn), an odd car count
+    (the last wave's pool is short), refill thresholds 1, 80 and 128; the
+    counters (lookups, rays) equal k_rays_fxn's."""
+    E = 203
+    sp = _spawns(A)
+    rng = np.random.default_rng(beams + A + 7)
+    poses = sp[rng.integers(0, sp.shape[0], E)]
+    acts = np.stack([rng.uniform(-0.4189, 0.4189, (25, E, A)), rng.uniform(0, 20, (25, E, A))], -1).astype(np.float32)
+    mask = rng.random(E) < 0.5
+    monkeypatch.setenv("F110_FX_ILP", "2")
+    monkeypatch.setenv("F110_HEAVY_T", "0")
+    monkeypatch.setenv("F110_FX_REFILL", "0")
+    outs, ctrs = [], []
+    for pool, T, pad in (("0", "80", "0"), ("1", "80", "1"), ("2", "80", "1"), ("2", "1", "1"), ("2", "128", "1")):
+        monkeypatch.setenv("F110_FX_POOL", pool)
+        monkeypatch.setenv("F110_FX_POOL_T", T)
+        monkeypatch.setenv("F110_FX_PAD", pad)
+        sim = _sim(tracks, gpu, n_envs=E, n_agents=A, num_beams=beams, noise_std=0.01, autoreset=True,
+                   spawn_poses=sp, seed=6, keep_f64_scans=True)
+        assert sim.ray_pool == int(pool)
+        sim.reset(poses)
+        sim.reset_counters()
+        rec = []
+        for t in range(25):
+            o = sim.reset(poses[::-1].copy(), env_mask=mask) if t == 12 else sim.step(acts[t])
+            rec.append((o.scans_f64.clone(), o.obs.clone(), o.collisions.clone(), sim.agent_states().clone()))
+        torch.cuda.synchronize()
+        outs.append(rec)
+        ctrs.append(sim.read_counters())
+        sim.close()
+    for k in range(1, len(outs)):
+        assert ctrs[0] == ctrs[k], k
+        for t, (a, b) in enumerate(zip(outs[0], outs[k])):
+            for x, y in zip(a, b):
+                assert torch.equal(x, y), f"variant {k} step {t}"

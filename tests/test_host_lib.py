@@ -262,3 +262,53 @@ def test_np_float32_sincos_matches_numpy():
         want = ref(x)
         same = (out == want) | (np.isnan(out) & np.isnan(want))
         assert same.all(), (op, x[~same][:5], out[~same][:5], want[~same][:5])
+
+
+def _dec_sincos(v):
+    """sin and cos of the double v to ~55 digits (Taylor series after reduction
+    by a 100-digit 2 pi): the correctly rounded double is float() of it."""
+    from decimal import Decimal, getcontext
+    getcontext().prec = 60
+    pi = Decimal("3.14159265358979323846264338327950288419716939937510582097494459230781640628620899862803")
+    x = Decimal(float(v))
+    r = x - (x / (2 * pi)).to_integral_value() * 2 * pi
+    out = []
+    for t, k in ((r, 1), (Decimal(1), 0)):
+        acc = Decimal(0)
+        while abs(t) > Decimal(10) ** -58:
+            acc += t
+            t = -t * r * r / ((k + 1) * (k + 2))
+            k += 2
+        out.append(float(acc))
+    return out
+
+
+def test_cr_sincos_matches_numpy():
+    """f110_device.h cr_sincos (the ray_cast beam direction, box vertices,
+    dynamics and start_rot sin / cos, double-double + one rounding) against
+    NumPy's float64 np.sin / np.cos (glibc here), the reference's own trig:
+    bit-exact but on a small rest (< 0.3 % of arguments over scan / yaw
+    ranges), and on a sample of that rest cr_sincos is the correctly rounded
+    value (checked to 55 digits), i.e. the rest is glibc's own last-ulp error.
+    Signed zeros, NaN and |x| >= 2^20 (library fallback) too."""
+    import ctypes
+    from f110_gymnasium_ros2_jazzy_amd import _lib
+    L = _lib.load()
+    rng = np.random.default_rng(17)
+    x = np.concatenate([rng.uniform(-8, 8, 600_000), rng.uniform(-1e-3, 1e-3, 50_000),
+                        np.arange(-64, 65) * (np.pi / 4), np.array([0.0, -0.0, 1e-300, 2.0 ** 20, 1e7])])
+    s, c = np.empty_like(x), np.empty_like(x)
+    L.f110_host_sincos(x.ctypes.data_as(ctypes.c_void_p), x.size, s.ctypes.data_as(ctypes.c_void_p),
+                       c.ctypes.data_as(ctypes.c_void_p))
+    for got, ref, name in ((s, np.sin(x), "sin"), (c, np.cos(x), "cos")):
+        bad = np.flatnonzero(got != ref)
+        assert bad.size < 0.003 * x.size, (name, bad.size)
+        for i in bad[:: max(1, bad.size // 40)]:
+            want = _dec_sincos(x[i])[0 if name == "sin" else 1]
+            assert got[i] == want, (name, x[i], got[i], ref[i], want)
+    assert np.signbit(s[x.size - 4]) and s[x.size - 4] == 0.0 and c[x.size - 4] == 1.0  # sin(-0.0) = -0.0
+    xn = np.array([np.nan, np.inf])
+    sn, cn = np.empty_like(xn), np.empty_like(xn)
+    L.f110_host_sincos(xn.ctypes.data_as(ctypes.c_void_p), 2, sn.ctypes.data_as(ctypes.c_void_p),
+                       cn.ctypes.data_as(ctypes.c_void_p))
+    assert np.isnan(sn).all() and np.isnan(cn).all()
