@@ -110,6 +110,7 @@ struct f110_ctx {
     int32_t fx_refill = 0;   // waves per car of k_rays_fxr (0 = k_rays_fxn; F110_FX_REFILL overrides)
     int32_t fx_pool = 0;     // cars per k_rays_fxp wave (lane-level refill; 0 = off; F110_FX_POOL)
     int32_t pool_T = 80;     // k_rays_fxp's refill threshold in ended slots (F110_FX_POOL_T)
+    bool fused = false;      // single-agent steps as one k_step1 launch (f110_set_fused / F110_FUSED)
     uint8_t *pcost = nullptr;  // [EA][nch] k_rays_fxp's per-chunk costs (queue order of the next launch)
     bool count_slots = false;  // f110_set_simt / F110_SIMT: lane-slot counter of the fixed-point loops (f110_read_simt)
     int fx_ilp = 1;         // rays per lane (F110_FX_ILP; default by car count)
@@ -543,6 +544,8 @@ static hipError_t acquire_map_tables(int device, const uint32_t *edt_k, int32_t 
     return hipSuccess;
 }
 
+static int ensure_padded_table(f110_ctx *ctx);
+
 extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cfg, const f110_params *params,
                            const uint32_t *edt_k, int32_t H, int32_t W, double resolution, const double origin[3],
                            const double *spawn_poses, int32_t n_spawn) {
@@ -733,6 +736,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (const char *v = std::getenv("F110_FX_REFILL")) c->fx_refill = std::max(0, std::min(16, std::atoi(v)));
     if (const char *v = std::getenv("F110_FX_SLOTS")) c->fx_slots = std::atoi(v) == 3 ? 3 : 2;
     if (const char *v = std::getenv("F110_FX_POOL")) c->fx_pool = std::max(0, std::min(2, std::atoi(v)));
+    if (const char *v = std::getenv("F110_FUSED")) c->fused = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FX_POOL_T")) c->pool_T = std::max(1, std::min(128, std::atoi(v)));
     if (fx_ok) {
         hipError_t ep = c->alloc(&c->pcost, EA * (size_t)c->nch);
@@ -763,6 +767,10 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) return cleanup(F110_E_HIP, std::string("f110_create upload: ") + hipGetErrorString(e));
+    if (c->fused && fx_ok) {  // F110_FUSED: k_step1 on the padded table, no heavy-first list
+        c->heavy_off = true;
+        if (ensure_padded_table(c) != F110_OK) return cleanup(F110_E_HIP, "f110_create: padded table");
+    }
     size_t lds = step_lds_bytes(C.n_agents, C.n_beams);
     if (lds > 160 * 1024) return cleanup(F110_E_INVALID, "f110_create: n_agents*n_beams too large for LDS");
     e = prepare_env_step(lds);
@@ -904,23 +912,72 @@ extern "C" int f110_reset(f110_ctx *ctx, const double *poses, const uint8_t *env
     return F110_OK;
 }
 
-extern "C" int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dtype, const f110_outputs *out,
-                         void *stream) {
-    if (!ctx || !actions) return fail(F110_E_INVALID, "f110_step: null argument");
+// k_step1 (the single-agent step in one launch) runs where the context traces
+// with the fixed-point kernels on the padded table, without heavy-first lists
+static bool fused_ok(const f110_ctx *c) {
+    return c->fused && c->cfg.n_agents == 1 && c->ray_kernel == 3 && !c->evict && !c->fx_tiled && c->fx_pad &&
+           c->rmp && (c->heavy_off || !c->wcost) && (c->cfg.n_beams + 63) / 64 <= kMaxChunks;
+}
+
+static int step_n(f110_ctx *ctx, const void *actions, int32_t actions_dtype, int32_t n, int64_t step_stride,
+                  const f110_outputs *out, void *stream, const char *who) {
+    if (!ctx || !actions) return fail(F110_E_INVALID, std::string(who) + ": null argument");
     if (actions_dtype != F110_F32 && actions_dtype != F110_F64)
-        return fail(F110_E_INVALID, "f110_step: actions_dtype must be F110_F32 or F110_F64");
+        return fail(F110_E_INVALID, std::string(who) + ": actions_dtype must be F110_F32 or F110_F64");
+    if (n < 1) return fail(F110_E_INVALID, std::string(who) + ": n_steps must be >= 1");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     if (out && out->obs_stride && out->obs_stride < (int64_t)ctx->cfg.n_beams + 4 * ctx->cfg.n_agents)
-        return fail(F110_E_INVALID, "f110_step: obs_stride < n_beams + 4*n_agents");
+        return fail(F110_E_INVALID, std::string(who) + ": obs_stride < n_beams + 4*n_agents");
     StepArgs a = make_step_args(ctx, out);
     a.mode = 0;
     a.heavy_build = a.heavy_use = (a.wcost && a.ray_kernel >= 2 && !ctx->heavy_off) ? 1 : 0;  // not on resets
-    if (actions_dtype == F110_F64)
-        a.actions_f64 = static_cast<const double *>(actions);
-    else
-        a.actions = static_cast<const float *>(actions);
-    HIP_TRY(launch_env_step(a, (hipStream_t)stream, ctx->next_prof_events()));
+    const int64_t packed = (int64_t)ctx->cfg.n_envs * ctx->cfg.n_agents * 2;  // action elements per step
+    if (step_stride != 0 && step_stride < packed)
+        return fail(F110_E_INVALID, std::string(who) + ": step_stride < n_envs * n_agents * 2");
+    const int64_t stride = step_stride ? step_stride : packed;
+    if (fused_ok(ctx)) {
+        if (actions_dtype == F110_F64)
+            a.actions_f64 = static_cast<const double *>(actions);
+        else
+            a.actions = static_cast<const float *>(actions);
+        HIP_TRY(launch_step1(a, n, stride, (hipStream_t)stream, ctx->next_prof_events()));
+        return F110_OK;
+    }
+    for (int32_t t = 0; t < n; ++t) {
+        if (actions_dtype == F110_F64)
+            a.actions_f64 = static_cast<const double *>(actions) + (size_t)t * stride;
+        else
+            a.actions = static_cast<const float *>(actions) + (size_t)t * stride;
+        if (t) a.parity = (int32_t)(ctx->launch_n++ & 1);
+        HIP_TRY(launch_env_step(a, (hipStream_t)stream, ctx->next_prof_events()));
+    }
     return F110_OK;
+}
+
+extern "C" int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dtype, const f110_outputs *out,
+                         void *stream) {
+    return step_n(ctx, actions, actions_dtype, 1, 0, out, stream, "f110_step");
+}
+
+extern "C" int f110_step_n(f110_ctx *ctx, const void *actions, int32_t actions_dtype, int32_t n_steps,
+                           int64_t step_stride, const f110_outputs *out, void *stream) {
+    return step_n(ctx, actions, actions_dtype, n_steps, step_stride, out, stream, "f110_step_n");
+}
+
+extern "C" int f110_set_fused(f110_ctx *ctx, int32_t on) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_set_fused: null context");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    ctx->fused = on != 0;
+    if (ctx->fused && ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled) {
+        ctx->heavy_off = true;  // k_step1 keeps no heavy-first list
+        return ensure_padded_table(ctx);
+    }
+    return F110_OK;
+}
+
+extern "C" int f110_fused(const f110_ctx *ctx) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_fused: null context");
+    return fused_ok(ctx) ? 1 : 0;
 }
 
 extern "C" int f110_set_reset_dtype(f110_ctx *ctx, int32_t dtype) {

@@ -180,6 +180,15 @@ struct RayArgs {
     int32_t pool_T;
 };
 
+// k_step1's argument block (the fused single-agent step over n steps): RayArgs
+// first, so the ray helpers that read the kernarg segment as a RayArgs work.
+struct FusedArgs {
+    RayArgs r;
+    StepArgs s;
+    int32_t nsteps;
+    int64_t act_stride;  // action elements between consecutive steps' [E][A][2] blocks
+};
+
 constexpr int kEvStride = 32;    // u32 per hand-off partition counter line (128 B)
 constexpr int kEvMaxParts = 256;
 
@@ -329,6 +338,8 @@ hipError_t launch_adam(const AdamArgs &a, hipStream_t s);
 size_t step_lds_bytes(int A, int B);
 hipError_t prepare_env_step(size_t lds_bytes);
 hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev = nullptr);  // ev: 4 events or null
+// k_step1: n single-agent steps in one launch (padded fixed-point table, mode 0, no mask)
+hipError_t launch_step1(const StepArgs &a, int32_t n, int64_t act_stride, hipStream_t s, hipEvent_t *ev = nullptr);
 hipError_t launch_scan_batch(const ScanArgs &a, hipStream_t s);
 hipError_t launch_gap_follow(const GapFollowArgs &a, hipStream_t s);
 hipError_t launch_reward(const RewardArgs &a, hipStream_t s);

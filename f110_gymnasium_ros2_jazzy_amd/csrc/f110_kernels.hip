@@ -1662,6 +1662,7 @@ struct EpiEnv {  // per env
     double tprev, ct, st;
     uint64_t nstep;
     uint32_t episode;
+    uint32_t pending;  // k_step1: the autoreset flag for the next step (env_epilogue's vs)
 };
 
 __device__ __forceinline__ void epilogue_load_car(const StepArgs &a, int g, EpiCar &c) {
@@ -1683,8 +1684,11 @@ __device__ __forceinline__ void epilogue_load_env(const StepArgs &a, int e, EpiE
 
 // stl: post-TTC state rows of its A agents (x at [i*stride], y at
 // [i*stride + 1]); col: collision flags; cars / env: the prefetched inputs.
+// vs / cs (optional, k_step1): the updated env / car bookkeeping, kept in
+// registers across the steps of one launch.
 __device__ void env_epilogue(const StepArgs &a, int e, const double *stl, int stride, const int32_t *col,
-                             int do_reset, const EpiEnv &v, const EpiCar *cars) {
+                             int do_reset, const EpiEnv &v, const EpiCar *cars, EpiEnv *vs = nullptr,
+                             EpiCar *cs = nullptr) {
     const int A = a.A;
     const double tnow = (do_reset ? 0.0 : v.tprev) + a.dt;
     a.sim_time[e] = tnow;
@@ -1714,6 +1718,11 @@ __device__ void env_epilogue(const StepArgs &a, int e, const double *stl, int st
         a.near_start[g] = (uint8_t)ns;
         float lc = (float)(tg / 2);
         float lt = tg < 4 ? (float)tnow : c.lt;
+        if (cs) {
+            cs[i].tg = tg;
+            cs[i].ns = ns;
+            cs[i].lt = lt;
+        }
         a.lap_counts[g] = lc;
         a.lap_times[g] = lt;
         if (a.out.lap_counts) a.out.lap_counts[g] = lc;
@@ -1728,8 +1737,15 @@ __device__ void env_epilogue(const StepArgs &a, int e, const double *stl, int st
     // autoreset spawn draws count episodes from the env's last explicit reset, so a
     // reset replays the same trajectory whatever ran before it (the bench's
     // trajectory digest compares N = 1 and N > 1 runs after a clock ramp)
-    if (do_reset) a.episode[e] = a.mode == 0 ? v.episode + 1 : 0u;
+    const uint32_t ep = do_reset ? (a.mode == 0 ? v.episode + 1 : 0u) : v.episode;
+    if (do_reset) a.episode[e] = ep;
     a.nstep[e] = v.nstep + 1;
+    if (vs) {
+        vs->tprev = tnow;
+        vs->episode = ep;
+        vs->nstep = v.nstep + 1;
+        vs->pending = (a.autoreset && term) ? 1u : 0u;
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -1910,6 +1926,373 @@ __global__ void __launch_bounds__(64) k_post_single(StepArgs a) {
     }
     if (a.out.collisions) a.out.collisions[e] = (uint8_t)col;
     env_epilogue(a, e, stl, 2, &col, do_reset, env, &car);
+}
+
+// ------------------------------------------------------------------------
+// k_step1: the whole single-agent step in ONE launch, for n consecutive steps
+// (f110_step / f110_step_n).  One wave per car (env); per step:
+//   1. lane 0: k_agents' work for the car (autoreset, RaceCar.update_pose,
+//      scan pose, first lookup, the beam-index runs into LDS);
+//   2. every lane: the theta index of each beam into LDS (get_scan's
+//      sequential index, from the runs);
+//   3. the car's 1080 rays as k_rays_fxr traces them (two 64-beam chunk slots
+//      refilled as chunks end, padded EDT, noise after the clamp), the TTC test
+//      of each ray folded into one wave ballot;
+//   4. lane 0: k_post_single's work (TTC response, obs pose entries,
+//      collisions, _check_done / lap logic, the next step's autoreset flag).
+// The car's state stays in lane 0's registers from step to step (written back
+// once at the end), so a launch of n steps carries no hand-off buffer and no
+// per-step launch boundary: an env whose rays run long in one step overlaps
+// other envs' next steps instead of holding every env at a step boundary.
+// Per ray and per car the arithmetic is the three kernels', so the results
+// are bit-identical to n calls of the three-launch step
+// (test_step1_matches_three_launch_step).
+struct Step1Shared {
+    BeamRun runs[kMaxSeg];
+    double sx, sy, d00, vel;
+    uint64_t nstep;
+    int32_t nruns, do_reset, pad_[2];
+    // the car's persistent state between steps (lane 0; kept out of registers
+    // so that the ray loop keeps its 64 VGPRs)
+    double st[7], b0, b1;
+    int32_t cnt, pad2_;
+    EpiCar car;
+    EpiEnv env;
+};
+
+__device__ __forceinline__ const FusedArgs &fused_args() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *reinterpret_cast<const FusedArgs *>(__builtin_amdgcn_kernarg_segment_ptr());
+#else
+    return *static_cast<const FusedArgs *>(nullptr);
+#endif
+}
+
+// k_step1's lane-0 sections as real calls: their register needs (RK4 of
+// vehicle_dynamics_st: ~150 VGPRs inline) stay out of the ray loop's 64.
+__device__ __noinline__ void step1_agent(Step1Shared &sh, int g, int t) {
+    const FusedArgs &fa = fused_args();
+    const int B = fa.r.B;
+            const StepArgs &S = fused_args().s;
+            double st[7];
+#pragma unroll
+            for (int q = 0; q < 7; ++q) st[q] = sh.st[q];
+            double b0 = sh.b0, b1 = sh.b1;
+            int cnt = sh.cnt;
+            EpiCar car = sh.car;
+            EpiEnv env = sh.env;
+            double raw_steer, vel;
+            if (S.actions_f64) {
+                const double *ac = S.actions_f64 + (size_t)t * fa.act_stride + (size_t)g * 2;
+                raw_steer = ac[0];
+                vel = ac[1];
+            } else {
+                const float *ac = S.actions + (size_t)t * fa.act_stride + (size_t)g * 2;
+                raw_steer = (double)ac[0];
+                vel = (double)ac[1];
+            }
+            const int do_reset = env.pending ? 1 : 0;
+            if (do_reset) {  // RaceCar.reset (base_classes.py:183-204), then F110Env.reset's zero-action step
+                const uint64_t genv = (uint64_t)(S.env_offset + g);
+                const uint32_t k = spawn_draw(S.seed, genv, env.episode) % (uint32_t)S.n_spawn;
+                const double *pz = S.spawn + (size_t)k * 3;
+                double px = pz[0], py = pz[1], pth = pz[2];
+                if (S.reset_f32) {
+                    px = (double)(float)px;
+                    py = (double)(float)py;
+                    pth = (double)(float)pth;
+                }
+#pragma unroll
+                for (int q = 0; q < 7; ++q) st[q] = 0.0;
+                st[0] = px;
+                st[1] = py;
+                st[4] = pth;
+                b0 = b1 = 0.0;
+                cnt = 0;
+                raw_steer = 0.0;
+                vel = 0.0;
+                S.start[g] = px;
+                S.start[S.E + g] = py;
+                S.start[2 * S.E + g] = pth;
+                car.sx = px;
+                car.sy = py;
+                if (S.ego == 0) {  // start_rot (f110_env.py:448-451), as k_agents
+                    if (S.reset_f32) {
+                        const float nt = -(float)pth;
+                        env.ct = (double)np_sincosf(nt, true);
+                        env.st = (double)np_sincosf(nt, false);
+                    } else {
+                        double sr, crr;
+                        cr_sincos(-pth, sr, crr);
+                        env.ct = crr;
+                        env.st = sr;
+                    }
+                    S.start_rot[g] = env.ct;
+                    S.start_rot[S.E + g] = env.st;
+                }
+                car.tg = 0;
+                car.ns = 1;
+                car.lt = 0.0f;
+                S.toggles[g] = 0;
+                S.near_start[g] = 1;
+                S.lap_times[g] = 0.0f;
+                S.lap_counts[g] = 0.0f;
+            }
+            update_pose(st, b0, b1, cnt, raw_steer, vel, S.pa[0], S.dt, S.integrator);
+            const bool no_offset = S.lidar_dist == 0.0 && isfinite(st[4]);
+            double sy4 = 0.0, cy4 = 1.0;
+            if (!no_offset) cr_sincos(st[4], sy4, cy4);
+            const double sx = no_offset ? st[0] + 0.0 : st[0] + S.lidar_dist * cy4;
+            const double sy = no_offset ? st[1] + 0.0 : st[1] + S.lidar_dist * sy4;
+            sh.sx = sx;
+            sh.sy = sy;
+            sh.d00 = S.map.dt[cell_index(S.map, sx, sy)];  // first lookup (laser_models.py:129)
+            sh.vel = st[3];
+            sh.nstep = do_reset ? 0ull : env.nstep;
+            sh.do_reset = do_reset;
+            const double t0 = first_theta_index(st[4], S.fov, S.theta_dis);
+            sh.nruns = build_beam_runs(t0, S.inc, S.theta_dis, B, sh.runs, kMaxSeg);
+#pragma unroll
+            for (int q = 0; q < 7; ++q) sh.st[q] = st[q];
+            sh.b0 = b0;
+            sh.b1 = b1;
+            sh.cnt = cnt;
+            sh.car = car;
+            sh.env = env;
+        }
+
+__device__ __noinline__ void step1_post(Step1Shared &sh, int g, bool col) {
+    const int B = fused_args().r.B;
+            const StepArgs &S = fused_args().s;
+            const int do_reset = sh.do_reset;
+            EpiCar car = sh.car;
+            EpiEnv env = sh.env;
+            if (col) {  // RaceCar.check_ttc (base_classes.py:246-249): state[3:] = 0, yaw included
+#pragma unroll
+                for (int q = 3; q < 7; ++q) sh.st[q] = 0.0;
+            }
+            double st[7];
+#pragma unroll
+            for (int q = 0; q < 7; ++q) st[q] = sh.st[q];
+            if (S.out.obs) {
+                float *o = S.out.obs + (size_t)g * obs_row(S) + B;
+                o[0] = (float)st[0];
+                o[1] = (float)st[1];
+                o[2] = (float)wrap_angle(st[4]);
+                o[3] = col ? 1.0f : 0.0f;
+            }
+            if (S.out.collisions) S.out.collisions[g] = (uint8_t)col;
+            const double stl[2] = {st[0], st[1]};
+            const int32_t coli = col ? 1 : 0;
+            EpiEnv ev = env;
+            ev.nstep = do_reset ? 0ull : env.nstep;  // the counter this step's noise used (k_agents' noise_step)
+            env_epilogue(S, g, stl, 2, &coli, do_reset, ev, &car, &env, &car);
+            sh.car = car;
+            sh.env = env;
+        }
+
+__global__ void __launch_bounds__(64, 8) k_step1(FusedArgs fa) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char s1_smem[];
+    Step1Shared &sh = *reinterpret_cast<Step1Shared *>(s1_smem);
+    uint16_t *s_ti = reinterpret_cast<uint16_t *>(s1_smem + sizeof(Step1Shared));  // [B]
+    const RayArgs &a = fa.r;
+    const int lane = (int)threadIdx.x;
+    const int g = (int)blockIdx.x;  // car == env (A = 1)
+    const int B = a.B;
+    const int nch = (B + 63) >> 6;
+    const FxLoop L = fx_loop<3>(a);
+    const uint32_t P = (uint32_t)a.fxp_P;
+    uint32_t zero_v;  // in a VGPR for the whole trace (the select's other operand is its SGPR mask)
+    asm volatile("v_mov_b32 %0, %1" : "=v"(zero_v) : "s"(a.fx_zero));
+
+    // lane 0: the car's persistent state, in LDS for the whole launch
+    if (lane == 0) {
+        const StepArgs &S = fused_args().s;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) sh.st[k] = S.st[(size_t)k * S.E + g];
+        sh.b0 = S.sb[g];
+        sh.b1 = S.sb[S.E + g];
+        sh.cnt = S.scnt[g];
+        EpiCar car;
+        epilogue_load_car(S, g, car);
+        sh.car = car;
+        EpiEnv env;
+        env.tprev = S.sim_time[g];
+        env.ct = S.start_rot[g];
+        env.st = S.start_rot[S.E + g];
+        env.nstep = S.nstep[g];
+        env.episode = (uint32_t)S.episode[g];
+        env.pending = S.autoreset ? S.pending[g] : 0u;
+        sh.env = env;
+    }
+    uint32_t lanes_total = 0, lane_iters = 0;
+    for (int t = 0; t < fa.nsteps; ++t) {
+        // ---- 1. k_agents for this car (lane 0) ----
+        if (lane == 0) step1_agent(sh, g, t);
+        __syncthreads();  // one wave: the LDS hand-off
+        const double x00 = sh.sx, y00 = sh.sy, d00 = sh.d00, vcar = sh.vel;
+        const uint64_t nstep = sh.nstep;
+        const int nr = sh.nruns;
+        // ---- 2. the theta index of every beam (get_scan, laser_models.py:167-184) ----
+        {
+            int vlo = 0;  // lane k < nch: the run holding beam 64 k
+            if (lane < nch) {
+                int lo = 0, hi = nr - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (sh.runs[mid].start <= lane * 64) lo = mid;
+                    else hi = mid - 1;
+                }
+                vlo = lo;
+            }
+            for (int k = 0; k < nch; ++k) {
+                const int b = k * 64 + lane;
+                const int lo = __builtin_amdgcn_readlane(vlo, k);
+                int rs = sh.runs[lo].start;
+                double rt0 = sh.runs[lo].t0, rdl = sh.runs[lo].delta;
+                for (int j = lo + 1; j < nr; ++j) {  // the runs that start inside this chunk
+                    const int s2 = sh.runs[j].start;
+                    if (s2 > k * 64 + 63) break;
+                    if (b >= s2) {
+                        rs = s2;
+                        rt0 = sh.runs[j].t0;
+                        rdl = sh.runs[j].delta;
+                    }
+                }
+                int ti = (int)(rt0 + (double)(b - rs) * rdl);  // int(theta_index), :124
+                if (ti >= a.theta_dis) ti = 0;
+                if (b < B) s_ti[b] = (uint16_t)ti;
+            }
+        }
+        __syncthreads();
+        // ---- 3. the rays (k_rays_fxr's two refilled chunk slots) ----
+        const double ux = fma(x00, L.ir, L.cxk) - kFxpBase, uy = fma(y00, L.ir, L.cyk) - kFxpBase;
+        const bool fast_car = (ux >= a.fxp_lo) & (ux < a.fxp_hx) & (uy >= a.fxp_lo) & (uy < a.fxp_hy);
+        const uint32_t key = noise_key(a.seed, (uint64_t)(a.env_offset + g));
+        bool hit = false;
+        double x[2], y[2], d[2], tot[2], c[2], sn[2];
+        int kk[2];
+        int next = nch - 1;
+        float cval[2] = {0.0f, 0.0f};
+        int ctag[2] = {-1, -1};
+        auto arm = [&](int r) {
+            const int k = next--;
+            kk[r] = k;
+            const int b = k * 64 + lane;
+            const int ti = s_ti[b < B ? b : B - 1];
+            c[r] = a.cosines[ti];
+            sn[r] = a.sines[ti];
+            x[r] = x00;
+            y[r] = y00;
+            d[r] = b < B ? d00 : 0.0;
+            tot[r] = d[r];  // :130
+        };
+        auto finish = [&](int r) {  // fx_epilogue with the TTC flag kept in the wave
+            const RayArgs &K = kernarg_here();
+            const int b = kk[r] * 64 + lane, bc = b < B ? b : B - 1;
+            double nz = 0.0;
+            if (K.noise_ext) {
+                nz = K.noise_ext[(size_t)g * B + bc];
+            } else if (K.noise_std > 0.0) {
+                const int pp = kk[r] >> 1, ci = pp & 1;
+                float nv;
+                if (ctag[ci] == pp) {
+                    nv = cval[ci];
+                    ctag[ci] = -1;
+                } else {
+                    float lo, hi;
+                    beam_normal_pair_k(key, nstep, beam_noise_pair(b), lo, hi);
+                    nv = (kk[r] & 1) ? hi : lo;
+                    cval[ci] = (kk[r] & 1) ? lo : hi;
+                    ctag[ci] = pp;
+                }
+                nz = K.noise_std * (double)nv;
+            }
+            if (b < B) {
+                double range = tot[r] > L.mr ? L.mr : tot[r];  // :143-144
+                if (K.noise_ext || K.noise_std > 0.0) range += nz;
+                // check_ttc_jit on the noisy scan (laser_models.py:188-217)
+                if (vcar != 0.0 && ttc_fires(range, K.side[b], vcar * K.beam_cos[b], K.ttc_thresh)) hit = true;
+                const int64_t rr = (int64_t)g * B + b;
+                if (K.obs) K.obs[(size_t)g * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
+                if (K.scans_f32) K.scans_f32[rr] = (float)range;
+                if (K.scans_f64) K.scans_f64[rr] = range;
+            }
+            lanes_total += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(b < B));
+        };
+        if (fast_car) {
+            kk[0] = kk[1] = -1;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) d[r] = tot[r] = x[r] = y[r] = c[r] = sn[r] = 0.0;
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                if (next >= 0) arm(r);
+            for (;;) {
+                uint64_t m[2], mall = 0;
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+                    m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+                double dn[2];
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+                    if (m[r]) {
+                        const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+                        dn[r] = fx_load<3>(a.m.dt, fxp_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero_v, P));
+                    }
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    mall |= m[r];
+                    lane_iters += (uint32_t)__popcll(m[r]);
+                }
+                bool open = false;
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+                    if (kk[r] >= 0 && !m[r]) {  // wave-uniform: the chunk has ended; refill the slot
+                        finish(r);
+                        if (next >= 0) arm(r);
+                        else kk[r] = -1;
+                    }
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    if (m[r]) {
+                        d[r] = dn[r];
+                        tot[r] += d[r];  // :141
+                    }
+                    open |= kk[r] >= 0;
+                }
+                if (mall == 0 && !open) break;
+            }
+        } else {  // the scan origin is off the map: the IEEE cell of every lookup, one chunk at a time
+            uint32_t cntl = 0;
+            while (next >= 0) {
+                arm(0);
+                while ((dhi(d[0]) != 0u) & (tot[0] <= L.mr)) {
+                    x[0] += d[0] * c[0];  // :135
+                    y[0] += d[0] * sn[0];  // :136
+                    d[0] = fx_load<3>(a.m.dt, exact_offset_pad(a.m, x[0], y[0], P));
+                    tot[0] += d[0];  // :141
+                    ++cntl;
+                }
+                finish(0);
+            }
+            lane_iters += wave_sum(cntl);
+        }
+        const bool col = __builtin_amdgcn_ballot_w64(hit) != 0ull;
+        // ---- 4. k_post_single for this car (lane 0) ----
+        if (lane == 0) step1_post(sh, g, col);
+        __syncthreads();  // the next step's LDS tables
+    }
+    if (lane == 0) {  // the persistent state, once
+        const StepArgs &S = fused_args().s;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) S.st[(size_t)k * S.E + g] = sh.st[k];
+        S.sb[g] = sh.b0;
+        S.sb[S.E + g] = sh.b1;
+        S.scnt[g] = sh.cnt;
+        unsigned long long *cs = a.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+        atomicAdd(cs, (unsigned long long)(lanes_total + lane_iters));  // + the first lookup of every ray
+        atomicAdd(cs + 1, (unsigned long long)lanes_total);
+    }
 }
 
 // k_post_multi: multi-agent envs after the tiled ray kernel (TTC flags are
@@ -2104,6 +2487,59 @@ hipError_t prepare_env_step(size_t lds_bytes) {
 }
 
 size_t step_lds_bytes(int A, int B) { return post_lds_bytes(A, B); }
+
+hipError_t launch_step1(const StepArgs &a, int32_t n, int64_t act_stride, hipStream_t s, hipEvent_t *ev) {
+    hipError_t e;
+    if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
+    if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
+    FusedArgs fa{};
+    RayArgs &ra = fa.r;
+    ra.m = a.tmap;
+    ra.sines = a.sines;
+    ra.cosines = a.cosines;
+    ra.noise_ext = a.noise_ext;
+    ra.ctr = a.ctr;
+    ra.eps = a.eps;
+    ra.max_range = a.max_range;
+    ra.noise_std = a.noise_std;
+    ra.seed = a.seed;
+    ra.env_offset = a.env_offset;
+    ra.EA = a.E * a.A;
+    ra.A = a.A;
+    ra.B = a.B;
+    ra.theta_dis = a.theta_dis;
+    ra.beam_cos = a.beam_cos;
+    ra.side = a.side;
+    ra.ttc_thresh = a.ttc_thresh;
+    ra.obs = a.out.obs;
+    ra.obs_len = (int32_t)obs_row(a);
+    ra.lidar_max = (float)a.p.lidar_max;
+    ra.scans_f32 = a.out.scans;
+    ra.scans_f64 = a.out.scans_f64;
+    // the padded table (see k_rays_fxn's PAD): t = x / res + 2^24 + P
+    const double P = (double)a.rmp_P, Rn = std::ceil(a.max_range * a.tmap.inv_res) + 2.0;
+    ra.m.dt = a.rmp;
+    ra.m.wt = a.rmp_w;
+    ra.m.oob = 0;
+    ra.fx_zero = a.rmp_zero;
+    ra.fxp_P = a.rmp_P;
+    ra.fx_cx = std::fma(-a.tmap.ox, a.tmap.inv_res, kFxpBase + P);
+    ra.fx_cy = std::fma(-a.tmap.oy, a.tmap.inv_res, kFxpBase + P);
+    ra.fxp_lo = Rn;
+    ra.fxp_hx = (double)a.tmap.W + 2.0 * P - Rn;
+    ra.fxp_hy = (double)a.tmap.H + 2.0 * P - Rn;
+    fa.s = a;
+    fa.nsteps = n;
+    fa.act_stride = act_stride;
+    void *args[] = {&fa};
+    const size_t lds = sizeof(Step1Shared) + ((size_t)a.B * 2 + 15) / 16 * 16;
+    if ((e = hipLaunchKernel(reinterpret_cast<const void *>(&k_step1), dim3((unsigned)a.E), dim3(64), args, lds, s)) !=
+        hipSuccess)
+        return e;
+    if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;
+    if (ev && (e = hipEventRecord(ev[3], s)) != hipSuccess) return e;
+    return hipSuccess;
+}
 
 hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     const int EA = a.E * a.A;

@@ -158,6 +158,32 @@ class BatchSim:
         _lib.check(self.L.f110_step(self.ctx, _ptr(a), dt, ctypes.byref(outs), self._stream()), "f110_step")
         return self.out
 
+    def step_n(self, actions, minimal_outputs: bool = False) -> StepOut:
+        """n consecutive steps with resident actions [n, E, A, 2] (f110_step_n:
+        one k_step1 launch when the context runs fused, else n three-launch
+        steps); the outputs hold the last step's values."""
+        a = torch.as_tensor(actions, device=self.device)
+        if a.dtype not in (torch.float32, torch.float64):
+            a = a.to(torch.float32)
+        if a.dim() != 4 or tuple(a.shape[1:]) != (self.E, self.A, 2):
+            raise ValueError(f"actions must be [n, {self.E}, {self.A}, 2]; got {tuple(a.shape)}")
+        a = a.contiguous()
+        self._keep_a = a
+        outs = self._outs_min if minimal_outputs else self._outs
+        dt = _lib.F64 if a.dtype == torch.float64 else _lib.F32
+        _lib.check(self.L.f110_step_n(self.ctx, _ptr(a), dt, int(a.shape[0]), 0, ctypes.byref(outs), self._stream()),
+                   "f110_step_n")
+        return self.out
+
+    def set_fused(self, on: bool = True):
+        """Single-agent steps as one k_step1 launch (f110_set_fused; results unchanged)."""
+        _lib.check(self.L.f110_set_fused(self.ctx, int(bool(on))), "f110_set_fused")
+
+    @property
+    def fused(self) -> bool:
+        """True when f110_step / f110_step_n run k_step1 (f110_fused)."""
+        return bool(_lib.check(self.L.f110_fused(self.ctx), "f110_fused"))
+
     def update_params(self, params: dict, agent_idx: int = -1):
         """Simulator.update_params (base_classes.py:527-546) for every env."""
         p = _lib.F110Params()

@@ -152,6 +152,23 @@ F110_API int f110_reset(f110_ctx *ctx, const double *poses, const uint8_t *env_m
  * F110_F64. */
 F110_API int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dtype, const f110_outputs *out,
                        void *stream);
+/* n_steps consecutive f110_step calls with resident actions: step t reads the
+ * [n_envs][n_agents][2] block at actions + t * step_stride elements
+ * (step_stride 0 = packed, n_envs * n_agents * 2) -- a rollout of open-loop
+ * actions; every output holds the last step's values, exactly as after the n
+ * calls.  Single-agent contexts with
+ * f110_set_fused on run the n steps in ONE k_step1 launch (each env's car
+ * advances through its steps in one wave, no per-step launch boundary);
+ * otherwise the three-launch step runs n times.  Bit-identical either way. */
+F110_API int f110_step_n(f110_ctx *ctx, const void *actions, int32_t actions_dtype, int32_t n_steps,
+                         int64_t step_stride, const f110_outputs *out, void *stream);
+/* Single-agent steps as one launch (k_step1: dynamics, rays and the post stage
+ * of each car in one wave) instead of k_agents + k_rays + k_post_single; on
+ * switches the context to the padded EDT and off its heavy-first list.
+ * F110_FUSED sets the default.  Scheduling only: results are unchanged. */
+F110_API int f110_set_fused(f110_ctx *ctx, int32_t on);
+/* 1 when this context's f110_step / f110_step_n run k_step1, else 0. */
+F110_API int f110_fused(const f110_ctx *ctx);
 
 /* Replaces F110Env.update_params / Simulator.update_params
  * (f110_env.py:487-498, base_classes.py:527-546): agent_idx < 0 updates every

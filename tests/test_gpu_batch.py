@@ -405,3 +405,54 @@ def test_pool_kernel_identical(tracks, gpu, monkeypatch, A, beams):
         for t, (a, b) in enumerate(zip(outs[0], outs[k])):
             for x, y in zip(a, b):
                 assert torch.equal(x, y), f"variant {k} step {t}"
+
+
+@pytest.mark.parametrize("beams,dtype", [(1080, "f32"), (333, "f64"), (64, "f32")])
+def test_step1_matches_three_launch_step(tracks, gpu, beams, dtype):
+    """k_step1 (f110_set_fused: the single-agent step -- dynamics, rays, post
+    stage -- in one launch per call, or n steps in one launch via
+    f110_step_n) against the three-launch step: obs, f64 / f32 scans,
+    collisions, terminated, was_reset, lap times / counts, sim time, states
+    and lookup counters bit-identical over 40 noisy random-action steps with
+    autoreset (crashes and respawns happen), a masked reset in the middle
+    (which runs the three-launch path in both) and float32 / float64 actions;
+    f110_step_n over 9 / 11 / 9 steps equals single calls."""
+    E = 203
+    sp = _spawns(1)
+    rng = np.random.default_rng(beams)
+    poses = sp[rng.integers(0, sp.shape[0], E)]
+    T = 40
+    acts = np.stack([rng.uniform(-0.4189, 0.4189, (T, E, 1)), rng.uniform(0, 20, (T, E, 1))], -1)
+    acts = torch.from_numpy(acts.astype(np.float32 if dtype == "f32" else np.float64)).to(gpu)
+    mask = rng.random(E) < 0.5
+    runs = []
+    for mode in ("three", "fused", "fused_n"):
+        sim = _sim(tracks, gpu, n_envs=E, n_agents=1, num_beams=beams, noise_std=0.01, autoreset=True,
+                   spawn_poses=sp, seed=9, keep_f64_scans=True)
+        sim.set_fused(mode != "three")
+        assert sim.fused == (mode != "three")
+        sim.reset(poses)
+        sim.reset_counters()
+        snaps = {}
+        t = 0
+        while t < T:
+            if t == 20:
+                sim.reset(poses[::-1].copy(), env_mask=mask)
+            n = {0: 9, 20: 11, 31: 9}.get(t, 1) if mode == "fused_n" else 1
+            o = sim.step_n(acts[t:t + n]) if n > 1 else sim.step(acts[t])
+            t += n
+            if t in (9, 31, 40):
+                torch.cuda.synchronize()
+                snaps[t] = (o.obs.clone(), o.scans.clone(), o.scans_f64.clone(), o.collisions.clone(),
+                            o.terminated.clone(), o.was_reset.clone(), o.lap_times.clone(), o.lap_counts.clone(),
+                            o.sim_time.clone(), sim.agent_states().clone())
+        runs.append((snaps, sim.read_counters()))
+        sim.close()
+    ref_snaps, ref_ctr = runs[0]
+    for k in (1, 2):
+        snaps, ctr = runs[k]
+        assert ctr == ref_ctr, k
+        assert sorted(snaps) == sorted(ref_snaps) == [9, 31, 40]
+        for t in ref_snaps:
+            for j, (x, y) in enumerate(zip(ref_snaps[t], snaps[t])):
+                assert torch.equal(x, y), f"mode {k} after step {t} field {j}"
