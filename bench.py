@@ -71,6 +71,12 @@ def parse():
                     help="sub-shards of the GPU's envs on concurrent dedicated-queue streams "
                          "(streams.StreamShards); 1 = one context on the current stream; 0 (default) = "
                          "auto_streams(envs per GPU)")
+    ap.add_argument("--runner", choices=["auto", "streams", "one", "fused", "rollout"], default="auto",
+                    help="the timed runner: streams = StreamShards sub-shards of the three-launch step; one = one "
+                         "context, three launches per step; fused = one context, one k_step1 launch per step (the "
+                         "policy-loop path); rollout = one context, k_step1 over --chunk resident steps per launch "
+                         "(open-loop random actions); auto = rollout for single-agent envs, else streams")
+    ap.add_argument("--chunk", type=int, default=50, help="steps per k_step1 launch of the rollout runner")
     ap.add_argument("--workload", choices=["step", "ddpg"], default="step",
                     help="step: the env step (headline); ddpg: config 5, the batched train_ddpg loop")
     ap.add_argument("--ddpg-batch", type=int, default=4096)
@@ -281,6 +287,9 @@ def scan_check(O, scanner, runner, act, threads):
 
 def ray_kernel_name(sm):
     names = {0: "k_rays", 1: "k_rays_tiled (flat)", 2: "k_rays_tiled (chunked)", 3: "k_rays_fx"}
+    if getattr(sm, "fused", False):
+        return ("k_step1 (the single-agent step in one launch: lane-0 dynamics, the car's rays in two refilled "
+                "64-beam chunk slots on the padded EDT, lane-0 post stage)")
     if sm.ray_kernel == 3 and getattr(sm, "ray_pool", 0) > 0:
         return f"k_rays_fxp ({sm.ray_pool} car(s) per wave, two ray slots per lane with lane-level refill)"
     if sm.ray_kernel == 3 and sm.ray_refill > 0:
@@ -352,7 +361,6 @@ def main():
     shard = D.shard_range(G, world, rank)
     E = shard.count
     K, W = args.steps, args.warmup
-    S = args.streams if args.streams > 0 else auto_streams(E, A)
     noise = 0.0 if args.no_noise else 0.01
 
     track = load_map(args.map)
@@ -378,12 +386,38 @@ def main():
     acts = actions(W + K + 1, E, shard.offset, G)
     stream = torch.cuda.current_stream(dev)
 
-    def make(n_envs, offset, s):
+    kind = args.runner
+    if kind == "auto":
+        kind = "rollout" if A == 1 else "streams"
+    if kind in ("fused", "rollout") and A != 1:
+        raise SystemExit("--runner fused / rollout: k_step1 is the single-agent step")
+    policy_kind = "fused" if A == 1 else "one"  # what a policy loop steps: one call per step, one context
+
+    def make(n_envs, offset, kind_):
         kw = dict(n_agents=A, device=dev, seed=args.seed, noise_std=noise, autoreset=True, spawn_poses=spawn,
                   keep_f64_scans=True)
-        if s > 1 and n_envs % s == 0:
-            return StreamShards(track, n_envs=n_envs, n_streams=s, env_offset=offset, **kw)
-        return BatchSim(track, n_envs=n_envs, env_offset=offset, **kw)
+        if kind_ == "streams":
+            s = args.streams if args.streams > 0 else auto_streams(n_envs, A)
+            if s > 1 and n_envs % s == 0:
+                r = StreamShards(track, n_envs=n_envs, n_streams=s, env_offset=offset, **kw)
+                r.kind = "streams"
+                return r
+        r = BatchSim(track, n_envs=n_envs, env_offset=offset, **kw)
+        if kind_ in ("fused", "rollout"):
+            r.set_fused(True)
+            assert r.fused, "k_step1 unavailable for this context"
+        r.kind = kind_ if kind_ != "streams" else "one"
+        return r
+
+    def steps(r, a, k0, n, minimal):
+        """Steps k0 .. k0 + n - 1 of the action block a: one call per step, or
+        step_n launches of --chunk steps for the rollout runner."""
+        if r.kind == "rollout":
+            for c in range(k0, k0 + n, args.chunk):
+                r.step_n(a[c:min(k0 + n, c + args.chunk)], minimal_outputs=minimal)
+        else:
+            for k in range(k0, k0 + n):
+                r.step(a[k], minimal_outputs=minimal)
 
     ramp = {"seconds": args.ramp_s, "steps": 0}
 
@@ -395,23 +429,20 @@ def main():
         t_end = time.perf_counter() + args.ramp_s
         n = 0
         while time.perf_counter() < t_end:
-            r.step(a[n % max(W, 1)], minimal_outputs=minimal)
-            n += 1
-            if n % 16 == 0:
-                torch.cuda.synchronize(dev)
+            steps(r, a, 0, max(W, 1), minimal)
+            n += max(W, 1)
+            torch.cuda.synchronize(dev)
         ramp["steps"] = max(ramp["steps"], n)
         if n:
             torch.cuda.synchronize(dev)
             r.reset(p0)
-        for w in range(W):
-            r.step(a[w], minimal_outputs=minimal)
+        steps(r, a, 0, W, minimal)
         torch.cuda.synchronize(dev)
         r.reset_counters()
         D.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for k in range(K):
-            r.step(a[W + k], minimal_outputs=minimal)
+        steps(r, a, W, K, minimal)
         if hasattr(r, "join"):
             r.join()
         torch.cuda.synchronize(dev)
@@ -436,44 +467,54 @@ def main():
         h = D.sum_tensor_over_ranks(h)
         return {"sha256": hashlib.sha256(h.numpy().tobytes()).hexdigest()[:32], "envs": len(ids), "stride": stride}
 
-    runner = make(E, shard.offset, S)
+    runner = make(E, shard.offset, kind)
     elapsed, (lookups, rays) = timed(runner, poses0, acts)
     traj = digest(runner)
     mean_look = lookups / max(rays, 1)
     total_env_steps = D.sum_over_ranks(E * K)
-    sim = runner if isinstance(runner, BatchSim) else make(E, shard.offset, 1)
+    RUNNER_TEXT = {
+        "streams": "StreamShards: unjoined stream sub-shards of the three-launch step, actions resident in HBM",
+        "one": "one BatchSim context, three launches per step (k_agents, ray kernel, k_post)",
+        "fused": "one BatchSim context, one k_step1 launch per step (the policy-loop path)",
+        "rollout": "one BatchSim context, k_step1 over --chunk resident random-action steps per launch"}
+    sim = runner if getattr(runner, "kind", "") == policy_kind else make(E, shard.offset, policy_kind)
     single = None
-    if sim is not runner:  # the same workload on one context / one stream (what a policy loop steps)
+    if sim is not runner:  # the same workload one call per step on one context (what a policy loop steps)
         el1, _ = timed(sim, poses0, acts)
         single = {"value": total_env_steps / el1, "ms_per_step": el1 / K * 1e3,
-                  "runner": "one BatchSim context on the caller's stream, minimal outputs"}
+                  "runner": RUNNER_TEXT[policy_kind] + ", minimal outputs"}
     el_full, _ = timed(sim, poses0, acts, minimal=False)
     full_outputs = {"value": total_env_steps / el_full, "ms_per_step": el_full / K * 1e3,
-                    "runner": "one context, every output (f32 + f64 scans, laps, sim_time, was_reset)"}
+                    "runner": RUNNER_TEXT[policy_kind] + ", every output (f32 + f64 scans, laps, sim_time, was_reset)"}
+    prof = runner if isinstance(runner, BatchSim) else sim  # the per-kernel pass: the headline's own kernel
 
     # second, separate pass: per-kernel HIP-event timing on the one-context run (not part of `value`).
     # It runs right after the timed passes, behind its own clock ramp and before the CPU-side scan
     # check (an idle GPU clocks down), over >= 100 steps whatever --steps is.
     KP = max(100, min(K, 300))
     t_end = time.perf_counter() + args.ramp_s
-    n = 0
     while time.perf_counter() < t_end:
-        sim.step(acts[W + (n % K)], minimal_outputs=True)
-        n += 1
-        if n % 16 == 0:
-            torch.cuda.synchronize(dev)
-    sim.profile_begin(KP)
-    for k in range(KP):
-        sim.step(acts[W + (k % K)], minimal_outputs=True)
-    per_kernel = sim.profile_end()
+        steps(prof, acts, W, min(K, 50), True)
+        torch.cuda.synchronize(dev)
+    pk = []
+    done = 0
+    prof.profile_begin(KP)
+    while done < KP:  # launches of the headline's shape (one step, or --chunk steps for the rollout)
+        n = min(KP - done, K, args.chunk if prof.kind == "rollout" else 1)
+        steps(prof, acts, W, n, True)
+        pk.append(n)
+        done += n
+    per_kernel = prof.profile_end()
+    per_launch = KP / max(len(pk), 1)  # steps per profiled launch
+    for key in ("k_agents_ms", "k_rays_ms", "k_post_ms"):
+        per_kernel[key] /= per_launch
     # SIMT efficiency of the ray loop: its lane-slot counter costs ~2 % of k_rays, so it runs on 50 more
     # steps after the timed passes, not inside them
-    sim.set_simt(True)
-    sim.reset_counters()
-    for k in range(min(K, 50)):
-        sim.step(acts[W + (k % K)], minimal_outputs=True)
-    loop_lookups, lane_slots = sim.read_simt()
-    sim.set_simt(False)
+    prof.set_simt(True)
+    prof.reset_counters()
+    steps(prof, acts, W, min(K, 50), True)
+    loop_lookups, lane_slots = prof.read_simt()
+    prof.set_simt(False)
 
     O = scanner = None
     checks = None
@@ -482,35 +523,41 @@ def main():
         scanner = O.OracleScanner(track.free_mask, track.resolution, track.origin)
         checks = scan_check(O, scanner, runner, acts[W + K], cpu_threads())
 
-    B = sim.B
-    # k_rays (the dominant kernel): per ray 4 B per EDT lookup (exact uint32 k
-    # cell) + 4 B of f32 range out; the 120 B/agent of state I/O
-    # belong to k_agents.
+    B = prof.B
+    fused_prof = prof.kind in ("fused", "rollout")
+    # the dominant kernel: k_rays, or k_step1 (the whole step) when fused.  Per
+    # ray 4 B per EDT lookup (exact uint32 k cell) + 4 B of f32 range out
+    # (SURVEY §8d); the 120 B/agent of state I/O go with the step (k_agents, or
+    # k_step1's own).
     rays_bytes_launch = E * A * B * (4.0 * mean_look + 4.0)
-    k_ms = per_kernel["k_rays_ms"]
-    achieved = rays_bytes_launch / (k_ms * 1e-3) / 1e9
+    kernel_bytes = E * algorithmic_bytes_per_env_step(B, A, mean_look) if fused_prof else rays_bytes_launch
+    k_ms = per_kernel["k_rays_ms"]  # per step
+    achieved = kernel_bytes / (k_ms * 1e-3) / 1e9
     pmc = load_profile("pmc_traffic", E, A)
     busy = load_profile("pmc_busy", E, A)
     traffic = pmc.get("bytes_per_launch") if pmc else None
     roof = {
-        "kernel": "k_rays",
-        "profiled_steps": per_kernel["steps"],
+        "kernel": "k_step1" if fused_prof else "k_rays",
+        "profiled_steps": KP,
+        "profiled_launches": per_kernel["steps"],
         "bound": ("VALU issue of the sphere-trace loop (valu_busy; HBM is not the limit: see hbm_traffic_frac and "
-                  "l2_hit_rate; DESIGN.md 3.4)" if sim.ray_kernel == 3 and sim.ray_refill > 0 else
+                  "l2_hit_rate; DESIGN.md 3.4)" if prof.ray_kernel == 3 and (prof.ray_refill > 0 or fused_prof) else
                   "latency of the dependent EDT gather chain (HBM is not the limit: see hbm_traffic_frac; capping "
                   "occupancy at 6/4/2 waves per SIMD costs 1.31x/1.62x/2.9x, DESIGN.md 3.2)"),
-        "ray_kernel": ray_kernel_name(sim),
+        "ray_kernel": ray_kernel_name(prof),
         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-        "traffic": traffic, "kernel_ms": k_ms, "algorithmic_bytes_per_launch": rays_bytes_launch,
+        "traffic": traffic, "kernel_ms": k_ms, "algorithmic_bytes_per_launch": kernel_bytes,
+        "kernel_ms_note": "per step (a profiled launch's time / its steps)",
         "mean_lookups_per_ray": mean_look,
-        "step_kernels_ms": {"k_agents": per_kernel["k_agents_ms"], "k_rays": k_ms, "k_post": per_kernel["k_post_ms"]},
+        "step_kernels_ms": {"k_agents": per_kernel["k_agents_ms"], "k_rays" if not fused_prof else "k_step1": k_ms,
+                            "k_post": per_kernel["k_post_ms"]},
         "step_algorithmic_bytes_per_env": algorithmic_bytes_per_env_step(B, A, mean_look),
         # lookups made in the loop / (loop trips x 64 lanes x rays per lane), from the kernel's own counters
         "simt_efficiency": loop_lookups / lane_slots if lane_slots else None,
     }
-    # consistency: the ray kernel runs inside the one-context step it is timed in
-    step_ms = (single or {"ms_per_step": elapsed / K * 1e3})["ms_per_step"]
-    roof["kernel_le_step"] = {"ok": bool(k_ms <= step_ms), "kernel_ms": k_ms, "one_context_step_ms": step_ms}
+    # consistency: the kernel runs inside the step it is timed in (the profiled runner's own wall time per step)
+    step_ms = elapsed / K * 1e3 if prof is runner else (single or {"ms_per_step": elapsed / K * 1e3})["ms_per_step"]
+    roof["kernel_le_step"] = {"ok": bool(k_ms <= step_ms), "kernel_ms": k_ms, "runner_step_ms": step_ms}
     if pmc and traffic:
         roof["hbm_traffic_gbs"] = traffic / (k_ms * 1e-3) / 1e9
         roof["hbm_traffic_frac"] = roof["hbm_traffic_gbs"] / HBM_PEAK_GBS
@@ -543,11 +590,12 @@ def main():
             "global_envs": G, "envs_per_gpu": E, "agents": A, "beams": B, "map": args.map,
             "integrator": "RK4", "scan_noise": not args.no_noise, "autoreset": True,
             "parallelism": f"env-shard x{world} (no collectives)",
-            "streams_per_gpu": S if not isinstance(runner, BatchSim) else 1,
+            "streams_per_gpu": runner.S if not isinstance(runner, BatchSim) else 1,
             "ramp": ramp,
-            "runner": ("StreamShards: S unjoined stream sub-shards, actions resident in HBM" if S > 1 else
-                       "one BatchSim context") + "; minimal outputs (obs, collisions, terminated): no f32 "
-                       "info['scans'] copy, lap_times/counts, sim_time, was_reset",
+            "runner": RUNNER_TEXT[runner.kind] + "; minimal outputs (obs, collisions, terminated): no f32 "
+                      "info['scans'] copy, lap_times/counts, sim_time, was_reset",
+            "runner_kind": runner.kind,
+            "chunk": args.chunk if runner.kind == "rollout" else 1,
         },
         "trajectory_digest": traj,
         "single_stream": single,
@@ -561,19 +609,18 @@ def main():
         for label, n in (("C3_shard_8192", 8192), ("C2_4096", 4096)):
             if n >= E:
                 continue
-            S2 = args.streams if args.streams > 0 else auto_streams(n, A)
-            r2 = make(n, 0, S2)
-            el2, _ = timed(r2, spawn[rng.integers(0, spawn.shape[0], size=n)], actions(W + K, n, 0, n))
-            line = {"envs": n, "value": n * K / el2, "ms_per_step": el2 / K * 1e3,
-                    "streams": S2 if not isinstance(r2, BatchSim) else 1}
-            if not isinstance(r2, BatchSim):
-                r2.close()
-                r1 = make(n, 0, 1)
-                el1, _ = timed(r1, spawn[rng.integers(0, spawn.shape[0], size=n)], actions(W + K, n, 0, n))
-                line["single_stream"] = {"value": n * K / el1, "ms_per_step": el1 / K * 1e3}
+            p2 = spawn[rng.integers(0, spawn.shape[0], size=n)]
+            a2 = actions(W + K, n, 0, n)
+            r2 = make(n, 0, kind)
+            el2, _ = timed(r2, p2, a2)
+            line = {"envs": n, "value": n * K / el2, "ms_per_step": el2 / K * 1e3, "runner_kind": r2.kind,
+                    "streams": r2.S if not isinstance(r2, BatchSim) else 1}
+            r2.close()
+            if kind != policy_kind:
+                r1 = make(n, 0, policy_kind)
+                el1, _ = timed(r1, p2, a2)
+                line["single_stream"] = {"value": n * K / el1, "ms_per_step": el1 / K * 1e3, "runner_kind": r1.kind}
                 r1.close()
-            else:
-                r2.close()
             sec[label] = line
         result["secondary"] = sec
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
