@@ -388,10 +388,10 @@ def main():
 
     kind = args.runner
     if kind == "auto":
-        kind = "rollout" if A == 1 else "streams"
+        kind = "streams"  # (k_step1's rollout measured slower at 65536: DESIGN §3.9)
     if kind in ("fused", "rollout") and A != 1:
         raise SystemExit("--runner fused / rollout: k_step1 is the single-agent step")
-    policy_kind = "fused" if A == 1 else "one"  # what a policy loop steps: one call per step, one context
+    policy_kind = "one"  # what a policy loop steps: one call per step, one context
 
     def make(n_envs, offset, kind_):
         kw = dict(n_agents=A, device=dev, seed=args.seed, noise_std=noise, autoreset=True, spawn_poses=spawn,

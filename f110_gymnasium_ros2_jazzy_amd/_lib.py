@@ -85,8 +85,8 @@ def load(build_if_missing: bool = True):
     global _lib
     if _lib is not None:
         return _lib
-    path = _build.LIB
-    if build_if_missing:
+    path = os.environ.get("F110_LIB") or _build.LIB  # F110_LIB: an alternate build (A/B runs)
+    if build_if_missing and path == _build.LIB:
         try:
             _build.build()
         except Exception as exc:  # pragma: no cover - toolchain missing

@@ -259,8 +259,13 @@ F110_HD void pid(double speed, double steer, double cur_speed, double cur_steer,
 
 // RaceCar.update_pose without the scan, base_classes.py:256-417.
 // s[7] in/out; b0 = newest buffered steer, b1 = older; cnt = buffer fill.
-F110_HD void update_pose(double s[7], double &b0, double &b1, int &cnt, double raw_steer, double vel,
-                         const f110_params &p, double dt, int integrator) {
+// RaceCar.update_pose on a state array s (and an accumulator scratch acc) that
+// are plain arrays (registers) or volatile LDS arrays (k_step1: every stage
+// re-reads s and acc from LDS, so that only one vehicle_dynamics_st evaluation
+// is in registers at a time).  Same operations in the same order either way.
+template <class V>
+F110_HD void update_pose_impl(V s, V acc, double &b0, double &b1, int &cnt, double raw_steer, double vel,
+                              const f110_params &p, double dt, int integrator) {
     double steer;
     if (cnt < 2) {  // :272-274
         steer = 0.0;
@@ -276,40 +281,56 @@ F110_HD void update_pose(double s[7], double &b0, double &b1, int &cnt, double r
     pid(vel, steer, s[3], s[2], p.sv_max, p.a_max, p.v_max, p.v_min, accl, sv);
     sv = clip(sv, p.sv_min, p.sv_max);
     accl = clip(accl, -p.a_max, p.a_max);
-    double ns[7];
+    double k[7], xs[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) xs[i] = s[i];
     if (integrator == F110_INTEGRATOR_RK4) {  // :285-374
-        double k1[7], k2[7], k3[7], k4[7], xs[7];
-        vehicle_dynamics_st(s, sv, accl, p, k1);
+        // k1 + 2*k2 + 2*k3 + k4 is summed left to right as the stages come
+        // (((k1 + 2k2) + 2k3) + k4: the reference's rounding order), so only
+        // one stage's k is live at a time
+        vehicle_dynamics_st(xs, sv, accl, p, k);
 #pragma unroll
-        for (int i = 0; i < 7; ++i) xs[i] = s[i] + dt * (k1[i] / 2);
-        vehicle_dynamics_st(xs, sv, accl, p, k2);
+        for (int i = 0; i < 7; ++i) {
+            acc[i] = k[i];
+            xs[i] = s[i] + dt * (k[i] / 2);
+        }
+        vehicle_dynamics_st(xs, sv, accl, p, k);
 #pragma unroll
-        for (int i = 0; i < 7; ++i) xs[i] = s[i] + dt * (k2[i] / 2);
-        vehicle_dynamics_st(xs, sv, accl, p, k3);
+        for (int i = 0; i < 7; ++i) {
+            acc[i] = acc[i] + 2 * k[i];
+            xs[i] = s[i] + dt * (k[i] / 2);
+        }
+        vehicle_dynamics_st(xs, sv, accl, p, k);
 #pragma unroll
-        for (int i = 0; i < 7; ++i) xs[i] = s[i] + dt * k3[i];
-        vehicle_dynamics_st(xs, sv, accl, p, k4);
+        for (int i = 0; i < 7; ++i) {
+            acc[i] = acc[i] + 2 * k[i];
+            xs[i] = s[i] + dt * k[i];
+        }
+        vehicle_dynamics_st(xs, sv, accl, p, k);
         const double w = dt * (1.0 / 6.0);
 #pragma unroll
-        for (int i = 0; i < 7; ++i) ns[i] = s[i] + w * (k1[i] + 2 * k2[i] + 2 * k3[i] + k4[i]);
+        for (int i = 0; i < 7; ++i) s[i] = s[i] + w * (acc[i] + k[i]);
     } else {                                  // :376-396
-        double fe[7];
-        vehicle_dynamics_st(s, sv, accl, p, fe);
+        vehicle_dynamics_st(xs, sv, accl, p, k);
 #pragma unroll
-        for (int i = 0; i < 7; ++i) ns[i] = s[i] + dt * fe[i];
+        for (int i = 0; i < 7; ++i) s[i] = s[i] + dt * k[i];
     }
-    ns[2] = clip(ns[2], p.s_min, p.s_max);   // :400-401
-    ns[3] = clip(ns[3], p.v_min, p.v_max);
-    ns[4] = wrap_angle(ns[4]);               // :408
-    double yr = ns[5];                       // :410-412
+    s[2] = clip(s[2], p.s_min, p.s_max);   // :400-401
+    s[3] = clip(s[3], p.v_min, p.v_max);
+    s[4] = wrap_angle(s[4]);               // :408
+    double yr = s[5];                      // :410-412
     if (yr != yr) yr = 0.0;
     else if (isinf(yr)) yr = yr > 0 ? kYawRateCap : -kYawRateCap;
-    ns[5] = clip(yr, -kYawRateCap, kYawRateCap);
-    double sl = ns[6];                       // :414-417
+    s[5] = clip(yr, -kYawRateCap, kYawRateCap);
+    double sl = s[6];                      // :414-417
     if (sl != sl) sl = 0.0;
-    ns[6] = clip(sl, -kSlipCap, kSlipCap);
-#pragma unroll
-    for (int i = 0; i < 7; ++i) s[i] = ns[i];
+    s[6] = clip(sl, -kSlipCap, kSlipCap);
+}
+
+F110_HD void update_pose(double s[7], double &b0, double &b1, int &cnt, double raw_steer, double vel,
+                         const f110_params &p, double dt, int integrator) {
+    double acc[7];
+    update_pose_impl<double *>(s, acc, b0, b1, cnt, raw_steer, vel, p, dt, integrator);
 }
 
 // -------------------------------------------------------------- the map --

@@ -67,6 +67,7 @@ struct StepArgs {
     int32_t fx_refill;  // F110_FX_REFILL: waves per car of k_rays_fxr (two chunk slots with refill; 0 = off)
     int32_t fx_pool;    // F110_FX_POOL: cars per k_rays_fxp wave (lane-level refill; 0 = off)
     int32_t pool_T;     // F110_FX_POOL_T: k_rays_fxp refills once this many slots have ended
+    int32_t fused_cpw;  // F110_FUSED_CPW: cars per k_step1 workgroup (1..8)
     uint8_t *pcost;     // [EA][nch] k_rays_fxp's per-chunk cost of the previous launch (its queue order)
     int32_t count_slots;  // F110_SIMT (default 1): lane-slot counter of the fixed-point loops
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2..4: k_rays_fxn)
@@ -186,6 +187,7 @@ struct FusedArgs {
     RayArgs r;
     StepArgs s;
     int32_t nsteps;
+    int32_t cpw;         // cars per workgroup (one wave each; their lane-parallel sections on wave 0)
     int64_t act_stride;  // action elements between consecutive steps' [E][A][2] blocks
 };
 

@@ -1333,11 +1333,17 @@ struct PoolCar {
 // The kernarg block behind an opaque copy of its pointer: loads through it
 // stay where they are written (in the refill pass) instead of being hoisted
 // out of the trace loop into SGPRs, which would spill there.
-__device__ __forceinline__ const RayArgs &kernarg_here() {
-    const RayArgs *p;
-    asm volatile("s_mov_b64 %0, %1" : "=s"(p) : "s"(kernarg_rays()));
-    return *p;
+// an opaque SGPR copy of a pointer to read-only kernel arguments, typed in the
+// constant address space: its field loads are scalar loads placed at the use
+// (a generic pointer out of the asm would make them flat vector loads)
+template <class T>
+__device__ __forceinline__ const T *launder_const(const T *ptr) {
+    const __attribute__((address_space(4))) T *p;
+    asm volatile("s_mov_b64 %0, %1" : "=s"(p) : "s"(ptr));
+    return (const T *)p;
 }
+
+__device__ __forceinline__ const RayArgs &kernarg_here() { return *launder_const(kernarg_rays()); }
 
 __device__ __forceinline__ bool lane_in(uint64_t mask) {
     return (uint32_t)(mask >> (threadIdx.x & 63)) & 1u;
@@ -1951,10 +1957,10 @@ struct Step1Shared {
     BeamRun runs[kMaxSeg];
     double sx, sy, d00, vel;
     uint64_t nstep;
-    int32_t nruns, do_reset, pad_[2];
-    // the car's persistent state between steps (lane 0; kept out of registers
+    int32_t nruns, do_reset, col, pad_;
+    // the car's persistent state between steps (wave 0, lane c; kept out of registers
     // so that the ray loop keeps its 64 VGPRs)
-    double st[7], b0, b1;
+    double st[7], acc[7], b0, b1;  // st / acc: update_pose_impl's volatile LDS arrays
     int32_t cnt, pad2_;
     EpiCar car;
     EpiEnv env;
@@ -1964,106 +1970,154 @@ __device__ __forceinline__ const FusedArgs &fused_args() {
 #if defined(__HIP_DEVICE_COMPILE__)
     return *reinterpret_cast<const FusedArgs *>(__builtin_amdgcn_kernarg_segment_ptr());
 #else
-    return *static_cast<const FusedArgs *>(nullptr);
+    static const FusedArgs none{};  // (host pass: never called)
+    return none;
 #endif
 }
 
 // k_step1's lane-0 sections as real calls: their register needs (RK4 of
 // vehicle_dynamics_st: ~150 VGPRs inline) stay out of the ray loop's 64.
-__device__ __noinline__ void step1_agent(Step1Shared &sh, int g, int t) {
-    const FusedArgs &fa = fused_args();
-    const int B = fa.r.B;
-            const StepArgs &S = fused_args().s;
-            double st[7];
-#pragma unroll
-            for (int q = 0; q < 7; ++q) st[q] = sh.st[q];
-            double b0 = sh.b0, b1 = sh.b1;
-            int cnt = sh.cnt;
-            EpiCar car = sh.car;
-            EpiEnv env = sh.env;
-            double raw_steer, vel;
-            if (S.actions_f64) {
-                const double *ac = S.actions_f64 + (size_t)t * fa.act_stride + (size_t)g * 2;
-                raw_steer = ac[0];
-                vel = ac[1];
-            } else {
-                const float *ac = S.actions + (size_t)t * fa.act_stride + (size_t)g * 2;
-                raw_steer = (double)ac[0];
-                vel = (double)ac[1];
-            }
-            const int do_reset = env.pending ? 1 : 0;
-            if (do_reset) {  // RaceCar.reset (base_classes.py:183-204), then F110Env.reset's zero-action step
-                const uint64_t genv = (uint64_t)(S.env_offset + g);
-                const uint32_t k = spawn_draw(S.seed, genv, env.episode) % (uint32_t)S.n_spawn;
-                const double *pz = S.spawn + (size_t)k * 3;
-                double px = pz[0], py = pz[1], pth = pz[2];
-                if (S.reset_f32) {
-                    px = (double)(float)px;
-                    py = (double)(float)py;
-                    pth = (double)(float)pth;
-                }
-#pragma unroll
-                for (int q = 0; q < 7; ++q) st[q] = 0.0;
-                st[0] = px;
-                st[1] = py;
-                st[4] = pth;
-                b0 = b1 = 0.0;
-                cnt = 0;
-                raw_steer = 0.0;
-                vel = 0.0;
-                S.start[g] = px;
-                S.start[S.E + g] = py;
-                S.start[2 * S.E + g] = pth;
-                car.sx = px;
-                car.sy = py;
-                if (S.ego == 0) {  // start_rot (f110_env.py:448-451), as k_agents
-                    if (S.reset_f32) {
-                        const float nt = -(float)pth;
-                        env.ct = (double)np_sincosf(nt, true);
-                        env.st = (double)np_sincosf(nt, false);
-                    } else {
-                        double sr, crr;
-                        cr_sincos(-pth, sr, crr);
-                        env.ct = crr;
-                        env.st = sr;
-                    }
-                    S.start_rot[g] = env.ct;
-                    S.start_rot[S.E + g] = env.st;
-                }
-                car.tg = 0;
-                car.ns = 1;
-                car.lt = 0.0f;
-                S.toggles[g] = 0;
-                S.near_start[g] = 1;
-                S.lap_times[g] = 0.0f;
-                S.lap_counts[g] = 0.0f;
-            }
-            update_pose(st, b0, b1, cnt, raw_steer, vel, S.pa[0], S.dt, S.integrator);
-            const bool no_offset = S.lidar_dist == 0.0 && isfinite(st[4]);
-            double sy4 = 0.0, cy4 = 1.0;
-            if (!no_offset) cr_sincos(st[4], sy4, cy4);
-            const double sx = no_offset ? st[0] + 0.0 : st[0] + S.lidar_dist * cy4;
-            const double sy = no_offset ? st[1] + 0.0 : st[1] + S.lidar_dist * sy4;
-            sh.sx = sx;
-            sh.sy = sy;
-            sh.d00 = S.map.dt[cell_index(S.map, sx, sy)];  // first lookup (laser_models.py:129)
-            sh.vel = st[3];
-            sh.nstep = do_reset ? 0ull : env.nstep;
-            sh.do_reset = do_reset;
-            const double t0 = first_theta_index(st[4], S.fov, S.theta_dis);
-            sh.nruns = build_beam_runs(t0, S.inc, S.theta_dis, B, sh.runs, kMaxSeg);
-#pragma unroll
-            for (int q = 0; q < 7; ++q) sh.st[q] = st[q];
-            sh.b0 = b0;
-            sh.b1 = b1;
-            sh.cnt = cnt;
-            sh.car = car;
-            sh.env = env;
-        }
+// (the argument block comes in as a pointer: a callee must not read the kernarg
+// segment pointer itself)
+template <class T>
+__device__ __forceinline__ const T *launder_s(const T *p) {  // an opaque SGPR copy (loads through it stay below)
+    return launder_const(p);
+}
 
-__device__ __noinline__ void step1_post(Step1Shared &sh, int g, bool col) {
-    const int B = fused_args().r.B;
-            const StepArgs &S = fused_args().s;
+// a callee's pointer argument arrives in VGPRs (not known to be uniform): its
+// loads would all be vector loads into VGPRs; readfirstlane makes it scalar
+template <class T>
+__device__ __forceinline__ T *uniform_ptr(T *p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (T *)(((uint64_t)hi << 32) | lo);
+}
+
+// k_step1's LDS, named at namespace scope so the callees address it directly
+// (ds_* instructions; a pointer argument would be generic: flat accesses):
+// [cpw] Step1Shared, then each car's theta indices [cpw][B, 16-byte rounded]
+extern __shared__ __attribute__((aligned(16))) unsigned char s1_smem[];
+__device__ __forceinline__ Step1Shared &step1_shared(int c) { return reinterpret_cast<Step1Shared *>(s1_smem)[c]; }
+__device__ __forceinline__ uint16_t *step1_ti(int c, int cpw, int B) {
+    const int tib = (B * 2 + 15) & ~15;
+    return reinterpret_cast<uint16_t *>(s1_smem + (size_t)cpw * sizeof(Step1Shared) + (size_t)c * tib);
+}
+
+// LDS hand-off between the lanes of ONE wave (no workgroup barrier).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __noinline__ void step1_agent(const FusedArgs *fap, int t, int c) {
+    fap = uniform_ptr(fap);
+    t = __builtin_amdgcn_readfirstlane(t);
+    const int g = (int)blockIdx.x * launder_s(fap)->cpw + c;
+    Step1Shared &sh = step1_shared(c);
+    typedef __attribute__((address_space(3))) volatile double lds_vd;  // ds_* accesses, kept in LDS (volatile)
+    lds_vd *st = (lds_vd *)sh.st;
+    double raw_steer, vel;
+    int do_reset;
+    {  // the action, the autoreset (RaceCar.reset, base_classes.py:183-204)
+        const FusedArgs &fa = *launder_s(fap);
+        const StepArgs &S = fa.s;
+        if (S.actions_f64) {
+            const double *ac = S.actions_f64 + (size_t)t * fa.act_stride + (size_t)g * 2;
+            raw_steer = ac[0];
+            vel = ac[1];
+        } else {
+            const float *ac = S.actions + (size_t)t * fa.act_stride + (size_t)g * 2;
+            raw_steer = (double)ac[0];
+            vel = (double)ac[1];
+        }
+        do_reset = sh.env.pending ? 1 : 0;
+        if (do_reset) {  // then F110Env.reset's zero-action step
+            const uint64_t genv = (uint64_t)(S.env_offset + g);
+            const uint32_t k = spawn_draw(S.seed, genv, sh.env.episode) % (uint32_t)S.n_spawn;
+            const double *pz = S.spawn + (size_t)k * 3;
+            double px = pz[0], py = pz[1], pth = pz[2];
+            if (S.reset_f32) {
+                px = (double)(float)px;
+                py = (double)(float)py;
+                pth = (double)(float)pth;
+            }
+#pragma unroll
+            for (int q = 0; q < 7; ++q) st[q] = 0.0;
+            st[0] = px;
+            st[1] = py;
+            st[4] = pth;
+            sh.b0 = sh.b1 = 0.0;
+            sh.cnt = 0;
+            raw_steer = 0.0;
+            vel = 0.0;
+            S.start[g] = px;
+            S.start[S.E + g] = py;
+            S.start[2 * S.E + g] = pth;
+            sh.car.sx = px;
+            sh.car.sy = py;
+            sh.car.tg = 0;
+            sh.car.ns = 1;
+            sh.car.lt = 0.0f;
+            S.toggles[g] = 0;
+            S.near_start[g] = 1;
+            S.lap_times[g] = 0.0f;
+            S.lap_counts[g] = 0.0f;
+            if (S.ego == 0) {  // start_rot (f110_env.py:448-451), as k_agents
+                double cr, sr;
+                if (S.reset_f32) {
+                    const float nt = -(float)pth;
+                    cr = (double)np_sincosf(nt, true);
+                    sr = (double)np_sincosf(nt, false);
+                } else {
+                    cr_sincos(-pth, sr, cr);
+                }
+                sh.env.ct = cr;
+                sh.env.st = sr;
+                S.start_rot[g] = cr;
+                S.start_rot[S.E + g] = sr;
+            }
+        }
+    }
+    {  // RaceCar.update_pose (state and RK4 accumulator in LDS)
+        const StepArgs &S = launder_s(fap)->s;
+        double b0 = sh.b0, b1 = sh.b1;
+        int cnt = sh.cnt;
+        update_pose_impl<lds_vd *>(st, (lds_vd *)sh.acc, b0, b1, cnt, raw_steer, vel, S.pa[0], S.dt, S.integrator);
+        sh.b0 = b0;
+        sh.b1 = b1;
+        sh.cnt = cnt;
+    }
+    const double yaw = st[4];
+    {  // scan pose (base_classes.py:420-422), first lookup (laser_models.py:129)
+        const StepArgs &S = launder_s(fap)->s;
+        const bool no_offset = S.lidar_dist == 0.0 && isfinite(yaw);
+        double sy4 = 0.0, cy4 = 1.0;
+        if (!no_offset) cr_sincos(yaw, sy4, cy4);
+        const double sx = no_offset ? st[0] + 0.0 : st[0] + S.lidar_dist * cy4;
+        const double sy = no_offset ? st[1] + 0.0 : st[1] + S.lidar_dist * sy4;
+        sh.sx = sx;
+        sh.sy = sy;
+        sh.d00 = S.map.dt[cell_index(S.map, sx, sy)];
+        sh.vel = st[3];
+        sh.nstep = do_reset ? 0ull : sh.env.nstep;
+        sh.do_reset = do_reset;
+    }
+    {  // get_scan's beam-index runs
+        const StepArgs &S = launder_s(fap)->s;
+        const double t0 = first_theta_index(yaw, S.fov, S.theta_dis);
+        sh.nruns = build_beam_runs(t0, S.inc, S.theta_dis, S.B, sh.runs, kMaxSeg);
+    }
+}
+
+__device__ __noinline__ void step1_post(const FusedArgs *fap, int c) {
+    fap = uniform_ptr(fap);
+    const int g = (int)blockIdx.x * fap->cpw + c;
+    Step1Shared &sh = step1_shared(c);
+    const bool col = sh.col != 0;
+    const int B = fap->r.B;
+            const StepArgs &S = fap->s;
             const int do_reset = sh.do_reset;
             EpiCar car = sh.car;
             EpiEnv env = sh.env;
@@ -2091,23 +2145,207 @@ __device__ __noinline__ void step1_post(Step1Shared &sh, int g, bool col) {
             sh.env = env;
         }
 
-__global__ void __launch_bounds__(64, 8) k_step1(FusedArgs fa) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char s1_smem[];
-    Step1Shared &sh = *reinterpret_cast<Step1Shared *>(s1_smem);
-    uint16_t *s_ti = reinterpret_cast<uint16_t *>(s1_smem + sizeof(Step1Shared));  // [B]
-    const RayArgs &a = fa.r;
-    const int lane = (int)threadIdx.x;
-    const int g = (int)blockIdx.x;  // car == env (A = 1)
+// the argument block behind an opaque copy of its pointer (as kernarg_here):
+// the lane-0 sections' field loads stay in their step instead of being hoisted
+// out of the step loop into SGPRs, which would spill there
+__device__ __forceinline__ const FusedArgs *fused_args_here() { return launder_const(&fused_args()); }
+
+// the ray phase of one step (get_scan for the car, k_rays_fxr's two refilled
+// chunk slots, the TTC ballot): a call of its own, so its constants are loaded
+// per step instead of living in registers across the lane-0 sections
+struct Step1Rays {
+    uint32_t lanes, iters;
+    int32_t col;
+};
+
+__device__ __noinline__ Step1Rays step1_rays(const FusedArgs *fap, int w) {
+    fap = uniform_ptr(fap);
+    w = __builtin_amdgcn_readfirstlane(w);
+    const int cpw = launder_s(fap)->cpw;
+    const int g = (int)blockIdx.x * cpw + w;
+    uint16_t *s_ti = step1_ti(w, cpw, launder_s(fap)->r.B);
+    Step1Shared &sh = step1_shared(w);
+    const int lane = (int)threadIdx.x & 63;
+    uint32_t lanes_total = 0, lane_iters = 0;
+    // the ray phase's constants, loaded per step (kept live across the lane-0
+    // sections they would take SGPRs / VGPRs those need)
+    const RayArgs &a = launder_s(fap)->r;
     const int B = a.B;
     const int nch = (B + 63) >> 6;
     const FxLoop L = fx_loop<3>(a);
     const uint32_t P = (uint32_t)a.fxp_P;
     uint32_t zero_v;  // in a VGPR for the whole trace (the select's other operand is its SGPR mask)
     asm volatile("v_mov_b32 %0, %1" : "=v"(zero_v) : "s"(a.fx_zero));
+    const double x00 = sh.sx, y00 = sh.sy, d00 = sh.d00, vcar = sh.vel;
+    const uint64_t nstep = sh.nstep;
+    const int nr = sh.nruns;
+    // ---- 2. the theta index of every beam (get_scan, laser_models.py:167-184) ----
+    {
+        int vlo = 0;  // lane k < nch: the run holding beam 64 k
+        if (lane < nch) {
+            int lo = 0, hi = nr - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (sh.runs[mid].start <= lane * 64) lo = mid;
+                else hi = mid - 1;
+            }
+            vlo = lo;
+        }
+        for (int k = 0; k < nch; ++k) {
+            const int b = k * 64 + lane;
+            const int lo = __builtin_amdgcn_readlane(vlo, k);
+            int rs = sh.runs[lo].start;
+            double rt0 = sh.runs[lo].t0, rdl = sh.runs[lo].delta;
+            for (int j = lo + 1; j < nr; ++j) {  // the runs that start inside this chunk
+                const int s2 = sh.runs[j].start;
+                if (s2 > k * 64 + 63) break;
+                if (b >= s2) {
+                    rs = s2;
+                    rt0 = sh.runs[j].t0;
+                    rdl = sh.runs[j].delta;
+                }
+            }
+            int ti = (int)(rt0 + (double)(b - rs) * rdl);  // int(theta_index), :124
+            if (ti >= a.theta_dis) ti = 0;
+            if (b < B) s_ti[b] = (uint16_t)ti;
+        }
+    }
+    wave_sync();  // the car's theta indices: this wave's own
+    // ---- 3. the rays (k_rays_fxr's two refilled chunk slots) ----
+    const double ux = fma(x00, L.ir, L.cxk) - kFxpBase, uy = fma(y00, L.ir, L.cyk) - kFxpBase;
+    const bool fast_car = (ux >= a.fxp_lo) & (ux < a.fxp_hx) & (uy >= a.fxp_lo) & (uy < a.fxp_hy);
+    const uint32_t key = noise_key(a.seed, (uint64_t)(a.env_offset + g));
+    bool hit = false;
+    double x[2], y[2], d[2], tot[2], c[2], sn[2];
+    int kk[2];
+    int next = nch - 1;
+    float cval[2] = {0.0f, 0.0f};
+    int ctag[2] = {-1, -1};
+    auto arm = [&](int r) {
+        const int k = next--;
+        kk[r] = k;
+        const int b = k * 64 + lane;
+        const int ti = s_ti[b < B ? b : B - 1];
+        c[r] = a.cosines[ti];
+        sn[r] = a.sines[ti];
+        x[r] = x00;
+        y[r] = y00;
+        d[r] = b < B ? d00 : 0.0;
+        tot[r] = d[r];  // :130
+    };
+    auto finish = [&](int r) {  // fx_epilogue with the TTC flag kept in the wave
+        const RayArgs &K = launder_s(fap)->r;
+        const int b = kk[r] * 64 + lane, bc = b < B ? b : B - 1;
+        double nz = 0.0;
+        if (K.noise_ext) {
+            nz = K.noise_ext[(size_t)g * B + bc];
+        } else if (K.noise_std > 0.0) {
+            const int pp = kk[r] >> 1, ci = pp & 1;
+            float nv;
+            if (ctag[ci] == pp) {
+                nv = cval[ci];
+                ctag[ci] = -1;
+            } else {
+                float lo, hi;
+                beam_normal_pair_k(key, nstep, beam_noise_pair(b), lo, hi);
+                nv = (kk[r] & 1) ? hi : lo;
+                cval[ci] = (kk[r] & 1) ? lo : hi;
+                ctag[ci] = pp;
+            }
+            nz = K.noise_std * (double)nv;
+        }
+        if (b < B) {
+            double range = tot[r] > L.mr ? L.mr : tot[r];  // :143-144
+            if (K.noise_ext || K.noise_std > 0.0) range += nz;
+            // check_ttc_jit on the noisy scan (laser_models.py:188-217)
+            if (vcar != 0.0 && ttc_fires(range, K.side[b], vcar * K.beam_cos[b], K.ttc_thresh)) hit = true;
+            const int64_t rr = (int64_t)g * B + b;
+            if (K.obs) K.obs[(size_t)g * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
+            if (K.scans_f32) K.scans_f32[rr] = (float)range;
+            if (K.scans_f64) K.scans_f64[rr] = range;
+        }
+        lanes_total += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(b < B));
+    };
+    if (fast_car) {
+        kk[0] = kk[1] = -1;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) d[r] = tot[r] = x[r] = y[r] = c[r] = sn[r] = 0.0;
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+            if (next >= 0) arm(r);
+        for (;;) {
+            uint64_t m[2], mall = 0;
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+            double dn[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                if (m[r]) {
+                    const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+                    dn[r] = fx_load<3>(a.m.dt, fxp_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero_v, P));
+                }
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                mall |= m[r];
+                lane_iters += (uint32_t)__popcll(m[r]);
+            }
+            bool open = false;
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                if (kk[r] >= 0 && !m[r]) {  // wave-uniform: the chunk has ended; refill the slot
+                    finish(r);
+                    if (next >= 0) arm(r);
+                    else kk[r] = -1;
+                }
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                if (m[r]) {
+                    d[r] = dn[r];
+                    tot[r] += d[r];  // :141
+                }
+                open |= kk[r] >= 0;
+            }
+            if (mall == 0 && !open) break;
+        }
+    } else {  // the scan origin is off the map: the IEEE cell of every lookup, one chunk at a time
+        uint32_t cntl = 0;
+        while (next >= 0) {
+            arm(0);
+            while ((dhi(d[0]) != 0u) & (tot[0] <= L.mr)) {
+                x[0] += d[0] * c[0];  // :135
+                y[0] += d[0] * sn[0];  // :136
+                d[0] = fx_load<3>(a.m.dt, exact_offset_pad(a.m, x[0], y[0], P));
+                tot[0] += d[0];  // :141
+                ++cntl;
+            }
+            finish(0);
+        }
+        lane_iters += wave_sum(cntl);
+    }
+    const bool col = __builtin_amdgcn_ballot_w64(hit) != 0ull;
+    return Step1Rays{lanes_total, lane_iters, col ? 1 : 0};
+}
 
-    // lane 0: the car's persistent state, in LDS for the whole launch
-    if (lane == 0) {
+// cpw cars per workgroup, one wave each for the rays; the lane-parallel
+// sections (k_agents' update_pose and scan set-up, k_post_single's epilogue)
+// run on wave 0, lane c for car c, as the three-launch step runs them on one
+// lane per car.  Two workgroup barriers per step: post(t) and agent(t + 1) of a
+// car are the same lane's back-to-back calls.
+constexpr int kStep1MaxCpw = 8;
+
+__global__ void __launch_bounds__(64 * kStep1MaxCpw, 8) k_step1(FusedArgs fa) {
+    const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    const int cpw = fa.cpw;
+    const int g0 = (int)blockIdx.x * cpw;
+    const int nc = min(cpw, fa.s.E - g0);  // cars of this workgroup
+    const int nsteps = fa.nsteps;
+    const bool lead = w == 0 && lane < nc;  // car `lane`'s lane-parallel sections
+
+    if (lead) {  // the car's persistent state, in LDS for the whole launch
+        Step1Shared &sh = step1_shared(lane);
         const StepArgs &S = fused_args().s;
+        const int g = g0 + lane;
 #pragma unroll
         for (int k = 0; k < 7; ++k) sh.st[k] = S.st[(size_t)k * S.E + g];
         sh.b0 = S.sb[g];
@@ -2126,170 +2364,34 @@ __global__ void __launch_bounds__(64, 8) k_step1(FusedArgs fa) {
         sh.env = env;
     }
     uint32_t lanes_total = 0, lane_iters = 0;
-    for (int t = 0; t < fa.nsteps; ++t) {
-        // ---- 1. k_agents for this car (lane 0) ----
-        if (lane == 0) step1_agent(sh, g, t);
-        __syncthreads();  // one wave: the LDS hand-off
-        const double x00 = sh.sx, y00 = sh.sy, d00 = sh.d00, vcar = sh.vel;
-        const uint64_t nstep = sh.nstep;
-        const int nr = sh.nruns;
-        // ---- 2. the theta index of every beam (get_scan, laser_models.py:167-184) ----
-        {
-            int vlo = 0;  // lane k < nch: the run holding beam 64 k
-            if (lane < nch) {
-                int lo = 0, hi = nr - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (sh.runs[mid].start <= lane * 64) lo = mid;
-                    else hi = mid - 1;
-                }
-                vlo = lo;
-            }
-            for (int k = 0; k < nch; ++k) {
-                const int b = k * 64 + lane;
-                const int lo = __builtin_amdgcn_readlane(vlo, k);
-                int rs = sh.runs[lo].start;
-                double rt0 = sh.runs[lo].t0, rdl = sh.runs[lo].delta;
-                for (int j = lo + 1; j < nr; ++j) {  // the runs that start inside this chunk
-                    const int s2 = sh.runs[j].start;
-                    if (s2 > k * 64 + 63) break;
-                    if (b >= s2) {
-                        rs = s2;
-                        rt0 = sh.runs[j].t0;
-                        rdl = sh.runs[j].delta;
-                    }
-                }
-                int ti = (int)(rt0 + (double)(b - rs) * rdl);  // int(theta_index), :124
-                if (ti >= a.theta_dis) ti = 0;
-                if (b < B) s_ti[b] = (uint16_t)ti;
-            }
+    for (int t = 0; t < nsteps; ++t) {
+        // ---- 1. k_agents (wave 0, a lane per car) ----
+        if (lead) step1_agent(fused_args_here(), t, lane);
+        __syncthreads();  // the cars' scan set-up
+        // ---- 2./3. the theta indices and the rays (a wave per car) ----
+        if (w < nc) {
+            const Step1Rays rr = step1_rays(fused_args_here(), w);
+            lanes_total += rr.lanes;
+            lane_iters += rr.iters;
+            if (lane == 0) step1_shared(w).col = rr.col;
         }
-        __syncthreads();
-        // ---- 3. the rays (k_rays_fxr's two refilled chunk slots) ----
-        const double ux = fma(x00, L.ir, L.cxk) - kFxpBase, uy = fma(y00, L.ir, L.cyk) - kFxpBase;
-        const bool fast_car = (ux >= a.fxp_lo) & (ux < a.fxp_hx) & (uy >= a.fxp_lo) & (uy < a.fxp_hy);
-        const uint32_t key = noise_key(a.seed, (uint64_t)(a.env_offset + g));
-        bool hit = false;
-        double x[2], y[2], d[2], tot[2], c[2], sn[2];
-        int kk[2];
-        int next = nch - 1;
-        float cval[2] = {0.0f, 0.0f};
-        int ctag[2] = {-1, -1};
-        auto arm = [&](int r) {
-            const int k = next--;
-            kk[r] = k;
-            const int b = k * 64 + lane;
-            const int ti = s_ti[b < B ? b : B - 1];
-            c[r] = a.cosines[ti];
-            sn[r] = a.sines[ti];
-            x[r] = x00;
-            y[r] = y00;
-            d[r] = b < B ? d00 : 0.0;
-            tot[r] = d[r];  // :130
-        };
-        auto finish = [&](int r) {  // fx_epilogue with the TTC flag kept in the wave
-            const RayArgs &K = kernarg_here();
-            const int b = kk[r] * 64 + lane, bc = b < B ? b : B - 1;
-            double nz = 0.0;
-            if (K.noise_ext) {
-                nz = K.noise_ext[(size_t)g * B + bc];
-            } else if (K.noise_std > 0.0) {
-                const int pp = kk[r] >> 1, ci = pp & 1;
-                float nv;
-                if (ctag[ci] == pp) {
-                    nv = cval[ci];
-                    ctag[ci] = -1;
-                } else {
-                    float lo, hi;
-                    beam_normal_pair_k(key, nstep, beam_noise_pair(b), lo, hi);
-                    nv = (kk[r] & 1) ? hi : lo;
-                    cval[ci] = (kk[r] & 1) ? lo : hi;
-                    ctag[ci] = pp;
-                }
-                nz = K.noise_std * (double)nv;
-            }
-            if (b < B) {
-                double range = tot[r] > L.mr ? L.mr : tot[r];  // :143-144
-                if (K.noise_ext || K.noise_std > 0.0) range += nz;
-                // check_ttc_jit on the noisy scan (laser_models.py:188-217)
-                if (vcar != 0.0 && ttc_fires(range, K.side[b], vcar * K.beam_cos[b], K.ttc_thresh)) hit = true;
-                const int64_t rr = (int64_t)g * B + b;
-                if (K.obs) K.obs[(size_t)g * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
-                if (K.scans_f32) K.scans_f32[rr] = (float)range;
-                if (K.scans_f64) K.scans_f64[rr] = range;
-            }
-            lanes_total += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(b < B));
-        };
-        if (fast_car) {
-            kk[0] = kk[1] = -1;
-#pragma unroll
-            for (int r = 0; r < 2; ++r) d[r] = tot[r] = x[r] = y[r] = c[r] = sn[r] = 0.0;
-#pragma unroll
-            for (int r = 0; r < 2; ++r)
-                if (next >= 0) arm(r);
-            for (;;) {
-                uint64_t m[2], mall = 0;
-#pragma unroll
-                for (int r = 0; r < 2; ++r)
-                    m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
-                double dn[2];
-#pragma unroll
-                for (int r = 0; r < 2; ++r)
-                    if (m[r]) {
-                        const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
-                        dn[r] = fx_load<3>(a.m.dt, fxp_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero_v, P));
-                    }
-#pragma unroll
-                for (int r = 0; r < 2; ++r) {
-                    mall |= m[r];
-                    lane_iters += (uint32_t)__popcll(m[r]);
-                }
-                bool open = false;
-#pragma unroll
-                for (int r = 0; r < 2; ++r)
-                    if (kk[r] >= 0 && !m[r]) {  // wave-uniform: the chunk has ended; refill the slot
-                        finish(r);
-                        if (next >= 0) arm(r);
-                        else kk[r] = -1;
-                    }
-#pragma unroll
-                for (int r = 0; r < 2; ++r) {
-                    if (m[r]) {
-                        d[r] = dn[r];
-                        tot[r] += d[r];  // :141
-                    }
-                    open |= kk[r] >= 0;
-                }
-                if (mall == 0 && !open) break;
-            }
-        } else {  // the scan origin is off the map: the IEEE cell of every lookup, one chunk at a time
-            uint32_t cntl = 0;
-            while (next >= 0) {
-                arm(0);
-                while ((dhi(d[0]) != 0u) & (tot[0] <= L.mr)) {
-                    x[0] += d[0] * c[0];  // :135
-                    y[0] += d[0] * sn[0];  // :136
-                    d[0] = fx_load<3>(a.m.dt, exact_offset_pad(a.m, x[0], y[0], P));
-                    tot[0] += d[0];  // :141
-                    ++cntl;
-                }
-                finish(0);
-            }
-            lane_iters += wave_sum(cntl);
-        }
-        const bool col = __builtin_amdgcn_ballot_w64(hit) != 0ull;
-        // ---- 4. k_post_single for this car (lane 0) ----
-        if (lane == 0) step1_post(sh, g, col);
-        __syncthreads();  // the next step's LDS tables
+        __syncthreads();  // the cars' TTC flags
+        // ---- 4. k_post_single (wave 0, a lane per car) ----
+        if (lead) step1_post(fused_args_here(), lane);
     }
-    if (lane == 0) {  // the persistent state, once
+    if (lead) {  // the persistent state, once
+        const Step1Shared &sh = step1_shared(lane);
         const StepArgs &S = fused_args().s;
+        const int g = g0 + lane;
 #pragma unroll
         for (int k = 0; k < 7; ++k) S.st[(size_t)k * S.E + g] = sh.st[k];
         S.sb[g] = sh.b0;
         S.sb[S.E + g] = sh.b1;
         S.scnt[g] = sh.cnt;
-        unsigned long long *cs = a.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+    }
+    if (w < nc && lane == 0) {
+        const RayArgs &a = fused_args().r;
+        unsigned long long *cs = a.ctr + (size_t)((blockIdx.x * kStep1MaxCpw + w) % kCtrSlots) * kCtrStride;
         atomicAdd(cs, (unsigned long long)(lanes_total + lane_iters));  // + the first lookup of every ray
         atomicAdd(cs + 1, (unsigned long long)lanes_total);
     }
@@ -2327,12 +2429,6 @@ __device__ __forceinline__ int pass_beams(const MultiShared &sh, int pr) {
     return (n0 > 0 ? n0 : 0) + (n1 > 0 ? n1 : 0);
 }
 
-// LDS hand-off between the lanes of ONE wave (no workgroup barrier).
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
     reset_next_heavy(a);
@@ -2531,9 +2627,11 @@ hipError_t launch_step1(const StepArgs &a, int32_t n, int64_t act_stride, hipStr
     fa.s = a;
     fa.nsteps = n;
     fa.act_stride = act_stride;
+    fa.cpw = a.fused_cpw < 1 ? 1 : (a.fused_cpw > kStep1MaxCpw ? kStep1MaxCpw : a.fused_cpw);
     void *args[] = {&fa};
-    const size_t lds = sizeof(Step1Shared) + ((size_t)a.B * 2 + 15) / 16 * 16;
-    if ((e = hipLaunchKernel(reinterpret_cast<const void *>(&k_step1), dim3((unsigned)a.E), dim3(64), args, lds, s)) !=
+    const size_t lds = (size_t)fa.cpw * (sizeof(Step1Shared) + ((size_t)a.B * 2 + 15) / 16 * 16);
+    const unsigned nblk = (unsigned)((a.E + fa.cpw - 1) / fa.cpw);
+    if ((e = hipLaunchKernel(reinterpret_cast<const void *>(&k_step1), dim3(nblk), dim3(64 * fa.cpw), args, lds, s)) !=
         hipSuccess)
         return e;
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;

@@ -407,8 +407,8 @@ def test_pool_kernel_identical(tracks, gpu, monkeypatch, A, beams):
                 assert torch.equal(x, y), f"variant {k} step {t}"
 
 
-@pytest.mark.parametrize("beams,dtype", [(1080, "f32"), (333, "f64"), (64, "f32")])
-def test_step1_matches_three_launch_step(tracks, gpu, beams, dtype):
+@pytest.mark.parametrize("beams,dtype,cpw", [(1080, "f32", 8), (333, "f64", 3), (64, "f32", 1), (1080, "f64", 5)])
+def test_step1_matches_three_launch_step(tracks, gpu, beams, dtype, cpw, monkeypatch):
     """k_step1 (f110_set_fused: the single-agent step -- dynamics, rays, post
     stage -- in one launch per call, or n steps in one launch via
     f110_step_n) against the three-launch step: obs, f64 / f32 scans,
@@ -416,7 +416,9 @@ def test_step1_matches_three_launch_step(tracks, gpu, beams, dtype):
     and lookup counters bit-identical over 40 noisy random-action steps with
     autoreset (crashes and respawns happen), a masked reset in the middle
     (which runs the three-launch path in both) and float32 / float64 actions;
-    f110_step_n over 9 / 11 / 9 steps equals single calls."""
+    f110_step_n over 9 / 11 / 9 steps equals single calls.  cpw cars per
+    workgroup (F110_FUSED_CPW); 203 envs leave a ragged last workgroup."""
+    monkeypatch.setenv("F110_FUSED_CPW", str(cpw))
     E = 203
     sp = _spawns(1)
     rng = np.random.default_rng(beams)
