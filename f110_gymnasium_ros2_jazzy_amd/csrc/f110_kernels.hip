@@ -1164,7 +1164,9 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
         }
         vlo = lo;
     }
-    auto arm = [&](int r) {
+    // in_loop: the loop's closing `tot += d` completes tot = d (:130) in the
+    // iteration that re-arms the slot, so the total is updated there without a select
+    auto arm = [&](int r, bool in_loop) {
         const int k = next;
         next -= wstride;
         kk[r] = k;
@@ -1177,7 +1179,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
         x[r] = x00;
         y[r] = y00;
         d[r] = b < B ? d00 : 0.0;
-        tot[r] = d[r];  // :130
+        tot[r] = in_loop ? 0.0 : d[r];  // :130
     };
     uint32_t lanes = 0;
     // device noise: chunks 2p and 2p + 1 (beams b and b + 64 of a 128-beam block) share one
@@ -1232,7 +1234,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
         }
 #pragma unroll
         for (int r = 0; r < NS; ++r)
-            if (next >= 0) arm(r);
+            if (next >= 0) arm(r, false);
         __builtin_amdgcn_s_waitcnt(0);
         for (;;) {
             uint64_t m[NS], mall = 0;
@@ -1240,15 +1242,16 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
             for (int r = 0; r < NS; ++r)
                 m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
             // the running slots' gathers go out first, so that they are in flight while
-            // an ended slot writes its chunk and re-arms (scalar run search, table loads)
-            double dn[NS];  // read only where m[r] (no per-iteration zeroing)
+            // an ended slot writes its chunk and re-arms (scalar run search, table loads).
+            // The gather lands in d[r] itself: a lane whose ray has ended reads the zero
+            // cell, so d = 0 keeps its total (no per-lane select of old and new values)
 #pragma unroll
             for (int r = 0; r < NS; ++r)
                 if (m[r]) {
                     const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
                     const uint32_t off = PAD ? fxp_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero_v, P)
                                              : fxn_offset(a.m, L, x[r], y[r], d[r], c[r], sn[r], act, m[r], zero);
-                    dn[r] = fx_load<3>(a.m.dt, off);
+                    d[r] = fx_load<3>(a.m.dt, off);
                 }
 #pragma unroll
             for (int r = 0; r < NS; ++r) {
@@ -1262,15 +1265,14 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
             for (int r = 0; r < NS; ++r)
                 if (kk[r] >= 0 && !m[r]) {  // wave-uniform: the chunk has ended; refill the slot
                     finish(r);
-                    if (next >= 0) arm(r);
+                    if (next >= 0) arm(r, true);
                     else kk[r] = -1;
                 }
+            // :141 for every slot: a running slot's ended lanes read d = 0, a re-armed slot
+            // completes tot = d00, a closed slot's total is no longer read
 #pragma unroll
             for (int r = 0; r < NS; ++r) {
-                if (m[r]) {
-                    d[r] = dn[r];
-                    tot[r] += d[r];  // :141
-                }
+                tot[r] += d[r];  // :141
                 open |= kk[r] >= 0;
             }
             if (!any && !open) break;
@@ -1278,7 +1280,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
     } else {
         uint32_t cnt = 0;
         while (next >= 0) {
-            arm(0);
+            arm(0, false);
             while ((dhi(d[0]) != 0u) & (tot[0] <= L.mr)) {
                 if (PAD) {  // an origin off the map: the IEEE cell of every lookup
                     x[0] += d[0] * c[0];  // :135
