@@ -112,6 +112,7 @@ struct f110_ctx {
     int32_t pool_T = 80;     // k_rays_fxp's refill threshold in ended slots (F110_FX_POOL_T)
     bool fused = false;      // single-agent steps as one k_step1 launch (f110_set_fused / F110_FUSED)
     int32_t fused_cpw = 8;   // cars per k_step1 workgroup (F110_FUSED_CPW, 1..8)
+    int32_t multi_block = 128;  // k_post_multi threads per env (F110_MULTI_BLOCK: 64 or 128)
     uint8_t *pcost = nullptr;  // [EA][nch] k_rays_fxp's per-chunk costs (queue order of the next launch)
     bool count_slots = false;  // f110_set_simt / F110_SIMT: lane-slot counter of the fixed-point loops (f110_read_simt)
     int fx_ilp = 1;         // rays per lane (F110_FX_ILP; default by car count)
@@ -739,6 +740,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (const char *v = std::getenv("F110_FX_POOL")) c->fx_pool = std::max(0, std::min(2, std::atoi(v)));
     if (const char *v = std::getenv("F110_FUSED")) c->fused = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FUSED_CPW")) c->fused_cpw = std::max(1, std::min(8, std::atoi(v)));
+    if (const char *v = std::getenv("F110_MULTI_BLOCK")) c->multi_block = std::atoi(v) == 64 ? 64 : 128;
     if (const char *v = std::getenv("F110_FX_POOL_T")) c->pool_T = std::max(1, std::min(128, std::atoi(v)));
     if (fx_ok) {
         hipError_t ep = c->alloc(&c->pcost, EA * (size_t)c->nch);
@@ -885,6 +887,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.fx_refill = c->fx_refill;
     a.fx_pool = c->fx_pool;
     a.fused_cpw = c->fused_cpw;
+    a.multi_block = c->multi_block;
     a.pool_T = c->pool_T;
     a.pcost = c->pcost;
     a.fx_slots = c->fx_slots;

@@ -68,6 +68,7 @@ struct StepArgs {
     int32_t fx_pool;    // F110_FX_POOL: cars per k_rays_fxp wave (lane-level refill; 0 = off)
     int32_t pool_T;     // F110_FX_POOL_T: k_rays_fxp refills once this many slots have ended
     int32_t fused_cpw;  // F110_FUSED_CPW: cars per k_step1 workgroup (1..8)
+    int32_t multi_block;  // F110_MULTI_BLOCK: k_post_multi threads per env (64 or 128)
     uint8_t *pcost;     // [EA][nch] k_rays_fxp's per-chunk cost of the previous launch (its queue order)
     int32_t count_slots;  // F110_SIMT (default 1): lane-slot counter of the fixed-point loops
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2..4: k_rays_fxn)

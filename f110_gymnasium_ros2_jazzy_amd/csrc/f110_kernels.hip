@@ -2405,7 +2405,7 @@ __global__ void __launch_bounds__(64 * kStep1MaxCpw, 8) k_step1(FusedArgs fa) {
 // and their serial phases overlap.  Wave 0 runs GJK (collision_multiple on
 // the pre-TTC poses) while wave 1 builds each (car, opponent) pair's box,
 // blocked beam range and beam window (on the post-TTC pose).
-constexpr int kMultiBlock = 128;
+constexpr int kMultiBlock = 128;  // default; F110_MULTI_BLOCK=64: one wave per env (GJK then the geometry)
 
 struct MultiShared {
     double stl[kMaxAgents][7];   // state after the TTC response
@@ -2432,7 +2432,8 @@ __device__ __forceinline__ int pass_beams(const MultiShared &sh, int pr) {
 }
 
 
-__global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
+template <int BLK>
+__global__ void __launch_bounds__(BLK, 6) k_post_multi(StepArgs a) {
     reset_next_heavy(a);
     __shared__ MultiShared sh;
     const int e = blockIdx.x;
@@ -2473,7 +2474,7 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
                     sh.col[j] = 1;
                 }
     }
-    if (kMultiBlock == 64 || tid >= 64) {
+    if (BLK == 64 || tid >= 64) {
         // per-pair geometry (on wave 1 when there are two), spread over lanes:
         // boxes and ego headings, then one (pair, vertex) per lane, then
         // per-pair reductions
@@ -2530,7 +2531,7 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
     for (int jj = 0; jj < A - 1; ++jj) {
         int total = 0;
         for (int i = 0; i < A; ++i) total += pass_beams(sh, i * (A - 1) + jj);
-        for (int item = tid; item < total; item += kMultiBlock) {
+        for (int item = tid; item < total; item += BLK) {
             int i = 0, k = item;
             for (int n = pass_beams(sh, jj); k >= n; n = pass_beams(sh, i * (A - 1) + jj)) {
                 k -= n;
@@ -2873,7 +2874,10 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     if (single)
         hipLaunchKernelGGL(k_post_single, dim3((a.E + 63) / 64), dim3(64), 0, s, a);
     else if (tiled)
-        hipLaunchKernelGGL(k_post_multi, dim3(a.E), dim3(kMultiBlock), 0, s, a);
+    {
+        if (a.multi_block == 64) hipLaunchKernelGGL(k_post_multi<64>, dim3(a.E), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL(k_post_multi<kMultiBlock>, dim3(a.E), dim3(kMultiBlock), 0, s, a);
+    }
     else
         hipLaunchKernelGGL(k_post, dim3(a.E), dim3(kBlock), post_lds_bytes(a.A, a.B), s, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -67,5 +67,34 @@ def main():
     print(json.dumps(res))
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("SC_CHUNK"):
     main()
+
+
+def chunk_order_model():
+    """Chunk-level orders for the two slots (whole 64-beam chunks, as
+    k_rays_fxr traces them): descending index (today) against the previous
+    step's per-chunk max lookups, longest first (LPT)."""
+    L0, L1 = two_step_counts()
+    n, B = L1.shape
+    nch = -(-B // 64)
+    pad0 = np.ones((n, nch * 64), np.int64)
+    pad1 = np.ones((n, nch * 64), np.int64)
+    pad0[:, :B] = L0
+    pad1[:, :B] = L1
+    c0 = pad0.reshape(n, nch, 64).max(2)
+    res = {}
+    for name, order in (("descending", np.tile(np.arange(nch)[::-1], (n, 1))),
+                        ("prev_lpt", np.argsort(-c0, axis=1, kind="stable")),
+                        ("this_lpt", np.argsort(-pad1.reshape(n, nch, 64).max(2), axis=1, kind="stable"))):
+        # sim_chunk traces chunks in descending index order: hand it the chunks
+        # already permuted and reversed
+        ch = pad1.reshape(n, nch, 64)
+        perm = np.take_along_axis(ch, order[:, :, None], 1)[:, ::-1].reshape(n, nch * 64)
+        it, ev = sim_chunk(perm[:, :nch * 64])
+        res[name] = {"wave_iters_per_car": float(it.mean()), "simt": float((L1 - 1).sum() / (it.sum() * 128))}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__" and os.environ.get("SC_CHUNK"):
+    chunk_order_model()

@@ -136,7 +136,8 @@ def test_ray_kernel_dispatch_variants_identical(tracks, gpu, monkeypatch, A):
     row-major EDT with 1, 2 and 3 rays per lane (F110_FX_ILP; k_rays_fxn for
     2 and 3, on the padded table or, F110_FX_PAD=0, the clamped one), on
     the 4x4-tiled EDT (F110_FX_TABLE=tiled), and with the
-    straggler hand-off to the refill tail kernel, F110_EVICT=1) give
+    straggler hand-off to the refill tail kernel, F110_EVICT=1; k_post_multi
+    with one wave per env, F110_MULTI_BLOCK=64) give
     bit-identical steps: scans, obs, collisions,
     states, with noise, autoreset and a masked reset."""
     E = 300  # not a multiple of 4 cars per chunked block
@@ -146,12 +147,13 @@ def test_ray_kernel_dispatch_variants_identical(tracks, gpu, monkeypatch, A):
     acts = np.stack([rng.uniform(-0.4189, 0.4189, (30, E, A)), rng.uniform(0, 20, (30, E, A))], -1).astype(np.float32)
     mask = rng.random(E) < 0.5
     outs = []
-    for k, wpb, evict, ilp, table, pad in (("0", "1", "0", "1", "rm", "1"), ("1", "1", "0", "1", "rm", "1"),
-                                           ("2", "1", "0", "1", "rm", "1"), ("2", "4", "0", "1", "rm", "1"),
-                                           ("3", "1", "0", "1", "rm", "1"), ("3", "1", "0", "2", "rm", "1"),
-                                           ("3", "1", "0", "2", "rm", "0"), ("3", "1", "0", "3", "rm", "1"),
-                                           ("3", "1", "0", "3", "rm", "0"), ("3", "1", "0", "1", "tiled", "1"),
-                                           ("3", "1", "1", "1", "rm", "1")):
+    for k, wpb, evict, ilp, table, pad, mb in (("0", "1", "0", "1", "rm", "1", "128"), ("1", "1", "0", "1", "rm", "1", "128"),
+                                               ("2", "1", "0", "1", "rm", "1", "128"), ("2", "4", "0", "1", "rm", "1", "128"),
+                                               ("3", "1", "0", "1", "rm", "1", "128"), ("3", "1", "0", "2", "rm", "1", "128"),
+                                               ("3", "1", "0", "2", "rm", "0", "128"), ("3", "1", "0", "3", "rm", "1", "128"),
+                                               ("3", "1", "0", "3", "rm", "0", "128"), ("3", "1", "0", "1", "tiled", "1", "128"),
+                                               ("3", "1", "1", "1", "rm", "1", "128"), ("3", "1", "0", "2", "rm", "1", "64")):
+        monkeypatch.setenv("F110_MULTI_BLOCK", mb)  # k_post_multi: one or two waves per env
         monkeypatch.setenv("F110_RAY_KERNEL", k)
         monkeypatch.setenv("F110_RAY_WPB", wpb)
         monkeypatch.setenv("F110_EVICT", evict)  # 3 + 1: k_rays_fx with the straggler hand-off to k_rays_fx_tail
