@@ -692,9 +692,11 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
         if (const char *v = std::getenv("F110_FX_ILP")) c->fx_ilp = std::max(1, std::min(4, std::atoi(v)));
         if (c->evict || c->fx_tiled) c->fx_ilp = 1;
     }
-    // heavy-first pays where one ray grid is a few rounds of waves deep (8192 cars: 0.175 vs 0.181 ms)
+    // heavy-first pays where one ray grid is a few rounds of waves deep (16384 cars: 0.281 vs 0.287 ms)
     // and costs where it is deep (65536 cars: 1.288 vs 1.251 ms without; profiles/r02_ray_ab/ab_heavy.json)
-    if (!std::getenv("F110_HEAVY_T") && EA > 32768) c->heavy_T = 0;
+    // or one round or less (round 3, every wave starts at once: 8192 cars 0.172 vs 0.167, 4096 cars
+    // 0.124 vs 0.109 ms without; profiles/r03_ab/small_shards.json)
+    if (!std::getenv("F110_HEAVY_T") && (EA > 32768 || EA <= 8192)) c->heavy_T = 0;
     if (c->ray_kernel >= 2 && c->heavy_T > 0) {
         // up to 1/8 of the waves, in blocks of 4 (measured: ~7% of the waves
         // have a ray longer than 40 lookups and carry ~46% of the wave-iterations)
