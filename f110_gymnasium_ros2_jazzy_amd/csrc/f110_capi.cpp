@@ -1291,7 +1291,10 @@ extern "C" int f110_profile_begin(f110_ctx *ctx, int32_t max_steps) {
     ctx->free_prof();
     ctx->prof_ev.resize((size_t)4 * max_steps);
     for (size_t i = 0; i < ctx->prof_ev.size(); ++i) {
-        hipError_t e = hipEventCreate(&ctx->prof_ev[i]);
+        // device-side timestamps only: no system-scope release / acquire fence, which would
+        // write back and invalidate the L2 between the step's kernels (the ray kernel would then
+        // start on a cold cache and read longer than it runs unprofiled)
+        hipError_t e = hipEventCreateWithFlags(&ctx->prof_ev[i], hipEventDisableSystemFence);
         if (e != hipSuccess) {
             ctx->prof_ev.resize(i);
             ctx->free_prof();
