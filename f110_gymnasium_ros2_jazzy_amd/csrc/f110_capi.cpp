@@ -71,7 +71,7 @@ struct f110_ctx {
     unsigned long long *ctr = nullptr;
     std::vector<void *> allocs;
     // f110_profile_begin/end
-    std::vector<hipEvent_t> prof_ev;  // 4 per recorded step
+    std::vector<hipEvent_t> prof_ev;  // 6 per recorded step: (start, stop) of k_agents, the ray kernel, k_post
     int prof_max = 0, prof_n = 0;
     const double *noise_ext = nullptr;  // f110_set_scan_noise (caller-owned)
     uint64_t *wtrace = nullptr;         // f110_debug_wave_trace buffer (diagnostics)
@@ -107,6 +107,7 @@ struct f110_ctx {
     uint32_t rmp_zero = 0;
     bool fx_pad = false;    // k_rays_fxn / k_rays_fxr on the padded table (default from 32768 cars; F110_FX_PAD)
     int32_t fx_slots = 2;    // F110_FX_SLOTS (A/B): chunk slots per k_rays_fxr wave
+    int32_t fxr_lean = 1;    // k_rays_fxs in place of k_rays_fxr<.., PAD, 2> (F110_FXR_LEAN=0: the round-3 kernel)
     int32_t fx_refill = 0;   // waves per car of k_rays_fxr (0 = k_rays_fxn; F110_FX_REFILL overrides)
     int32_t fx_pool = 0;     // cars per k_rays_fxp wave (lane-level refill; 0 = off; F110_FX_POOL)
     int32_t pool_T = 80;     // k_rays_fxp's refill threshold in ended slots (F110_FX_POOL_T)
@@ -123,7 +124,7 @@ struct f110_ctx {
 
     hipEvent_t *next_prof_events() {
         if (prof_n >= prof_max) return nullptr;
-        return &prof_ev[(size_t)4 * prof_n++];
+        return &prof_ev[(size_t)6 * prof_n++];
     }
     void free_prof() {
         for (hipEvent_t e : prof_ev) (void)hipEventDestroy(e);
@@ -454,7 +455,9 @@ static hipError_t upload(T **p, const std::vector<T> &h) {
 static hipError_t build_padded_table(MapTables *t, int32_t pad, const std::vector<double> &d) {
     const int32_t H = t->H, W = t->W;
     const size_t N = (size_t)H * W;
-    const size_t P = (size_t)pad, Wp = ((size_t)W + 2 * P + 15) / 16 * 16, Hp = (size_t)H + 2 * P;
+    // rows of Wp = 511 mod 512 cells: the row stride Wp * 8 is 8 bytes short of a multiple of
+    // 4096, which k_rays_fxs's offset arithmetic needs (kFxsBase); any width serves the others
+    const size_t P = (size_t)pad, Wp = ((size_t)W + 2 * P + 1 + 511) / 512 * 512 - 1, Hp = (size_t)H + 2 * P;
     if ((Wp * Hp + 16) * 8 >= (1ull << 32) || Wp * 8 >= (1u << 24)) return hipSuccess;
     std::vector<double> rmp(Wp * Hp + 16, d[N - 1]);
     for (int r = 0; r < H; ++r)
@@ -739,6 +742,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     c->fx_refill = EA >= 32768 ? 1 : 0;
     if (const char *v = std::getenv("F110_FX_REFILL")) c->fx_refill = std::max(0, std::min(16, std::atoi(v)));
     if (const char *v = std::getenv("F110_FX_SLOTS")) c->fx_slots = std::atoi(v) == 3 ? 3 : 2;
+    if (const char *v = std::getenv("F110_FXR_LEAN")) c->fxr_lean = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FX_POOL")) c->fx_pool = std::max(0, std::min(2, std::atoi(v)));
     if (const char *v = std::getenv("F110_FUSED")) c->fused = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FUSED_CPW")) c->fused_cpw = std::max(1, std::min(8, std::atoi(v)));
@@ -893,6 +897,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.pool_T = c->pool_T;
     a.pcost = c->pcost;
     a.fx_slots = c->fx_slots;
+    a.fxr_lean = c->fxr_lean;
     a.fx_tiled = c->fx_tiled ? 1 : 0;
     a.fx_lds = c->fx_lds;
     a.fx_nolean = c->fx_nolean ? 1 : 0;
@@ -1289,11 +1294,11 @@ extern "C" int f110_profile_begin(f110_ctx *ctx, int32_t max_steps) {
     if (!ctx || max_steps < 0) return fail(F110_E_INVALID, "f110_profile_begin: bad arguments");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     ctx->free_prof();
-    ctx->prof_ev.resize((size_t)4 * max_steps);
+    ctx->prof_ev.resize((size_t)6 * max_steps);
     for (size_t i = 0; i < ctx->prof_ev.size(); ++i) {
-        // device-side timestamps only: no system-scope release / acquire fence, which would
-        // write back and invalidate the L2 between the step's kernels (the ray kernel would then
-        // start on a cold cache and read longer than it runs unprofiled)
+        // the events go with the kernels' own dispatches (hipExtLaunchKernel in launch_env_step):
+        // each pair holds that kernel's begin / end timestamps, as rocprofv3's kernel trace does,
+        // and no marker packet (nor its cache release) sits between the step's kernels
         hipError_t e = hipEventCreateWithFlags(&ctx->prof_ev[i], hipEventDisableSystemFence);
         if (e != hipSuccess) {
             ctx->prof_ev.resize(i);
@@ -1311,11 +1316,11 @@ extern "C" int f110_profile_end(f110_ctx *ctx, double ms_out[3], int32_t *steps_
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     double acc[3] = {0, 0, 0};
     for (int i = 0; i < ctx->prof_n; ++i) {
-        hipEvent_t *ev = &ctx->prof_ev[(size_t)4 * i];
-        HIP_TRY(hipEventSynchronize(ev[3]));
+        hipEvent_t *ev = &ctx->prof_ev[(size_t)6 * i];
+        HIP_TRY(hipEventSynchronize(ev[5]));
         for (int k = 0; k < 3; ++k) {
             float ms = 0.f;
-            HIP_TRY(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+            HIP_TRY(hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]));
             acc[k] += ms;
         }
     }

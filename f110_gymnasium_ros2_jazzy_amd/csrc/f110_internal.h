@@ -64,6 +64,7 @@ struct StepArgs {
     uint32_t rmp_zero;
     int32_t fx_pad;     // F110_FX_PAD: k_rays_fxn on the padded table
     int32_t fx_slots;   // F110_FX_SLOTS (A/B): chunk slots per k_rays_fxr wave, 2 or 3
+    int32_t fxr_lean;   // k_rays_fxs for k_rays_fxr's padded two-slot kernel (F110_FXR_LEAN=0: off, A/B)
     int32_t fx_refill;  // F110_FX_REFILL: waves per car of k_rays_fxr (two chunk slots with refill; 0 = off)
     int32_t fx_pool;    // F110_FX_POOL: cars per k_rays_fxp wave (lane-level refill; 0 = off)
     int32_t pool_T;     // F110_FX_POOL_T: k_rays_fxp refills once this many slots have ended
@@ -112,6 +113,14 @@ struct StepArgs {
     unsigned long long *ctr;    // [kCtrSlots][16]: [0] lookups, [1] rays (see count_rays), [2] lane slots of the fixed-point loops
 };
 
+// RN(1 / lidar_max) in f32 for k_rays_fxs's obs division, or 0 (the IEEE
+// divide) outside [2^-30, 2^30], where an intermediate could be subnormal
+inline float obs_reciprocal(float lmax) {
+    if (!(lmax >= 0x1p-30f && lmax <= 0x1p30f)) return 0.0f;
+    volatile float l = lmax;  // one IEEE f32 divide (not folded into a double one)
+    return 1.0f / l;
+}
+
 // k_rays_tiled's own argument block: only what the ray loop and its epilogue
 // read (the full StepArgs kept 90 SGPRs live: 7 instead of 8 blocks per CU).
 struct RayArgs {
@@ -139,6 +148,7 @@ struct RayArgs {
     double *scans_f64;         // [EA][B] or null
     int32_t obs_len;
     float lidar_max;
+    float obs_rinv;            // RN(1 / lidar_max) for k_rays_fxs's obs division (0: IEEE divide)
     // chunked dispatch (k_rays_tiled<.., CH = true>)
     int32_t G4;                // blocks per chunk slot (4 cars per block)
     uint8_t order[kMaxChunks]; // chunk of each slot
@@ -162,6 +172,7 @@ struct RayArgs {
     // inside the padded table (see fxp_offset)
     double fxp_lo, fxp_hx, fxp_hy;
     int32_t fxp_P;
+    double fxs_cx, fxs_cy;  // k_rays_fxs: 2^20 + P + 2^-26 - origin / res (see kFxsBase)
     int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_read_simt; F110_SIMT)
     // straggler hand-off of k_rays_fx (EVICT) -> k_rays_fx_tail: SoA records
     // ev[7][ev_cap] = x, y, d, tot, cos, sin, noise; ev_gb[2][ev_cap] = car, beam.
@@ -213,6 +224,21 @@ constexpr uint32_t kFxBand = 4u;
 // 2^-28 = 2^-26.
 constexpr double kFxpBase = 16777216.0;
 constexpr uint32_t kFxpBand = 4u;
+// k_rays_fxs: t = fma(x, inv_res, 2^20 + P + 2^-26 - origin / res) lies in
+// [2^20, 2^21), ulp 2^-32: t's low dword is the fraction of q + P + 2^-26 and
+// its high dword's low 24 bits are 3 * 2^20 (the exponent's low bits) +
+// floor(q + P + 2^-26) -- the u24 multiplies read the high dwords as they are
+// (no v_alignbit).  The 3 * 2^20 terms add 3 * 2^20 * (k1 + 8) to the byte
+// offset, which vanishes mod 2^32 because the padded table's row stride k1 is
+// 8 bytes short of a multiple of 4096 (build_padded_table).  The +2^-26 shift
+// makes the guard band one compare: a lane is near a cell edge when the low
+// dword is below 2 * kFxsBand (= 2^-25, a band of 2^-26 on either side of the
+// edge, as kFxpBand); such lanes take the IEEE cell, so the shifted integer
+// part of the others is floor(q + P).  Error budget (units of q): t's and the
+// constant's roundings (2^-33 each) and those of kFxpBase's analysis: < 2^-27.4.
+constexpr double kFxsBase = 1048576.0;
+constexpr double kFxsShift = 0x1p-26;
+constexpr uint32_t kFxsBand = 64u;  // 2^-26 in units of 2^-32
 
 struct ScanArgs {
     MapView map;

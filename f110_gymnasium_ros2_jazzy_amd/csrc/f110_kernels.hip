@@ -18,6 +18,7 @@
 //  k_scan_batch / k_dynamics: the C-ABI building blocks (f110_scan_batch,
 //  f110_dynamics_batch).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -1305,6 +1306,290 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxr(RayArgs a) {  // 8 waves per
     }
 }
 
+// The kernarg block behind an opaque copy of its pointer: loads through it
+// stay where they are written (in the refill pass) instead of being hoisted
+// out of the trace loop into SGPRs, which would spill there.
+// an opaque SGPR copy of a pointer to read-only kernel arguments, typed in the
+// constant address space: its field loads are scalar loads placed at the use
+// (a generic pointer out of the asm would make them flat vector loads)
+template <class T>
+__device__ __forceinline__ const T *launder_const(const T *ptr) {
+    const __attribute__((address_space(4))) T *p;
+    asm volatile("s_mov_b64 %0, %1" : "=s"(p) : "s"(ptr));
+    return (const T *)p;
+}
+
+__device__ __forceinline__ const RayArgs &kernarg_here() { return *launder_const(kernarg_rays()); }
+
+__device__ __forceinline__ bool lane_in(uint64_t mask) {
+    return (uint32_t)(mask >> (threadIdx.x & 63)) & 1u;
+}
+
+// ------------------------------------------------------------------------
+// k_rays_fxs: k_rays_fxr<HANDOFF, PAD = true, 2> with a lean refill pass (the
+// default where k_rays_fxr runs; F110_FXR_LEAN=0 for the round-3 kernel).
+// A chunk's finish / re-arm pass was ~176 VALU per chunk, 43 % of the
+// kernel's VALU.  Here:
+// - nothing the pass or the rare IEEE cell path reads is held in SGPRs across
+//   the loop (kernel arguments are re-read at the use through kernarg_here,
+//   the scan origin and first lookup sit in VGPRs): no SGPR spills into VGPR
+//   lanes (k_rays_fxr: 92 v_readlane / v_writelane);
+// - table loads and the obs store take 32-bit lane offsets from an SGPR base
+//   (saddr form) instead of 64-bit address arithmetic;
+// - the obs entry's f32 division by lidar_max is q = v * y, r = fma(-q, lm, v),
+//   q' = fma(r, y, q) with y = RN(1 / lm): q is within one ulp of v / lm, so
+//   q' is the correctly rounded quotient (Markstein's theorem) when no
+//   intermediate is subnormal; lanes with v < 2^-60 (and lidar_max outside
+//   [2^-30, 2^30], obs_rinv = 0) take the IEEE divide.  Checked exhaustively
+//   against the divide for every f32 v in [0, lm] (tests/test_host_lib.py).
+// Same per-ray arithmetic as k_rays_fxr, so bit-identical.
+__device__ __forceinline__ float obs_scan_value_fast(double r, float lmax, float rinv) {
+    // obs_scan_value's NaN -> lmax, +inf -> lmax, -inf -> 0, clip: v_min_f32 returns its
+    // other operand for a NaN, and -0.0 stays -0.0 (not < 0)
+    float v = __builtin_fminf((float)r, lmax);
+    v = v < 0.0f ? 0.0f : v;
+    const float q = v * rinv;
+    float q2 = __builtin_fmaf(__builtin_fmaf(-q, lmax, v), rinv, q);
+    const bool ieee = !(v >= 0x1p-60f) | (rinv == 0.0f);
+    if (__builtin_amdgcn_ballot_w64(ieee)) {  // rare (wave-uniform branch)
+        asm volatile("" ::: "memory");  // the divide stays in the branch (not speculated and selected)
+        if (ieee) q2 = v / lmax;
+    }
+    return q2;
+}
+
+template <class T>
+__device__ __forceinline__ T ld_off(const T *base, uint32_t byte_off) {  // global_load v, v_off, s[base]
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + byte_off);
+}
+
+// fxp_offset with the rare IEEE path's map fields read from the kernel
+// arguments at the use (not held in SGPRs across the loop)
+__device__ __forceinline__ uint32_t fxs_offset(const FxLoop &L, double &x, double &y, double d, double c, double s,
+                                               bool act, uint64_t amask, uint32_t zero_v) {
+    x += d * c;  // :135
+    y += d * s;  // :136
+    double tx, ty;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tx) : "v"(x), "v"(L.ir), "s"(L.cxk));
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(ty) : "v"(y), "v"(L.ir), "s"(L.cyk));
+    const uint32_t lx = dlo(tx), ly = dlo(ty);
+    const uint32_t col = __builtin_amdgcn_alignbit(dhi(tx), lx, 28);
+    const uint32_t row = __builtin_amdgcn_alignbit(dhi(ty), ly, 28);
+    const uint32_t band = min((lx << 4) + 16u * kFxpBand, (ly << 4) + 16u * kFxpBand);
+    const uint32_t prow = __umul24(row, L.k1);
+    uint32_t fast;
+    asm volatile("v_mad_u32_u24 %0, %1, 8, %2" : "=v"(fast) : "v"(col), "v"(prow));
+    uint32_t off = act ? fast : zero_v;
+    if (__builtin_amdgcn_ballot_w64(band < 32u * kFxpBand) & amask) {  // wave-uniform, rare
+        const RayArgs &K = kernarg_here();
+        if (act & (band < 32u * kFxpBand)) off = exact_offset_pad(K.m, x, y, (uint32_t)K.fxp_P);
+    }
+    return off;
+}
+
+// fxs_offset without the rare branch: the fixed-point offset (the zero cell's
+// for an ended ray) and whether the lane lies within the guard band of a cell
+// edge (the caller takes the IEEE path for those lanes, both slots at once)
+// (kFxsBase: the high dwords of t feed the u24 multiplies directly, the low
+// dwords hold the shifted fractions; cx / cy are RayArgs::fxs_cx / fxs_cy)
+__device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, double cy, double &x, double &y,
+                                                  double d, double c, double s, bool act, uint32_t zero_v,
+                                                  bool &near) {
+    x += d * c;  // :135
+    y += d * s;  // :136
+    double tx, ty;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tx) : "v"(x), "v"(L.ir), "s"(cx));
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(ty) : "v"(y), "v"(L.ir), "s"(cy));
+    near = min(dlo(tx), dlo(ty)) < 2u * kFxsBand;
+    const uint32_t prow = __umul24(dhi(ty), L.k1);
+    uint32_t fast;
+    asm volatile("v_mad_u32_u24 %0, %1, 8, %2" : "=v"(fast) : "v"(dhi(tx)), "v"(prow));
+    return act ? fast : zero_v;
+}
+
+template <bool HANDOFF>
+__global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
+    const int wj = (int)blockIdx.x / a.EA;
+    const int g = (int)blockIdx.x - wj * a.EA;
+    const int lane = (int)threadIdx.x;
+    const int B = a.B;
+    const int e = HANDOFF ? g / a.A : g;
+    const int nch = (B + 63) >> 6;
+    const int wstride = a.G4;
+    const double *dt = a.m.dt;
+    const FxLoop L = fx_loop<3>(a);
+    // the scan origin and first lookup in VGPRs (re-arm copies them into a slot)
+    double x00, y00, d00;
+    asm volatile("v_mov_b64 %0, %1" : "=v"(x00) : "s"(ld_const(a.ray0 + g)));
+    asm volatile("v_mov_b64 %0, %1" : "=v"(y00) : "s"(ld_const(a.ray0 + a.EA + g)));
+    asm volatile("v_mov_b64 %0, %1" : "=v"(d00) : "s"(ld_const(a.ray0 + 2 * a.EA + g)));  // :129
+    uint32_t zero_v;  // the zero cell's offset in a VGPR (the select's other operand is its SGPR mask)
+    asm volatile("v_mov_b32 %0, %1" : "=v"(zero_v) : "s"(a.fx_zero));
+
+    double x[2], y[2], d[2], tot[2], c[2], sn[2];
+    int kk[2];
+    int next = nch - 1 - wj;
+    int vlo = 0;  // lane k < nch: the run holding beam 64 k (as k_rays_fxr)
+    if (lane < nch) {
+        const BeamRun *R = a.runs + (size_t)g * kMaxSeg;
+        int lo = 0, hi = ld_const(a.nruns + g) - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (R[mid].start <= lane * 64) lo = mid;
+            else hi = mid - 1;
+        }
+        vlo = lo;
+    }
+    auto arm = [&](int r, bool in_loop) {
+        const RayArgs &K = kernarg_here();
+        const int k = next;
+        next -= wstride;
+        kk[r] = k;
+        const int b = k * 64 + lane, bc = b < B ? b : B - 1;
+        const int lo = __builtin_amdgcn_readlane(vlo, k);
+        int ti = (int)beam_theta(K.runs + (size_t)g * kMaxSeg, ld_const(K.nruns + g), lo, k * 64, bc);  // :124
+        if (ti >= K.theta_dis) ti = 0;
+        c[r] = ld_off(K.cosines, (uint32_t)ti * 8u);
+        sn[r] = ld_off(K.sines, (uint32_t)ti * 8u);
+        x[r] = x00;
+        y[r] = y00;
+        d[r] = b < B ? d00 : 0.0;
+        tot[r] = in_loop ? 0.0 : d[r];  // :130
+    };
+    uint32_t lanes = 0;
+    float cval[2] = {0.0f, 0.0f};  // k_rays_fxr's two-entry cache of the unused half of a pair draw
+    int ctag[2] = {-1, -1};
+    auto finish = [&](int r) {
+        const RayArgs &K = kernarg_here();
+        const int b = kk[r] * 64 + lane;
+        const bool inb = b < B;
+        const int bc = inb ? b : B - 1;
+        double nz = 0.0;
+        if (K.noise_ext) {
+            nz = K.noise_ext[(size_t)e * B + bc];
+        } else if (K.noise_std > 0.0) {
+            const int pp = kk[r] >> 1, ci = pp & 1;
+            float nv;
+            if (ctag[ci] == pp) {
+                nv = cval[ci];
+                ctag[ci] = -1;
+            } else {
+                const uint32_t key = noise_key(K.seed, (uint64_t)(K.env_offset + e));
+                float lo, hi;
+                beam_normal_pair_k(key, ld_const(K.noise_step + e), beam_noise_pair(b), lo, hi);
+                nv = (kk[r] & 1) ? hi : lo;
+                cval[ci] = (kk[r] & 1) ? lo : hi;
+                ctag[ci] = pp;
+            }
+            nz = K.noise_std * (double)nv;
+        }
+        if (inb) {  // fx_epilogue
+            const double mr = K.max_range;
+            double range = tot[r] > mr ? mr : tot[r];  // :143-144
+            if (K.noise_ext || K.noise_std > 0.0) range += nz;
+            const double v = ld_const(K.vel + g);
+            const uint32_t boff = (uint32_t)bc * 8u;
+            if (v != 0.0 && ttc_fires(range, ld_off(K.side, boff), v * ld_off(K.beam_cos, boff), K.ttc_thresh))
+                K.ttc_hit[g] = 1;
+            if (K.obs && (!HANDOFF || g == e * K.A)) {
+                float *orow = K.obs + (size_t)e * K.obs_len;
+                *reinterpret_cast<float *>(reinterpret_cast<char *>(orow) + (uint32_t)b * 4u) =
+                    obs_scan_value_fast(range, K.lidar_max, K.obs_rinv);
+            }
+            const size_t row = (size_t)g * B;
+            if (K.scans_f32) *reinterpret_cast<float *>(reinterpret_cast<char *>(K.scans_f32 + row) + (uint32_t)b * 4u) = (float)range;
+            if (K.scans_f64) *reinterpret_cast<double *>(reinterpret_cast<char *>(K.scans_f64 + row) + (uint32_t)b * 8u) = range;
+            if (HANDOFF) *reinterpret_cast<double *>(reinterpret_cast<char *>(K.scan + row) + (uint32_t)b * 8u) = range;
+        }
+        lanes += (uint32_t)min(64, B - kk[r] * 64);  // the chunk's beams (scalar)
+    };
+
+    uint32_t lane_iters = 0, iters = 0;
+    const double ux = fma(ld_const(a.ray0 + g), L.ir, L.cxk) - kFxpBase;
+    const double uy = fma(ld_const(a.ray0 + a.EA + g), L.ir, L.cyk) - kFxpBase;
+    // q + P of the scan origin inside [fxp_lo, fxp_h*): its rays stay in the padded table (false for NaN)
+    const bool fast_car = (ux >= a.fxp_lo) & (ux < a.fxp_hx) & (uy >= a.fxp_lo) & (uy < a.fxp_hy);
+    if (fast_car) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            kk[r] = -1;
+            d[r] = tot[r] = x[r] = y[r] = c[r] = sn[r] = 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+            if (next >= 0) arm(r, false);
+        __builtin_amdgcn_s_waitcnt(0);
+        // The loop's scalar control is kept to what a trip needs (the CU's one scalar unit
+        // serves its 32 resident waves: k_rays_fxr spent ~30 SALU per trip against 36 VALU):
+        // the slots' active-lane counts drive both branches and the lookup count, and the
+        // refill / exit tests run only when a slot has no active lane.
+        uint32_t trips = 0, idle = 0;
+        for (;;) {
+            uint64_t m[2];
+            uint32_t cnt[2], off[2];
+            bool near[2];
+            // both slots step unconditionally (a slot without active lanes reads the zero cell:
+            // ~15 VALU wasted in the car's last chunk instead of a branch per slot per trip)
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+                m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+                cnt[r] = (uint32_t)__popcll(m[r]);
+                off[r] = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act, zero_v, near[r]);
+            }
+            const uint64_t nb0 = __builtin_amdgcn_ballot_w64(near[0]) & m[0];
+            const uint64_t nb1 = __builtin_amdgcn_ballot_w64(near[1]) & m[1];
+            if (nb0 | nb1) {  // rare: lanes within the guard band take tiled_cell's IEEE path
+                const RayArgs &K = kernarg_here();
+                if (lane_in(nb0)) off[0] = exact_offset_pad(K.m, x[0], y[0], (uint32_t)K.fxp_P);
+                if (lane_in(nb1)) off[1] = exact_offset_pad(K.m, x[1], y[1], (uint32_t)K.fxp_P);
+            }
+#pragma unroll
+            for (int r = 0; r < 2; ++r) d[r] = ld_off(dt, off[r]);
+            lane_iters += cnt[0] + cnt[1];
+            ++trips;
+            if (min(cnt[0], cnt[1]) == 0u) {  // rare: a slot's chunk has ended, or the slot is closed
+                const bool none = cnt[0] + cnt[1] == 0u;
+                idle += none ? 1u : 0u;
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+                    if (kk[r] >= 0 && cnt[r] == 0u) {  // wave-uniform: the chunk has ended; refill the slot
+                        finish(r);
+                        if (next >= 0) arm(r, true);
+                        else kk[r] = -1;
+                    }
+                if (none && kk[0] < 0 && kk[1] < 0) break;
+            }
+#pragma unroll
+            for (int r = 0; r < 2; ++r) tot[r] += d[r];  // :141 (a re-armed slot completes tot = d00, as k_rays_fxr)
+        }
+        iters = trips - idle;  // trips with an active lane (k_rays_fxr's count)
+    } else {  // an origin off the map: the IEEE cell of every lookup, chunk after chunk
+        uint32_t cnt = 0;
+        while (next >= 0) {
+            arm(0, false);
+            const RayArgs &K = kernarg_here();
+            while ((dhi(d[0]) != 0u) & (tot[0] <= L.mr)) {
+                x[0] += d[0] * c[0];  // :135
+                y[0] += d[0] * sn[0];  // :136
+                d[0] = fx_load<3>(dt, exact_offset_pad(K.m, x[0], y[0], (uint32_t)K.fxp_P));
+                tot[0] += d[0];  // :141
+                ++cnt;
+            }
+            finish(0);
+        }
+        lane_iters = wave_sum(cnt);
+        iters = wave_max(cnt);
+    }
+    if (lane == 0) {
+        const RayArgs &K = kernarg_here();
+        unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+        atomicAdd(cs, (unsigned long long)(lanes + lane_iters));  // the first lookup came from k_agents
+        atomicAdd(cs + 1, (unsigned long long)lanes);
+        if (K.count_slots) atomicAdd(cs + 2, (unsigned long long)iters * (fast_car ? 128ull : 64ull));
+    }
+}
+
 // ------------------------------------------------------------------------
 // k_rays_fxp (F110_FX_POOL = NCAR cars per wave): lane-level refill over a
 // pool of cars.  k_rays_fxr refills a slot only when its whole 64-beam chunk
@@ -1331,25 +1616,6 @@ struct PoolCar {
     uint64_t step;           // noise counter (steps since reset)
     uint32_t key, pad_;      // noise key of the car's env
 };
-
-// The kernarg block behind an opaque copy of its pointer: loads through it
-// stay where they are written (in the refill pass) instead of being hoisted
-// out of the trace loop into SGPRs, which would spill there.
-// an opaque SGPR copy of a pointer to read-only kernel arguments, typed in the
-// constant address space: its field loads are scalar loads placed at the use
-// (a generic pointer out of the asm would make them flat vector loads)
-template <class T>
-__device__ __forceinline__ const T *launder_const(const T *ptr) {
-    const __attribute__((address_space(4))) T *p;
-    asm volatile("s_mov_b64 %0, %1" : "=s"(p) : "s"(ptr));
-    return (const T *)p;
-}
-
-__device__ __forceinline__ const RayArgs &kernarg_here() { return *launder_const(kernarg_rays()); }
-
-__device__ __forceinline__ bool lane_in(uint64_t mask) {
-    return (uint32_t)(mask >> (threadIdx.x & 63)) & 1u;
-}
 
 template <bool HANDOFF, int NCAR>
 __global__ void __launch_bounds__(64, 8) k_rays_fxp(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
@@ -2589,6 +2855,9 @@ size_t step_lds_bytes(int A, int B) { return post_lds_bytes(A, B); }
 
 hipError_t launch_step1(const StepArgs &a, int32_t n, int64_t act_stride, hipStream_t s, hipEvent_t *ev) {
     hipError_t e;
+    // f110_profile_begin: 6 events per step, (start, stop) of k_agents / the ray kernel / k_post,
+    // attached to the kernel's own dispatch (hipExtLaunchKernel: its begin / end timestamps, no
+    // marker packets between the kernels).  The fused step is one kernel: the ray pair.
     if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
     FusedArgs fa{};
@@ -2613,6 +2882,7 @@ hipError_t launch_step1(const StepArgs &a, int32_t n, int64_t act_stride, hipStr
     ra.obs = a.out.obs;
     ra.obs_len = (int32_t)obs_row(a);
     ra.lidar_max = (float)a.p.lidar_max;
+    ra.obs_rinv = obs_reciprocal(ra.lidar_max);
     ra.scans_f32 = a.out.scans;
     ra.scans_f64 = a.out.scans_f64;
     // the padded table (see k_rays_fxn's PAD): t = x / res + 2^24 + P
@@ -2634,22 +2904,21 @@ hipError_t launch_step1(const StepArgs &a, int32_t n, int64_t act_stride, hipStr
     void *args[] = {&fa};
     const size_t lds = (size_t)fa.cpw * (sizeof(Step1Shared) + ((size_t)a.B * 2 + 15) / 16 * 16);
     const unsigned nblk = (unsigned)((a.E + fa.cpw - 1) / fa.cpw);
-    if ((e = hipLaunchKernel(reinterpret_cast<const void *>(&k_step1), dim3(nblk), dim3(64 * fa.cpw), args, lds, s)) !=
-        hipSuccess)
+    if ((e = hipExtLaunchKernel(reinterpret_cast<const void *>(&k_step1), dim3(nblk), dim3(64 * fa.cpw), args, lds, s,
+                                ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0)) != hipSuccess)
         return e;
-    if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;
-    if (ev && (e = hipEventRecord(ev[3], s)) != hipSuccess) return e;
+    if (ev && (e = hipEventRecord(ev[4], s)) != hipSuccess) return e;
+    if (ev && (e = hipEventRecord(ev[5], s)) != hipSuccess) return e;
     return hipSuccess;
 }
 
 hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     const int EA = a.E * a.A;
     hipError_t e;
-    if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
+    auto evk = [&](int i) -> hipEvent_t { return ev ? ev[i] : nullptr; };  // (start, stop) pairs (launch_step1)
     // 64-thread blocks: a few thousand cars must still spread over all CUs
-    hipLaunchKernelGGL(k_agents, dim3((EA + 63) / 64), dim3(64), 0, s, a);
+    hipExtLaunchKernelGGL(k_agents, dim3((EA + 63) / 64), dim3(64), 0, s, evk(0), evk(1), 0, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
     if (a.gate_wait && (e = hipStreamWaitEvent(s, a.gate_wait, 0)) != hipSuccess) return e;
     const int64_t R = (int64_t)EA * a.B;
     const dim3 grid((unsigned)((R + kBlock - 1) / kBlock));
@@ -2658,7 +2927,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     const bool tiled = a.ray_kernel != 0;
     const bool single = a.A == 1 && tiled;
     if (a.ray_kernel == 0) {
-        hipLaunchKernelGGL(k_rays, grid, dim3(kBlock), 0, s, a);
+        hipExtLaunchKernelGGL(k_rays, grid, dim3(kBlock), 0, s, evk(2), evk(3), 0, a);
     } else {
         RayArgs ra{};
         ra.m = a.tmap;
@@ -2690,6 +2959,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         ra.obs = a.out.obs;
         ra.obs_len = (int32_t)obs_row(a);
         ra.lidar_max = (float)a.p.lidar_max;
+        ra.obs_rinv = obs_reciprocal(ra.lidar_max);
         ra.scans_f32 = a.out.scans;
         ra.scans_f64 = a.out.scans_f64;
         const bool rot = !(a.tmap.os == 0.0 && a.tmap.oc == 1.0);
@@ -2813,6 +3083,8 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                         ra.fxp_lo = Rn;
                         ra.fxp_hx = (double)a.tmap.W + 2.0 * P - Rn;
                         ra.fxp_hy = (double)a.tmap.H + 2.0 * P - Rn;
+                        ra.fxs_cx = std::fma(-a.tmap.ox, a.tmap.inv_res, kFxsBase + P + kFxsShift);
+                        ra.fxs_cy = std::fma(-a.tmap.oy, a.tmap.inv_res, kFxsBase + P + kFxsShift);
                         f = fn_p[N - 2][v2];
                     }
                     const int pool = a.fx_pool;
@@ -2840,6 +3112,9 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                                              reinterpret_cast<const void *>(&k_rays_fxr<false, true, 3>),
                                              reinterpret_cast<const void *>(&k_rays_fxr<true, true, 3>)};
                         f = fr[(a.fx_slots == 3 ? 4 : 0) + (pad ? 2 : 0) + (single ? 0 : 1)];
+                        if (pad && a.fx_slots != 3 && a.fxr_lean)  // the lean refill pass (same outputs)
+                            f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false>)
+                                       : reinterpret_cast<const void *>(&k_rays_fxs<true>);
                         ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
                         g2 = dim3((unsigned)(ra.EA * ra.G4));
                     }
@@ -2859,29 +3134,30 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                        : reinterpret_cast<const void *>(&k_rays_tiled<false, false, true, true, true>);
         ra.wtrace = a.wtrace;
         const unsigned bdim = ch ? 64u * (unsigned)ra.wpb : (unsigned)kBlock;
-        if ((e = hipLaunchKernel(f, g2, dim3(bdim), args, fx ? lds_bytes : 0u, s)) != hipSuccess) return e;
-        if (fx && a.ev) {  // the handed-off stragglers (the queue is read on the device)
+        const bool tail = fx && a.ev;
+        if ((e = hipExtLaunchKernel(f, g2, dim3(bdim), args, fx ? lds_bytes : 0u, s, evk(2), tail ? nullptr : evk(3),
+                                    0)) != hipSuccess)
+            return e;
+        if (tail) {  // the handed-off stragglers (the queue is read on the device)
             const unsigned tg = (unsigned)std::max<int64_t>(
                 a.ev_P, std::min<int64_t>(kTailWaves, ((int64_t)a.ev_cap + 63) / 64) / a.ev_P * a.ev_P);
             const void *tf = single ? reinterpret_cast<const void *>(&k_rays_fx_tail<false>)
                                     : reinterpret_cast<const void *>(&k_rays_fx_tail<true>);
-            if ((e = hipLaunchKernel(tf, dim3(tg), dim3(64), args, 0, s)) != hipSuccess) return e;
+            if ((e = hipExtLaunchKernel(tf, dim3(tg), dim3(64), args, 0, s, nullptr, evk(3), 0)) != hipSuccess) return e;
         }
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (a.gate_record && (e = hipEventRecord(a.gate_record, s)) != hipSuccess) return e;
-    if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;
     if (single)
-        hipLaunchKernelGGL(k_post_single, dim3((a.E + 63) / 64), dim3(64), 0, s, a);
+        hipExtLaunchKernelGGL(k_post_single, dim3((a.E + 63) / 64), dim3(64), 0, s, evk(4), evk(5), 0, a);
     else if (tiled)
     {
-        if (a.multi_block == 64) hipLaunchKernelGGL(k_post_multi<64>, dim3(a.E), dim3(64), 0, s, a);
-        else hipLaunchKernelGGL(k_post_multi<kMultiBlock>, dim3(a.E), dim3(kMultiBlock), 0, s, a);
+        if (a.multi_block == 64) hipExtLaunchKernelGGL(k_post_multi<64>, dim3(a.E), dim3(64), 0, s, evk(4), evk(5), 0, a);
+        else hipExtLaunchKernelGGL(k_post_multi<kMultiBlock>, dim3(a.E), dim3(kMultiBlock), 0, s, evk(4), evk(5), 0, a);
     }
     else
-        hipLaunchKernelGGL(k_post, dim3(a.E), dim3(kBlock), post_lds_bytes(a.A, a.B), s, a);
+        hipExtLaunchKernelGGL(k_post, dim3(a.E), dim3(kBlock), post_lds_bytes(a.A, a.B), s, evk(4), evk(5), 0, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (ev && (e = hipEventRecord(ev[3], s)) != hipSuccess) return e;
     return hipSuccess;
 }
 

@@ -263,8 +263,10 @@ F110_API int f110_set_simt(f110_ctx *ctx, int32_t on);
 F110_API int f110_read_simt(f110_ctx *ctx, uint64_t *loop_lookups, uint64_t *lane_slots, void *stream);
 
 /* ---- per-kernel timing ----------------------------------------------------
- * Records HIP events around each of the three launches of the next
- * max_steps f110_step/f110_reset calls (k_agents, k_rays, k_post).
+ * Attaches a (start, stop) HIP event pair to the dispatch of each of the
+ * three kernels of the next max_steps f110_step/f110_reset calls (k_agents,
+ * k_rays, k_post; hipExtLaunchKernel: the kernel's own begin / end
+ * timestamps, no marker packet between the kernels).
  * f110_profile_end waits for them and returns the summed milliseconds per
  * kernel and the number of steps recorded.  Used by bench.py for the
  * roofline of the dominant kernel (k_rays). */

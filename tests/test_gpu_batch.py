@@ -343,9 +343,12 @@ def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
     monkeypatch.setenv("F110_FX_ILP", "2")
     monkeypatch.setenv("F110_HEAVY_T", "0")  # k_rays_fxr has no heavy-first dispatch
     outs, ctrs = [], []
-    for refill, pad in (("0", "0"), ("1", "0"), ("3", "0"), ("1", "1")):  # off; 1 or 3 waves per car; padded EDT
+    # off; 1 or 3 waves per car; padded EDT with k_rays_fxr's round-3 pass (lean 0) and k_rays_fxs (lean 1)
+    for refill, pad, lean in (("0", "0", "1"), ("1", "0", "1"), ("3", "0", "1"), ("1", "1", "0"), ("1", "1", "1"),
+                              ("3", "1", "1")):
         monkeypatch.setenv("F110_FX_REFILL", refill)
         monkeypatch.setenv("F110_FX_PAD", pad)
+        monkeypatch.setenv("F110_FXR_LEAN", lean)
         sim = _sim(tracks, gpu, n_envs=E, n_agents=A, num_beams=beams, noise_std=0.01, autoreset=True,
                    spawn_poses=sp, seed=6, keep_f64_scans=True)
         assert sim.ray_refill == min(int(refill), (beams + 63) // 64)
@@ -359,7 +362,7 @@ def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
         outs.append(rec)
         ctrs.append(sim.read_counters())
         sim.close()
-    for k in (1, 2, 3):
+    for k in range(1, len(outs)):
         assert ctrs[0] == ctrs[k]
         for t, (a, b) in enumerate(zip(outs[0], outs[k])):
             for x, y in zip(a, b):

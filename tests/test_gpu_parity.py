@@ -296,13 +296,13 @@ def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A, nonexact
     nonexact_budget(f"ray_cast_adversarial_A{A}", nonexact)
 
 
-@pytest.mark.parametrize("kernel,ilp,table,pad,refill,pool", [
-    ("2", "1", "rm", "1", "0", "0"), ("3", "1", "rm", "1", "0", "0"), ("3", "2", "rm", "0", "0", "0"),
-    ("3", "2", "rm", "1", "0", "0"), ("3", "3", "rm", "1", "0", "0"), ("3", "1", "tiled", "1", "0", "0"),
-    ("3", "2", "rm", "0", "1", "0"), ("3", "2", "rm", "1", "1", "0"), ("3", "2", "rm", "1", "0", "1"),
-    ("3", "2", "rm", "1", "0", "2")])
+@pytest.mark.parametrize("kernel,ilp,table,pad,refill,pool,lean", [
+    ("2", "1", "rm", "1", "0", "0", "1"), ("3", "1", "rm", "1", "0", "0", "1"), ("3", "2", "rm", "0", "0", "0", "1"),
+    ("3", "2", "rm", "1", "0", "0", "1"), ("3", "3", "rm", "1", "0", "0", "1"), ("3", "1", "tiled", "1", "0", "0", "1"),
+    ("3", "2", "rm", "0", "1", "0", "1"), ("3", "2", "rm", "1", "1", "0", "1"), ("3", "2", "rm", "1", "1", "0", "0"),
+    ("3", "2", "rm", "1", "0", "1", "1"), ("3", "2", "rm", "1", "0", "2", "1")])
 def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanners, monkeypatch, kernel, ilp, table,
-                                                      pad, refill, pool):
+                                                      pad, refill, pool, lean):
     """k_rays_fx's fixed-point cell index (F110_RAY_KERNEL=3, the default;
     on the row-major EDT with 1 or 2 rays per lane, k_rays_fxn for 2, and on
     the 4x4-tiled EDT) against the oracle's IEEE xy_2_rc
@@ -317,7 +317,8 @@ def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanne
     binade, u24 offsets, no clamp) or the clamped one (0, the default); origins 1-20
     cells outside the map edges straddle its per-car test (fast loop up to
     6 cells out, the IEEE loop beyond); with F110_FX_REFILL=1 the same
-    through k_rays_fxr, with F110_FX_POOL=1/2 through k_rays_fxp (lane-level
+    through k_rays_fxr (k_rays_fxs on the padded table, F110_FXR_LEAN=0 the
+    round-3 pass), with F110_FX_POOL=1/2 through k_rays_fxp (lane-level
     refill over a pool of cars; a pool holding an off-map origin takes the
     IEEE loop for all its cars)."""
     from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
@@ -327,6 +328,7 @@ def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanne
     monkeypatch.setenv("F110_FX_PAD", pad)
     monkeypatch.setenv("F110_FX_REFILL", refill)  # k_rays_fxr (one wave per car, chunk slots with refill)
     monkeypatch.setenv("F110_FX_POOL", pool)  # k_rays_fxp (lane-level refill over a pool of cars)
+    monkeypatch.setenv("F110_FXR_LEAN", lean)  # padded k_rays_fxr: k_rays_fxs's lean pass (1) or round 3's (0)
     monkeypatch.setenv("F110_HEAVY_T", "0" if refill == "1" or pool != "0" else "16")
     tm = tracks("Spielberg_map")
     ox, oy, _ = tm.origin
