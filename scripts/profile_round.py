@@ -22,7 +22,7 @@ COLLECT = "--collect" in sys.argv
 PROF = os.path.join(REPO, "profiles") if COLLECT else os.path.join(OUT, "summary")
 ENVS = int(os.environ.get("PROFILE_ENVS", "65536"))  # the headline configuration (bench.py default)
 BENCH = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "300", "--warmup", "50", "--no-cpu-baseline",
-         "--no-secondary", "--global-envs", str(ENVS)]
+         "--no-secondary", "--no-full-outputs", "--global-envs", str(ENVS)]
 env = dict(os.environ, TMPDIR="/tmp")
 
 
@@ -133,5 +133,21 @@ try:
                     "SQ_WAVE_CYCLES*4 / (1024 * GRBM_GUI_ACTIVE/8); mean per k_rays dispatch, scripts/ray_pmc.py (minimal outputs)")
 except Exception as exc:
     busy["error"] = repr(exc)
+# 4. issue mix: instructions per wave by type and the scalar unit's load (one SALU per CU on
+#    MI300 / MI355X serves the CU's 32 resident waves: SQ_INST_CYCLES_SALU / SQ_ACTIVE_INST_SCA are
+#    quad-cycles summed per SE, so CU-cycles = x * 4 / 256 CUs)
+grp = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_RD", "SQ_INSTS_BRANCH",
+       "SQ_INST_CYCLES_SALU", "SQ_ACTIVE_INST_SCA", "GRBM_GUI_ACTIVE"]
+try:
+    dd = run("pmc_issue", ["--pmc"] + grp, target=RAYPMC)
+    iss = counters(dd, os.path.join(PROF, f"{tag}_pmc_issue.csv"))
+    busy.update(iss)
+    cyc = iss["GRBM_GUI_ACTIVE"] / 8.0
+    busy["salu_busy"] = iss["SQ_INST_CYCLES_SALU"] * 4.0 / (256 * cyc)
+    busy["scalar_busy"] = iss["SQ_ACTIVE_INST_SCA"] * 4.0 / (256 * cyc)
+    for k in ("VALU", "SALU", "SMEM", "VMEM_RD", "BRANCH"):
+        busy[f"insts_{k.lower()}_per_wave"] = iss[f"SQ_INSTS_{k}"] / max(1.0, iss["SQ_WAVES"])
+except Exception as exc:
+    busy["issue_error"] = repr(exc)
 json.dump(busy, open(os.path.join(PROF, f"pmc_busy_E{ENVS}_A1.json"), "w"), indent=1)
 print(json.dumps(busy))
