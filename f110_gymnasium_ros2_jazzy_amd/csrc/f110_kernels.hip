@@ -1407,8 +1407,8 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
     return act ? fast : zero_v;
 }
 
-template <bool HANDOFF>
-__global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
+template <bool HANDOFF, int NS>
+__global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  // <= 64 / 72 VGPRs
     const int wj = (int)blockIdx.x / a.EA;
     const int g = (int)blockIdx.x - wj * a.EA;
     const int lane = (int)threadIdx.x;
@@ -1426,8 +1426,8 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
     uint32_t zero_v;  // the zero cell's offset in a VGPR (the select's other operand is its SGPR mask)
     asm volatile("v_mov_b32 %0, %1" : "=v"(zero_v) : "s"(a.fx_zero));
 
-    double x[2], y[2], d[2], tot[2], c[2], sn[2];
-    int kk[2];
+    double x[NS], y[NS], d[NS], tot[NS], c[NS], sn[NS];
+    int kk[NS];
     int next = nch - 1 - wj;
     int vlo = 0;  // lane k < nch: the run holding beam 64 k (as k_rays_fxr)
     if (lane < nch) {
@@ -1457,7 +1457,8 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
         tot[r] = in_loop ? 0.0 : d[r];  // :130
     };
     uint32_t lanes = 0;
-    float cval[2] = {0.0f, 0.0f};  // k_rays_fxr's two-entry cache of the unused half of a pair draw
+    float cval[2] = {0.0f, 0.0f};  // k_rays_fxr's two-entry cache of the unused half of a pair draw (tagged:
+    // with three slots a third open pair may evict an entry; its partner then draws again)
     int ctag[2] = {-1, -1};
     auto finish = [&](int r) {
         const RayArgs &K = kernarg_here();
@@ -1511,57 +1512,74 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
     const bool fast_car = (ux >= a.fxp_lo) & (ux < a.fxp_hx) & (uy >= a.fxp_lo) & (uy < a.fxp_hy);
     if (fast_car) {
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
+        for (int r = 0; r < NS; ++r) {
             kk[r] = -1;
             d[r] = tot[r] = x[r] = y[r] = c[r] = sn[r] = 0.0;
         }
 #pragma unroll
-        for (int r = 0; r < 2; ++r)
+        for (int r = 0; r < NS; ++r)
             if (next >= 0) arm(r, false);
         __builtin_amdgcn_s_waitcnt(0);
         // The loop's scalar control is kept to what a trip needs (the CU's one scalar unit
-        // serves its 32 resident waves: k_rays_fxr spent ~30 SALU per trip against 36 VALU):
-        // the slots' active-lane counts drive both branches and the lookup count, and the
-        // refill / exit tests run only when a slot has no active lane.
+        // serves its resident waves: k_rays_fxr spent ~30 SALU per trip against 36 VALU):
+        // the slots' active-lane counts drive the lookup count, and the refill / exit tests
+        // run only when a slot has no active lane.
         uint32_t trips = 0, idle = 0;
         for (;;) {
-            uint64_t m[2];
-            uint32_t cnt[2], off[2];
-            bool near[2];
-            // both slots step unconditionally (a slot without active lanes reads the zero cell:
-            // ~15 VALU wasted in the car's last chunk instead of a branch per slot per trip)
+            uint64_t m[NS];
+            uint32_t cnt[NS], off[NS];
+            bool near[NS];  // the lane's cell is within the guard band of an edge
+            // every slot steps unconditionally (a slot without active lanes reads the zero cell:
+            // ~15 VALU wasted in the car's last chunks instead of a branch per slot per trip)
 #pragma unroll
-            for (int r = 0; r < 2; ++r) {
+            for (int r = 0; r < NS; ++r) {
                 const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
                 m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
                 cnt[r] = (uint32_t)__popcll(m[r]);
                 off[r] = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act, zero_v, near[r]);
             }
-            const uint64_t nb0 = __builtin_amdgcn_ballot_w64(near[0]) & m[0];
-            const uint64_t nb1 = __builtin_amdgcn_ballot_w64(near[1]) & m[1];
-            if (nb0 | nb1) {  // rare: lanes within the guard band take tiled_cell's IEEE path
-                const RayArgs &K = kernarg_here();
-                if (lane_in(nb0)) off[0] = exact_offset_pad(K.m, x[0], y[0], (uint32_t)K.fxp_P);
-                if (lane_in(nb1)) off[1] = exact_offset_pad(K.m, x[1], y[1], (uint32_t)K.fxp_P);
+            // the gathers go out on the fixed-point cells at once (the guard-band test is off the
+            // dependent chain d -> x, y -> cell -> d); the rare lanes within the band of a cell edge
+            // then re-gather from tiled_cell's IEEE cell (loads return in order: the second wins)
+#pragma unroll
+            for (int r = 0; r < NS; ++r) d[r] = ld_off(dt, off[r]);
+            uint64_t nb[NS], nball = 0;
+#pragma unroll
+            for (int r = 0; r < NS; ++r) {
+                nb[r] = __builtin_amdgcn_ballot_w64(near[r]) & m[r];
+                nball |= nb[r];
             }
+            if (nball) {  // rare (wave-uniform)
+                const RayArgs &K = kernarg_here();
 #pragma unroll
-            for (int r = 0; r < 2; ++r) d[r] = ld_off(dt, off[r]);
-            lane_iters += cnt[0] + cnt[1];
+                for (int r = 0; r < NS; ++r)
+                    if (lane_in(nb[r])) d[r] = ld_off(dt, exact_offset_pad(K.m, x[r], y[r], (uint32_t)K.fxp_P));
+            }
+            uint32_t cmin = cnt[0], csum = cnt[0];
+#pragma unroll
+            for (int r = 1; r < NS; ++r) {
+                cmin = min(cmin, cnt[r]);
+                csum += cnt[r];
+            }
+            lane_iters += csum;
             ++trips;
-            if (min(cnt[0], cnt[1]) == 0u) {  // rare: a slot's chunk has ended, or the slot is closed
-                const bool none = cnt[0] + cnt[1] == 0u;
+            if (cmin == 0u) {  // rare: a slot's chunk has ended, or the slot is closed
+                const bool none = csum == 0u;
                 idle += none ? 1u : 0u;
+                bool open = false;
 #pragma unroll
-                for (int r = 0; r < 2; ++r)
+                for (int r = 0; r < NS; ++r) {
                     if (kk[r] >= 0 && cnt[r] == 0u) {  // wave-uniform: the chunk has ended; refill the slot
                         finish(r);
                         if (next >= 0) arm(r, true);
                         else kk[r] = -1;
                     }
-                if (none && kk[0] < 0 && kk[1] < 0) break;
+                    open |= kk[r] >= 0;
+                }
+                if (none && !open) break;
             }
 #pragma unroll
-            for (int r = 0; r < 2; ++r) tot[r] += d[r];  // :141 (a re-armed slot completes tot = d00, as k_rays_fxr)
+            for (int r = 0; r < NS; ++r) tot[r] += d[r];  // :141 (a re-armed slot completes tot = d00, as k_rays_fxr)
         }
         iters = trips - idle;  // trips with an active lane (k_rays_fxr's count)
     } else {  // an origin off the map: the IEEE cell of every lookup, chunk after chunk
@@ -1586,7 +1604,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
         unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
         atomicAdd(cs, (unsigned long long)(lanes + lane_iters));  // the first lookup came from k_agents
         atomicAdd(cs + 1, (unsigned long long)lanes);
-        if (K.count_slots) atomicAdd(cs + 2, (unsigned long long)iters * (fast_car ? 128ull : 64ull));
+        if (K.count_slots) atomicAdd(cs + 2, (unsigned long long)iters * (fast_car ? 64ull * NS : 64ull));
     }
 }
 
@@ -3112,9 +3130,13 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                                              reinterpret_cast<const void *>(&k_rays_fxr<false, true, 3>),
                                              reinterpret_cast<const void *>(&k_rays_fxr<true, true, 3>)};
                         f = fr[(a.fx_slots == 3 ? 4 : 0) + (pad ? 2 : 0) + (single ? 0 : 1)];
-                        if (pad && a.fx_slots != 3 && a.fxr_lean)  // the lean refill pass (same outputs)
-                            f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false>)
-                                       : reinterpret_cast<const void *>(&k_rays_fxs<true>);
+                        if (pad && a.fxr_lean) {  // the lean refill pass (same outputs), 2 or 3 slots
+                            const void *fs[4] = {reinterpret_cast<const void *>(&k_rays_fxs<false, 2>),
+                                                 reinterpret_cast<const void *>(&k_rays_fxs<true, 2>),
+                                                 reinterpret_cast<const void *>(&k_rays_fxs<false, 3>),
+                                                 reinterpret_cast<const void *>(&k_rays_fxs<true, 3>)};
+                            f = fs[(a.fx_slots == 3 ? 2 : 0) + (single ? 0 : 1)];
+                        }
                         ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
                         g2 = dim3((unsigned)(ra.EA * ra.G4));
                     }
