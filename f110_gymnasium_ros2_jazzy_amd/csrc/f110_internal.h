@@ -65,7 +65,6 @@ struct StepArgs {
     int32_t fx_pad;     // F110_FX_PAD: k_rays_fxn on the padded table
     int32_t fx_slots;   // F110_FX_SLOTS (A/B): chunk slots per k_rays_fxr wave, 2 or 3
     int32_t fxr_lean;   // k_rays_fxs for k_rays_fxr's padded two-slot kernel (F110_FXR_LEAN=0: off, A/B)
-    int32_t fxs_pf;     // k_rays_fxs's long-ray prefetch threshold in trips (F110_FXS_PF, 0: off)
     int32_t fx_refill;  // F110_FX_REFILL: waves per car of k_rays_fxr (two chunk slots with refill; 0 = off)
     int32_t fx_pool;    // F110_FX_POOL: cars per k_rays_fxp wave (lane-level refill; 0 = off)
     int32_t pool_T;     // F110_FX_POOL_T: k_rays_fxp refills once this many slots have ended
@@ -174,7 +173,6 @@ struct RayArgs {
     double fxp_lo, fxp_hx, fxp_hy;
     int32_t fxp_P;
     double fxs_cx, fxs_cy;  // k_rays_fxs: 2^20 + P + 2^-26 - origin / res (see kFxsBase)
-    int32_t fxs_pf;         // k_rays_fxs: prefetch along the wave's rays after this many trips (0: off)
     int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_read_simt; F110_SIMT)
     // straggler hand-off of k_rays_fx (EVICT) -> k_rays_fx_tail: SoA records
     // ev[7][ev_cap] = x, y, d, tot, cos, sin, noise; ev_gb[2][ev_cap] = car, beam.

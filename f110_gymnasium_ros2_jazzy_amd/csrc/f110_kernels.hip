@@ -1407,7 +1407,7 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
     return act ? fast : zero_v;
 }
 
-template <bool HANDOFF, int NS, bool PF = false>
+template <bool HANDOFF, int NS>
 __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  // <= 64 / 72 VGPRs
     const int wj = (int)blockIdx.x / a.EA;
     const int g = (int)blockIdx.x - wj * a.EA;
@@ -1525,9 +1525,6 @@ __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  
         // the slots' active-lane counts drive the lookup count, and the refill / exit tests
         // run only when a slot has no active lane.
         uint32_t trips = 0, idle = 0;
-        uint32_t offp[NS], pfv[NS];  // PF: the previous trip's gather offsets, the touches' sink
-#pragma unroll
-        for (int r = 0; r < NS; ++r) offp[r] = pfv[r] = zero_v;
         for (;;) {
             uint64_t m[NS];
             uint32_t cnt[NS], off[NS];
@@ -1558,25 +1555,6 @@ __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  
                 for (int r = 0; r < NS; ++r)
                     if (lane_in(nb[r])) d[r] = ld_off(dt, exact_offset_pad(K.m, x[r], y[r], (uint32_t)K.fxp_P));
             }
-            if (PF) {
-                // long rays (a launch's tail: grazing beams that take hundreds of ~1-cell steps, each
-                // a new line that misses L2): once the wave has run fxs_pf trips, touch the cell 3
-                // steps ahead at this step's stride in the table.  The touch is a plain load into a
-                // loop-carried register that is only read after the loop (so no trip waits for it: the
-                // next touch overwrites it in order); it is issued every trip as the last load (on the
-                // gathers' own cells before fxs_pf trips), so that the compiler's vmcnt waits for the
-                // real gathers stay exact and in-order completion never delays one.  A predicted offset is clamped
-                // into the table (the position may leave the map); the value is never read.
-                const bool tail = trips >= (uint32_t)a.fxs_pf;
-#pragma unroll
-                for (int r = 0; r < NS; ++r) {
-                    uint32_t po = off[r];
-                    // 3 steps ahead at this step's cell stride (4 off - 3 prev, mod 2^32), clamped
-                    if (tail) po = min(4u * off[r] - 3u * offp[r], zero_v);  // wave-uniform branch
-                    offp[r] = off[r];
-                    pfv[r] = ld_off(reinterpret_cast<const uint32_t *>(dt), po);
-                }
-            }
             uint32_t cmin = cnt[0], csum = cnt[0];
 #pragma unroll
             for (int r = 1; r < NS; ++r) {
@@ -1604,12 +1582,6 @@ __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  
             for (int r = 0; r < NS; ++r) tot[r] += d[r];  // :141 (a re-armed slot completes tot = d00, as k_rays_fxr)
         }
         iters = trips - idle;  // trips with an active lane (k_rays_fxr's count)
-        if (PF) {  // the touches' values are read once, here (a table cell never holds this bit pattern)
-            uint32_t acc = 0;
-#pragma unroll
-            for (int r = 0; r < NS; ++r) acc |= pfv[r];
-            if (acc == 0xFFFFFFFFu) lane_iters += 0x80000000u;
-        }
     } else {  // an origin off the map: the IEEE cell of every lookup, chunk after chunk
         uint32_t cnt = 0;
         while (next >= 0) {
@@ -3158,16 +3130,12 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                                              reinterpret_cast<const void *>(&k_rays_fxr<false, true, 3>),
                                              reinterpret_cast<const void *>(&k_rays_fxr<true, true, 3>)};
                         f = fr[(a.fx_slots == 3 ? 4 : 0) + (pad ? 2 : 0) + (single ? 0 : 1)];
-                        ra.fxs_pf = a.fxs_pf;
                         if (pad && a.fxr_lean) {  // the lean refill pass (same outputs), 2 or 3 slots
                             const void *fs[4] = {reinterpret_cast<const void *>(&k_rays_fxs<false, 2>),
                                                  reinterpret_cast<const void *>(&k_rays_fxs<true, 2>),
                                                  reinterpret_cast<const void *>(&k_rays_fxs<false, 3>),
                                                  reinterpret_cast<const void *>(&k_rays_fxs<true, 3>)};
                             f = fs[(a.fx_slots == 3 ? 2 : 0) + (single ? 0 : 1)];
-                            if (a.fxs_pf > 0 && a.fx_slots != 3)  // long-ray prefetch (F110_FXS_PF, A/B)
-                                f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true>)
-                                           : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true>);
                         }
                         ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
                         g2 = dim3((unsigned)(ra.EA * ra.G4));
