@@ -1859,6 +1859,246 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxp(RayArgs a) {  // 8 waves per
     }
 }
 
+// k_rays_fxq (F110_FX_LPOOL): k_rays_fxp's lane-level refill for one car per
+// wave, with k_rays_fxs's loop and a refill pass cut to the rays' own work.
+// k_rays_fxp lost because a refill pass cost what a chunk pass costs (~170
+// VALU, Philox draw included) and it ran ~25 times per car.  Here the car's
+// scan noise is drawn once at the start into LDS (the same pair draws as
+// k_rays_fxr / k_rays_fxs: beams b and b + 64 of a 128-beam block share one
+// Philox2x32 draw), beside its theta-index table, so a pass is: an LDS read of
+// the noise, the clamp, the TTC test, the obs entry (k_rays_fxs's Markstein
+// division), and for the re-armed lanes an LDS read of the theta index and
+// the two table gathers.  LDS: B * 6 bytes + 256 per wave (6 waves per SIMD at
+// 1080 beams).  Lanes take the queue's next beam (lanes_below) once >= pool_T
+// of the 128 slots have ended, or when none is still tracing; the queue is
+// the car's 64-beam chunks in descending order of the previous launch's cost
+// (pcost).  Per-ray arithmetic is k_rays_fxs's, so bit-identical.
+template <bool HANDOFF>
+__global__ void __launch_bounds__(64, 6) k_rays_fxq(RayArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char fxq_smem[];
+    const int lane = (int)threadIdx.x;
+    const int g = (int)blockIdx.x;  // one car per wave
+    const int B = a.B;
+    const int nch = (B + 63) >> 6;
+    const int e = HANDOFF ? g / a.A : g;
+    float *s_nz = reinterpret_cast<float *>(fxq_smem);                                        // [B]
+    uint32_t *s_cost = reinterpret_cast<uint32_t *>(fxq_smem + (size_t)((B + 63) & ~63) * 4);  // [64]
+    uint16_t *s_ti = reinterpret_cast<uint16_t *>(fxq_smem + (size_t)((B + 63) & ~63) * 4 + 256);  // [B]
+    const double *dt = a.m.dt;
+    const FxLoop L = fx_loop<3>(a);
+    double x00, y00, d00;
+    asm volatile("v_mov_b64 %0, %1" : "=v"(x00) : "s"(ld_const(a.ray0 + g)));
+    asm volatile("v_mov_b64 %0, %1" : "=v"(y00) : "s"(ld_const(a.ray0 + a.EA + g)));
+    asm volatile("v_mov_b64 %0, %1" : "=v"(d00) : "s"(ld_const(a.ray0 + 2 * a.EA + g)));  // :129
+    uint32_t zero_v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(zero_v) : "s"(a.fx_zero));
+
+    // ---- the car's theta indices and scan noise into LDS ----
+    {
+        const BeamRun *R = a.runs + (size_t)g * kMaxSeg;
+        const int n = ld_const(a.nruns + g);
+        int vlo = 0;  // lane k < nch: the run holding beam 64 k
+        if (lane < nch) {
+            int lo = 0, hi = n - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (R[mid].start <= lane * 64) lo = mid;
+                else hi = mid - 1;
+            }
+            vlo = lo;
+        }
+        for (int k = 0; k < nch; ++k) {
+            const int b = k * 64 + lane, bc = b < B ? b : B - 1;
+            int ti = (int)beam_theta(R, n, __builtin_amdgcn_readlane(vlo, k), k * 64, bc);  // int(theta_index), :124
+            if (ti >= a.theta_dis) ti = 0;
+            if (b < B) s_ti[b] = (uint16_t)ti;
+        }
+        const RayArgs &K = kernarg_here();
+        if (!K.noise_ext && K.noise_std > 0.0) {  // k_rays_fxs's draws: pair p serves beams b and b + 64
+            const uint32_t key = noise_key(K.seed, (uint64_t)(K.env_offset + e));
+            const uint64_t step = ld_const(K.noise_step + e);
+            for (int k = 0; k < nch; k += 2) {
+                const int b = k * 64 + lane;
+                float lo, hi;
+                beam_normal_pair_k(key, step, beam_noise_pair(b), lo, hi);
+                if (b < B) s_nz[b] = lo;
+                if (b + 64 < B) s_nz[b + 64] = hi;
+            }
+        }
+        if (lane < nch) s_cost[lane] = 0u;
+    }
+    // the queue: the car's chunks by the previous launch's cost (ties: descending chunk index)
+    uint32_t ukey = lane < nch ? (((a.pcost ? (uint32_t)a.pcost[(size_t)g * nch + lane] : 0u) << 8) | (uint32_t)lane) : 0u;
+    uint32_t rank = lane < nch ? 0u : (uint32_t)lane;
+    for (int j = 0; j < nch; ++j) rank += (uint32_t)(__builtin_amdgcn_readlane(ukey, j) > ukey) & (lane < nch ? 1u : 0u);
+    const uint32_t sorted = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank << 2), lane);  // lane r: chunk of rank r
+    __syncthreads();  // the LDS tables (one wave)
+
+    uint32_t rays = 0, lane_iters = 0, iters = 0, passes = 0, refills = 0;
+    const double ux = fma(ld_const(a.ray0 + g), L.ir, L.cxk) - kFxpBase;
+    const double uy = fma(ld_const(a.ray0 + a.EA + g), L.ir, L.cyk) - kFxpBase;
+    const bool fast_car = (ux >= a.fxp_lo) & (ux < a.fxp_hx) & (uy >= a.fxp_lo) & (uy < a.fxp_hy);
+    const uint32_t NQ = (uint32_t)nch * 64u;
+    if (fast_car) {
+        double x[2], y[2], d[2], tot[2], c[2], sn[2];
+        uint32_t code[2] = {0u, 0u};  // (trip armed << 12) | beam
+        uint64_t occ[2] = {0ull, 0ull};
+        uint32_t nxt = 0;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) x[r] = y[r] = d[r] = tot[r] = c[r] = sn[r] = 0.0;
+        auto arm = [&](int r, uint64_t m) {  // slot r of the lanes in m takes the queue's next beams
+            const uint32_t p = nxt + lanes_below(m);
+            const uint32_t ck = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(p >> 6, 63u) << 2), (int)sorted);
+            const int b = (int)((ck << 6) | (p & 63u));
+            const bool mine = lane_in(m) && p < NQ;
+            if (mine) {
+                const RayArgs &Ka = kernarg_here();
+                const uint32_t toff = (uint32_t)s_ti[b < B ? b : B - 1] * 8u;
+                c[r] = ld_off(Ka.cosines, toff);
+                sn[r] = ld_off(Ka.sines, toff);
+                x[r] = x00;
+                y[r] = y00;
+                d[r] = b < B ? d00 : 0.0;  // past the last beam: a ray that has ended
+                tot[r] = d[r];  // :130
+                code[r] = (iters << 12) | (uint32_t)b;
+            }
+            occ[r] |= __builtin_amdgcn_ballot_w64(mine);
+            nxt = min(nxt + (uint32_t)__popcll(m), NQ);
+        };
+        auto finish = [&](int r, uint64_t m) {  // the ended rays of slot r in m: fx_epilogue
+            const int b = (int)(code[r] & 4095u);
+            const bool real = lane_in(m) && b < B;
+            if (real) {
+                const RayArgs &K = kernarg_here();
+                const double mr = K.max_range;
+                double range = tot[r] > mr ? mr : tot[r];  // :143-144
+                if (K.noise_ext) range += K.noise_ext[(size_t)e * B + b];
+                else if (K.noise_std > 0.0) range += K.noise_std * (double)s_nz[b];
+                const double v = ld_const(K.vel + g);
+                const uint32_t boff = (uint32_t)b * 8u;
+                if (v != 0.0 && ttc_fires(range, ld_off(K.side, boff), v * ld_off(K.beam_cos, boff), K.ttc_thresh))
+                    K.ttc_hit[g] = 1;
+                if (K.obs && (!HANDOFF || g == e * K.A)) {
+                    float *orow = K.obs + (size_t)e * K.obs_len;
+                    *reinterpret_cast<float *>(reinterpret_cast<char *>(orow) + (uint32_t)b * 4u) =
+                        obs_scan_value_fast(range, K.lidar_max, K.obs_rinv);
+                }
+                const size_t row = (size_t)g * B;
+                if (K.scans_f32) *reinterpret_cast<float *>(reinterpret_cast<char *>(K.scans_f32 + row) + (uint32_t)b * 4u) = (float)range;
+                if (K.scans_f64) *reinterpret_cast<double *>(reinterpret_cast<char *>(K.scans_f64 + row) + (uint32_t)b * 8u) = range;
+                if (HANDOFF) *reinterpret_cast<double *>(reinterpret_cast<char *>(K.scan + row) + (uint32_t)b * 8u) = range;
+                atomicMax(s_cost + (b >> 6), iters - (code[r] >> 12) + 1u);
+            }
+            rays += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(real));
+            occ[r] &= ~m;
+        };
+        arm(0, ~0ull);
+        arm(1, ~0ull);
+        __builtin_amdgcn_s_waitcnt(0);
+        const uint32_t T = (uint32_t)a.pool_T;
+        for (;;) {
+            uint64_t m[2];
+            uint32_t cnt[2], off[2];
+            bool near[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+                cnt[r] = (uint32_t)__popcll(m[r]);
+            }
+            const uint64_t e0 = occ[0] & ~m[0], e1 = occ[1] & ~m[1];
+            const uint32_t ne = (uint32_t)(__popcll(e0) + __popcll(e1));
+            uint32_t tracing = cnt[0] + cnt[1];
+            if (!tracing && !ne) break;  // nothing in flight and nothing to finish (every wave gets here)
+            if (ne >= T || !tracing) {  // wave-uniform: finish the ended rays, refill their slots
+                if (!tracing && nxt >= NQ) {  // the last rays: outputs, then done
+                    if (e0) finish(0, e0);
+                    if (e1) finish(1, e1);
+                    break;
+                }
+                ++passes;
+                refills += (e0 ? 1u : 0u) + (e1 ? 1u : 0u);
+                if (e0) {
+                    finish(0, e0);
+                    if (nxt < NQ) arm(0, e0);
+                }
+                if (e1) {
+                    finish(1, e1);
+                    if (nxt < NQ) arm(1, e1);
+                }
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+                    cnt[r] = (uint32_t)__popcll(m[r]);
+                }
+                tracing = cnt[0] + cnt[1];
+                if (!tracing) continue;  // (every re-armed ray starts inside a wall: d00 == 0)
+            }
+            ++iters;
+            lane_iters += tracing;
+            // trace_ray's step (laser_models.py:135-141) for every slot (ended / empty lanes read the
+            // zero cell: d = 0 keeps their total), gathers before the guard-band test (k_rays_fxs)
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+                off[r] = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act, zero_v, near[r]);
+            }
+#pragma unroll
+            for (int r = 0; r < 2; ++r) d[r] = ld_off(dt, off[r]);
+            const uint64_t nb0 = __builtin_amdgcn_ballot_w64(near[0]) & m[0];
+            const uint64_t nb1 = __builtin_amdgcn_ballot_w64(near[1]) & m[1];
+            if (nb0 | nb1) {  // rare (wave-uniform)
+                const RayArgs &K = kernarg_here();
+                if (lane_in(nb0)) d[0] = ld_off(dt, exact_offset_pad(K.m, x[0], y[0], (uint32_t)K.fxp_P));
+                if (lane_in(nb1)) d[1] = ld_off(dt, exact_offset_pad(K.m, x[1], y[1], (uint32_t)K.fxp_P));
+            }
+#pragma unroll
+            for (int r = 0; r < 2; ++r) tot[r] += d[r];  // :141
+        }
+        __syncthreads();
+        if (a.pcost && lane < nch) {  // this launch's per-chunk cost: the next launch's order
+            const uint32_t cst = s_cost[lane];
+            a.pcost[(size_t)g * nch + lane] = (uint8_t)(cst < 255u ? cst : 255u);
+        }
+    } else {  // an origin off the map: the IEEE cell of every lookup, one ray per lane, chunk by chunk
+        uint32_t cnt = 0;
+        const RayArgs &K = kernarg_here();
+        for (int k = 0; k < nch; ++k) {
+            const int b = k * 64 + lane;
+            if (b < B) {
+                const uint32_t toff = (uint32_t)s_ti[b] * 8u;
+                const double cc = ld_off(K.cosines, toff), ss = ld_off(K.sines, toff);
+                double x = x00, y = y00, d = d00;
+                double tot = d;  // :130
+                while ((dhi(d) != 0u) & (tot <= L.mr)) {
+                    x += d * cc;  // :135
+                    y += d * ss;  // :136
+                    d = fx_load<3>(dt, exact_offset_pad(K.m, x, y, (uint32_t)K.fxp_P));
+                    tot += d;  // :141
+                    ++cnt;
+                }
+                double nz = 0.0;
+                if (K.noise_ext) nz = K.noise_ext[(size_t)e * B + b];
+                else if (K.noise_std > 0.0) nz = K.noise_std * (double)s_nz[b];
+                fx_epilogue<HANDOFF>(K, g, e, b, tot, L.mr, nz, ld_const(K.vel + g), K.beam_cos[b], K.side[b]);
+            }
+            rays += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(b < B));
+        }
+        lane_iters = wave_sum(cnt);
+        iters = wave_max(cnt);
+    }
+    if (lane == 0) {
+        const RayArgs &K = kernarg_here();
+        unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+        atomicAdd(cs, (unsigned long long)(rays + lane_iters));  // the first lookup came from k_agents
+        atomicAdd(cs + 1, (unsigned long long)rays);
+        if (K.count_slots) {
+            atomicAdd(cs + 2, (unsigned long long)iters * (fast_car ? 128ull : 64ull));
+            atomicAdd(cs + 3, (unsigned long long)passes);
+            atomicAdd(cs + 4, (unsigned long long)refills);
+        }
+    }
+}
+
 // k_rays_fx_tail: the handed-off rays, traced to the end with lane refill.
 // Persistent waves take records from the queue (one atomic per refill);
 // whenever >= kTailRefill lanes are idle, the finished lanes write their
@@ -3136,6 +3376,14 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                                                  reinterpret_cast<const void *>(&k_rays_fxs<false, 3>),
                                                  reinterpret_cast<const void *>(&k_rays_fxs<true, 3>)};
                             f = fs[(a.fx_slots == 3 ? 2 : 0) + (single ? 0 : 1)];
+                            if (a.fx_lpool && a.pcost && a.fx_slots != 3 && a.fx_refill == 1 && (a.B + 63) / 64 <= 64) {
+                                // k_rays_fxq: lane-level refill over the car's beams (F110_FX_LPOOL)
+                                f = single ? reinterpret_cast<const void *>(&k_rays_fxq<false>)
+                                           : reinterpret_cast<const void *>(&k_rays_fxq<true>);
+                                ra.pcost = a.pcost;
+                                ra.pool_T = a.pool_T;
+                                lds_bytes = (unsigned)(((a.B + 63) & ~63) * 4 + 256 + ((a.B * 2 + 15) & ~15));
+                            }
                         }
                         ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
                         g2 = dim3((unsigned)(ra.EA * ra.G4));

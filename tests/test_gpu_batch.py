@@ -343,12 +343,16 @@ def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
     monkeypatch.setenv("F110_FX_ILP", "2")
     monkeypatch.setenv("F110_HEAVY_T", "0")  # k_rays_fxr has no heavy-first dispatch
     outs, ctrs = [], []
-    # off; 1 or 3 waves per car; padded EDT with k_rays_fxr's round-3 pass (lean 0) and k_rays_fxs (lean 1)
-    for refill, pad, lean in (("0", "0", "1"), ("1", "0", "1"), ("3", "0", "1"), ("1", "1", "0"), ("1", "1", "1"),
-                              ("3", "1", "1")):
+    # off; 1 or 3 waves per car; padded EDT with k_rays_fxr's round-3 pass (lean 0), k_rays_fxs (lean 1) and
+    # k_rays_fxq (lane-level refill over the car's beams, refill thresholds 1 / 80 / 128)
+    for refill, pad, lean, lpool in (("0", "0", "1", "0:80"), ("1", "0", "1", "0:80"), ("3", "0", "1", "0:80"),
+                                     ("1", "1", "0", "0:80"), ("1", "1", "1", "0:80"), ("3", "1", "1", "0:80"),
+                                     ("1", "1", "1", "1:80"), ("1", "1", "1", "1:1"), ("1", "1", "1", "1:128")):
         monkeypatch.setenv("F110_FX_REFILL", refill)
         monkeypatch.setenv("F110_FX_PAD", pad)
         monkeypatch.setenv("F110_FXR_LEAN", lean)
+        monkeypatch.setenv("F110_FX_LPOOL", lpool.split(":")[0])
+        monkeypatch.setenv("F110_FX_POOL_T", lpool.split(":")[1])
         sim = _sim(tracks, gpu, n_envs=E, n_agents=A, num_beams=beams, noise_std=0.01, autoreset=True,
                    spawn_poses=sp, seed=6, keep_f64_scans=True)
         assert sim.ray_refill == min(int(refill), (beams + 63) // 64)
