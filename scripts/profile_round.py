@@ -134,8 +134,7 @@ try:
 except Exception as exc:
     busy["error"] = repr(exc)
 # 4. issue mix: instructions per wave by type and the scalar unit's load (one SALU per CU on
-#    MI300 / MI355X serves the CU's 32 resident waves: SQ_INST_CYCLES_SALU / SQ_ACTIVE_INST_SCA are
-#    quad-cycles summed per SE, so CU-cycles = x * 4 / 256 CUs)
+#    MI300 / MI355X serves the CU's 32 resident waves)
 grp = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_RD", "SQ_INSTS_BRANCH",
        "SQ_INST_CYCLES_SALU", "SQ_ACTIVE_INST_SCA", "GRBM_GUI_ACTIVE"]
 try:
@@ -143,8 +142,10 @@ try:
     iss = counters(dd, os.path.join(PROF, f"{tag}_pmc_issue.csv"))
     busy.update(iss)
     cyc = iss["GRBM_GUI_ACTIVE"] / 8.0
-    busy["salu_busy"] = iss["SQ_INST_CYCLES_SALU"] * 4.0 / (256 * cyc)
-    busy["scalar_busy"] = iss["SQ_ACTIVE_INST_SCA"] * 4.0 / (256 * cyc)
+    # SALU instructions issued per CU per kernel cycle (one scalar ALU per CU: 1.0 = every cycle);
+    # SQ_INST_CYCLES_SALU equals SQ_INSTS_SALU here, so its unit cannot be quad-cycles of one unit
+    busy["salu_insts_per_cu_cycle"] = iss["SQ_INSTS_SALU"] / (256 * cyc)
+    busy["valu_insts_per_simd_cycle"] = iss["SQ_INSTS_VALU"] / (1024 * cyc)
     for k in ("VALU", "SALU", "SMEM", "VMEM_RD", "BRANCH"):
         busy[f"insts_{k.lower()}_per_wave"] = iss[f"SQ_INSTS_{k}"] / max(1.0, iss["SQ_WAVES"])
 except Exception as exc:
