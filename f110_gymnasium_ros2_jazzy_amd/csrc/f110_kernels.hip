@@ -1407,7 +1407,7 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
     return act ? fast : zero_v;
 }
 
-template <bool HANDOFF, int NS>
+template <bool HANDOFF, int NS, bool PIPE = false>
 __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  // <= 64 / 72 VGPRs
     const int wj = (int)blockIdx.x / a.EA;
     const int g = (int)blockIdx.x - wj * a.EA;
@@ -1510,7 +1510,59 @@ __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  
     const double uy = fma(ld_const(a.ray0 + a.EA + g), L.ir, L.cyk) - kFxpBase;
     // q + P of the scan origin inside [fxp_lo, fxp_h*): its rays stay in the padded table (false for NaN)
     const bool fast_car = (ux >= a.fxp_lo) & (ux < a.fxp_hx) & (uy >= a.fxp_lo) & (uy < a.fxp_hy);
-    if (fast_car) {
+    if (fast_car && PIPE) {
+        // Software-pipelined slots: each slot's gather is waited for right before that slot's
+        // next step, so one slot's gather is in flight while the other slot's data is consumed
+        // (the compiler's waits are vmcnt(1): both slots gather every trip, a closed slot on
+        // the zero cell).  Per slot and trip: the total (:141), the activity test (:133), the
+        // refill when the slot's chunk has ended, the step (:135-136) and its gather.
+#pragma unroll
+        for (int r = 0; r < NS; ++r) {
+            kk[r] = -1;
+            d[r] = tot[r] = x[r] = y[r] = c[r] = sn[r] = 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < NS; ++r)
+            if (next >= 0) arm(r, true);  // tot = 0: the first trip's total completes tot = d00
+        __builtin_amdgcn_s_waitcnt(0);
+        for (;;) {
+#pragma unroll
+            for (int r = 0; r < NS; ++r) {
+                tot[r] += d[r];  // :141 (d00 for a freshly armed slot: tot = d00, :130)
+                bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+                uint64_t m = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+                if (!m && kk[r] >= 0) {  // wave-uniform, rare: the slot's chunk has ended; refill it
+                    finish(r);
+                    if (next >= 0) {
+                        arm(r, false);  // tot = d = d00
+                        act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+                        m = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+                    } else {
+                        kk[r] = -1;
+                    }
+                    // the refill's own loads (tables) land here, so that the common path's wait
+                    // before the step stays vmcnt(1) (the other slot's gather may be in flight)
+                    __builtin_amdgcn_s_waitcnt(0);
+                }
+                lane_iters += (uint32_t)__popcll(m);
+                iters += m ? 1u : 0u;  // slot-trips with an active lane
+                bool near;
+                const uint32_t off = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act,
+                                                   zero_v, near);
+                d[r] = ld_off(dt, off);
+                const uint64_t nb = __builtin_amdgcn_ballot_w64(near) & m;
+                if (nb) {  // rare: lanes within the guard band re-gather from the IEEE cell
+                    const RayArgs &K = kernarg_here();
+                    if (lane_in(nb)) d[r] = ld_off(dt, exact_offset_pad(K.m, x[r], y[r], (uint32_t)K.fxp_P));
+                }
+            }
+            bool open = false;
+#pragma unroll
+            for (int r = 0; r < NS; ++r) open |= kk[r] >= 0;
+            if (!open) break;
+        }
+        iters = (iters + NS - 1) / NS;  // ~trips (SIMT diagnostic only)
+    } else if (fast_car) {
 #pragma unroll
         for (int r = 0; r < NS; ++r) {
             kk[r] = -1;
@@ -3376,6 +3428,9 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                                                  reinterpret_cast<const void *>(&k_rays_fxs<false, 3>),
                                                  reinterpret_cast<const void *>(&k_rays_fxs<true, 3>)};
                             f = fs[(a.fx_slots == 3 ? 2 : 0) + (single ? 0 : 1)];
+                            if (a.fxs_pipe && a.fx_slots != 3)  // software-pipelined slots (F110_FXS_PIPE, A/B)
+                                f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true>)
+                                           : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true>);
                             if (a.fx_lpool && a.pcost && a.fx_slots != 3 && a.fx_refill == 1 && (a.B + 63) / 64 <= 64) {
                                 // k_rays_fxq: lane-level refill over the car's beams (F110_FX_LPOOL)
                                 f = single ? reinterpret_cast<const void *>(&k_rays_fxq<false>)
