@@ -109,7 +109,7 @@ struct f110_ctx {
     int32_t fx_slots = 2;    // F110_FX_SLOTS (A/B): chunk slots per k_rays_fxr wave
     int32_t fxr_lean = 1;    // k_rays_fxs in place of k_rays_fxr<.., PAD, 2> (F110_FXR_LEAN=0: the round-3 kernel)
     int32_t fx_lpool = 0;    // k_rays_fxq in place of k_rays_fxs (F110_FX_LPOOL)
-    int32_t fxs_pipe = 0;    // k_rays_fxs with software-pipelined slots (F110_FXS_PIPE)
+    int32_t fxs_pipe = 1;    // k_rays_fxs with software-pipelined slots (F110_FXS_PIPE=0: in lock-step, A/B)
     int32_t fx_refill = 0;   // waves per car of k_rays_fxr (0 = k_rays_fxn; F110_FX_REFILL overrides)
     int32_t fx_pool = 0;     // cars per k_rays_fxp wave (lane-level refill; 0 = off; F110_FX_POOL)
     int32_t pool_T = 80;     // k_rays_fxp's refill threshold in ended slots (F110_FX_POOL_T)

@@ -37,9 +37,10 @@ def run(p, steps=50):
         sim.step(zero, minimal_outputs=True)
     pk = sim.profile_end()
     lk, rays = sim.read_counters()
+    rk, rf = sim.ray_kernel, sim.ray_refill
     sim.close()
     return {"k_rays_ms": pk["k_rays_ms"], "k_agents_ms": pk["k_agents_ms"], "k_post_ms": pk["k_post_ms"],
-            "mean_lookups": lk / max(rays, 1), "ray_kernel": sim.ray_kernel if hasattr(sim, "ray_kernel") else None}
+            "mean_lookups": lk / max(rays, 1), "ray_kernel": rk, "ray_refill": rf}
 
 
 for n in (1, 64, 1024, 8192):
