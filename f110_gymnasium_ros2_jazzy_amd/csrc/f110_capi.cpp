@@ -105,10 +105,6 @@ struct f110_ctx {
     const double *rmp = nullptr;  // k_rays_fxn's padded table (shared, see MapTables)
     int32_t rmp_w = 0, rmp_P = 0;
     uint32_t rmp_zero = 0;
-    const double *rmt = nullptr;  // the padded table in 4x4 tiles (k_rays_fxs<TILE>)
-    int32_t rmt_k1 = 0;
-    uint32_t rmt_zero = 0;
-    int32_t fxs_tile = 0;         // F110_FXS_TILE: k_rays_fxs on the tiled padded table
     bool fx_pad = false;    // k_rays_fxn / k_rays_fxr on the padded table (default from 32768 cars; F110_FX_PAD)
     int32_t fx_slots = 2;    // F110_FX_SLOTS (A/B): chunk slots per k_rays_fxr wave
     int32_t fxr_lean = 1;    // k_rays_fxs in place of k_rays_fxr<.., PAD, 2> (F110_FXR_LEAN=0: the round-3 kernel)
@@ -411,9 +407,9 @@ struct MapTables {
     int32_t H = 0, W = 0;
     uint64_t res_bits = 0;
     std::vector<uint32_t> k;  // the EDT the tables were built from (exact match, not a hash)
-    double *dt = nullptr, *dt_tiled = nullptr, *rm = nullptr, *rmp = nullptr, *rmt = nullptr;
-    int32_t rm_w = 0, rmp_w = 0, rmp_P = 0, rmt_k1 = 0;
-    uint32_t rm_oob = 0, rm_zero = 0, rmp_zero = 0, rmt_zero = 0;
+    double *dt = nullptr, *dt_tiled = nullptr, *rm = nullptr, *rmp = nullptr;
+    int32_t rm_w = 0, rmp_w = 0, rmp_P = 0;
+    uint32_t rm_oob = 0, rm_zero = 0, rmp_zero = 0;
     int refs = 0;
     bool shared = true;
 };
@@ -426,7 +422,6 @@ static void free_map_tables(MapTables *t) {
     if (t->dt_tiled) (void)hipFree(t->dt_tiled);
     if (t->rm) (void)hipFree(t->rm);
     if (t->rmp) (void)hipFree(t->rmp);
-    if (t->rmt) (void)hipFree(t->rmt);
     delete t;
 }
 
@@ -470,34 +465,11 @@ static hipError_t build_padded_table(MapTables *t, int32_t pad, const std::vecto
     for (int r = 0; r < H; ++r)
         for (int q = 0; q < W; ++q) rmp[((size_t)r + P) * Wp + q + P] = d[(size_t)r * W + q];
     rmp[Wp * Hp] = 0.0;
-    hipError_t e = upload(&t->rmp, rmp);
+    const hipError_t e = upload(&t->rmp, rmp);
     if (e == hipSuccess) {
         t->rmp_w = (int32_t)Wp;
         t->rmp_P = (int32_t)P;
         t->rmp_zero = (uint32_t)(Wp * Hp * 8);
-    }
-    // the same padded cells in 4x4 tiles of one 128-B line (column-major inside a tile: cell
-    // (R, C) at byte (R >> 2) * k1 + C * 32 + (R & 3) * 8), for k_rays_fxs<TILE>: the 64 beams of
-    // a chunk fan out in 2-D, and a tile holds a 2-D neighbourhood where a row-major line holds 16
-    // cells of one row.  Tiles per tile-row = 127 mod 128, so the tile-row stride k1 is 128 bytes
-    // short of a multiple of 16384 (the kFxsBase exponent terms then vanish mod 2^32)
-    if (e == hipSuccess) {
-        const size_t wtile = ((W + 2 * P + 3) / 4 + 1 + 127) / 128 * 128 - 1, Hq = (Hp + 3) / 4 * 4;
-        const size_t cells = Hq * wtile * 4;  // doubles before the zero cell
-        if ((cells + 16) * 8 < (1ull << 32) && wtile * 128 < (1u << 24)) {
-            std::vector<double> rmt(cells + 16, d[N - 1]);
-            for (int r = 0; r < H; ++r)
-                for (int q = 0; q < W; ++q) {
-                    const size_t R = (size_t)r + P, C = (size_t)q + P;
-                    rmt[(R >> 2) * wtile * 16 + C * 4 + (R & 3)] = d[(size_t)r * W + q];
-                }
-            rmt[cells] = 0.0;
-            e = upload(&t->rmt, rmt);
-            if (e == hipSuccess) {
-                t->rmt_k1 = (int32_t)(wtile * 128);
-                t->rmt_zero = (uint32_t)(cells * 8);
-            }
-        }
     }
     return e;
 }
@@ -775,7 +747,6 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (const char *v = std::getenv("F110_FXR_LEAN")) c->fxr_lean = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FX_LPOOL")) c->fx_lpool = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FXS_PIPE")) c->fxs_pipe = std::atoi(v) != 0;
-    if (const char *v = std::getenv("F110_FXS_TILE")) c->fxs_tile = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FX_POOL")) c->fx_pool = std::max(0, std::min(2, std::atoi(v)));
     if (const char *v = std::getenv("F110_FUSED")) c->fused = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FUSED_CPW")) c->fused_cpw = std::max(1, std::min(8, std::atoi(v)));
@@ -805,9 +776,6 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
                 c->rmp_w = c->maps->rmp_w;
                 c->rmp_P = c->maps->rmp_P;
                 c->rmp_zero = c->maps->rmp_zero;
-                c->rmt = c->maps->rmt;
-                c->rmt_k1 = c->maps->rmt_k1;
-                c->rmt_zero = c->maps->rmt_zero;
             }
         }
     }
@@ -924,10 +892,6 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.rmp_w = c->rmp_w;
     a.rmp_P = c->rmp_P;
     a.rmp_zero = c->rmp_zero;
-    a.rmt = c->rmt;
-    a.rmt_k1 = c->rmt_k1;
-    a.rmt_zero = c->rmt_zero;
-    a.fxs_tile = c->fxs_tile;
     a.fx_pad = c->rmp ? 1 : 0;
     a.count_slots = c->count_slots ? 1 : 0;
     a.fx_refill = c->fx_refill;
@@ -1093,9 +1057,6 @@ static int ensure_padded_table(f110_ctx *ctx) {
         ctx->rmp_w = ctx->maps->rmp_w;
         ctx->rmp_P = ctx->maps->rmp_P;
         ctx->rmp_zero = ctx->maps->rmp_zero;
-        ctx->rmt = ctx->maps->rmt;
-        ctx->rmt_k1 = ctx->maps->rmt_k1;
-        ctx->rmt_zero = ctx->maps->rmt_zero;
     }
     return F110_OK;
 }

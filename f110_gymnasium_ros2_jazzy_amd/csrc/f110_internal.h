@@ -62,12 +62,6 @@ struct StepArgs {
     const double *rmp;
     int32_t rmp_w, rmp_P;
     uint32_t rmp_zero;
-    // the same padded cells in 4x4 tiles (k_rays_fxs<TILE>): cell (R, C) of the padded grid at
-    // byte (R >> 2) * rmt_k1 + C * 32 + (R & 3) * 8, a 0.0 at byte rmt_zero; null = not built
-    const double *rmt;
-    int32_t rmt_k1;
-    uint32_t rmt_zero;
-    int32_t fxs_tile;   // F110_FXS_TILE: k_rays_fxs on rmt
     int32_t fx_pad;     // F110_FX_PAD: k_rays_fxn on the padded table
     int32_t fx_slots;   // F110_FX_SLOTS (A/B): chunk slots per k_rays_fxr wave, 2 or 3
     int32_t fxr_lean;   // k_rays_fxs for k_rays_fxr's padded two-slot kernel (F110_FXR_LEAN=0: off, A/B)
@@ -181,7 +175,6 @@ struct RayArgs {
     double fxp_lo, fxp_hx, fxp_hy;
     int32_t fxp_P;
     double fxs_cx, fxs_cy;  // k_rays_fxs: 2^20 + P + 2^-26 - origin / res (see kFxsBase)
-    int32_t fxt_k1;         // k_rays_fxs<TILE>: tile-row stride of the tiled padded table (bytes)
     int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_read_simt; F110_SIMT)
     // straggler hand-off of k_rays_fx (EVICT) -> k_rays_fx_tail: SoA records
     // ev[7][ev_cap] = x, y, d, tot, cos, sin, noise; ev_gb[2][ev_cap] = car, beam.

@@ -1407,41 +1407,7 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
     return act ? fast : zero_v;
 }
 
-// fxs_offset_nb on the 4x4-tiled padded table (TILE): byte (R >> 2) * k1t + C * 32 + (R & 3) * 8
-// from the high dwords hy = 3 * 2^20 + R, hx = 3 * 2^20 + C: their exponent terms add
-// 3 * 2^18 * (k1t + 128) = 0 mod 2^32 (k1t = 128 bytes short of a multiple of 16384)
-__device__ __forceinline__ uint32_t fxt_offset_nb(const FxLoop &L, double cx, double cy, uint32_t k1t, double &x,
-                                                  double &y, double d, double c, double s, bool act,
-                                                  uint32_t zero_v, bool &near) {
-    x += d * c;  // :135
-    y += d * s;  // :136
-    double tx, ty;
-    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tx) : "v"(x), "v"(L.ir), "s"(cx));
-    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(ty) : "v"(y), "v"(L.ir), "s"(cy));
-    near = min(dlo(tx), dlo(ty)) < 2u * kFxsBand;
-    const uint32_t hy = dhi(ty);
-    const uint32_t fast = __umul24(hy >> 2, k1t) + (dhi(tx) << 5) + ((hy & 3u) << 3);
-    return act ? fast : zero_v;
-}
-
-// exact_offset_pad on the tiled padded table (0: cell (0, 0), padding, for off-map)
-__device__ __forceinline__ uint32_t exact_offset_tile(const TiledMapView &m, double x, double y, uint32_t P,
-                                                      uint32_t k1t) {
-    const double xr = x - m.ox, yr = y - m.oy;
-    const bool inb = (xr >= 0) & (xr < m.wres) & (yr >= 0) & (yr < m.hres);  // false for NaN
-    if (!inb) return 0u;
-    int32_t c = (int32_t)(xr / m.res);
-    int32_t r = (int32_t)(yr / m.res);
-    if (c >= m.W) {  // dt[r, W] is dt[r+1, 0] in the reference's row-major read
-        c = 0;
-        ++r;
-    }
-    if (r >= m.H) return 0u;
-    const uint32_t R = (uint32_t)r + P, C = (uint32_t)c + P;
-    return (R >> 2) * k1t + C * 32u + (R & 3u) * 8u;
-}
-
-template <bool HANDOFF, int NS, bool PIPE = false, bool TILE = false>
+template <bool HANDOFF, int NS, bool PIPE = false>
 __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  // <= 64 / 72 VGPRs
     const int wj = (int)blockIdx.x / a.EA;
     const int g = (int)blockIdx.x - wj * a.EA;
@@ -1581,17 +1547,13 @@ __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  
                 lane_iters += (uint32_t)__popcll(m);
                 iters += m ? 1u : 0u;  // slot-trips with an active lane
                 bool near;
-                const uint32_t off =
-                    TILE ? fxt_offset_nb(L, a.fxs_cx, a.fxs_cy, (uint32_t)a.fxt_k1, x[r], y[r], d[r], c[r], sn[r], act,
-                                         zero_v, near)
-                         : fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act, zero_v, near);
+                const uint32_t off = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act,
+                                                   zero_v, near);
                 d[r] = ld_off(dt, off);
                 const uint64_t nb = __builtin_amdgcn_ballot_w64(near) & m;
                 if (nb) {  // rare: lanes within the guard band re-gather from the IEEE cell
                     const RayArgs &K = kernarg_here();
-                    if (lane_in(nb))
-                        d[r] = ld_off(dt, TILE ? exact_offset_tile(K.m, x[r], y[r], (uint32_t)K.fxp_P, (uint32_t)K.fxt_k1)
-                                               : exact_offset_pad(K.m, x[r], y[r], (uint32_t)K.fxp_P));
+                    if (lane_in(nb)) d[r] = ld_off(dt, exact_offset_pad(K.m, x[r], y[r], (uint32_t)K.fxp_P));
                 }
             }
             bool open = false;
@@ -1680,8 +1642,7 @@ __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  
             while ((dhi(d[0]) != 0u) & (tot[0] <= L.mr)) {
                 x[0] += d[0] * c[0];  // :135
                 y[0] += d[0] * sn[0];  // :136
-                d[0] = fx_load<3>(dt, TILE ? exact_offset_tile(K.m, x[0], y[0], (uint32_t)K.fxp_P, (uint32_t)K.fxt_k1)
-                                           : exact_offset_pad(K.m, x[0], y[0], (uint32_t)K.fxp_P));
+                d[0] = fx_load<3>(dt, exact_offset_pad(K.m, x[0], y[0], (uint32_t)K.fxp_P));
                 tot[0] += d[0];  // :141
                 ++cnt;
             }
@@ -3470,14 +3431,6 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                             if (a.fxs_pipe && a.fx_slots != 3)  // software-pipelined slots (F110_FXS_PIPE, A/B)
                                 f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true>)
                                            : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true>);
-                            if (a.fxs_pipe && a.fx_slots != 3 && a.fxs_tile && a.rmt) {
-                                // on the 4x4-tiled padded table (F110_FXS_TILE, A/B)
-                                f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true, true>)
-                                           : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true, true>);
-                                ra.m.dt = a.rmt;
-                                ra.fx_zero = a.rmt_zero;
-                                ra.fxt_k1 = a.rmt_k1;
-                            }
                             if (a.fx_lpool && a.pcost && a.fx_slots != 3 && a.fx_refill == 1 && (a.B + 63) / 64 <= 64) {
                                 // k_rays_fxq: lane-level refill over the car's beams (F110_FX_LPOOL)
                                 f = single ? reinterpret_cast<const void *>(&k_rays_fxq<false>)

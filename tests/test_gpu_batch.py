@@ -348,13 +348,11 @@ def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
     for refill, pad, lean, lpool in (("0", "0", "1", "0:80"), ("1", "0", "1", "0:80"), ("3", "0", "1", "0:80"),
                                      ("1", "1", "0", "0:80"), ("1", "1", "1", "0:80"), ("3", "1", "1", "0:80"),
                                      ("1", "1", "1", "1:80"), ("1", "1", "1", "1:1"), ("1", "1", "1", "1:128"),
-                                     ("1", "1", "2", "0:80"), ("3", "1", "2", "0:80"), ("1", "1", "t", "0:80"),
-                                     ("3", "1", "t", "0:80")):
+                                     ("1", "1", "2", "0:80"), ("3", "1", "2", "0:80")):
         monkeypatch.setenv("F110_FX_REFILL", refill)
         monkeypatch.setenv("F110_FX_PAD", pad)
-        monkeypatch.setenv("F110_FXR_LEAN", "0" if lean == "0" else "1")
+        monkeypatch.setenv("F110_FXR_LEAN", "1" if lean == "2" else lean)
         monkeypatch.setenv("F110_FXS_PIPE", "0" if lean == "2" else "1")  # "2": k_rays_fxs with lock-step slots
-        monkeypatch.setenv("F110_FXS_TILE", "1" if lean == "t" else "0")  # "t": on the 4x4-tiled padded table
         monkeypatch.setenv("F110_FX_LPOOL", lpool.split(":")[0])
         monkeypatch.setenv("F110_FX_POOL_T", lpool.split(":")[1])
         sim = _sim(tracks, gpu, n_envs=E, n_agents=A, num_beams=beams, noise_std=0.01, autoreset=True,
