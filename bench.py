@@ -43,6 +43,7 @@ def metric_name(global_envs: int, agents: int) -> str:
     who = "parallel envs" if agents == 1 else f"parallel {agents}-agent envs"
     return f"env-steps/sec at {global_envs} {who}, 1080-beam lidar; scan L2 vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+GATHER_PEAK_GLOOKUPS = 256 * 2.4  # CUs x max clock (GHz): one lane-lookup per CU per clock
 
 
 def parse():
@@ -591,6 +592,15 @@ def main():
         # lookups made in the loop / (loop trips x 64 lanes x rays per lane), from the kernel's own counters
         "simt_efficiency": loop_lookups / lane_slots if lane_slots else None,
     }
+    # the gather roofline: each lane's EDT lookup is its own L1 tag access (the active
+    # lanes of a wave-level gather touch distinct lines: ~30 accesses per gather at 65536 cars), and a
+    # CU's vector-memory address path takes one per clock: 256 CUs x 2.4 GHz = 614 G lookups/s
+    if not fused_prof:
+        look_launch = E * A * B * (mean_look - 1.0)  # the kernel's own lookups (the first is k_agents')
+        roof["gather_roofline"] = {
+            "bound": "vector-memory address path: one L1 tag access per lane-lookup, one per CU per clock",
+            "achieved_glookups_s": look_launch / (k_ms * 1e-3) / 1e9, "peak_glookups_s": GATHER_PEAK_GLOOKUPS,
+            "frac": look_launch / (k_ms * 1e-3) / 1e9 / GATHER_PEAK_GLOOKUPS, "lookups_per_launch": look_launch}
     # consistency: the kernel runs inside the step it is timed in (the one-context runner's own wall time
     # per step, measured in the chunks interleaved with the profiled ones)
     roof["kernel_le_step"] = {"ok": bool(k_ms <= plain_step_ms), "kernel_ms": k_ms, "runner_step_ms": plain_step_ms,
