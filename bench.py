@@ -503,10 +503,19 @@ def main():
     plain_s, plain_n, prof_s, prof_n = 0.0, 0, 0.0, 0
     acc = {"k_agents_ms": 0.0, "k_rays_ms": 0.0, "k_post_ms": 0.0}
     launches = 0
-    k0 = W
+    koff = 0
+
+    def chunk_rows(n):
+        """First action row of a chunk of n <= K steps inside the timed block [W, W + K)."""
+        nonlocal koff
+        k = W + koff % (K - n + 1)
+        koff += n
+        return k
+
     while plain_n < K or prof_n < KP:
         if plain_n < K:
             n = min(PC, K - plain_n)
+            k0 = chunk_rows(n)
             D.barrier()
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
@@ -515,7 +524,8 @@ def main():
             plain_s += D.max_over_ranks(time.perf_counter() - t0)
             plain_n += n
         if prof_n < KP:
-            n = min(PC, KP - prof_n)
+            n = min(PC, KP - prof_n, K)
+            k0 = chunk_rows(n)
             per = args.chunk if prof.kind == "rollout" else 1  # steps per launch
             t0 = time.perf_counter()
             prof.profile_begin(n)
@@ -528,7 +538,6 @@ def main():
                 acc[key] += pk[key] * nl / per  # per step
             launches += nl
             prof_n += n
-        k0 = W + (k0 - W + PC) % max(K - PC, 1)
     per_kernel = {key: acc[key] / max(launches, 1) for key in acc}
     per_kernel["steps"] = launches
     prof_step_ms = prof_s / max(prof_n, 1) * 1e3  # wall time per profiled step (events included)
