@@ -217,7 +217,8 @@ def auto_streams(envs, agents=1):
     concurrent sub-shards fill; large ones fill the GPU themselves.  Counted
     in cars (envs x agents).  Round 2, end (k_rays_fxn / k_rays_fxr): 16384 envs
     61.3 / 63.1 M at S = 2 / 4 (fxn), 65.3 M at S = 4 with k_rays_fxr
-    (profiles/r02_refill_small/): S = 4 up to 16384 cars."""
+    (profiles/r02_refill_small/): S = 4 up to 16384 cars.  Round 3 (k_rays_fxs): 32768 envs 76.7 M at
+    S = 2, 78.7 / 75.8 M at S = 4 on two boxes (profiles/r03_ab/e32768_*.json): no change."""
     return 4 if envs * agents <= 16384 else 2
 
 
@@ -297,7 +298,15 @@ def ray_kernel_name(sm):
     if sm.ray_kernel == 3 and getattr(sm, "ray_pool", 0) > 0:
         return f"k_rays_fxp ({sm.ray_pool} car(s) per wave, two ray slots per lane with lane-level refill)"
     if sm.ray_kernel == 3 and sm.ray_refill > 0:
-        return f"k_rays_fxr ({sm.ray_refill} wave(s) per car, 2 chunk slots with refill)"
+        env = os.environ
+        slots = 3 if env.get("F110_FX_SLOTS") == "3" else 2
+        if env.get("F110_FXR_LEAN", "1") != "0" and env.get("F110_FX_PAD", "1") != "0":  # launch_env_step's rule
+            if env.get("F110_FX_LPOOL", "0") != "0" and sm.ray_refill == 1 and slots == 2:
+                return "k_rays_fxq (one car per wave, lane-level refill over its beams)"
+            pipe = env.get("F110_FXS_PIPE", "1") != "0" and slots == 2
+            return (f"k_rays_fxs ({sm.ray_refill} wave(s) per car, {slots} chunk slots with refill"
+                    f"{', software-pipelined' if pipe else ''}, padded EDT)")
+        return f"k_rays_fxr ({sm.ray_refill} wave(s) per car, {slots} chunk slots with refill)"
     if sm.ray_kernel == 3 and sm.ray_lanes > 1:
         return f"k_rays_fxn ({sm.ray_lanes} rays per lane)"
     return names.get(sm.ray_kernel, str(sm.ray_kernel))

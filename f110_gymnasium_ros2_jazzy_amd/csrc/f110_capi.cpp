@@ -700,8 +700,10 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     // heavy-first pays where one ray grid is a few rounds of waves deep (16384 cars: 0.281 vs 0.287 ms)
     // and costs where it is deep (65536 cars: 1.288 vs 1.251 ms without; profiles/r02_ray_ab/ab_heavy.json)
     // or one round or less (round 3, every wave starts at once: 8192 cars 0.172 vs 0.167, 4096 cars
-    // 0.124 vs 0.109 ms without; profiles/r03_ab/small_shards.json)
-    if (!std::getenv("F110_HEAVY_T") && (EA > 32768 || EA <= 8192)) c->heavy_T = 0;
+    // 0.124 vs 0.109 ms without; profiles/r03_ab/small_shards.json); off from 32768 cars, where the
+    // refill kernel (which takes no heavy-first list) runs: at exactly 32768 it used to stay on and
+    // turn the refill off (one context 57.0 M env-steps/s, profiles/r03_ab/e32768_*.json)
+    if (!std::getenv("F110_HEAVY_T") && (EA >= 32768 || EA <= 8192)) c->heavy_T = 0;
     if (c->ray_kernel >= 2 && c->heavy_T > 0) {
         // up to 1/8 of the waves, in blocks of 4 (measured: ~7% of the waves
         // have a ray longer than 40 lookups and carry ~46% of the wave-iterations)
