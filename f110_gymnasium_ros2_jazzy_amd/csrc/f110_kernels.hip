@@ -649,6 +649,65 @@ __device__ __forceinline__ void fx_step_safe(const TiledMapView &m, const FxLoop
     tot += d;  // :141
 }
 
+// fx_step_safe<3>'s cell offset of the position (x, y).
+__device__ __forceinline__ uint32_t fx_safe_offset3(const TiledMapView &m, const FxLoop &L, double x, double y) {
+    double tx, ty;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tx) : "v"(x), "v"(L.ir), "s"(L.cxk));
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(ty) : "v"(y), "v"(L.ir), "s"(L.cyk));
+    const uint32_t lx = dlo(tx), ly = dlo(ty);
+    const uint32_t col = __builtin_amdgcn_alignbit(dhi(tx), lx, 30) - kFxU0;
+    const uint32_t row = __builtin_amdgcn_alignbit(dhi(ty), ly, 30) - kFxU0;
+    const bool near = ((lx << 2) + 4u * kFxBand < 8u * kFxBand) | ((ly << 2) + 4u * kFxBand < 8u * kFxBand);
+    uint32_t off = fx_offset<3>(L.k1, min(row, L.H), min(col, L.W));  // clamped into the padding
+    if (__builtin_amdgcn_ballot_w64(near)) {  // wave-uniform, rare
+        if (near) off = exact_offset<3>(m, x, y, L.oobv);
+    }
+    return off;
+}
+
+// SPEC: fx_step_safe<3> that also guesses the ray's next K - 1 steps.  Where
+// the EDT value repeats along a ray (a ray running beside a wall), its next
+// positions are x + d c, (x + d c) + d c, ... -- the same sequence of adds
+// as the serial loop's -- so their cells are gathered together with this
+// step's.  The guesses are checked in order: step j + 1 is kept only while
+// every earlier lookup returned d itself and the ray goes on (tot <= mr; a
+// lookup equal to d != 0 is not the end).  The kept positions and totals are
+// the serial loop's bit for bit: only the chain of dependent gathers is
+// shorter.  Every guessed offset is clamped into the table like any other.
+// Returns the steps taken (the lookups that count).
+template <int K>
+__device__ __forceinline__ uint32_t fx_step_spec(const TiledMapView &m, const FxLoop &L, double &x, double &y,
+                                                 double &d, double &tot, double c, double s) {
+    const double d0 = d;
+    double xs[K], ys[K], dd[K];
+    uint32_t off[K];
+    double xc = x, yc = y;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        xc += d0 * c;  // :135
+        yc += d0 * s;  // :136
+        xs[j] = xc;
+        ys[j] = yc;
+        off[j] = fx_safe_offset3(m, L, xc, yc);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) dd[j] = fx_load<3>(m.dt, off[j]);
+    uint32_t n = 0;
+    bool go = true;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        if (go) {
+            x = xs[j];
+            y = ys[j];
+            d = dd[j];
+            tot += d;  // :141
+            ++n;
+            go = (d == d0) & (tot <= L.mr);
+        }
+    }
+    return n;
+}
+
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
@@ -690,7 +749,10 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {  // set bits of
 // rays stay in t's binade take fx_step_safe: ~36 instead of ~59 instructions
 // per iteration on the wave's serial path (the kernel is latency-bound: at
 // 6 / 4 / 2 waves per SIMD it takes 1.31x / 1.62x / 2.9x as long).
-template <bool MASK, bool HANDOFF, bool EVICT, int FMT = 0, bool LEAN = !EVICT>
+//
+// SPEC (F110_FX_SPEC=K:T, row-major table, A/B): once <= fx_spec_t lanes of
+// the wave still trace, each iteration takes fx_step_spec<SPEC>.
+template <bool MASK, bool HANDOFF, bool EVICT, int FMT = 0, bool LEAN = !EVICT, int SPEC = 1>
 __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
     int g, k;
     if ((int)blockIdx.x < a.HB) {  // heavy-first blocks: the listed waves
@@ -768,7 +830,17 @@ __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
         uint32_t cnt = 0;
         const double qx = fma(x00, L.ir, L.cxk) - kFxMagic, qy = fma(y00, L.ir, L.cyk) - kFxMagic;
         __builtin_amdgcn_s_waitcnt(0);  // the set-up loads (c, s) land before the loop, not in it
-        if (fabs(qx) < a.fx_lim && fabs(qy) < a.fx_lim) {  // wave-uniform (false for NaN)
+        if (SPEC > 1 && FMT == 3 && fabs(qx) < a.fx_lim && fabs(qy) < a.fx_lim) {
+            const uint32_t T = (uint32_t)a.fx_spec_t;
+            while ((dhi(d) != 0u) & (tot <= L.mr)) {
+                if ((uint32_t)__popcll(__builtin_amdgcn_ballot_w64(true)) <= T) {  // wave-uniform: the tail
+                    cnt += fx_step_spec<SPEC>(a.m, L, x, y, d, tot, c, s);
+                } else {
+                    fx_step_safe<FMT>(a.m, L, x, y, d, tot, c, s);
+                    ++cnt;
+                }
+            }
+        } else if (fabs(qx) < a.fx_lim && fabs(qy) < a.fx_lim) {  // wave-uniform (false for NaN)
             while ((dhi(d) != 0u) & (tot <= L.mr)) {
                 fx_step_safe<FMT>(a.m, L, x, y, d, tot, c, s);
                 ++cnt;
@@ -3449,6 +3521,19 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                                            reinterpret_cast<const void *>(&k_rays_fx<true, false, false, 3>),
                                            reinterpret_cast<const void *>(&k_rays_fx<true, true, false, 3>)};
                     f = fn_1[v2];
+                    if (a.fx_spec_k > 1 && a.fx_spec_t > 0) {  // speculative steps in the tail (F110_FX_SPEC, A/B)
+                        const void *fn_s[2][4] = {
+                            {reinterpret_cast<const void *>(&k_rays_fx<false, false, false, 3, true, 2>),
+                             reinterpret_cast<const void *>(&k_rays_fx<false, true, false, 3, true, 2>),
+                             reinterpret_cast<const void *>(&k_rays_fx<true, false, false, 3, true, 2>),
+                             reinterpret_cast<const void *>(&k_rays_fx<true, true, false, 3, true, 2>)},
+                            {reinterpret_cast<const void *>(&k_rays_fx<false, false, false, 3, true, 4>),
+                             reinterpret_cast<const void *>(&k_rays_fx<false, true, false, 3, true, 4>),
+                             reinterpret_cast<const void *>(&k_rays_fx<true, false, false, 3, true, 4>),
+                             reinterpret_cast<const void *>(&k_rays_fx<true, true, false, 3, true, 4>)}};
+                        f = fn_s[a.fx_spec_k == 4 ? 1 : 0][v2];
+                        ra.fx_spec_t = a.fx_spec_t;
+                    }
                 }
             }
             if (a.fx_nolean && single && !mask && !a.ev)  // A/B: the round-2 loop (tiled EDT)

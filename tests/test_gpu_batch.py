@@ -375,6 +375,46 @@ def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
                 assert torch.equal(x, y), f"step {t}"
 
 
+@pytest.mark.parametrize("A,beams", [(1, 1080), (2, 1080), (1, 333)])
+def test_spec_step_identical(tracks, gpu, monkeypatch, A, beams):
+    """k_rays_fx's speculative step (F110_FX_SPEC=K:T: once <= T lanes of a
+    wave still trace, each lookup round gathers the cells of the next K
+    steps as if the EDT value repeated, and keeps the prefix whose guesses
+    held) against the serial loop: scans, obs, collisions and states
+    bit-identical over 25 noisy steps with autoreset and a masked reset, for
+    K = 2 / 4 on every iteration (T = 64) and in the tail only (T = 8); the
+    counters (lookups, rays, lane slots) equal the serial loop's."""
+    E = 300
+    sp = _spawns(A)
+    rng = np.random.default_rng(beams + A + 3)
+    poses = sp[rng.integers(0, sp.shape[0], E)]
+    acts = np.stack([rng.uniform(-0.4189, 0.4189, (25, E, A)), rng.uniform(0, 20, (25, E, A))], -1).astype(np.float32)
+    mask = rng.random(E) < 0.5
+    monkeypatch.setenv("F110_FX_ILP", "1")
+    monkeypatch.setenv("F110_FX_REFILL", "0")
+    monkeypatch.setenv("F110_FX_PAD", "0")
+    outs, ctrs = [], []
+    for spec in ("1:0", "2:64", "4:64", "4:8", "2:16"):
+        monkeypatch.setenv("F110_FX_SPEC", spec)
+        sim = _sim(tracks, gpu, n_envs=E, n_agents=A, num_beams=beams, noise_std=0.01, autoreset=True,
+                   spawn_poses=sp, seed=9, keep_f64_scans=True)
+        sim.reset(poses)
+        sim.reset_counters()
+        rec = []
+        for t in range(25):
+            o = sim.reset(poses[::-1].copy(), env_mask=mask) if t == 12 else sim.step(acts[t])
+            rec.append((o.scans_f64.clone(), o.obs.clone(), o.collisions.clone(), sim.agent_states().clone()))
+        torch.cuda.synchronize()
+        outs.append(rec)
+        ctrs.append(sim.read_counters())
+        sim.close()
+    for k in range(1, len(outs)):
+        assert ctrs[0] == ctrs[k]
+        for t, (a, b) in enumerate(zip(outs[0], outs[k])):
+            for x, y in zip(a, b):
+                assert torch.equal(x, y), f"step {t}"
+
+
 @pytest.mark.parametrize("A,beams", [(1, 1080), (2, 1080), (1, 333), (1, 64)])
 def test_pool_kernel_identical(tracks, gpu, monkeypatch, A, beams):
     """k_rays_fxp (F110_FX_POOL = 1 or 2 cars per wave: two ray slots per
