@@ -110,6 +110,7 @@ struct f110_ctx {
     int32_t fxr_lean = 1;    // k_rays_fxs in place of k_rays_fxr<.., PAD, 2> (F110_FXR_LEAN=0: the round-3 kernel)
     int32_t fx_lpool = 0;    // k_rays_fxq in place of k_rays_fxs (F110_FX_LPOOL)
     int32_t fx_spec_k = 1, fx_spec_t = 0;  // F110_FX_SPEC=K:T (A/B): k_rays_fx speculative steps in its tail
+    int32_t fxs_maskld = 0;  // k_rays_fxs: ended lanes issue no gather (F110_FXS_MASKLD, A/B)
     int32_t fxs_pipe = 1;    // k_rays_fxs with software-pipelined slots (F110_FXS_PIPE=0: in lock-step, A/B)
     int32_t fx_refill = 0;   // waves per car of k_rays_fxr (0 = k_rays_fxn; F110_FX_REFILL overrides)
     int32_t fx_pool = 0;     // cars per k_rays_fxp wave (lane-level refill; 0 = off; F110_FX_POOL)
@@ -750,6 +751,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (const char *v = std::getenv("F110_FXR_LEAN")) c->fxr_lean = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FX_LPOOL")) c->fx_lpool = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FXS_PIPE")) c->fxs_pipe = std::atoi(v) != 0;
+    if (const char *v = std::getenv("F110_FXS_MASKLD")) c->fxs_maskld = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FX_SPEC")) {
         int k = 1, t = 0;
         if (std::sscanf(v, "%d:%d", &k, &t) >= 1) {
@@ -914,6 +916,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.fxr_lean = c->fxr_lean;
     a.fx_lpool = c->fx_lpool;
     a.fxs_pipe = c->fxs_pipe;
+    a.fxs_maskld = c->fxs_maskld;
     a.fx_spec_k = c->fx_spec_k;
     a.fx_spec_t = c->fx_spec_t;
     a.fx_tiled = c->fx_tiled ? 1 : 0;

@@ -67,6 +67,7 @@ struct StepArgs {
     int32_t fxr_lean;   // k_rays_fxs for k_rays_fxr's padded two-slot kernel (F110_FXR_LEAN=0: off, A/B)
     int32_t fx_lpool;   // k_rays_fxq (lane-level refill, one car per wave) where k_rays_fxs runs (F110_FX_LPOOL)
     int32_t fxs_pipe;   // k_rays_fxs with software-pipelined slots (F110_FXS_PIPE)
+    int32_t fxs_maskld; // k_rays_fxs: ended lanes issue no gather (F110_FXS_MASKLD)
     int32_t fx_spec_k, fx_spec_t;  // F110_FX_SPEC=K:T: k_rays_fx guesses K steps per lookup once <= T lanes trace
     int32_t fx_refill;  // F110_FX_REFILL: waves per car of k_rays_fxr (two chunk slots with refill; 0 = off)
     int32_t fx_pool;    // F110_FX_POOL: cars per k_rays_fxp wave (lane-level refill; 0 = off)

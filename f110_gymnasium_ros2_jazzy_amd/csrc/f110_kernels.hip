@@ -1479,7 +1479,10 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
     return act ? fast : zero_v;
 }
 
-template <bool HANDOFF, int NS, bool PIPE = false>
+// ML (F110_FXS_MASKLD, PIPE only): the slot gathers are buffer loads through a descriptor
+// whose range ends at the zero cell, so an ended lane's zero-cell offset fails the range
+// check: it reads 0.0 as before, without a cache access of its own.
+template <bool HANDOFF, int NS, bool PIPE = false, bool ML = false>
 __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  // <= 64 / 72 VGPRs
     const int wj = (int)blockIdx.x / a.EA;
     const int g = (int)blockIdx.x - wj * a.EA;
@@ -1582,6 +1585,8 @@ __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  
     const double uy = fma(ld_const(a.ray0 + a.EA + g), L.ir, L.cyk) - kFxpBase;
     // q + P of the scan origin inside [fxp_lo, fxp_h*): its rays stay in the padded table (false for NaN)
     const bool fast_car = (ux >= a.fxp_lo) & (ux < a.fxp_hx) & (uy >= a.fxp_lo) & (uy < a.fxp_hy);
+    // ML: the table's descriptor, records up to (not including) the zero cell
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)dt, (short)0, (int)a.fx_zero, 0x00020000);
     if (fast_car && PIPE) {
         // Software-pipelined slots: each slot's gather is waited for right before that slot's
         // next step, so one slot's gather is in flight while the other slot's data is consumed
@@ -1621,7 +1626,12 @@ __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  
                 bool near;
                 const uint32_t off = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act,
                                                    zero_v, near);
-                d[r] = ld_off(dt, off);
+                if (ML) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, 0);
+                    d[r] = __builtin_bit_cast(double, v);
+                } else {
+                    d[r] = ld_off(dt, off);
+                }
                 const uint64_t nb = __builtin_amdgcn_ballot_w64(near) & m;
                 if (nb) {  // rare: lanes within the guard band re-gather from the IEEE cell
                     const RayArgs &K = kernarg_here();
@@ -3503,6 +3513,9 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                             if (a.fxs_pipe && a.fx_slots != 3)  // software-pipelined slots (F110_FXS_PIPE, A/B)
                                 f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true>)
                                            : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true>);
+                            if (a.fxs_pipe && a.fx_slots != 3 && a.fxs_maskld)  // no zero-cell gathers (F110_FXS_MASKLD)
+                                f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true, true>)
+                                           : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true, true>);
                             if (a.fx_lpool && a.pcost && a.fx_slots != 3 && a.fx_refill == 1 && (a.B + 63) / 64 <= 64) {
                                 // k_rays_fxq: lane-level refill over the car's beams (F110_FX_LPOOL)
                                 f = single ? reinterpret_cast<const void *>(&k_rays_fxq<false>)
