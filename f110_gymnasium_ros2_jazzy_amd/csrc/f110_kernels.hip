@@ -1479,10 +1479,13 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
     return act ? fast : zero_v;
 }
 
-// ML (F110_FXS_MASKLD, PIPE only): the slot gathers are buffer loads through a descriptor
-// whose range ends at the zero cell, so an ended lane's zero-cell offset fails the range
-// check: it reads 0.0 as before, without a cache access of its own.
-template <bool HANDOFF, int NS, bool PIPE = false, bool ML = false>
+// ML (F110_FXS_MASKLD, PIPE only), 1: the slot gathers are buffer loads through a
+// descriptor whose range ends at the zero cell, so an ended lane's zero-cell offset fails
+// the range check: it reads 0.0 as before, without a cache access of its own.  2: an ended
+// lane issues no gather at all (exec mask) and keeps its d: a ray ended by its range then
+// goes on adding d to a total past max_range, which the clamp (:143-144) maps to max_range
+// all the same.
+template <bool HANDOFF, int NS, bool PIPE = false, int ML = 0>
 __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  // <= 64 / 72 VGPRs
     const int wj = (int)blockIdx.x / a.EA;
     const int g = (int)blockIdx.x - wj * a.EA;
@@ -1626,9 +1629,11 @@ __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  
                 bool near;
                 const uint32_t off = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act,
                                                    zero_v, near);
-                if (ML) {
+                if (ML == 1) {
                     const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, 0);
                     d[r] = __builtin_bit_cast(double, v);
+                } else if (ML == 2) {
+                    if (act) d[r] = ld_off(dt, off);
                 } else {
                     d[r] = ld_off(dt, off);
                 }
@@ -3514,8 +3519,11 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                                 f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true>)
                                            : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true>);
                             if (a.fxs_pipe && a.fx_slots != 3 && a.fxs_maskld)  // no zero-cell gathers (F110_FXS_MASKLD)
-                                f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true, true>)
-                                           : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true, true>);
+                                f = a.fxs_maskld == 2
+                                        ? (single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true, 2>)
+                                                  : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true, 2>))
+                                        : (single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true, 1>)
+                                                  : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true, 1>));
                             if (a.fx_lpool && a.pcost && a.fx_slots != 3 && a.fx_refill == 1 && (a.B + 63) / 64 <= 64) {
                                 // k_rays_fxq: lane-level refill over the car's beams (F110_FX_LPOOL)
                                 f = single ? reinterpret_cast<const void *>(&k_rays_fxq<false>)
