@@ -751,7 +751,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (const char *v = std::getenv("F110_FXR_LEAN")) c->fxr_lean = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FX_LPOOL")) c->fx_lpool = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FXS_PIPE")) c->fxs_pipe = std::atoi(v) != 0;
-    if (const char *v = std::getenv("F110_FXS_MASKLD")) c->fxs_maskld = std::max(0, std::min(2, std::atoi(v)));
+    if (const char *v = std::getenv("F110_FXS_MASKLD")) c->fxs_maskld = std::max(0, std::min(3, std::atoi(v)));
     if (const char *v = std::getenv("F110_FX_SPEC")) {
         int k = 1, t = 0;
         if (std::sscanf(v, "%d:%d", &k, &t) >= 1) {

@@ -1484,7 +1484,8 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
 // the range check: it reads 0.0 as before, without a cache access of its own.  2: an ended
 // lane issues no gather at all (exec mask) and keeps its d: a ray ended by its range then
 // goes on adding d to a total past max_range, which the clamp (:143-144) maps to max_range
-// all the same.
+// all the same.  3 (lock-step slots, F110_FXS_PIPE=0): a trip in which no lane has both
+// slots' rays active issues one gather for the two slots.
 template <bool HANDOFF, int NS, bool PIPE = false, int ML = 0>
 __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  // <= 64 / 72 VGPRs
     const int wj = (int)blockIdx.x / a.EA;
@@ -1668,20 +1669,30 @@ __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  
             uint64_t m[NS];
             uint32_t cnt[NS], off[NS];
             bool near[NS];  // the lane's cell is within the guard band of an edge
+            bool ac[NS];
             // every slot steps unconditionally (a slot without active lanes reads the zero cell:
             // ~15 VALU wasted in the car's last chunks instead of a branch per slot per trip)
 #pragma unroll
             for (int r = 0; r < NS; ++r) {
                 const bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+                ac[r] = act;
                 m[r] = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
                 cnt[r] = (uint32_t)__popcll(m[r]);
                 off[r] = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act, zero_v, near[r]);
             }
+            if (ML == 3 && NS == 2 && !(m[0] & m[1])) {
+                // ML 3: no lane has both slots' rays active, so one gather serves both slots
+                // (an ended ray reads 0.0, as from the zero cell)
+                const double v = ld_off(dt, ac[0] ? off[0] : off[1]);
+                d[0] = ac[0] ? v : 0.0;
+                d[NS - 1] = ac[NS - 1] ? v : 0.0;
+            } else {
+#pragma unroll
+                for (int r = 0; r < NS; ++r) d[r] = ld_off(dt, off[r]);
+            }
             // the gathers go out on the fixed-point cells at once (the guard-band test is off the
             // dependent chain d -> x, y -> cell -> d); the rare lanes within the band of a cell edge
             // then re-gather from tiled_cell's IEEE cell (loads return in order: the second wins)
-#pragma unroll
-            for (int r = 0; r < NS; ++r) d[r] = ld_off(dt, off[r]);
             uint64_t nb[NS], nball = 0;
 #pragma unroll
             for (int r = 0; r < NS; ++r) {
@@ -3518,7 +3529,10 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                             if (a.fxs_pipe && a.fx_slots != 3)  // software-pipelined slots (F110_FXS_PIPE, A/B)
                                 f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true>)
                                            : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true>);
-                            if (a.fxs_pipe && a.fx_slots != 3 && a.fxs_maskld)  // no zero-cell gathers (F110_FXS_MASKLD)
+                            if (!a.fxs_pipe && a.fx_slots != 3 && a.fxs_maskld == 3)  // merged slot gathers (A/B)
+                                f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, false, 3>)
+                                           : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, false, 3>);
+                            if (a.fxs_pipe && a.fx_slots != 3 && a.fxs_maskld && a.fxs_maskld != 3)  // no zero-cell gathers (F110_FXS_MASKLD)
                                 f = a.fxs_maskld == 2
                                         ? (single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true, 2>)
                                                   : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true, 2>))

@@ -349,13 +349,14 @@ def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
                                      ("1", "1", "0", "0:80"), ("1", "1", "1", "0:80"), ("3", "1", "1", "0:80"),
                                      ("1", "1", "1", "1:80"), ("1", "1", "1", "1:1"), ("1", "1", "1", "1:128"),
                                      ("1", "1", "2", "0:80"), ("3", "1", "2", "0:80"), ("1", "1", "m", "0:80"),
-                                     ("1", "1", "x", "0:80")):
+                                     ("1", "1", "x", "0:80"), ("1", "1", "j", "0:80")):
         monkeypatch.setenv("F110_FX_REFILL", refill)
         monkeypatch.setenv("F110_FX_PAD", pad)
-        monkeypatch.setenv("F110_FXR_LEAN", "1" if lean in ("2", "m", "x") else lean)
-        # "m": range-checked buffer gathers, "x": ended lanes issue no gather (exec mask)
-        monkeypatch.setenv("F110_FXS_MASKLD", {"m": "1", "x": "2"}.get(lean, "0"))
-        monkeypatch.setenv("F110_FXS_PIPE", "0" if lean == "2" else "1")  # "2": k_rays_fxs with lock-step slots
+        monkeypatch.setenv("F110_FXR_LEAN", "1" if lean in ("2", "m", "x", "j") else lean)
+        # "m": range-checked buffer gathers, "x": ended lanes issue no gather (exec mask), "j": lock-step
+        # slots sharing one gather when no lane has both rays active
+        monkeypatch.setenv("F110_FXS_MASKLD", {"m": "1", "x": "2", "j": "3"}.get(lean, "0"))
+        monkeypatch.setenv("F110_FXS_PIPE", "0" if lean in ("2", "j") else "1")  # "2": k_rays_fxs with lock-step slots
         monkeypatch.setenv("F110_FX_LPOOL", lpool.split(":")[0])
         monkeypatch.setenv("F110_FX_POOL_T", lpool.split(":")[1])
         sim = _sim(tracks, gpu, n_envs=E, n_agents=A, num_beams=beams, noise_std=0.01, autoreset=True,
