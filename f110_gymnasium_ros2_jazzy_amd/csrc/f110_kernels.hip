@@ -1635,6 +1635,7 @@ __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  
                     d[r] = __builtin_bit_cast(double, v);
                 } else if (ML == 2) {
                     if (act) d[r] = ld_off(dt, off);
+
                 } else {
                     d[r] = ld_off(dt, off);
                 }
