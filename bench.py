@@ -44,6 +44,7 @@ def metric_name(global_envs: int, agents: int) -> str:
     return f"env-steps/sec at {global_envs} {who}, 1080-beam lidar; scan L2 vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GATHER_PEAK_GLOOKUPS = 256 * 2.4  # CUs x max clock (GHz): one lane-lookup per CU per clock
+TA_CYCLES_PER_LOAD = 20.1  # texture-address cycles per wave-level 8-byte gather, measured
 
 
 def parse():
@@ -595,7 +596,10 @@ def main():
         "kernel": "k_step1" if fused_prof else "k_rays",
         "profiled_steps": KP,
         "profiled_launches": per_kernel["steps"],
-        "bound": ("VALU issue of the sphere-trace loop (valu_busy; HBM is not the limit: see hbm_traffic_frac and "
+        "bound": ("the texture-address path, per wave-level load (~20 TA cycles each whatever its lanes do; HBM is "
+                  "not the limit: see hbm_traffic_frac; DESIGN.md 3.9)" if prof.ray_kernel == 3 and prof.ray_refill > 0
+                  and not fused_prof else
+                  "VALU issue of the sphere-trace loop (valu_busy; HBM is not the limit: see hbm_traffic_frac and "
                   "l2_hit_rate; DESIGN.md 3.4)" if prof.ray_kernel == 3 and (prof.ray_refill > 0 or fused_prof) else
                   "latency of the dependent EDT gather chain (HBM is not the limit: see hbm_traffic_frac; capping "
                   "occupancy at 6/4/2 waves per SIMD costs 1.31x/1.62x/2.9x, DESIGN.md 3.2)"),
@@ -610,15 +614,24 @@ def main():
         # lookups made in the loop / (loop trips x 64 lanes x rays per lane), from the kernel's own counters
         "simt_efficiency": loop_lookups / lane_slots if lane_slots else None,
     }
-    # the gather roofline: each lane's EDT lookup is its own L1 tag access (the active
-    # lanes of a wave-level gather touch distinct lines: ~30 accesses per gather at 65536 cars), and a
-    # CU's vector-memory address path takes one per clock: 256 CUs x 2.4 GHz = 614 G lookups/s
+    # the gather roofline, per lane-lookup: one per CU per clock, 256 CUs x 2.4 GHz = 614 G
+    # lookups/s (it holds at the kernel's SIMT); and per instruction, the form the counters show: the
+    # texture-address unit spends ~20.1 cycles on every wave-level 8-byte load whatever its lanes do
+    # (profiles/r03_ab/pmc_ended_lanes/), so the loop's slot gathers (lane slots / 64) need at least
+    # gathers x 20.1 / 256 CUs / 2.4 GHz (the refills' table loads come on top)
     if not fused_prof:
         look_launch = E * A * B * (mean_look - 1.0)  # the kernel's own lookups (the first is k_agents')
         roof["gather_roofline"] = {
-            "bound": "vector-memory address path: one L1 tag access per lane-lookup, one per CU per clock",
+            "bound": "vector-memory address path: one lane-lookup per CU per clock",
             "achieved_glookups_s": look_launch / (k_ms * 1e-3) / 1e9, "peak_glookups_s": GATHER_PEAK_GLOOKUPS,
             "frac": look_launch / (k_ms * 1e-3) / 1e9 / GATHER_PEAK_GLOOKUPS, "lookups_per_launch": look_launch}
+        if lane_slots:
+            gathers = lane_slots / 64.0 / max(1, min(K, 50))  # per launch (the counters ran min(K, 50) steps)
+            min_ms = gathers * TA_CYCLES_PER_LOAD / 256 / 2.4e9 * 1e3
+            roof["gather_roofline"]["slot_gathers_per_launch"] = gathers
+            roof["gather_roofline"]["ta_cycles_per_load"] = TA_CYCLES_PER_LOAD
+            roof["gather_roofline"]["slot_gather_min_ms"] = min_ms
+            roof["gather_roofline"]["slot_gather_frac"] = min_ms / k_ms
     # consistency: the kernel runs inside the step it is timed in (the one-context runner's own wall time
     # per step, measured in the chunks interleaved with the profiled ones)
     roof["kernel_le_step"] = {"ok": bool(k_ms <= plain_step_ms), "kernel_ms": k_ms, "runner_step_ms": plain_step_ms,

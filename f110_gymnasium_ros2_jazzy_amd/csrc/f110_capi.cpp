@@ -59,6 +59,7 @@ struct f110_ctx {
     uint8_t chunk_order[kMaxChunks] = {};
     double *dt = nullptr, *sines = nullptr, *cosines = nullptr, *angles = nullptr, *beam_cos = nullptr,
            *side = nullptr, *spawn = nullptr;
+    double *cs2 = nullptr, *bs2 = nullptr;  // interleaved (cos, sin)[theta_dis], (side, beam_cos)[B] (F110_FXS_PACK)
     double *start_rot = nullptr;
     double *st = nullptr, *sb = nullptr, *start = nullptr, *sim_time = nullptr, *ray0 = nullptr, *scan = nullptr;
     BeamRun *runs = nullptr;
@@ -110,6 +111,7 @@ struct f110_ctx {
     int32_t fxr_lean = 1;    // k_rays_fxs in place of k_rays_fxr<.., PAD, 2> (F110_FXR_LEAN=0: the round-3 kernel)
     int32_t fx_lpool = 0;    // k_rays_fxq in place of k_rays_fxs (F110_FX_LPOOL)
     int32_t fx_spec_k = 1, fx_spec_t = 0;  // F110_FX_SPEC=K:T (A/B): k_rays_fx speculative steps in its tail
+    int32_t fxs_pack = 1;  // k_rays_fxs: one 16-byte load for (cos, sin) and for (side, beam_cos) (F110_FXS_PACK=0: two, A/B)
     int32_t fxs_maskld = 0;  // k_rays_fxs: ended lanes issue no gather (F110_FXS_MASKLD, A/B)
     int32_t fxs_pipe = 1;    // k_rays_fxs with software-pipelined slots (F110_FXS_PIPE=0: in lock-step, A/B)
     int32_t fx_refill = 0;   // waves per car of k_rays_fxr (0 = k_rays_fxn; F110_FX_REFILL overrides)
@@ -643,6 +645,8 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     ALLOC(c->angles, (size_t)C.n_beams);
     ALLOC(c->beam_cos, (size_t)C.n_beams);
     ALLOC(c->side, (size_t)C.n_beams);
+    ALLOC(c->cs2, 2 * (size_t)C.theta_dis);
+    ALLOC(c->bs2, 2 * (size_t)C.n_beams);
     ALLOC(c->st, 7 * EA);
     ALLOC(c->sb, 2 * EA);
     ALLOC(c->scnt, EA);
@@ -727,6 +731,19 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (e == hipSuccess) e = hipMemcpy(c->angles, an.data(), an.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->beam_cos, bc.data(), bc.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->side, sd.data(), sd.size() * sizeof(double), hipMemcpyHostToDevice);
+    {
+        std::vector<double> cs2(2 * (size_t)C.theta_dis), bs2(2 * (size_t)C.n_beams);
+        for (int i = 0; i < C.theta_dis; ++i) {
+            cs2[2 * (size_t)i] = co[i];
+            cs2[2 * (size_t)i + 1] = s[i];
+        }
+        for (int i = 0; i < C.n_beams; ++i) {
+            bs2[2 * (size_t)i] = sd[i];
+            bs2[2 * (size_t)i + 1] = bc[i];
+        }
+        if (e == hipSuccess) e = hipMemcpy(c->cs2, cs2.data(), cs2.size() * sizeof(double), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(c->bs2, bs2.data(), bs2.size() * sizeof(double), hipMemcpyHostToDevice);
+    }
     c->agent_p.assign((size_t)C.n_agents, *params);
     if (e == hipSuccess)
         e = hipMemcpy(c->pa, c->agent_p.data(), c->agent_p.size() * sizeof(f110_params), hipMemcpyHostToDevice);
@@ -751,6 +768,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (const char *v = std::getenv("F110_FXR_LEAN")) c->fxr_lean = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FX_LPOOL")) c->fx_lpool = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FXS_PIPE")) c->fxs_pipe = std::atoi(v) != 0;
+    if (const char *v = std::getenv("F110_FXS_PACK")) c->fxs_pack = std::atoi(v) != 0;
     if (const char *v = std::getenv("F110_FXS_MASKLD")) c->fxs_maskld = std::max(0, std::min(3, std::atoi(v)));
     if (const char *v = std::getenv("F110_FX_SPEC")) {
         int k = 1, t = 0;
@@ -829,6 +847,8 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.angles = c->angles;
     a.beam_cos = c->beam_cos;
     a.side = c->side;
+    a.cs2 = c->fxs_pack ? c->cs2 : nullptr;
+    a.bs2 = c->fxs_pack ? c->bs2 : nullptr;
     a.p = c->p;
     a.E = c->cfg.n_envs;
     a.A = c->cfg.n_agents;

@@ -24,6 +24,7 @@ struct StepArgs {
     TiledMapView tmap;
     const double *sines, *cosines;            // [theta_dis]  ScanSimulator2D tables
     const double *angles, *beam_cos, *side;   // [B] RaceCar class-level beam tables
+    const double *cs2, *bs2;  // k_rays_fxs (F110_FXS_PACK): (cos, sin)[theta_dis], (side, beam_cos)[B] interleaved, or null
     f110_params p;                            // Simulator / F110Env params (GJK boxes, lidar_max)
     const f110_params *pa;                    // [A] RaceCar params (update_pose, ray_cast boxes)
     int32_t E, A, B, theta_dis, integrator, ego, autoreset, mode;  // mode 0 step, 1 reset
@@ -196,6 +197,7 @@ struct RayArgs {
     uint8_t *pcost;
     int32_t pool_T;
     int32_t fx_spec_t;  // k_rays_fx<.., SPEC>: the speculative step runs once <= fx_spec_t lanes still trace
+    const double *cs2, *bs2;  // k_rays_fxs: interleaved (cos, sin) / (side, beam_cos) tables (F110_FXS_PACK), or null
 };
 
 // k_step1's argument block (the fused single-agent step over n steps): RayArgs

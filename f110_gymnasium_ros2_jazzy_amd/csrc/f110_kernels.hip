@@ -1486,7 +1486,9 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
 // goes on adding d to a total past max_range, which the clamp (:143-144) maps to max_range
 // all the same.  3 (lock-step slots, F110_FXS_PIPE=0): a trip in which no lane has both
 // slots' rays active issues one gather for the two slots.
-template <bool HANDOFF, int NS, bool PIPE = false, int ML = 0>
+// PK (F110_FXS_PACK): the arm's (cos, sin) and the epilogue's (side, beam_cos) as one 16-byte
+// load each from the interleaved tables RayArgs::cs2 / bs2.
+template <bool HANDOFF, int NS, bool PIPE = false, int ML = 0, bool PK = false>
 __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  // <= 64 / 72 VGPRs
     const int wj = (int)blockIdx.x / a.EA;
     const int g = (int)blockIdx.x - wj * a.EA;
@@ -1528,8 +1530,14 @@ __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  
         const int lo = __builtin_amdgcn_readlane(vlo, k);
         int ti = (int)beam_theta(K.runs + (size_t)g * kMaxSeg, ld_const(K.nruns + g), lo, k * 64, bc);  // :124
         if (ti >= K.theta_dis) ti = 0;
-        c[r] = ld_off(K.cosines, (uint32_t)ti * 8u);
-        sn[r] = ld_off(K.sines, (uint32_t)ti * 8u);
+        if (PK) {  // one 16-byte load (F110_FXS_PACK)
+            const double2 t2 = ld_off(reinterpret_cast<const double2 *>(K.cs2), (uint32_t)ti * 16u);
+            c[r] = t2.x;
+            sn[r] = t2.y;
+        } else {
+            c[r] = ld_off(K.cosines, (uint32_t)ti * 8u);
+            sn[r] = ld_off(K.sines, (uint32_t)ti * 8u);
+        }
         x[r] = x00;
         y[r] = y00;
         d[r] = b < B ? d00 : 0.0;
@@ -1569,8 +1577,18 @@ __global__ void __launch_bounds__(64, NS == 2 ? 8 : 7) k_rays_fxs(RayArgs a) {  
             if (K.noise_ext || K.noise_std > 0.0) range += nz;
             const double v = ld_const(K.vel + g);
             const uint32_t boff = (uint32_t)bc * 8u;
-            if (v != 0.0 && ttc_fires(range, ld_off(K.side, boff), v * ld_off(K.beam_cos, boff), K.ttc_thresh))
-                K.ttc_hit[g] = 1;
+            if (v != 0.0) {
+                double sd, bcs;
+                if (PK) {  // one 16-byte load (F110_FXS_PACK)
+                    const double2 t2 = ld_off(reinterpret_cast<const double2 *>(K.bs2), boff * 2u);
+                    sd = t2.x;
+                    bcs = t2.y;
+                } else {
+                    sd = ld_off(K.side, boff);
+                    bcs = ld_off(K.beam_cos, boff);
+                }
+                if (ttc_fires(range, sd, v * bcs, K.ttc_thresh)) K.ttc_hit[g] = 1;
+            }
             if (K.obs && (!HANDOFF || g == e * K.A)) {
                 float *orow = K.obs + (size_t)e * K.obs_len;
                 *reinterpret_cast<float *>(reinterpret_cast<char *>(orow) + (uint32_t)b * 4u) =
@@ -3363,6 +3381,8 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
         ra.vel = a.st + (size_t)3 * EA;
         ra.beam_cos = a.beam_cos;
         ra.side = a.side;
+        ra.cs2 = a.cs2;
+        ra.bs2 = a.bs2;
         ra.ttc_thresh = a.ttc_thresh;
         ra.ttc_hit = a.ttc_hit;
         ra.obs = a.out.obs;
@@ -3530,6 +3550,9 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                             if (a.fxs_pipe && a.fx_slots != 3)  // software-pipelined slots (F110_FXS_PIPE, A/B)
                                 f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true>)
                                            : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true>);
+                            if (a.fxs_pipe && a.fx_slots != 3 && a.cs2 && a.bs2)  // packed tables (F110_FXS_PACK, A/B)
+                                f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, true, 0, true>)
+                                           : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, true, 0, true>);
                             if (!a.fxs_pipe && a.fx_slots != 3 && a.fxs_maskld == 3)  // merged slot gathers (A/B)
                                 f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false, 2, false, 3>)
                                            : reinterpret_cast<const void *>(&k_rays_fxs<true, 2, false, 3>);

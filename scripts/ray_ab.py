@@ -17,7 +17,7 @@ from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns, load_map  # no
 from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim  # noqa: E402
 
 KNOBS = ("F110_RAY_KERNEL", "F110_CHUNK_ORDER", "F110_HEAVY_T", "F110_RAY_WPB", "F110_HEAVY_DIV", "F110_EVICT",
-         "F110_EVICT_T", "F110_EVICT_K", "F110_FX_LDS", "F110_FX_LEAN", "F110_FX_ILP", "F110_FX_TABLE", "F110_FX_PAIR", "F110_FX_PAD", "F110_SIMT", "F110_FX_REFILL", "F110_FX_SLOTS", "F110_FX_POOL", "F110_FX_POOL_T", "F110_FXR_LEAN", "F110_FX_LPOOL", "F110_FXS_PIPE", "F110_FX_SPEC", "F110_FXS_MASKLD")
+         "F110_EVICT_T", "F110_EVICT_K", "F110_FX_LDS", "F110_FX_LEAN", "F110_FX_ILP", "F110_FX_TABLE", "F110_FX_PAIR", "F110_FX_PAD", "F110_SIMT", "F110_FX_REFILL", "F110_FX_SLOTS", "F110_FX_POOL", "F110_FX_POOL_T", "F110_FXR_LEAN", "F110_FX_LPOOL", "F110_FXS_PIPE", "F110_FX_SPEC", "F110_FXS_MASKLD", "F110_FXS_PACK")
 
 
 def parse_variants(spec):

@@ -349,10 +349,12 @@ def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
                                      ("1", "1", "0", "0:80"), ("1", "1", "1", "0:80"), ("3", "1", "1", "0:80"),
                                      ("1", "1", "1", "1:80"), ("1", "1", "1", "1:1"), ("1", "1", "1", "1:128"),
                                      ("1", "1", "2", "0:80"), ("3", "1", "2", "0:80"), ("1", "1", "m", "0:80"),
-                                     ("1", "1", "x", "0:80"), ("1", "1", "j", "0:80")):
+                                     ("1", "1", "x", "0:80"), ("1", "1", "j", "0:80"),
+                                     ("1", "1", "p", "0:80")):
         monkeypatch.setenv("F110_FX_REFILL", refill)
         monkeypatch.setenv("F110_FX_PAD", pad)
-        monkeypatch.setenv("F110_FXR_LEAN", "1" if lean in ("2", "m", "x", "j") else lean)
+        monkeypatch.setenv("F110_FXR_LEAN", "1" if lean in ("2", "m", "x", "j", "p") else lean)
+        monkeypatch.setenv("F110_FXS_PACK", "1" if lean == "p" else "0")  # "p": interleaved trig / beam tables
         # "m": range-checked buffer gathers, "x": ended lanes issue no gather (exec mask), "j": lock-step
         # slots sharing one gather when no lane has both rays active
         monkeypatch.setenv("F110_FXS_MASKLD", {"m": "1", "x": "2", "j": "3"}.get(lean, "0"))

@@ -300,7 +300,7 @@ def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A, nonexact
     ("2", "1", "rm", "1", "0", "0", "1"), ("3", "1", "rm", "1", "0", "0", "1"), ("3", "2", "rm", "0", "0", "0", "1"),
     ("3", "2", "rm", "1", "0", "0", "1"), ("3", "3", "rm", "1", "0", "0", "1"), ("3", "1", "tiled", "1", "0", "0", "1"),
     ("3", "2", "rm", "0", "1", "0", "1"), ("3", "2", "rm", "1", "1", "0", "1"), ("3", "2", "rm", "1", "1", "0", "0"),
-    ("3", "2", "rm", "1", "1", "0", "q"), ("3", "2", "rm", "1", "1", "0", "m"), ("3", "2", "rm", "1", "1", "0", "x"), ("3", "2", "rm", "1", "1", "0", "j"), ("3", "1", "rm", "0", "0", "0", "s2"), ("3", "1", "rm", "0", "0", "0", "s4"),
+    ("3", "2", "rm", "1", "1", "0", "q"), ("3", "2", "rm", "1", "1", "0", "m"), ("3", "2", "rm", "1", "1", "0", "x"), ("3", "2", "rm", "1", "1", "0", "j"), ("3", "2", "rm", "1", "1", "0", "p"), ("3", "1", "rm", "0", "0", "0", "s2"), ("3", "1", "rm", "0", "0", "0", "s4"),
     ("3", "2", "rm", "1", "0", "1", "1"), ("3", "2", "rm", "1", "0", "2", "1")])
 def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanners, monkeypatch, kernel, ilp, table,
                                                       pad, refill, pool, lean):
@@ -334,6 +334,7 @@ def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanne
     # k_rays_fxs's range-checked gathers (m) / no gathers for ended lanes (x)
     monkeypatch.setenv("F110_FXS_MASKLD", {"m": "1", "x": "2", "j": "3"}.get(lean, "0"))
     monkeypatch.setenv("F110_FXS_PIPE", "0" if lean == "j" else "1")  # j: lock-step slots sharing a gather
+    monkeypatch.setenv("F110_FXS_PACK", "1" if lean == "p" else "0")  # p: interleaved trig / beam tables
     monkeypatch.setenv("F110_FXR_LEAN", "0" if lean == "0" else "1")  # padded k_rays_fxr: k_rays_fxs (1), round 3's (0)
     monkeypatch.setenv("F110_FX_LPOOL", "1" if lean == "q" else "0")  # k_rays_fxq: lane-level refill (q)
     # k_rays_fx with its speculative step on every iteration (s2 / s4: 2 / 4 guessed steps per lookup round)
