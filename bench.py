@@ -43,8 +43,10 @@ def metric_name(global_envs: int, agents: int) -> str:
     who = "parallel envs" if agents == 1 else f"parallel {agents}-agent envs"
     return f"env-steps/sec at {global_envs} {who}, 1080-beam lidar; scan L2 vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-GATHER_PEAK_GLOOKUPS = 256 * 2.4  # CUs x max clock (GHz): one lane-lookup per CU per clock
-TA_CYCLES_PER_LOAD = 20.1  # texture-address cycles per wave-level 8-byte gather, measured
+# texture-address cycles per wave-level 8-byte load whatever its lanes do: a MEASURED constant
+# (rocprofv3 TA_BUSY / SQ_INSTS_VMEM_RD at 65536 cars), not a datasheet figure
+TA_CYCLES_PER_LOAD = 20.1
+N_CU, CLOCK_GHZ = 256, 2.4  # MI355X_MICROARCH.md
 
 
 def parse():
@@ -76,12 +78,9 @@ def parse():
                     help="sub-shards of the GPU's envs on concurrent dedicated-queue streams "
                          "(streams.StreamShards); 1 = one context on the current stream; 0 (default) = "
                          "auto_streams(envs per GPU)")
-    ap.add_argument("--runner", choices=["auto", "streams", "one", "fused", "rollout"], default="auto",
+    ap.add_argument("--runner", choices=["auto", "streams", "one"], default="auto",
                     help="the timed runner: streams = StreamShards sub-shards of the three-launch step; one = one "
-                         "context, three launches per step; fused = one context, one k_step1 launch per step (the "
-                         "policy-loop path); rollout = one context, k_step1 over --chunk resident steps per launch "
-                         "(open-loop random actions); auto = rollout for single-agent envs, else streams")
-    ap.add_argument("--chunk", type=int, default=50, help="steps per k_step1 launch of the rollout runner")
+                         "context, three launches per step (the policy-loop path); auto = streams")
     ap.add_argument("--workload", choices=["step", "ddpg"], default="step",
                     help="step: the env step (headline); ddpg: config 5, the batched train_ddpg loop")
     ap.add_argument("--ddpg-batch", type=int, default=4096)
@@ -292,22 +291,11 @@ def scan_check(O, scanner, runner, act, threads):
 
 
 def ray_kernel_name(sm):
-    names = {0: "k_rays", 1: "k_rays_tiled (flat)", 2: "k_rays_tiled (chunked)", 3: "k_rays_fx"}
-    if getattr(sm, "fused", False):
-        return ("k_step1 (the single-agent step in one launch: lane-0 dynamics, the car's rays in two refilled "
-                "64-beam chunk slots on the padded EDT, lane-0 post stage)")
-    if sm.ray_kernel == 3 and getattr(sm, "ray_pool", 0) > 0:
-        return f"k_rays_fxp ({sm.ray_pool} car(s) per wave, two ray slots per lane with lane-level refill)"
+    """The ray kernel launch_env_step picks for this context's unmasked steps."""
+    names = {1: "k_rays_tiled (flat)", 2: "k_rays_tiled (chunked)", 3: "k_rays_fx"}
     if sm.ray_kernel == 3 and sm.ray_refill > 0:
-        env = os.environ
-        slots = 3 if env.get("F110_FX_SLOTS") == "3" else 2
-        if env.get("F110_FXR_LEAN", "1") != "0" and env.get("F110_FX_PAD", "1") != "0":  # launch_env_step's rule
-            if env.get("F110_FX_LPOOL", "0") != "0" and sm.ray_refill == 1 and slots == 2:
-                return "k_rays_fxq (one car per wave, lane-level refill over its beams)"
-            pipe = env.get("F110_FXS_PIPE", "1") != "0" and slots == 2
-            return (f"k_rays_fxs ({sm.ray_refill} wave(s) per car, {slots} chunk slots with refill"
-                    f"{', software-pipelined' if pipe else ''}, padded EDT)")
-        return f"k_rays_fxr ({sm.ray_refill} wave(s) per car, {slots} chunk slots with refill)"
+        return (f"k_rays_fxs ({sm.ray_refill} wave(s) per car, 2 software-pipelined chunk slots with refill, "
+                f"padded EDT)")
     if sm.ray_kernel == 3 and sm.ray_lanes > 1:
         return f"k_rays_fxn ({sm.ray_lanes} rays per lane)"
     return names.get(sm.ray_kernel, str(sm.ray_kernel))
@@ -402,9 +390,7 @@ def main():
 
     kind = args.runner
     if kind == "auto":
-        kind = "streams"  # (k_step1's rollout measured slower at 65536: DESIGN §3.9)
-    if kind in ("fused", "rollout") and A != 1:
-        raise SystemExit("--runner fused / rollout: k_step1 is the single-agent step")
+        kind = "streams"
     policy_kind = "one"  # what a policy loop steps: one call per step, one context
 
     def make(n_envs, offset, kind_):
@@ -417,21 +403,13 @@ def main():
                 r.kind = "streams"
                 return r
         r = BatchSim(track, n_envs=n_envs, env_offset=offset, **kw)
-        if kind_ in ("fused", "rollout"):
-            r.set_fused(True)
-            assert r.fused, "k_step1 unavailable for this context"
-        r.kind = kind_ if kind_ != "streams" else "one"
+        r.kind = "one"
         return r
 
     def steps(r, a, k0, n, minimal):
-        """Steps k0 .. k0 + n - 1 of the action block a: one call per step, or
-        step_n launches of --chunk steps for the rollout runner."""
-        if r.kind == "rollout":
-            for c in range(k0, k0 + n, args.chunk):
-                r.step_n(a[c:min(k0 + n, c + args.chunk)], minimal_outputs=minimal)
-        else:
-            for k in range(k0, k0 + n):
-                r.step(a[k], minimal_outputs=minimal)
+        """Steps k0 .. k0 + n - 1 of the action block a, one call per step."""
+        for k in range(k0, k0 + n):
+            r.step(a[k], minimal_outputs=minimal)
 
     ramp = {"seconds": args.ramp_s, "steps": 0}
 
@@ -488,9 +466,7 @@ def main():
     total_env_steps = D.sum_over_ranks(E * K)
     RUNNER_TEXT = {
         "streams": "StreamShards: unjoined stream sub-shards of the three-launch step, actions resident in HBM",
-        "one": "one BatchSim context, three launches per step (k_agents, ray kernel, k_post)",
-        "fused": "one BatchSim context, one k_step1 launch per step (the policy-loop path)",
-        "rollout": "one BatchSim context, k_step1 over --chunk resident random-action steps per launch"}
+        "one": "one BatchSim context, three launches per step (k_agents, ray kernel, k_post)"}
     sim = runner if getattr(runner, "kind", "") == policy_kind else make(E, shard.offset, policy_kind)
     prof = runner if isinstance(runner, BatchSim) else sim  # the per-kernel pass: the headline's own kernel
 
@@ -501,7 +477,7 @@ def main():
     # halves see the same clock and thermal state (measured one after the other, the later pass ran
     # on a hotter, slower GPU: BENCH r02 / r03 kernel_le_step), so the kernel time is checked against
     # the step that contains it.  >= 100 profiled steps whatever --steps is; not part of `value`.
-    PC = 50 if prof.kind != "rollout" else max(args.chunk, 1)
+    PC = 50
     KP = max(100, min(K, 300))
     prof.reset(poses0)
     t_end = time.perf_counter() + args.ramp_s
@@ -536,16 +512,15 @@ def main():
         if prof_n < KP:
             n = min(PC, KP - prof_n, K)
             k0 = chunk_rows(n)
-            per = args.chunk if prof.kind == "rollout" else 1  # steps per launch
             t0 = time.perf_counter()
             prof.profile_begin(n)
             steps(prof, acts, k0, n, True)
             pk = prof.profile_end()  # per-launch means over this chunk
             torch.cuda.synchronize(dev)
             prof_s += time.perf_counter() - t0
-            nl = pk["steps"]
+            nl = pk["steps"]  # one launch of each kernel per step
             for key in acc:
-                acc[key] += pk[key] * nl / per  # per step
+                acc[key] += pk[key] * nl
             launches += nl
             prof_n += n
     per_kernel = {key: acc[key] / max(launches, 1) for key in acc}
@@ -562,8 +537,10 @@ def main():
     # steps after the timed passes, not inside them
     prof.set_simt(True)
     prof.reset_counters()
-    steps(prof, acts, W, min(K, 50), True)
+    simt_steps = min(K, 50)
+    steps(prof, acts, W, simt_steps, True)
     loop_lookups, lane_slots = prof.read_simt()
+    other_loads = prof.read_counter(3)  # the loop's other wave-level vector loads (tables, re-gathers)
     prof.set_simt(False)
     full_outputs = None
     if not args.no_full_outputs:
@@ -580,58 +557,48 @@ def main():
         checks = scan_check(O, scanner, runner, acts[W + K], cpu_threads())
 
     B = prof.B
-    fused_prof = prof.kind in ("fused", "rollout")
-    # the dominant kernel: k_rays, or k_step1 (the whole step) when fused.  Per
-    # ray 4 B per EDT lookup (exact uint32 k cell) + 4 B of f32 range out
-    # (SURVEY §8d); the 120 B/agent of state I/O go with the step (k_agents, or
-    # k_step1's own).
-    rays_bytes_launch = E * A * B * (4.0 * mean_look + 4.0)
-    kernel_bytes = E * algorithmic_bytes_per_env_step(B, A, mean_look) if fused_prof else rays_bytes_launch
+    # the dominant kernel: k_rays.  Per ray 4 B per EDT lookup (exact uint32 k
+    # cell) + 4 B of f32 range out; the 120 B/agent of state I/O
+    # go with the step (k_agents).
+    kernel_bytes = E * A * B * (4.0 * mean_look + 4.0)
     k_ms = per_kernel["k_rays_ms"]  # per step
     achieved = kernel_bytes / (k_ms * 1e-3) / 1e9
     pmc = load_profile("pmc_traffic", E, A)
     busy = load_profile("pmc_busy", E, A)
     traffic = pmc.get("bytes_per_launch") if pmc else None
     roof = {
-        "kernel": "k_step1" if fused_prof else "k_rays",
+        "kernel": "k_rays",
         "profiled_steps": KP,
         "profiled_launches": per_kernel["steps"],
         "bound": ("the texture-address path, per wave-level load (~20 TA cycles each whatever its lanes do; HBM is "
                   "not the limit: see hbm_traffic_frac; DESIGN.md 3.9)" if prof.ray_kernel == 3 and prof.ray_refill > 0
-                  and not fused_prof else
-                  "VALU issue of the sphere-trace loop (valu_busy; HBM is not the limit: see hbm_traffic_frac and "
-                  "l2_hit_rate; DESIGN.md 3.4)" if prof.ray_kernel == 3 and (prof.ray_refill > 0 or fused_prof) else
-                  "latency of the dependent EDT gather chain (HBM is not the limit: see hbm_traffic_frac; capping "
+                  else "latency of the dependent EDT gather chain (HBM is not the limit: see hbm_traffic_frac; capping "
                   "occupancy at 6/4/2 waves per SIMD costs 1.31x/1.62x/2.9x, DESIGN.md 3.2)"),
         "ray_kernel": ray_kernel_name(prof),
         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
         "traffic": traffic, "kernel_ms": k_ms, "algorithmic_bytes_per_launch": kernel_bytes,
         "kernel_ms_note": "per step (a profiled launch's time / its steps)",
         "mean_lookups_per_ray": mean_look,
-        "step_kernels_ms": {"k_agents": per_kernel["k_agents_ms"], "k_rays" if not fused_prof else "k_step1": k_ms,
-                            "k_post": per_kernel["k_post_ms"]},
+        "step_kernels_ms": {"k_agents": per_kernel["k_agents_ms"], "k_rays": k_ms, "k_post": per_kernel["k_post_ms"]},
         "step_algorithmic_bytes_per_env": algorithmic_bytes_per_env_step(B, A, mean_look),
-        # lookups made in the loop / (loop trips x 64 lanes x rays per lane), from the kernel's own counters
+        # lookups made in the loop / (64 x the wave-level gathers the loop issued, an ended or closed
+        # slot's zero-cell gathers included), from the kernel's own counters
         "simt_efficiency": loop_lookups / lane_slots if lane_slots else None,
     }
-    # the gather roofline, per lane-lookup: one per CU per clock, 256 CUs x 2.4 GHz = 614 G
-    # lookups/s (it holds at the kernel's SIMT); and per instruction, the form the counters show: the
-    # texture-address unit spends ~20.1 cycles on every wave-level 8-byte load whatever its lanes do
-    # (profiles/r03_ab/pmc_ended_lanes/), so the loop's slot gathers (lane slots / 64) need at least
-    # gathers x 20.1 / 256 CUs / 2.4 GHz (the refills' table loads come on top)
-    if not fused_prof:
-        look_launch = E * A * B * (mean_look - 1.0)  # the kernel's own lookups (the first is k_agents')
-        roof["gather_roofline"] = {
-            "bound": "vector-memory address path: one lane-lookup per CU per clock",
-            "achieved_glookups_s": look_launch / (k_ms * 1e-3) / 1e9, "peak_glookups_s": GATHER_PEAK_GLOOKUPS,
-            "frac": look_launch / (k_ms * 1e-3) / 1e9 / GATHER_PEAK_GLOOKUPS, "lookups_per_launch": look_launch}
-        if lane_slots:
-            gathers = lane_slots / 64.0 / max(1, min(K, 50))  # per launch (the counters ran min(K, 50) steps)
-            min_ms = gathers * TA_CYCLES_PER_LOAD / 256 / 2.4e9 * 1e3
-            roof["gather_roofline"]["slot_gathers_per_launch"] = gathers
-            roof["gather_roofline"]["ta_cycles_per_load"] = TA_CYCLES_PER_LOAD
-            roof["gather_roofline"]["slot_gather_min_ms"] = min_ms
-            roof["gather_roofline"]["slot_gather_frac"] = min_ms / k_ms
+    # the gather bound, per instruction, the form the counters show: the texture-address
+    # unit spends ~20.1 cycles (measured) on every wave-level load whatever its lanes do, so the
+    # kernel's vector loads need at least loads x 20.1 / 256 CUs / 2.4 GHz.  Loads per launch from the
+    # kernel's own counters: the loop's gathers (lane slots / 64) + its table loads and guard-band
+    # re-gathers (counter 3); compare with SQ_INSTS_VMEM_RD in profiles/
+    look_launch = E * A * B * (mean_look - 1.0)  # the kernel's own lookups (the first is k_agents')
+    roof["gather_roofline"] = {"bound": "texture-address cycles per wave-level vector load (measured constant)",
+                               "lookups_per_launch": look_launch, "ta_cycles_per_load": TA_CYCLES_PER_LOAD}
+    if lane_slots:
+        gathers = lane_slots / 64.0 / max(1, simt_steps)  # per launch
+        loads = gathers + other_loads / max(1, simt_steps)
+        min_ms = loads * TA_CYCLES_PER_LOAD / N_CU / (CLOCK_GHZ * 1e9) * 1e3
+        roof["gather_roofline"].update({"slot_gathers_per_launch": gathers, "vmem_loads_per_launch": loads,
+                                        "ta_min_ms": min_ms, "ta_frac": min_ms / k_ms})
     # consistency: the kernel runs inside the step it is timed in (the one-context runner's own wall time
     # per step, measured in the chunks interleaved with the profiled ones)
     roof["kernel_le_step"] = {"ok": bool(k_ms <= plain_step_ms), "kernel_ms": k_ms, "runner_step_ms": plain_step_ms,
@@ -674,7 +641,6 @@ def main():
             "runner": RUNNER_TEXT[runner.kind] + "; minimal outputs (obs, collisions, terminated): no f32 "
                       "info['scans'] copy, lap_times/counts, sim_time, was_reset",
             "runner_kind": runner.kind,
-            "chunk": args.chunk if runner.kind == "rollout" else 1,
         },
         "trajectory_digest": traj,
         "single_stream": single,

@@ -2,8 +2,9 @@
 //
 // Cold path (once per map): exact EDT (Felzenszwalb-Huttenlocher lower
 // envelopes, integer arithmetic), the reference's trig tables, device buffers.
-// Hot path: f110_step / f110_reset fill a StepArgs and enqueue ONE kernel
-// (k_env_step) on the caller's stream; no allocation, no synchronisation.
+// Hot path: f110_step / f110_reset fill a StepArgs and enqueue three kernels
+// (k_agents, a ray kernel, a post kernel) on the caller's stream; no
+// allocation, no synchronisation.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -54,12 +55,12 @@ struct f110_ctx {
     // device buffers
     double *dt_tiled = nullptr;
     int32_t wt = 0, tiles_h = 0;
-    int ray_kernel = 3;  // F110_RAY_KERNEL: 0 row-major k_rays, 1 tiled flat order, 2 tiled chunked,
-                         // 3 chunked k_rays_fx (default; falls back to 2 where its preconditions fail)
+    int ray_kernel = 3;  // F110_RAY_KERNEL: 1 tiled flat order, 2 tiled chunked, 3 the fixed-point
+                         // kernels (default; falls back to 2 where their preconditions fail)
     uint8_t chunk_order[kMaxChunks] = {};
     double *dt = nullptr, *sines = nullptr, *cosines = nullptr, *angles = nullptr, *beam_cos = nullptr,
            *side = nullptr, *spawn = nullptr;
-    double *cs2 = nullptr, *bs2 = nullptr;  // interleaved (cos, sin)[theta_dis], (side, beam_cos)[B] (F110_FXS_PACK)
+    double *cs2 = nullptr, *bs2 = nullptr;  // interleaved (cos, sin)[theta_dis], (side, beam_cos)[B] (k_rays_fxs)
     double *start_rot = nullptr;
     double *st = nullptr, *sb = nullptr, *start = nullptr, *sim_time = nullptr, *ray0 = nullptr, *scan = nullptr;
     BeamRun *runs = nullptr;
@@ -83,50 +84,23 @@ struct f110_ctx {
     // heavy-first ray dispatch (chunked kernel)
     uint8_t *wcost = nullptr;
     uint32_t *heavy_list = nullptr, *heavy_mask = nullptr, *heavy_count = nullptr;
-    int32_t heavy_cap = 0, heavy_T = 16, nch = 0;  // F110_HEAVY_T (with one-wave blocks and a 1/6 list: 16 best)
+    int32_t heavy_cap = 0, heavy_T = 16, nch = 0;  // with one-wave blocks and a 1/6 list: 16 best
     uint64_t launch_n = 0;
-    int ray_wpb = 1;  // F110_RAY_WPB: 1 (one-wave blocks, default) or 4
-    // k_rays_fx straggler hand-off (opt-in, F110_EVICT=1; F110_EVICT_T / _K tune it).  Measured
-    // (DESIGN §3.2): the hand-off cuts the main pass's wave-iterations by a third but not its
-    // L1 accesses, which set its time (-4.5 %), and the tail's longest residual ray chains
-    // (~0.27 ms at 65536 envs) run after it: off by default
-    bool evict = false;
-    double *ev = nullptr;
-    int32_t *ev_gb = nullptr;
-    uint32_t *ev_ctr = nullptr;
-    uint32_t ev_cap = 0, ev_capp = 0;
-    int32_t ev_P = 1;
-    int32_t ev_T = 16, ev_K = 8;
+    int ray_wpb = 1;  // one-wave blocks (4-car blocks measured slower)
     int64_t wtrace_n = 0;
     bool wtrace_armed = false;
     // the fixed-point ray kernel's row-major EDT (see StepArgs::rm)
     double *rm = nullptr;
     int32_t rm_w = 0;
     uint32_t rm_oob = 0, rm_zero = 0;
-    const double *rmp = nullptr;  // k_rays_fxn's padded table (shared, see MapTables)
-    int32_t rmp_w = 0, rmp_P = 0;
+    const double *rmp = nullptr;  // the padded table of k_rays_fxn / k_rays_fxs (shared, see MapTables)
+    int32_t rmp_w = 0, rmp_P = 0, rmp_h = 0;
     uint32_t rmp_zero = 0;
-    bool fx_pad = false;    // k_rays_fxn / k_rays_fxr on the padded table (default from 32768 cars; F110_FX_PAD)
-    int32_t fx_slots = 2;    // F110_FX_SLOTS (A/B): chunk slots per k_rays_fxr wave
-    int32_t fxr_lean = 1;    // k_rays_fxs in place of k_rays_fxr<.., PAD, 2> (F110_FXR_LEAN=0: the round-3 kernel)
-    int32_t fx_lpool = 0;    // k_rays_fxq in place of k_rays_fxs (F110_FX_LPOOL)
-    int32_t fx_spec_k = 1, fx_spec_t = 0;  // F110_FX_SPEC=K:T (A/B): k_rays_fx speculative steps in its tail
-    int32_t fxs_pack = 1;  // k_rays_fxs: one 16-byte load for (cos, sin) and for (side, beam_cos) (F110_FXS_PACK=0: two, A/B)
-    int32_t fxs_maskld = 0;  // k_rays_fxs: ended lanes issue no gather (F110_FXS_MASKLD, A/B)
-    int32_t fxs_pipe = 1;    // k_rays_fxs with software-pipelined slots (F110_FXS_PIPE=0: in lock-step, A/B)
-    int32_t fx_refill = 0;   // waves per car of k_rays_fxr (0 = k_rays_fxn; F110_FX_REFILL overrides)
-    int32_t fx_pool = 0;     // cars per k_rays_fxp wave (lane-level refill; 0 = off; F110_FX_POOL)
-    int32_t pool_T = 80;     // k_rays_fxp's refill threshold in ended slots (F110_FX_POOL_T)
-    bool fused = false;      // single-agent steps as one k_step1 launch (f110_set_fused / F110_FUSED)
-    int32_t fused_cpw = 8;   // cars per k_step1 workgroup (F110_FUSED_CPW, 1..8)
-    int32_t multi_block = 128;  // k_post_multi threads per env (F110_MULTI_BLOCK: 64 or 128)
-    uint8_t *pcost = nullptr;  // [EA][nch] k_rays_fxp's per-chunk costs (queue order of the next launch)
-    bool count_slots = false;  // f110_set_simt / F110_SIMT: lane-slot counter of the fixed-point loops (f110_read_simt)
-    int fx_ilp = 1;         // rays per lane (F110_FX_ILP; default by car count)
-    bool fx_tiled = false;  // F110_FX_TABLE=tiled: A/B of the 4x4-tiled EDT
-    uint32_t fx_lds = 0;  // F110_FX_LDS: diagnostic occupancy cap of the ray kernel
-    bool fx_nolean = false;
-  // F110_FX_LEAN=0: A/B of the round-2 ray loop
+    bool fx_pad = false;    // the padded table is wanted (from 32768 cars or with refill; F110_FX_PAD=0: never)
+    int32_t fx_refill = 0;   // waves per car of k_rays_fxs (0 = k_rays_fxn; f110_set_ray_refill)
+    int32_t fxs_variant = 0;  // f110_set_ray_variant (A/B)
+    bool count_slots = false;  // f110_set_simt: lane-slot counter of the fixed-point loops (f110_read_simt)
+    int fx_ilp = 1;         // rays per lane (f110_set_ray_lanes; default by car count)
 
     hipEvent_t *next_prof_events() {
         if (prof_n >= prof_max) return nullptr;
@@ -412,7 +386,7 @@ struct MapTables {
     uint64_t res_bits = 0;
     std::vector<uint32_t> k;  // the EDT the tables were built from (exact match, not a hash)
     double *dt = nullptr, *dt_tiled = nullptr, *rm = nullptr, *rmp = nullptr;
-    int32_t rm_w = 0, rmp_w = 0, rmp_P = 0;
+    int32_t rm_w = 0, rmp_w = 0, rmp_P = 0, rmp_h = 0;
     uint32_t rm_oob = 0, rm_zero = 0, rmp_zero = 0;
     int refs = 0;
     bool shared = true;
@@ -453,7 +427,7 @@ static hipError_t upload(T **p, const std::vector<T> &h) {
     return hipSuccess;
 }
 
-// k_rays_fxn / k_rays_fxr's padded table (PAD, see kFxpBase): cell (r, c) at
+// k_rays_fxn / k_rays_fxs's padded table (PAD, see kFxpBase): cell (r, c) at
 // row r + P, column c + P; every other cell holds dt[-1,-1] (the reference's
 // off-map read), and a 0.0 after the last row is the zero cell.  Built only
 // where its byte offsets stay 32-bit and a row stride stays a 24-bit
@@ -472,6 +446,7 @@ static hipError_t build_padded_table(MapTables *t, int32_t pad, const std::vecto
     const hipError_t e = upload(&t->rmp, rmp);
     if (e == hipSuccess) {
         t->rmp_w = (int32_t)Wp;
+        t->rmp_h = (int32_t)Hp;
         t->rmp_P = (int32_t)P;
         t->rmp_zero = (uint32_t)(Wp * Hp * 8);
     }
@@ -557,6 +532,20 @@ static hipError_t acquire_map_tables(int device, const uint32_t *edt_k, int32_t 
 
 static int ensure_padded_table(f110_ctx *ctx);
 
+// the map entry's padded table (if it was built) for the context
+static void adopt_padded_table(f110_ctx *c) {
+    if (!c->maps || !c->maps->rmp) return;
+    c->rmp = c->maps->rmp;
+    c->rmp_w = c->maps->rmp_w;
+    c->rmp_h = c->maps->rmp_h;
+    c->rmp_P = c->maps->rmp_P;
+    c->rmp_zero = c->maps->rmp_zero;
+}
+
+// k_rays_fxs's offsets (kFxsBase) need q + P below 2^20 for every lookup: the padded
+// table's rows and columns below 2^20 (else the refill runs k_rays_fxn instead)
+static bool fxs_ok(const f110_ctx *c) { return c->rmp && c->rmp_w < (1 << 20) && c->rmp_h < (1 << 20); }
+
 extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cfg, const f110_params *params,
                            const uint32_t *edt_k, int32_t H, int32_t W, double resolution, const double origin[3],
                            const double *spawn_poses, int32_t n_spawn) {
@@ -594,35 +583,20 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     c->inc = (double)C.theta_dis * (C.fov / (double)(C.n_beams - 1)) / (2. * kPi);  // laser_models.py:367-368
     c->beam_incr = C.fov / (double)(C.n_beams - 1);
     c->n_spawn = n_spawn;
+    // F110_RAY_KERNEL (A/B): 1 k_rays_tiled in flat ray order, 2 chunked, 3 the fixed-point kernels
     if (const char *v = std::getenv("F110_RAY_KERNEL")) {
         const int k = std::atoi(v);
-        c->ray_kernel = k == 0 ? 0 : (k >= 2 && k <= 3 ? k : 1);
+        c->ray_kernel = k >= 2 && k <= 3 ? k : 1;
     }
     {
         // chunked dispatch order: descending beam chunks (the scan's left edge
-        // to its right edge), or F110_CHUNK_ORDER="16,15,...".  Measured
-        // against the flat order and five other chunk orders
-        // (scripts/chunk_ab.py): fastest at 4096 and 8192 envs,
-        // 1 and 2 agents.
+        // to its right edge).  Measured against the flat order and five other
+        // chunk orders (scripts/chunk_ab.py): fastest at 4096
+        // and 8192 envs, 1 and 2 agents.
         const int nch = (C.n_beams + 63) / 64;
         if (nch > kMaxChunks && c->ray_kernel >= 2) c->ray_kernel = 1;
         c->nch = nch;
         for (int i = 0; i < nch && i < kMaxChunks; ++i) c->chunk_order[i] = (uint8_t)(nch - 1 - i);
-        if (const char *v = std::getenv("F110_CHUNK_ORDER")) {
-            std::vector<int> seen(nch, 0), ord;
-            for (const char *q = v; *q;) {
-                char *end = nullptr;
-                long k = std::strtol(q, &end, 10);
-                if (end == q) break;
-                if (k >= 0 && k < nch && !seen[k]) {
-                    seen[k] = 1;
-                    ord.push_back((int)k);
-                }
-                q = *end ? end + 1 : end;
-            }
-            if ((int)ord.size() == nch)
-                for (int i = 0; i < nch; ++i) c->chunk_order[i] = (uint8_t)ord[i];
-        }
     }
     const size_t EA = (size_t)C.n_envs * C.n_agents;
 
@@ -670,38 +644,18 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     ALLOC(c->ctr, (size_t)kCtrSlots * kCtrStride);
     ALLOC(c->pa, (size_t)C.n_agents);
     if (spawn_poses && n_spawn > 0) ALLOC(c->spawn, (size_t)n_spawn * C.n_agents * 3);
-    if (const char *v = std::getenv("F110_RAY_WPB")) c->ray_wpb = std::atoi(v) == 1 ? 1 : 4;
-    if (const char *v = std::getenv("F110_HEAVY_T")) c->heavy_T = std::atoi(v);  // 0: no heavy-first dispatch
     if (c->ray_kernel == 3 && !fx_eligible(H, W, resolution, origin, C.eps, edt_k, c->ray_wpb)) c->ray_kernel = 2;
-    if (const char *v = std::getenv("F110_EVICT")) c->evict = std::atoi(v) != 0;
-    if (const char *v = std::getenv("F110_EVICT_T")) c->ev_T = std::max(0, std::min(63, std::atoi(v)));
-    if (const char *v = std::getenv("F110_EVICT_K")) c->ev_K = std::max(0, std::atoi(v));
-    if (c->ray_kernel == 3 && c->evict) {
-        // records for 1/8 of the rays (measured: ~5 % are handed off at T = 16, K = 8);
-        // a wave whose hand-off would overflow keeps tracing its rays itself
-        const size_t rays = EA * (size_t)C.n_beams;
-        const size_t cap = std::min<size_t>(std::max<size_t>(4096, rays / 8), (size_t)1 << 30);
-        c->ev_P = (int32_t)std::max<size_t>(1, std::min<size_t>(kEvMaxParts, cap / 4096));
-        c->ev_capp = (uint32_t)(cap / (size_t)c->ev_P);
-        c->ev_cap = c->ev_capp * (uint32_t)c->ev_P;
-        ALLOC(c->ev, 7 * (size_t)c->ev_cap);
-        ALLOC(c->ev_gb, 2 * (size_t)c->ev_cap);
-        ALLOC(c->ev_ctr, (size_t)kEvMaxParts * kEvStride);
-        // the hand-off absorbs the long waves' tails: heavy-first is off unless asked for
-        if (!std::getenv("F110_HEAVY_T")) c->heavy_T = 0;
-    }
     if (c->ray_kernel == 3) {
         // the row-major table's byte offsets (one padding column / row, a zero cell) stay 32-bit
         const uint64_t rm_bytes = ((uint64_t)W + 16) / 16 * 16 * ((uint64_t)H + 1) * 8 + 128;
-        if (const char *v = std::getenv("F110_FX_TABLE")) c->fx_tiled = std::string(v) == "tiled";
-        if (rm_bytes >= (1ull << 32)) c->fx_tiled = true;
-        // rays per lane: N > 1 keeps N gathers in flight per lane where the grid
-        // is deep enough (measured); the evicting kernel is single-ray
-        // (k_rays ms, 1 vs 2 rays per lane: 4096 cars 0.107 / 0.124, 8192 0.165 / 0.175,
-        // 16384 0.304 / 0.284, 32768 0.637 / 0.547, 65536 1.190 / 1.054; profiles/r02_ray_ab/)
+        if (rm_bytes >= (1ull << 32)) c->ray_kernel = 2;
+    }
+    if (c->ray_kernel == 3) {
+        // rays per lane: 2 keeps 2 gathers in flight per lane where the grid is deep enough
+        // (measured; k_rays ms, 1 vs 2 rays per lane: 4096 cars 0.107 / 0.124,
+        // 8192 0.165 / 0.175, 16384 0.304 / 0.284, 32768 0.637 / 0.547, 65536 1.190 / 1.054;
+        // profiles/r02_ray_ab/)
         c->fx_ilp = EA >= 12288 ? 2 : 1;
-        if (const char *v = std::getenv("F110_FX_ILP")) c->fx_ilp = std::max(1, std::min(4, std::atoi(v)));
-        if (c->evict || c->fx_tiled) c->fx_ilp = 1;
     }
     // heavy-first pays where one ray grid is a few rounds of waves deep (16384 cars: 0.281 vs 0.287 ms)
     // and costs where it is deep (65536 cars: 1.288 vs 1.251 ms without; profiles/r02_ray_ab/ab_heavy.json)
@@ -709,12 +663,11 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     // 0.124 vs 0.109 ms without; profiles/r03_ab/small_shards.json); off from 32768 cars, where the
     // refill kernel (which takes no heavy-first list) runs: at exactly 32768 it used to stay on and
     // turn the refill off (one context 57.0 M env-steps/s, profiles/r03_ab/e32768_*.json)
-    if (!std::getenv("F110_HEAVY_T") && (EA >= 32768 || EA <= 8192)) c->heavy_T = 0;
+    if (EA >= 32768 || EA <= 8192) c->heavy_T = 0;
     if (c->ray_kernel >= 2 && c->heavy_T > 0) {
-        // up to 1/8 of the waves, in blocks of 4 (measured: ~7% of the waves
-        // have a ray longer than 40 lookups and carry ~46% of the wave-iterations)
-        size_t div = 6;  // F110_HEAVY_DIV: list capacity = 1/div of the waves
-        if (const char *v = std::getenv("F110_HEAVY_DIV")) div = (size_t)std::max(1, std::atoi(v));
+        // up to 1/6 of the waves (measured: ~7% of the waves have a ray longer
+        // than 40 lookups and carry ~46% of the wave-iterations)
+        const size_t div = 6;  // list capacity = 1/div of the waves
         c->heavy_cap = (int32_t)std::max<size_t>(64, (EA * (size_t)c->nch / div + 3) / 4 * 4);
         ALLOC(c->wcost, EA * (size_t)c->nch);
         ALLOC(c->heavy_list, 2 * (size_t)c->heavy_cap);
@@ -750,75 +703,36 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (e == hipSuccess && c->spawn)
         e = hipMemcpy(c->spawn, spawn_poses, (size_t)n_spawn * C.n_agents * 3 * sizeof(double),
                       hipMemcpyHostToDevice);
-    if (const char *v = std::getenv("F110_FX_LEAN")) c->fx_nolean = std::atoi(v) == 0;
-    // PAD: k_rays_fxn's clamp-free loop on a table padded by the max range (+ 8 cells of margin)
-    // on where k_rays_fxr runs (from 32768 cars): there the loop is issue-bound (VALU busy 88 %) and
-    // the clamp-free offsets (46 -> 36 VALU per two-ray iteration) measured 0.999 -> 0.956 ms at 65536;
-    // k_rays_fxn, latency-bound, did not gain from them (1.029 vs 1.026 ms), DESIGN §3.3
-    const bool fx_ok = c->ray_kernel == 3 && !c->fx_tiled && !c->evict;
+    // PAD: the clamp-free loop on a table padded by the max range (+ 8 cells of margin) where
+    // k_rays_fxs runs (from 32768 cars): there the loop is issue-bound (VALU busy 88 %) and the
+    // clamp-free offsets (46 -> 36 VALU per two-ray iteration) measured 0.999 -> 0.956 ms at 65536;
+    // k_rays_fxn, latency-bound, did not gain from them (1.029 vs 1.026 ms), DESIGN §3.3.
+    // F110_FX_PAD (A/B): 1 builds the table at any size (k_rays_fxn then runs on it), 0 never.
+    const bool fx_ok = c->ray_kernel == 3;
     c->fx_pad = fx_ok && EA >= 32768;
     if (const char *v = std::getenv("F110_FX_PAD")) c->fx_pad = fx_ok && std::atoi(v) != 0;
-    if (const char *v = std::getenv("F110_SIMT")) c->count_slots = std::atoi(v) != 0;
-    // k_rays_fxr (one wave per car, two chunk slots with refill) where the grid is deep:
+    // k_rays_fxs (one wave per car, two chunk slots with refill) where the grid is deep:
     // 65536 envs as 2 x 32768 67.1 vs 63.0 M env-steps/s; at 16384 cars its long waves
-    // leave a tail (0.324 vs 0.289 ms); it runs only without heavy-first and masks (DESIGN §3.3)
+    // leave a tail (0.324 vs 0.289 ms); it runs only without heavy-first and masks (DESIGN §3.4)
     c->fx_refill = EA >= 32768 ? 1 : 0;
-    if (const char *v = std::getenv("F110_FX_REFILL")) c->fx_refill = std::max(0, std::min(16, std::atoi(v)));
-    if (const char *v = std::getenv("F110_FX_SLOTS")) c->fx_slots = std::atoi(v) == 3 ? 3 : 2;
-    if (const char *v = std::getenv("F110_FXR_LEAN")) c->fxr_lean = std::atoi(v) != 0;
-    if (const char *v = std::getenv("F110_FX_LPOOL")) c->fx_lpool = std::atoi(v) != 0;
-    if (const char *v = std::getenv("F110_FXS_PIPE")) c->fxs_pipe = std::atoi(v) != 0;
-    if (const char *v = std::getenv("F110_FXS_PACK")) c->fxs_pack = std::atoi(v) != 0;
-    if (const char *v = std::getenv("F110_FXS_MASKLD")) c->fxs_maskld = std::max(0, std::min(3, std::atoi(v)));
-    if (const char *v = std::getenv("F110_FX_SPEC")) {
-        int k = 1, t = 0;
-        if (std::sscanf(v, "%d:%d", &k, &t) >= 1) {
-            c->fx_spec_k = (k == 2 || k == 4) ? k : 1;
-            c->fx_spec_t = std::max(0, std::min(64, t ? t : 64));
-        }
-    }
-    if (const char *v = std::getenv("F110_FX_POOL")) c->fx_pool = std::max(0, std::min(2, std::atoi(v)));
-    if (const char *v = std::getenv("F110_FUSED")) c->fused = std::atoi(v) != 0;
-    if (const char *v = std::getenv("F110_FUSED_CPW")) c->fused_cpw = std::max(1, std::min(8, std::atoi(v)));
-    if (const char *v = std::getenv("F110_MULTI_BLOCK")) c->multi_block = std::atoi(v) == 64 ? 64 : 128;
-    if (const char *v = std::getenv("F110_FX_POOL_T")) c->pool_T = std::max(1, std::min(128, std::atoi(v)));
-    if (fx_ok) {
-        hipError_t ep = c->alloc(&c->pcost, EA * (size_t)c->nch);
-        if (ep == hipSuccess) ep = hipMemset(c->pcost, 0, EA * (size_t)c->nch);
-        if (ep != hipSuccess) return cleanup(F110_E_ALLOC, std::string("hipMalloc pcost: ") + hipGetErrorString(ep));
-    }
     const double pad_q = std::ceil(C.max_range / resolution) + 8.0;
     const int32_t fx_pad_cells = pad_q > 0.0 && pad_q < 65536.0 ? (int32_t)pad_q : 0;  // else no padded table
-    if (const char *v = std::getenv("F110_FX_LDS")) c->fx_lds = (uint32_t)std::max(0, std::min(65536, std::atoi(v)));
     if (e == hipSuccess)
-        e = acquire_map_tables(device, edt_k, H, W, resolution, c->wt, c->tiles_h, c->ray_kernel == 3 && !c->fx_tiled,
+        e = acquire_map_tables(device, edt_k, H, W, resolution, c->wt, c->tiles_h, fx_ok,
                                c->fx_pad ? fx_pad_cells : 0, &c->maps);
     if (e == hipSuccess) {
         c->dt = c->maps->dt;
         c->dt_tiled = c->maps->dt_tiled;
-        if (c->ray_kernel == 3 && !c->fx_tiled) {
+        if (fx_ok) {
             c->rm = c->maps->rm;
             c->rm_w = c->maps->rm_w;
             c->rm_oob = c->maps->rm_oob;
             c->rm_zero = c->maps->rm_zero;
-            if (c->fx_pad && c->maps->rmp) {
-                c->rmp = c->maps->rmp;
-                c->rmp_w = c->maps->rmp_w;
-                c->rmp_P = c->maps->rmp_P;
-                c->rmp_zero = c->maps->rmp_zero;
-            }
+            if (c->fx_pad) adopt_padded_table(c);
         }
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) return cleanup(F110_E_HIP, std::string("f110_create upload: ") + hipGetErrorString(e));
-    if (c->fused && fx_ok) {  // F110_FUSED: k_step1 on the padded table, no heavy-first list
-        c->heavy_off = true;
-        if (ensure_padded_table(c) != F110_OK) return cleanup(F110_E_HIP, "f110_create: padded table");
-    }
-    size_t lds = step_lds_bytes(C.n_agents, C.n_beams);
-    if (lds > 160 * 1024) return cleanup(F110_E_INVALID, "f110_create: n_agents*n_beams too large for LDS");
-    e = prepare_env_step(lds);
-    if (e != hipSuccess) return cleanup(F110_E_HIP, std::string("f110_create: LDS attribute: ") + hipGetErrorString(e));
     *out = c;
     return F110_OK;
 }
@@ -847,8 +761,8 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.angles = c->angles;
     a.beam_cos = c->beam_cos;
     a.side = c->side;
-    a.cs2 = c->fxs_pack ? c->cs2 : nullptr;
-    a.bs2 = c->fxs_pack ? c->bs2 : nullptr;
+    a.cs2 = c->cs2;
+    a.bs2 = c->bs2;
     a.p = c->p;
     a.E = c->cfg.n_envs;
     a.A = c->cfg.n_agents;
@@ -905,16 +819,6 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
         a.heavy_T = c->heavy_T;
         a.heavy_on = c->heavy_off ? 0 : 1;
     }
-    if (c->ev) {
-        a.ev = c->ev;
-        a.ev_gb = c->ev_gb;
-        a.ev_ctr = c->ev_ctr;
-        a.ev_cap = c->ev_cap;
-        a.ev_capp = c->ev_capp;
-        a.ev_P = c->ev_P;
-        a.ev_T = c->ev_T;
-        a.ev_K = c->ev_K;
-    }
     a.reset_f32 = c->reset_f32 ? 1 : 0;
     a.rm = c->rm;
     a.rm_w = c->rm_w;
@@ -925,23 +829,10 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.rmp_P = c->rmp_P;
     a.rmp_zero = c->rmp_zero;
     a.fx_pad = c->rmp ? 1 : 0;
+    a.fxs_ok = fxs_ok(c) ? 1 : 0;
     a.count_slots = c->count_slots ? 1 : 0;
     a.fx_refill = c->fx_refill;
-    a.fx_pool = c->fx_pool;
-    a.fused_cpw = c->fused_cpw;
-    a.multi_block = c->multi_block;
-    a.pool_T = c->pool_T;
-    a.pcost = c->pcost;
-    a.fx_slots = c->fx_slots;
-    a.fxr_lean = c->fxr_lean;
-    a.fx_lpool = c->fx_lpool;
-    a.fxs_pipe = c->fxs_pipe;
-    a.fxs_maskld = c->fxs_maskld;
-    a.fx_spec_k = c->fx_spec_k;
-    a.fx_spec_t = c->fx_spec_t;
-    a.fx_tiled = c->fx_tiled ? 1 : 0;
-    a.fx_lds = c->fx_lds;
-    a.fx_nolean = c->fx_nolean ? 1 : 0;
+    a.fxs_variant = c->fxs_variant;
     a.fx_ilp = c->fx_ilp;
     a.gate_wait = c->gate_wait;
     a.gate_record = c->gate_record;
@@ -966,13 +857,6 @@ extern "C" int f110_reset(f110_ctx *ctx, const double *poses, const uint8_t *env
     return F110_OK;
 }
 
-// k_step1 (the single-agent step in one launch) runs where the context traces
-// with the fixed-point kernels on the padded table, without heavy-first lists
-static bool fused_ok(const f110_ctx *c) {
-    return c->fused && c->cfg.n_agents == 1 && c->ray_kernel == 3 && !c->evict && !c->fx_tiled && c->fx_pad &&
-           c->rmp && (c->heavy_off || !c->wcost) && (c->cfg.n_beams + 63) / 64 <= kMaxChunks;
-}
-
 static int step_n(f110_ctx *ctx, const void *actions, int32_t actions_dtype, int32_t n, int64_t step_stride,
                   const f110_outputs *out, void *stream, const char *who) {
     if (!ctx || !actions) return fail(F110_E_INVALID, std::string(who) + ": null argument");
@@ -989,14 +873,6 @@ static int step_n(f110_ctx *ctx, const void *actions, int32_t actions_dtype, int
     if (step_stride != 0 && step_stride < packed)
         return fail(F110_E_INVALID, std::string(who) + ": step_stride < n_envs * n_agents * 2");
     const int64_t stride = step_stride ? step_stride : packed;
-    if (fused_ok(ctx)) {
-        if (actions_dtype == F110_F64)
-            a.actions_f64 = static_cast<const double *>(actions);
-        else
-            a.actions = static_cast<const float *>(actions);
-        HIP_TRY(launch_step1(a, n, stride, (hipStream_t)stream, ctx->next_prof_events()));
-        return F110_OK;
-    }
     for (int32_t t = 0; t < n; ++t) {
         if (actions_dtype == F110_F64)
             a.actions_f64 = static_cast<const double *>(actions) + (size_t)t * stride;
@@ -1016,22 +892,6 @@ extern "C" int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dty
 extern "C" int f110_step_n(f110_ctx *ctx, const void *actions, int32_t actions_dtype, int32_t n_steps,
                            int64_t step_stride, const f110_outputs *out, void *stream) {
     return step_n(ctx, actions, actions_dtype, n_steps, step_stride, out, stream, "f110_step_n");
-}
-
-extern "C" int f110_set_fused(f110_ctx *ctx, int32_t on) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_set_fused: null context");
-    if (use_device(ctx) != F110_OK) return F110_E_HIP;
-    ctx->fused = on != 0;
-    if (ctx->fused && ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled) {
-        ctx->heavy_off = true;  // k_step1 keeps no heavy-first list
-        return ensure_padded_table(ctx);
-    }
-    return F110_OK;
-}
-
-extern "C" int f110_fused(const f110_ctx *ctx) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_fused: null context");
-    return fused_ok(ctx) ? 1 : 0;
 }
 
 extern "C" int f110_set_reset_dtype(f110_ctx *ctx, int32_t dtype) {
@@ -1059,16 +919,15 @@ extern "C" int f110_ray_lanes(const f110_ctx *ctx) {
     return ctx->ray_kernel == 3 ? ctx->fx_ilp : 1;
 }
 
-static int effective_pool(const f110_ctx *ctx);
-
+// k_rays_fxs's waves per car for unmasked steps, as launch_env_step decides it
 extern "C" int f110_ray_refill(const f110_ctx *ctx) {
     if (!ctx) return fail(F110_E_INVALID, "f110_ray_refill: null context");
-    const bool fx = ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled && ctx->fx_ilp == 2;
+    const bool fx = ctx->ray_kernel == 3 && ctx->fx_ilp == 2 && fxs_ok(ctx);
     const int waves = std::min<int>(ctx->fx_refill, (ctx->cfg.n_beams + 63) / 64);  // as the launch clamps it
-    return fx && waves > 0 && (ctx->heavy_off || !ctx->wcost) && !effective_pool(ctx) ? waves : 0;
+    return fx && waves > 0 && (ctx->heavy_off || !ctx->wcost) ? waves : 0;
 }
 
-// The padded EDT of k_rays_fxr / k_rays_fxp (built on first use, shared with
+// The padded EDT of k_rays_fxn / k_rays_fxs (built on first use, shared with
 // the map entry): F110_FX_PAD=0 keeps the clamped table (A/B runs).
 static int ensure_padded_table(f110_ctx *ctx) {
     bool pad = true;
@@ -1088,51 +947,23 @@ static int ensure_padded_table(f110_ctx *ctx) {
     }
     if (ctx->maps->rmp) {
         ctx->fx_pad = true;
-        ctx->rmp = ctx->maps->rmp;
-        ctx->rmp_w = ctx->maps->rmp_w;
-        ctx->rmp_P = ctx->maps->rmp_P;
-        ctx->rmp_zero = ctx->maps->rmp_zero;
+        adopt_padded_table(ctx);
     }
     return F110_OK;
 }
 
+// waves > 0 also turns heavy-first off: k_rays_fxs takes no heavy-first list
 extern "C" int f110_set_ray_refill(f110_ctx *ctx, int32_t waves) {
     if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_refill: null context");
     if (waves < 0 || waves > 16) return fail(F110_E_INVALID, "f110_set_ray_refill: waves must be in 0..16");
-    const bool fx = ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled;
+    const bool fx = ctx->ray_kernel == 3;
     if (!fx && waves != 0) return fail(F110_E_INVALID, "f110_set_ray_refill: this context's ray kernel has no refill");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     ctx->fx_refill = waves;
-    if (waves > 0) return ensure_padded_table(ctx);  // the padded table goes with k_rays_fxr
-    return F110_OK;
-}
-
-// k_rays_fxp runs for unmasked steps of a fixed-point context with two rays per
-// lane, the padded table and no heavy-first list, when the pool's chunks fit one
-// wave's queue (cars x chunks <= 64)
-static int effective_pool(const f110_ctx *ctx) {
-    const int nch = (ctx->cfg.n_beams + 63) / 64;
-    const bool fx = ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled && ctx->fx_ilp == 2 && ctx->fx_pad &&
-                    ctx->rmp && ctx->pcost;
-    const int pool = ctx->fx_pool;
-    return fx && pool > 0 && pool * nch <= 64 && (ctx->heavy_off || !ctx->wcost) ? pool : 0;
-}
-
-extern "C" int f110_ray_pool(const f110_ctx *ctx) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_ray_pool: null context");
-    return effective_pool(ctx);
-}
-
-extern "C" int f110_set_ray_pool(f110_ctx *ctx, int32_t cars, int32_t threshold) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_pool: null context");
-    if (cars < 0 || cars > 2) return fail(F110_E_INVALID, "f110_set_ray_pool: cars per wave must be in 0..2");
-    if (threshold < 0 || threshold > 128) return fail(F110_E_INVALID, "f110_set_ray_pool: threshold must be in 0..128");
-    const bool fx = ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled && ctx->pcost;
-    if (!fx && cars != 0) return fail(F110_E_INVALID, "f110_set_ray_pool: this context's ray kernel has no pool");
-    if (use_device(ctx) != F110_OK) return F110_E_HIP;
-    ctx->fx_pool = cars;
-    if (threshold > 0) ctx->pool_T = threshold;
-    if (cars > 0) return ensure_padded_table(ctx);
+    if (waves > 0) {
+        ctx->heavy_off = true;
+        return ensure_padded_table(ctx);  // the padded table goes with k_rays_fxs
+    }
     return F110_OK;
 }
 
@@ -1144,12 +975,19 @@ extern "C" int f110_disable_heavy_first(f110_ctx *ctx) {
 
 extern "C" int f110_set_ray_lanes(f110_ctx *ctx, int32_t n) {
     if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_lanes: null context");
-    if (n < 1 || n > 4) return fail(F110_E_INVALID, "f110_set_ray_lanes: n must be in 1..4");
+    if (n < 1 || n > 2) return fail(F110_E_INVALID, "f110_set_ray_lanes: n must be 1 or 2");
     if (ctx->launch_n != 0)
         return fail(F110_E_INVALID, "f110_set_ray_lanes: call before the first reset/step (heavy-first state is per group)");
-    const bool fx = ctx->ray_kernel == 3 && !ctx->evict && !ctx->fx_tiled;
+    const bool fx = ctx->ray_kernel == 3;
     if (!fx && n != 1) return fail(F110_E_INVALID, "f110_set_ray_lanes: this context's ray kernel traces one ray per lane");
-    if (fx && !std::getenv("F110_FX_ILP")) ctx->fx_ilp = n;  // the env override still wins (A/B runs)
+    if (fx) ctx->fx_ilp = n;
+    return F110_OK;
+}
+
+extern "C" int f110_set_ray_variant(f110_ctx *ctx, int32_t variant) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_variant: null context");
+    if (variant < 0 || variant > 7) return fail(F110_E_INVALID, "f110_set_ray_variant: variant must be in 0..7");
+    ctx->fxs_variant = variant;
     return F110_OK;
 }
 
@@ -1213,8 +1051,6 @@ extern "C" int f110_scan_batch(f110_ctx *ctx, const double *poses, int64_t M, do
     a.lookups = lookups;
     a.hit_rc = hit_rc;
     a.ctr = ctx->ctr;
-    const char *v = std::getenv("F110_SCAN_VARIANT");
-    a.variant = v ? std::atoi(v) : 0;
     HIP_TRY(launch_scan_batch(a, (hipStream_t)stream));
     return F110_OK;
 }

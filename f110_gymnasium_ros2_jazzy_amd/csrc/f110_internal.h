@@ -18,20 +18,20 @@ constexpr int kRayBlock = 256; // threads per block of the ray kernels
 constexpr int kMaxMultiBodies = 64;  // f110_collision_multiple: bodies per set
 constexpr int kMaxChunks = 32;  // 64-beam chunks per scan (n_beams <= 2048) for the chunked ray dispatch
 
-// Everything one launch of the fused env-step kernel needs, passed by value.
+// Everything one env step (k_agents, a ray kernel, a post kernel) needs, passed by value.
 struct StepArgs {
     MapView map;
     TiledMapView tmap;
     const double *sines, *cosines;            // [theta_dis]  ScanSimulator2D tables
     const double *angles, *beam_cos, *side;   // [B] RaceCar class-level beam tables
-    const double *cs2, *bs2;  // k_rays_fxs (F110_FXS_PACK): (cos, sin)[theta_dis], (side, beam_cos)[B] interleaved, or null
+    const double *cs2, *bs2;  // k_rays_fxs: (cos, sin)[theta_dis], (side, beam_cos)[B] interleaved
     f110_params p;                            // Simulator / F110Env params (GJK boxes, lidar_max)
     const f110_params *pa;                    // [A] RaceCar params (update_pose, ray_cast boxes)
     int32_t E, A, B, theta_dis, integrator, ego, autoreset, mode;  // mode 0 step, 1 reset
     int32_t reset_f32;        // resets follow F110Env.reset(options=float32 poses) (f110_set_reset_dtype)
-    int32_t ray_wpb;          // chunked ray kernel: waves (cars) per block, 1 or 4 (F110_RAY_WPB)
-    int32_t ray_kernel;       // 0: k_rays on the row-major EDT; 1: k_rays_tiled, flat ray order; 2: chunked;
-                              // 3: chunked k_rays_fx (fixed-point cell index, scalar per-car set-up)
+    int32_t ray_wpb;          // chunked ray kernel: waves (cars) per block (1)
+    int32_t ray_kernel;       // 1: k_rays_tiled, flat ray order; 2: chunked; 3: the fixed-point kernels
+                              // (k_rays_fx / k_rays_fxn / k_rays_fxs: fixed-point cell index, scalar per-car set-up)
     uint8_t chunk_order[kMaxChunks];  // beam-chunk dispatch order of the chunked ray kernel
     uint64_t *wtrace;         // diagnostic wave trace of the next ray launch (f110_debug_wave_trace) or null
     hipEvent_t gate_wait;     // f110_set_ray_gate: waited on before the ray launch, or null
@@ -42,13 +42,6 @@ struct StepArgs {
     uint32_t *heavy_list;     // [2][heavy_cap] (car << 8 | chunk), by step parity
     uint32_t *heavy_mask;     // [EA] chunks of the car that are in the heavy list
     uint32_t *heavy_count;    // [2] list lengths, by step parity
-    // k_rays_fx straggler hand-off (see RayArgs::ev); null = off
-    double *ev;
-    int32_t *ev_gb;
-    uint32_t *ev_ctr;
-    uint32_t ev_cap, ev_capp;
-    int32_t ev_P;
-    int32_t ev_T, ev_K;
     int32_t heavy_cap, heavy_T, heavy_build, heavy_use, parity, ray_nch;
     int32_t heavy_on;         // heavy-first enabled for this context (wcost is written for the next step)
     // k_rays_fx / k_rays_fxn's row-major EDT: rows of rm_w cells (128-B
@@ -63,24 +56,12 @@ struct StepArgs {
     const double *rmp;
     int32_t rmp_w, rmp_P;
     uint32_t rmp_zero;
-    int32_t fx_pad;     // F110_FX_PAD: k_rays_fxn on the padded table
-    int32_t fx_slots;   // F110_FX_SLOTS (A/B): chunk slots per k_rays_fxr wave, 2 or 3
-    int32_t fxr_lean;   // k_rays_fxs for k_rays_fxr's padded two-slot kernel (F110_FXR_LEAN=0: off, A/B)
-    int32_t fx_lpool;   // k_rays_fxq (lane-level refill, one car per wave) where k_rays_fxs runs (F110_FX_LPOOL)
-    int32_t fxs_pipe;   // k_rays_fxs with software-pipelined slots (F110_FXS_PIPE)
-    int32_t fxs_maskld; // k_rays_fxs: ended lanes issue no gather (F110_FXS_MASKLD)
-    int32_t fx_spec_k, fx_spec_t;  // F110_FX_SPEC=K:T: k_rays_fx guesses K steps per lookup once <= T lanes trace
-    int32_t fx_refill;  // F110_FX_REFILL: waves per car of k_rays_fxr (two chunk slots with refill; 0 = off)
-    int32_t fx_pool;    // F110_FX_POOL: cars per k_rays_fxp wave (lane-level refill; 0 = off)
-    int32_t pool_T;     // F110_FX_POOL_T: k_rays_fxp refills once this many slots have ended
-    int32_t fused_cpw;  // F110_FUSED_CPW: cars per k_step1 workgroup (1..8)
-    int32_t multi_block;  // F110_MULTI_BLOCK: k_post_multi threads per env (64 or 128)
-    uint8_t *pcost;     // [EA][nch] k_rays_fxp's per-chunk cost of the previous launch (its queue order)
-    int32_t count_slots;  // F110_SIMT (default 1): lane-slot counter of the fixed-point loops
-    int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2..4: k_rays_fxn)
-    int32_t fx_tiled;   // F110_FX_TABLE=tiled (A/B): k_rays_fx on the 4x4-tiled EDT
-    int32_t fx_nolean;  // F110_FX_LEAN=0 (A/B): the ballot-per-iteration loop of round 2
-    uint32_t fx_lds;  // F110_FX_LDS (diagnostic): unused dynamic LDS per k_rays_fx block (occupancy cap)
+    int32_t fx_pad;     // the padded table is built (k_rays_fxn on it unless F110_FX_PAD=0; k_rays_fxs)
+    int32_t fxs_ok;     // the padded table's rows and columns are below 2^20 (kFxsBase's offsets)
+    int32_t fx_refill;  // waves per car of k_rays_fxs (two chunk slots with refill; 0 = off)
+    int32_t fxs_variant;  // f110_set_ray_variant (A/B of k_rays_fxs variants; 0 = the default)
+    int32_t count_slots;  // f110_set_simt: lane-slot counter of the fixed-point loops
+    int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2: k_rays_fxn / k_rays_fxs)
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
     uint64_t seed;
     int64_t env_offset;
@@ -178,40 +159,9 @@ struct RayArgs {
     double fxp_lo, fxp_hx, fxp_hy;
     int32_t fxp_P;
     double fxs_cx, fxs_cy;  // k_rays_fxs: 2^20 + P + 2^-26 - origin / res (see kFxsBase)
-    int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_read_simt; F110_SIMT)
-    // straggler hand-off of k_rays_fx (EVICT) -> k_rays_fx_tail: SoA records
-    // ev[7][ev_cap] = x, y, d, tot, cos, sin, noise; ev_gb[2][ev_cap] = car, beam.
-    // The queue is split in ev_P partitions of ev_capp records (partition p =
-    // records [p*ev_capp, (p+1)*ev_capp)), each with its own counters on a
-    // 128-B line: ev_ctr[p*kEvStride] records written, [p*kEvStride+1] taken.
-    // (~10^6 waves appending to ONE counter serialise at the memory side.)
-    double *ev;
-    int32_t *ev_gb;
-    uint32_t *ev_ctr;
-    uint32_t ev_cap, ev_capp;
-    int32_t ev_P;
-    int32_t ev_T, ev_K;  // evict a wave's active rays once <= ev_T remain after >= ev_K iterations
-    // k_rays_fxp (lane-level refill over a pool of cars): per (car, 64-beam chunk) the
-    // longest ray's lookups of the previous launch (min 255), read for the queue order and
-    // rewritten; refill once pool_T ray slots of a wave have ended
-    uint8_t *pcost;
-    int32_t pool_T;
-    int32_t fx_spec_t;  // k_rays_fx<.., SPEC>: the speculative step runs once <= fx_spec_t lanes still trace
-    const double *cs2, *bs2;  // k_rays_fxs: interleaved (cos, sin) / (side, beam_cos) tables (F110_FXS_PACK), or null
+    int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_read_simt)
+    const double *cs2, *bs2;  // k_rays_fxs: interleaved (cos, sin) / (side, beam_cos) tables
 };
-
-// k_step1's argument block (the fused single-agent step over n steps): RayArgs
-// first, so the ray helpers that read the kernarg segment as a RayArgs work.
-struct FusedArgs {
-    RayArgs r;
-    StepArgs s;
-    int32_t nsteps;
-    int32_t cpw;         // cars per workgroup (one wave each; their lane-parallel sections on wave 0)
-    int64_t act_stride;  // action elements between consecutive steps' [E][A][2] blocks
-};
-
-constexpr int kEvStride = 32;    // u32 per hand-off partition counter line (128 B)
-constexpr int kEvMaxParts = 256;
 
 // k_rays_fx's magic offset: 1.5 * 2^22.  t = M + q for q in [0, 2^21) lies in
 // the binade [2^22, 2^23), whose ulp is 2^-30, so the low 30 mantissa bits of
@@ -258,7 +208,6 @@ struct ScanArgs {
     int32_t *lookups;     // [M][B] or null
     int32_t *hit_rc;      // [M][B][2] or null
     unsigned long long *ctr;
-    int32_t variant;      // A/B experiments (F110_SCAN_VARIANT): 0 default
 };
 
 // gap_follow_action over M float32 scans (f110_gap_follow).
@@ -371,11 +320,7 @@ struct AdamArgs {
 };
 hipError_t launch_adam(const AdamArgs &a, hipStream_t s);
 
-size_t step_lds_bytes(int A, int B);
-hipError_t prepare_env_step(size_t lds_bytes);
-hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev = nullptr);  // ev: 4 events or null
-// k_step1: n single-agent steps in one launch (padded fixed-point table, mode 0, no mask)
-hipError_t launch_step1(const StepArgs &a, int32_t n, int64_t act_stride, hipStream_t s, hipEvent_t *ev = nullptr);
+hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev = nullptr);  // ev: 6 events or null
 hipError_t launch_scan_batch(const ScanArgs &a, hipStream_t s);
 hipError_t launch_gap_follow(const GapFollowArgs &a, hipStream_t s);
 hipError_t launch_reward(const RewardArgs &a, hipStream_t s);

@@ -160,8 +160,8 @@ class BatchSim:
 
     def step_n(self, actions, minimal_outputs: bool = False) -> StepOut:
         """n consecutive steps with resident actions [n, E, A, 2] (f110_step_n:
-        one k_step1 launch when the context runs fused, else n three-launch
-        steps); the outputs hold the last step's values."""
+        n three-launch steps, no host work in between); the outputs hold the
+        last step's values."""
         a = torch.as_tensor(actions, device=self.device)
         if a.dtype not in (torch.float32, torch.float64):
             a = a.to(torch.float32)
@@ -174,15 +174,6 @@ class BatchSim:
         _lib.check(self.L.f110_step_n(self.ctx, _ptr(a), dt, int(a.shape[0]), 0, ctypes.byref(outs), self._stream()),
                    "f110_step_n")
         return self.out
-
-    def set_fused(self, on: bool = True):
-        """Single-agent steps as one k_step1 launch (f110_set_fused; results unchanged)."""
-        _lib.check(self.L.f110_set_fused(self.ctx, int(bool(on))), "f110_set_fused")
-
-    @property
-    def fused(self) -> bool:
-        """True when f110_step / f110_step_n run k_step1 (f110_fused)."""
-        return bool(_lib.check(self.L.f110_fused(self.ctx), "f110_fused"))
 
     def update_params(self, params: dict, agent_idx: int = -1):
         """Simulator.update_params (base_classes.py:527-546) for every env."""
@@ -315,33 +306,32 @@ class BatchSim:
 
     @property
     def ray_kernel(self) -> int:
-        """The ray kernel this context launches (f110_ray_kernel: 3 = k_rays_fx)."""
+        """The ray kernel this context launches (f110_ray_kernel: 3 = the fixed-point kernels)."""
         return _lib.check(self.L.f110_ray_kernel(self.ctx), "f110_ray_kernel")
 
     @property
     def ray_lanes(self) -> int:
-        """Rays per lane of the fixed-point ray kernel (f110_ray_lanes: 1 = k_rays_fx, 2 = k_rays_fxn)."""
+        """Rays per lane of the fixed-point ray kernel (f110_ray_lanes: 1 = k_rays_fx, 2 = k_rays_fxn / fxs)."""
         return _lib.check(self.L.f110_ray_lanes(self.ctx), "f110_ray_lanes")
 
+    def set_ray_lanes(self, n: int):
+        """Rays per lane, 1 or 2 (f110_set_ray_lanes; before the first reset / step)."""
+        _lib.check(self.L.f110_set_ray_lanes(self.ctx, int(n)), "f110_set_ray_lanes")
+
     def set_ray_refill(self, waves: int):
-        """k_rays_fxr's waves per car (0: k_rays_fxn), with the padded EDT (f110_set_ray_refill)."""
+        """k_rays_fxs's waves per car (0: k_rays_fxn), with the padded EDT and heavy-first off
+        (f110_set_ray_refill)."""
         _lib.check(self.L.f110_set_ray_refill(self.ctx, int(waves)), "f110_set_ray_refill")
 
     @property
     def ray_refill(self) -> int:
-        """k_rays_fxr's waves per car for unmasked steps (f110_ray_refill), 0 when k_rays_fxn /
+        """k_rays_fxs's waves per car for unmasked steps (f110_ray_refill), 0 when k_rays_fxn /
         k_rays_fx trace this context's rays."""
         return _lib.check(self.L.f110_ray_refill(self.ctx), "f110_ray_refill")
 
-    def set_ray_pool(self, cars: int, threshold: int = 0):
-        """k_rays_fxp's cars per wave (0: off) and refill threshold (0: keep), with the padded EDT
-        (f110_set_ray_pool)."""
-        _lib.check(self.L.f110_set_ray_pool(self.ctx, int(cars), int(threshold)), "f110_set_ray_pool")
-
-    @property
-    def ray_pool(self) -> int:
-        """k_rays_fxp's cars per wave for unmasked steps (f110_ray_pool), 0 when another ray kernel runs."""
-        return _lib.check(self.L.f110_ray_pool(self.ctx), "f110_ray_pool")
+    def disable_heavy_first(self):
+        """Heavy-first ray dispatch off for good (f110_disable_heavy_first; results unchanged)."""
+        _lib.check(self.L.f110_disable_heavy_first(self.ctx), "f110_disable_heavy_first")
 
     def close(self):
         if getattr(self, "ctx", None):

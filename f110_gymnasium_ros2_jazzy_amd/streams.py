@@ -26,7 +26,6 @@ from __future__ import annotations
 
 import collections
 import ctypes
-import os
 
 import torch
 
@@ -92,7 +91,7 @@ class StreamShards:
             ray_lanes = 2 if n_envs * self.n_agents >= 12288 else 1
         self.ray_lanes = ray_lanes
         if refill is None:
-            # k_rays_fxr (one wave per car, refilled chunk slots, padded EDT) from 32768 cars on the
+            # k_rays_fxs (one wave per car, refilled chunk slots, padded EDT) from 32768 cars on the
             # GPU, as f110_create's rule for one context: 32768 envs as 2 x 16384 69.2 vs 62.6 M
             # env-steps/s, 16384 as 2 x 8192 58.7 vs 61.5 M (profiles/r02_refill_sizes/)
             # (with 4 sub-shards from 16384 cars: 65.3 vs 63.1 M; with 2 it lost there, 58.3 vs 61.3 M)
@@ -109,10 +108,9 @@ class StreamShards:
                     _lib.check(sm.L.f110_disable_heavy_first(sm.ctx), "f110_disable_heavy_first")
                 if sm.ray_kernel == 3:  # the fixed-point kernel (the others trace one ray per lane)
                     _lib.check(sm.L.f110_set_ray_lanes(sm.ctx, int(ray_lanes)), "f110_set_ray_lanes")
-                    if os.environ.get("F110_FX_REFILL") is None:  # the env knob still wins (A/B runs)
-                        _lib.check(sm.L.f110_set_ray_refill(sm.ctx, int(refill)), "f110_set_ray_refill")
+                    _lib.check(sm.L.f110_set_ray_refill(sm.ctx, int(refill)), "f110_set_ray_refill")
                 self.sims.append(sm)
-        # what the contexts actually run (the env knob or an unsupported map can override the request)
+        # what the contexts actually run (an unsupported map can override the request)
         self.refill = self.sims[0].ray_refill
         self._sl = [slice(s * self.Es, (s + 1) * self.Es) for s in range(self.S)]
         self._handles = [ctypes.c_void_p(st.cuda_stream) for st in self.streams]

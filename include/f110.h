@@ -156,19 +156,9 @@ F110_API int f110_step(f110_ctx *ctx, const void *actions, int32_t actions_dtype
  * [n_envs][n_agents][2] block at actions + t * step_stride elements
  * (step_stride 0 = packed, n_envs * n_agents * 2) -- a rollout of open-loop
  * actions; every output holds the last step's values, exactly as after the n
- * calls.  Single-agent contexts with
- * f110_set_fused on run the n steps in ONE k_step1 launch (each env's car
- * advances through its steps in one wave, no per-step launch boundary);
- * otherwise the three-launch step runs n times.  Bit-identical either way. */
+ * calls (the three-launch step runs n times, no host work in between). */
 F110_API int f110_step_n(f110_ctx *ctx, const void *actions, int32_t actions_dtype, int32_t n_steps,
                          int64_t step_stride, const f110_outputs *out, void *stream);
-/* Single-agent steps as one launch (k_step1: dynamics, rays and the post stage
- * of each car in one wave) instead of k_agents + k_rays + k_post_single; on
- * switches the context to the padded EDT and off its heavy-first list.
- * F110_FUSED sets the default.  Scheduling only: results are unchanged. */
-F110_API int f110_set_fused(f110_ctx *ctx, int32_t on);
-/* 1 when this context's f110_step / f110_step_n run k_step1, else 0. */
-F110_API int f110_fused(const f110_ctx *ctx);
 
 /* Replaces F110Env.update_params / Simulator.update_params
  * (f110_env.py:487-498, base_classes.py:527-546): agent_idx < 0 updates every
@@ -247,14 +237,15 @@ F110_API int f110_collision_multiple(const double *verts, int64_t M, int32_t N, 
 F110_API int f110_read_counters(f110_ctx *ctx, uint64_t *lookups, uint64_t *rays, void *stream);
 F110_API int f110_reset_counters(f110_ctx *ctx, void *stream);
 /* Diagnostic: the sum over the counter lines of counter idx (0..15): 0
- * lookups, 1 rays, 2 lane slots (f110_read_simt), 3 / 4 k_rays_fxp's refill
- * passes / slot refills (with f110_set_simt on). */
+ * lookups, 1 rays, 2 lane slots (f110_read_simt). */
 F110_API int f110_read_counter(f110_ctx *ctx, int32_t idx, uint64_t *value, void *stream);
-/* SIMT efficiency of the fixed-point ray loops (k_rays_fx / k_rays_fxn, the
- * default kernels) since the last counter reset: loop_lookups = lookups made
- * inside the loop (all lookups less the first one per ray, which k_agents
- * makes), lane_slots = the loop's trip counts x 64 lanes x rays per lane,
- * summed over waves; efficiency = loop_lookups / lane_slots.  Other ray
+/* SIMT efficiency of the fixed-point ray loops (k_rays_fx / k_rays_fxn /
+ * k_rays_fxs, the default kernels) since the last counter reset: loop_lookups
+ * = lookups made inside the loop (all lookups less the first one per ray,
+ * which k_agents makes), lane_slots = 64 x the wave-level gathers the loop
+ * issued (k_rays_fx / k_rays_fxn: trip count x rays per lane; k_rays_fxs:
+ * trips x 2 slots, a closed slot's zero-cell gather included), summed over
+ * waves; efficiency = loop_lookups / lane_slots.  Other ray
  * kernels, and launches made while the count is off, leave lane_slots as
  * they are.  f110_set_simt(ctx, 1) turns the count on (off by default: its
  * extra atomic per wave costs ~2 % of k_rays).  Diagnostics (no reference
@@ -301,43 +292,41 @@ F110_API int f110_set_ray_gate(f110_ctx *ctx, void *wait_event, void *record_eve
 F110_API int f110_disable_heavy_first(f110_ctx *ctx);
 
 /* The ray kernel this context launches (>= 0), or a negative error code:
- * 0 row-major k_rays, 1 tiled flat ray order, 2 tiled chunked, 3 chunked
- * k_rays_fx (fixed-point cell index; the default where its preconditions
- * hold: axis-aligned map, one-wave blocks, EDT entries 0 or > eps).
- * Selected at f110_create (env F110_RAY_KERNEL overrides the default). */
+ * 1 k_rays_tiled in flat ray order, 2 tiled chunked, 3 the fixed-point
+ * kernels k_rays_fx / k_rays_fxn / k_rays_fxs (the default where their
+ * preconditions hold: axis-aligned map, EDT entries 0 or > eps).  Selected at
+ * f110_create (env F110_RAY_KERNEL overrides the default, A/B only). */
 F110_API int f110_ray_kernel(const f110_ctx *ctx);
 
-/* Rays traced per lane by the fixed-point ray kernel (1: k_rays_fx, 2..4:
- * k_rays_fxn; F110_FX_ILP overrides the size-based default); 1 for the
+/* Rays traced per lane by the fixed-point ray kernel (1: k_rays_fx, 2:
+ * k_rays_fxn / k_rays_fxs; size-based default, f110_set_ray_lanes); 1 for the
  * other ray kernels.  Diagnostic, no reference counterpart. */
 F110_API int f110_ray_lanes(const f110_ctx *ctx);
-/* k_rays_fxr's waves per car for unmasked steps (one wave per car traces the
+/* k_rays_fxs's waves per car for unmasked steps (one wave per car traces the
  * car's 64-beam chunks two at a time, refilling a slot as soon as its chunk
  * ends), or 0 when the context steps with k_rays_fxn / k_rays_fx (heavy-first
- * on, one ray per lane, or F110_FX_REFILL=0).  Default: 1 from 32768 cars. */
+ * on, one ray per lane, no padded table).  Default: 1 from 32768 cars. */
 F110_API int f110_ray_refill(const f110_ctx *ctx);
-/* Set k_rays_fxr's waves per car (0: k_rays_fxn) and, when on, switch the
- * context to the padded EDT (built on first use).  For callers that split one
- * GPU's cars over several contexts (streams.StreamShards): the size rule is
- * about the cars the GPU traces at once, not one context's.  Any time. */
+/* Set k_rays_fxs's waves per car (0: k_rays_fxn) and, when on, switch the
+ * context to the padded EDT (built on first use) and off its heavy-first list.
+ * For callers that split one GPU's cars over several contexts
+ * (streams.StreamShards): the size rule is about the cars the GPU traces at
+ * once, not one context's.  Any time.  Scheduling only: results are unchanged. */
 F110_API int f110_set_ray_refill(f110_ctx *ctx, int32_t waves);
-/* Cars per wave of k_rays_fxp (lane-level refill over a pool of cars: every
- * lane has two ray slots, a slot whose ray has ended takes the pool's next ray;
- * the pool's 64-beam chunks are queued by the previous step's per-chunk cost),
- * or 0 when the context steps with k_rays_fxr / k_rays_fxn / k_rays_fx.
- * Scheduling only: results are bit-identical to the other ray kernels. */
-F110_API int f110_ray_pool(const f110_ctx *ctx);
-/* Set k_rays_fxp's cars per wave (0..2; 0 = off) and its refill threshold
- * (ended slots, 1..128; 0 keeps the current one); switches the context to the
- * padded EDT.  F110_FX_POOL / F110_FX_POOL_T set the defaults.  Any time. */
-F110_API int f110_set_ray_pool(f110_ctx *ctx, int32_t cars, int32_t threshold);
 
-/* Sets the rays per lane of the fixed-point ray kernel (1..4) before the
+/* A/B of k_rays_fxs's variants for the following steps (0 = the default;
+ * bit 0: the slot left alone once the other has closed runs a one-slot loop;
+ * bits 1-2 = 1 / 2 / 3: slots with at most 1 / 2 / 4 active lanes gather by
+ * scalar loads).  Scheduling only: results are bit-identical.  Measurement
+ * hook (scripts/ray_ab.py), no reference counterpart. */
+F110_API int f110_set_ray_variant(f110_ctx *ctx, int32_t variant);
+
+/* Sets the rays per lane of the fixed-point ray kernel (1 or 2) before the
  * context's first reset/step.  The size-based default looks at this
  * context's cars only; a caller stepping S contexts concurrently on one GPU
  * (streams.StreamShards) knows the GPU's total and passes the choice for
- * that.  Scheduling only: results are unchanged.  F110_FX_ILP
- * still overrides.  Diagnostic / tuning, no reference counterpart. */
+ * that.  Scheduling only: results are unchanged.
+ * Diagnostic / tuning, no reference counterpart. */
 F110_API int f110_set_ray_lanes(f110_ctx *ctx, int32_t n);
 
 /* The dtype of the reset poses whose F110Env.reset semantics the following
@@ -390,8 +379,12 @@ F110_API int f110_host_cell_index(int32_t H, int32_t W, double resolution, const
  * origin is center +- half (world frame), for a car at yaw.  Host only; the
  * CPU tests check they contain every beam inside the window. */
 /* Host copy of the device's cr_sincos (the ray_cast / box / dynamics sin and
- * cos: double-double evaluation, one rounding; matches NumPy's (glibc's)
- * np.sin / np.cos).  Test hook, no reference counterpart. */
+ * cos: double-double evaluation, one rounding, i.e. correctly rounded).  It
+ * equals NumPy's (glibc's) np.sin / np.cos except where glibc is itself off
+ * by one ulp (< 0.3 % of the sampled arguments, test_cr_sincos_matches_numpy);
+ * on those the device differs from the reference's trig by that ulp, which
+ * the non-exact budgets (tests/golden/nonexact_beams.json) pin.  Test hook,
+ * no reference counterpart. */
 F110_API void f110_host_sincos(const double *x, int64_t n, double *sn, double *cs);
 /* NumPy's float32 np.cos (cos_op != 0) / np.sin over n values, as the
  * device evaluates F110Env.reset's float32 start_rot (test hook). */

@@ -14,7 +14,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+# F110_ORACLE_LIB: an alternate build of the same source (scripts/sanitize.sh: ASan/UBSan)
+LIB_PATH = os.environ.get("F110_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 
 _D = ctypes.POINTER(ctypes.c_double)
 _I32 = ctypes.POINTER(ctypes.c_int32)
@@ -53,6 +54,8 @@ _lib = None
 
 def build(force: bool = False) -> str:
     src = os.path.join(HERE, "f110_oracle.c")
+    if os.environ.get("F110_ORACLE_LIB"):
+        return LIB_PATH  # prebuilt by its own recipe
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
         subprocess.check_call(["make", "-s", "-C", HERE, "-B", "liboracle.so"])
     return LIB_PATH

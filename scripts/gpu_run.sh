@@ -1,0 +1,54 @@
+# One parameterised GPU-box job (run through gpurun from the repo root):
+#
+#   bash scripts/gpu_run.sh TAG STEP [STEP ...]
+#
+# Steps run in order, each under its own time limit; the first failure ends
+# the job (no GPU step runs after a failed / faulted / timed-out one).  Output
+# goes to gpurun_out/TAG/.  Steps:
+#   suite      pytest -m gpu (one process, per-test timeout)
+#   smoke      __graft_entry__.smoke()
+#   bench      python bench.py (defaults) -> bench.json
+#   bench20    python bench.py --steps 20 --warmup 5 (the driver's settings) -> bench20.json
+#   prof       rocprofv3 --kernel-trace --stats over bench.py (no cpu leg) -> prof/, kernel_stats.csv
+#   pmc        scripts/profile_round.py TAG (kernel trace + PMC passes of the headline ray kernel)
+#   ab         scripts/ray_ab.py with the caller's AB_* environment -> ab.json
+#   c4 / c5    bench.py --agents 2 --global-envs 8192 / --workload ddpg -> c4.json / c5.json
+set -o pipefail
+TAG=${1:?tag}
+shift
+cd /tmp && export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-/root/repo}
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$R"
+run() {  # name seconds cmd...
+    local name=$1 secs=$2
+    shift 2
+    echo "[$(date +%T)] $name" >&2
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+    local rc=$?
+    if [ $rc -ne 0 ]; then
+        echo "step $name failed rc=$rc" >&2
+        tail -30 "$OUT/$name.err" >&2
+        tail -30 "$OUT/$name.out" >&2
+        exit $rc
+    fi
+}
+for step in "$@"; do
+    case $step in
+        suite) run suite 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+        smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench) run bench 600 python -u bench.py && cp "$OUT/bench.out" "$OUT/bench.json" ;;
+        bench20) run bench20 600 python -u bench.py --steps 20 --warmup 5 && cp "$OUT/bench20.out" "$OUT/bench20.json" ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 bench.py --steps 300 \
+                  --no-cpu-baseline --no-secondary --no-full-outputs &&
+              find "$OUT/prof" -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} "$OUT/kernel_stats.csv" ;;
+        pmc) run pmc 900 python -u scripts/profile_round.py "$TAG" ;;
+        ab) run ab 900 python -u scripts/ray_ab.py && cp "$OUT/ab.out" "$OUT/ab.json" ;;
+        c4) run c4 600 python -u bench.py --agents 2 --global-envs 8192 --no-cpu-baseline --no-secondary &&
+            cp "$OUT/c4.out" "$OUT/c4.json" ;;
+        c5) run c5 600 python -u bench.py --workload ddpg --steps 200 --warmup 20 && cp "$OUT/c5.out" "$OUT/c5.json" ;;
+        *) echo "unknown step $step" >&2; exit 2 ;;
+    esac
+done
+echo "[$(date +%T)] done" >&2

@@ -150,5 +150,19 @@ try:
         busy[f"insts_{k.lower()}_per_wave"] = iss[f"SQ_INSTS_{k}"] / max(1.0, iss["SQ_WAVES"])
 except Exception as exc:
     busy["issue_error"] = repr(exc)
+# 5. the vector-memory address path: wave-level vector reads against texture-address
+#    busy cycles (TA_BUSY_avr: per TA instance, one per CU), the bound of the gather loop
+grp = ["SQ_INSTS_VMEM_RD", "SQ_WAVES", "TA_BUSY_avr", "TA_FLAT_READ_WAVEFRONTS_sum", "GRBM_GUI_ACTIVE"]
+try:
+    dd = run("pmc_ta", ["--pmc"] + grp, target=RAYPMC)
+    ta = counters(dd, os.path.join(PROF, f"{tag}_pmc_ta.csv"))
+    cyc = ta["GRBM_GUI_ACTIVE"] / 8.0
+    busy["vmem_rd_per_launch"] = ta["SQ_INSTS_VMEM_RD"]
+    busy["ta_flat_read_wavefronts"] = ta["TA_FLAT_READ_WAVEFRONTS_sum"]
+    busy["ta_busy_cycles_per_cu"] = ta["TA_BUSY_avr"]
+    busy["ta_busy"] = ta["TA_BUSY_avr"] / max(1.0, cyc)
+    busy["ta_cycles_per_vmem_rd"] = ta["TA_BUSY_avr"] * 256 / max(1.0, ta["SQ_INSTS_VMEM_RD"])
+except Exception as exc:
+    busy["ta_error"] = repr(exc)
 json.dump(busy, open(os.path.join(PROF, f"pmc_busy_E{ENVS}_A1.json"), "w"), indent=1)
 print(json.dumps(busy))

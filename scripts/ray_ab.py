@@ -1,9 +1,15 @@
 """A/B of ray-kernel variants in one process (GPU box): per-kernel times
-(HIP events on the launch stream, interleaved rounds) and a bit-identity check
-of every variant's outputs against the first one (obs, f64 scans, states,
-collisions after the same steps, noise + autoreset on).  Prints one JSON line.
+(HIP events on each kernel's own dispatch, interleaved rounds) and a
+bit-identity check of every variant's outputs against the first one (obs, f64
+scans, states, collisions after the same steps, noise + autoreset on, a masked
+reset in the middle).  Prints one JSON line.
 
-    AB_ENVS=8192,65536 AB_VARIANTS='k2:F110_RAY_KERNEL=2;k3:F110_RAY_KERNEL=3' python scripts/ray_ab.py
+A variant is `name:KEY=V,KEY=V`; keys: F110_RAY_KERNEL / F110_FX_PAD (env at
+create), LANES (f110_set_ray_lanes), REFILL (f110_set_ray_refill), VARIANT
+(f110_set_ray_variant: k_rays_fxs's experimental variants), HEAVY=0
+(f110_disable_heavy_first), NOISE.
+
+    AB_ENVS=8192,65536 AB_VARIANTS='fxn:REFILL=0,LANES=2;fxs:REFILL=1,LANES=2' python scripts/ray_ab.py
 """
 import json
 import os
@@ -13,11 +19,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+from f110_gymnasium_ros2_jazzy_amd import _lib  # noqa: E402
 from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns, load_map  # noqa: E402
 from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim  # noqa: E402
 
-KNOBS = ("F110_RAY_KERNEL", "F110_CHUNK_ORDER", "F110_HEAVY_T", "F110_RAY_WPB", "F110_HEAVY_DIV", "F110_EVICT",
-         "F110_EVICT_T", "F110_EVICT_K", "F110_FX_LDS", "F110_FX_LEAN", "F110_FX_ILP", "F110_FX_TABLE", "F110_FX_PAIR", "F110_FX_PAD", "F110_SIMT", "F110_FX_REFILL", "F110_FX_SLOTS", "F110_FX_POOL", "F110_FX_POOL_T", "F110_FXR_LEAN", "F110_FX_LPOOL", "F110_FXS_PIPE", "F110_FX_SPEC", "F110_FXS_MASKLD", "F110_FXS_PACK")
+ENV_KNOBS = ("F110_RAY_KERNEL", "F110_FX_PAD")
 
 
 def parse_variants(spec):
@@ -35,15 +41,24 @@ def parse_variants(spec):
     return out
 
 
-def make(tm, sp, E, A, env, **kw):
-    env = dict(env)
-    for k in KNOBS:
+def make(tm, sp, E, A, spec, **kw):
+    for k in ENV_KNOBS:
         os.environ.pop(k, None)
-    os.environ.update({k: v for k, v in env.items() if k != "NOISE"})
-    noise = float(env.pop("NOISE", os.environ.get("AB_NOISE", "0.01"))) if "NOISE" in env else \
-        float(os.environ.get("AB_NOISE", "0.01"))
-    return BatchSim(tm, n_envs=E, n_agents=A, noise_std=noise, autoreset=True, spawn_poses=sp, seed=7,
-                    keep_f64_scans=True, **kw)
+    os.environ.update({k: v for k, v in spec.items() if k in ENV_KNOBS})
+    noise = float(spec.get("NOISE", os.environ.get("AB_NOISE", "0.01")))
+    sm = BatchSim(tm, n_envs=E, n_agents=A, noise_std=noise, autoreset=True, spawn_poses=sp, seed=7,
+                  keep_f64_scans=True, **kw)
+    for k in ENV_KNOBS:
+        os.environ.pop(k, None)
+    if "LANES" in spec:
+        sm.set_ray_lanes(int(spec["LANES"]))
+    if "REFILL" in spec:
+        sm.set_ray_refill(int(spec["REFILL"]))
+    if "VARIANT" in spec:
+        _lib.check(sm.L.f110_set_ray_variant(sm.ctx, int(spec["VARIANT"])), "f110_set_ray_variant")
+    if spec.get("HEAVY") == "0":
+        sm.disable_heavy_first()
+    return sm
 
 
 def snapshot(sm):
@@ -58,6 +73,7 @@ def main():
     variants = parse_variants(os.environ.get("AB_VARIANTS", "k2:F110_RAY_KERNEL=2;k3:F110_RAY_KERNEL=3"))
     steps = int(os.environ.get("AB_STEPS", 100))
     rounds = int(os.environ.get("AB_ROUNDS", 3))
+    simt = os.environ.get("AB_SIMT") == "1"
     tm = load_map(os.environ.get("AB_MAP", "Spielberg_map"))
     sp = centerline_spawns(os.environ.get("AB_MAP", "Spielberg_map").replace("_map", ""), A)
     res = {"agents": A, "variants": variants, "by_envs": {}}
@@ -69,7 +85,9 @@ def main():
         acts = torch.rand(40 + steps, E, A, 2, device="cuda", generator=g)
         acts[..., 0] = acts[..., 0] * 0.8378 - 0.4189
         acts[..., 1] *= 20
-        sims = {n: make(tm, sp, E, A, env) for n, env in variants.items()}
+        sims = {n: make(tm, sp, E, A, spec) for n, spec in variants.items()}
+        kernels = {n: {"ray_kernel": sm.ray_kernel, "lanes": sm.ray_lanes, "refill": sm.ray_refill}
+                   for n, sm in sims.items()}
         # bit identity: 40 steps with every output, plus a masked reset in the middle
         ref = None
         ident = {}
@@ -106,14 +124,21 @@ def main():
                 pk = sm.profile_end()
                 lk, rays = sm.read_counters()
                 look[n] = lk / max(rays, 1)
-                if os.environ.get("F110_SIMT") == "1" or "F110_SIMT" in variants[n]:
-                    cars = E * A * steps
-                    diag[n] = {"simt": (lk - rays) / max(sm.read_counter(2), 1),
-                               "slot_iters_per_car": sm.read_counter(2) / cars,
-                               "passes_per_car": sm.read_counter(3) / cars,
-                               "refills_per_car": sm.read_counter(4) / cars}
                 times[n].append(pk)
-        line = {"identical": ident, "mean_lookups": look, "diag": diag}
+        if simt:  # counters in a separate pass (their atomics are not part of the timed launches)
+            for n, sm in sims.items():
+                sm.reset(p0)
+                sm.set_simt(True)
+                sm.reset_counters()
+                for k in range(steps):
+                    sm.step(acts[40 + k], minimal_outputs=True)
+                lk, rays = sm.read_counters()
+                slots = sm.read_counter(2)
+                cars = E * A * steps
+                diag[n] = {"simt": (lk - rays) / max(slots, 1), "slot_gathers_per_car": slots / 64 / cars,
+                           "other_loads_per_car": sm.read_counter(3) / cars}
+                sm.set_simt(False)
+        line = {"kernels": kernels, "identical": ident, "mean_lookups": look, "diag": diag}
         for n, ts in times.items():
             line[n] = {key: float(np.median([t[key] for t in ts])) for key in ts[0]}
         res["by_envs"][str(E)] = line

@@ -129,17 +129,12 @@ def test_full_size_properties(tracks, gpu):
 
 @pytest.mark.parametrize("A", [1, 2])
 def test_ray_kernel_dispatch_variants_identical(tracks, gpu, monkeypatch, A):
-    """The ray-kernel dispatches (F110_RAY_KERNEL: 0 row-major EDT +
-    k_post, 1 tiled flat ray order, 2 tiled chunked in descending chunk
-    order in one-wave blocks, the same with 4-car blocks (F110_RAY_WPB=4),
-    3 chunked k_rays_fx -- the default, fixed-point cell index -- on the
-    row-major EDT with 1, 2 and 3 rays per lane (F110_FX_ILP; k_rays_fxn for
-    2 and 3, on the padded table or, F110_FX_PAD=0, the clamped one), on
-    the 4x4-tiled EDT (F110_FX_TABLE=tiled), and with the
-    straggler hand-off to the refill tail kernel, F110_EVICT=1; k_post_multi
-    with one wave per env, F110_MULTI_BLOCK=64) give
-    bit-identical steps: scans, obs, collisions,
-    states, with noise, autoreset and a masked reset."""
+    """The ray-kernel dispatches (F110_RAY_KERNEL: 1 k_rays_tiled in flat ray
+    order, 2 tiled chunked in descending chunk order, 3 the fixed-point
+    kernels -- the default -- with 1 ray per lane (k_rays_fx) and 2
+    (k_rays_fxn on the padded table, or, F110_FX_PAD=0, the clamped one))
+    give bit-identical steps: scans, obs, collisions, states, with noise,
+    autoreset and a masked reset."""
     E = 300  # not a multiple of 4 cars per chunked block
     sp = _spawns(A)
     rng = np.random.default_rng(7)
@@ -147,21 +142,14 @@ def test_ray_kernel_dispatch_variants_identical(tracks, gpu, monkeypatch, A):
     acts = np.stack([rng.uniform(-0.4189, 0.4189, (30, E, A)), rng.uniform(0, 20, (30, E, A))], -1).astype(np.float32)
     mask = rng.random(E) < 0.5
     outs = []
-    for k, wpb, evict, ilp, table, pad, mb in (("0", "1", "0", "1", "rm", "1", "128"), ("1", "1", "0", "1", "rm", "1", "128"),
-                                               ("2", "1", "0", "1", "rm", "1", "128"), ("2", "4", "0", "1", "rm", "1", "128"),
-                                               ("3", "1", "0", "1", "rm", "1", "128"), ("3", "1", "0", "2", "rm", "1", "128"),
-                                               ("3", "1", "0", "2", "rm", "0", "128"), ("3", "1", "0", "3", "rm", "1", "128"),
-                                               ("3", "1", "0", "3", "rm", "0", "128"), ("3", "1", "0", "1", "tiled", "1", "128"),
-                                               ("3", "1", "1", "1", "rm", "1", "128"), ("3", "1", "0", "2", "rm", "1", "64")):
-        monkeypatch.setenv("F110_MULTI_BLOCK", mb)  # k_post_multi: one or two waves per env
+    for k, lanes, pad in (("1", 1, "1"), ("2", 1, "1"), ("3", 1, "1"), ("3", 2, "1"), ("3", 2, "0")):
         monkeypatch.setenv("F110_RAY_KERNEL", k)
-        monkeypatch.setenv("F110_RAY_WPB", wpb)
-        monkeypatch.setenv("F110_EVICT", evict)  # 3 + 1: k_rays_fx with the straggler hand-off to k_rays_fx_tail
-        monkeypatch.setenv("F110_FX_ILP", ilp)
-        monkeypatch.setenv("F110_FX_TABLE", table)
         monkeypatch.setenv("F110_FX_PAD", pad)  # k_rays_fxn on the padded table (1) or the clamped one (0)
         sim = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=4,
                    keep_f64_scans=True)
+        assert sim.ray_kernel == int(k)
+        if k == "3":
+            sim.set_ray_lanes(lanes)
         sim.reset(poses)
         rec = []
         for t in range(30):
@@ -186,7 +174,7 @@ def test_stream_shards_match_single_context(tracks, gpu, lanes, refill):
     to one context stepping all envs (noise and autoreset on; the actions are
     resident before the loop, as in the bench), with the sub-shards' map
     tables shared and 1 or 2 rays per lane (f110_set_ray_lanes), and with
-    k_rays_fxr switched on per sub-shard (f110_set_ray_refill)."""
+    k_rays_fxs switched on per sub-shard (f110_set_ray_refill)."""
     from f110_gymnasium_ros2_jazzy_amd import _lib
     from f110_gymnasium_ros2_jazzy_amd.streams import StreamShards
     E, A, T = 256, 1, 60
@@ -199,7 +187,7 @@ def test_stream_shards_match_single_context(tracks, gpu, lanes, refill):
     sh = StreamShards(tracks("Spielberg_map"), n_envs=E, n_streams=4, ray_lanes=lanes, refill=refill,
                       n_agents=A, device=gpu, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=9)
     assert all(sm.ray_lanes == lanes for sm in sh.sims)
-    assert all(sm.ray_refill == refill for sm in sh.sims)  # f110_set_ray_refill (k_rays_fxr + padded EDT)
+    assert all(sm.ray_refill == refill for sm in sh.sims)  # f110_set_ray_refill (k_rays_fxs + padded EDT)
     full.reset(poses)
     sh.reset(poses)
     with pytest.raises(RuntimeError, match="before the first"):
@@ -267,11 +255,11 @@ def test_stream_shards_broadcast_reset(tracks, gpu):
 
 
 @pytest.mark.parametrize("beams,A", [(64, 1), (333, 2), (2048, 1), (1080, 3)])
-def test_rays_per_lane_identical_across_beam_counts(tracks, gpu, monkeypatch, beams, A):
-    """k_rays_fxn (2 and 3 rays per lane) against k_rays_fx (1) for scan sizes
-    whose 64-beam chunks do not pair evenly (1, 6, 32 chunks; 17 with three
-    agents): scans, obs, collisions and states bit-identical over 25 noisy
-    steps with autoreset and a masked reset."""
+def test_rays_per_lane_identical_across_beam_counts(tracks, gpu, beams, A):
+    """k_rays_fxn (2 rays per lane) against k_rays_fx (1) for scan sizes whose
+    64-beam chunks do not pair evenly (1, 6, 32 chunks; 17 with three agents):
+    scans, obs, collisions and states bit-identical over 25 noisy steps with
+    autoreset and a masked reset."""
     E = 96
     sp = _spawns(A)
     rng = np.random.default_rng(beams)
@@ -279,11 +267,11 @@ def test_rays_per_lane_identical_across_beam_counts(tracks, gpu, monkeypatch, be
     acts = np.stack([rng.uniform(-0.4189, 0.4189, (25, E, A)), rng.uniform(0, 20, (25, E, A))], -1).astype(np.float32)
     mask = rng.random(E) < 0.5
     outs = []
-    for ilp in ("1", "2", "3"):
-        monkeypatch.setenv("F110_FX_ILP", ilp)
+    for lanes in (1, 2):
         sim = _sim(tracks, gpu, n_envs=E, n_agents=A, num_beams=beams, noise_std=0.01, autoreset=True,
                    spawn_poses=sp, seed=9, keep_f64_scans=True)
-        assert sim.ray_kernel == 3 and sim.ray_lanes == int(ilp)
+        sim.set_ray_lanes(lanes)
+        assert sim.ray_kernel == 3 and sim.ray_lanes == lanes
         sim.reset(poses)
         rec = []
         for t in range(25):
@@ -298,17 +286,21 @@ def test_rays_per_lane_identical_across_beam_counts(tracks, gpu, monkeypatch, be
                 assert torch.equal(x, y), f"step {t}"
 
 
-@pytest.mark.parametrize("ilp", ["1", "2"])
-def test_simt_counters(tracks, gpu, monkeypatch, ilp):
-    """f110_set_simt / f110_read_simt: the fixed-point loops count the lane slots they issue
-    (trip count x 64 x rays per lane); loop lookups = all lookups less the
-    first lookup of each ray (k_agents'), and never exceed the slots."""
-    monkeypatch.setenv("F110_FX_ILP", ilp)
+@pytest.mark.parametrize("lanes,refill", [(1, 0), (2, 0), (2, 1)])
+def test_simt_counters(tracks, gpu, lanes, refill):
+    """f110_set_simt / f110_read_simt: the fixed-point loops count the lane
+    slots of the gathers they issue (64 per wave-level gather: trip count x
+    rays per lane, or k_rays_fxs's trips x 2 slots, closed slots included);
+    loop lookups = all lookups less the first lookup of each ray (k_agents'),
+    and never exceed the slots.  k_rays_fxs also counts its other vector loads
+    (counter 3: tables, guard-band re-gathers): at least one arm per chunk."""
     E, A = 512, 1
     sp = _spawns(A)
     rng = np.random.default_rng(3)
     sim = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=2)
-    assert sim.ray_kernel == 3 and sim.ray_lanes == int(ilp)
+    sim.set_ray_lanes(lanes)
+    sim.set_ray_refill(refill)
+    assert sim.ray_kernel == 3 and sim.ray_lanes == lanes and sim.ray_refill == refill
     sim.reset(sp[rng.integers(0, sp.shape[0], E)])
     sim.set_simt(True)
     sim.reset_counters()
@@ -320,6 +312,9 @@ def test_simt_counters(tracks, gpu, monkeypatch, ilp):
     assert loop == lookups - rays
     assert 0 < loop <= slots
     assert 0.2 < loop / slots <= 1.0
+    other = sim.read_counter(3)
+    if refill:
+        assert other >= 5 * E * ((sim.B + 63) // 64)  # one (cos, sin) load per arm
     sim.set_simt(False)
     sim.step(np.zeros((E, A, 2), np.float32))
     assert sim.read_simt()[1] == slots  # off: no lane slots added
@@ -328,42 +323,26 @@ def test_simt_counters(tracks, gpu, monkeypatch, ilp):
 
 @pytest.mark.parametrize("A,beams", [(1, 1080), (2, 1080), (1, 333), (1, 64)])
 def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
-    """k_rays_fxr (F110_FX_REFILL=1: one wave per car, two chunk slots, a
-    slot refilled with the car's next chunk as soon as its chunk ends)
-    against k_rays_fxn's adjacent pairs: scans, obs, collisions and states
-    bit-identical over 25 noisy steps with autoreset and a masked reset
-    (which runs k_rays_fxn), for 17, 6 and 1 chunks per car; its counters
-    (lookups, rays) equal k_rays_fxn's."""
+    """k_rays_fxs (f110_set_ray_refill: one wave per car, two chunk slots, a
+    slot refilled with the car's next chunk as soon as its chunk ends; 1 and
+    3 waves per car) against k_rays_fxn's adjacent pairs on the clamped and
+    the padded table: scans, obs, collisions and states bit-identical over 25
+    noisy steps with autoreset and a masked reset (which runs k_rays_fxn), for
+    17, 6 and 1 chunks per car; the counters (lookups, rays) equal."""
     E = 200
     sp = _spawns(A)
     rng = np.random.default_rng(beams + A)
     poses = sp[rng.integers(0, sp.shape[0], E)]
     acts = np.stack([rng.uniform(-0.4189, 0.4189, (25, E, A)), rng.uniform(0, 20, (25, E, A))], -1).astype(np.float32)
     mask = rng.random(E) < 0.5
-    monkeypatch.setenv("F110_FX_ILP", "2")
-    monkeypatch.setenv("F110_HEAVY_T", "0")  # k_rays_fxr has no heavy-first dispatch
     outs, ctrs = [], []
-    # off; 1 or 3 waves per car; padded EDT with k_rays_fxr's round-3 pass (lean 0), k_rays_fxs (lean 1) and
-    # k_rays_fxq (lane-level refill over the car's beams, refill thresholds 1 / 80 / 128)
-    for refill, pad, lean, lpool in (("0", "0", "1", "0:80"), ("1", "0", "1", "0:80"), ("3", "0", "1", "0:80"),
-                                     ("1", "1", "0", "0:80"), ("1", "1", "1", "0:80"), ("3", "1", "1", "0:80"),
-                                     ("1", "1", "1", "1:80"), ("1", "1", "1", "1:1"), ("1", "1", "1", "1:128"),
-                                     ("1", "1", "2", "0:80"), ("3", "1", "2", "0:80"), ("1", "1", "m", "0:80"),
-                                     ("1", "1", "x", "0:80"), ("1", "1", "j", "0:80"),
-                                     ("1", "1", "p", "0:80")):
-        monkeypatch.setenv("F110_FX_REFILL", refill)
+    for refill, pad in ((0, "0"), (0, "1"), (1, "1"), (3, "1")):
         monkeypatch.setenv("F110_FX_PAD", pad)
-        monkeypatch.setenv("F110_FXR_LEAN", "1" if lean in ("2", "m", "x", "j", "p") else lean)
-        monkeypatch.setenv("F110_FXS_PACK", "1" if lean == "p" else "0")  # "p": interleaved trig / beam tables
-        # "m": range-checked buffer gathers, "x": ended lanes issue no gather (exec mask), "j": lock-step
-        # slots sharing one gather when no lane has both rays active
-        monkeypatch.setenv("F110_FXS_MASKLD", {"m": "1", "x": "2", "j": "3"}.get(lean, "0"))
-        monkeypatch.setenv("F110_FXS_PIPE", "0" if lean in ("2", "j") else "1")  # "2": k_rays_fxs with lock-step slots
-        monkeypatch.setenv("F110_FX_LPOOL", lpool.split(":")[0])
-        monkeypatch.setenv("F110_FX_POOL_T", lpool.split(":")[1])
         sim = _sim(tracks, gpu, n_envs=E, n_agents=A, num_beams=beams, noise_std=0.01, autoreset=True,
                    spawn_poses=sp, seed=6, keep_f64_scans=True)
-        assert sim.ray_refill == min(int(refill), (beams + 63) // 64)
+        sim.set_ray_lanes(2)
+        sim.set_ray_refill(refill)
+        assert sim.ray_refill == min(refill, (beams + 63) // 64)
         sim.reset(poses)
         sim.reset_counters()
         rec = []
@@ -381,137 +360,32 @@ def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
                 assert torch.equal(x, y), f"step {t}"
 
 
-@pytest.mark.parametrize("A,beams", [(1, 1080), (2, 1080), (1, 333)])
-def test_spec_step_identical(tracks, gpu, monkeypatch, A, beams):
-    """k_rays_fx's speculative step (F110_FX_SPEC=K:T: once <= T lanes of a
-    wave still trace, each lookup round gathers the cells of the next K
-    steps as if the EDT value repeated, and keeps the prefix whose guesses
-    held) against the serial loop: scans, obs, collisions and states
-    bit-identical over 25 noisy steps with autoreset and a masked reset, for
-    K = 2 / 4 on every iteration (T = 64) and in the tail only (T = 8); the
-    counters (lookups, rays, lane slots) equal the serial loop's."""
-    E = 300
+
+def test_step_n_matches_single_steps(tracks, gpu):
+    """f110_step_n (n resident steps, no host work in between) equals n
+    f110_step calls: obs, scans, states and counters bit-identical, f32 and
+    f64 action blocks."""
+    E, A, T = 203, 1, 11
     sp = _spawns(A)
-    rng = np.random.default_rng(beams + A + 3)
+    rng = np.random.default_rng(21)
     poses = sp[rng.integers(0, sp.shape[0], E)]
-    acts = np.stack([rng.uniform(-0.4189, 0.4189, (25, E, A)), rng.uniform(0, 20, (25, E, A))], -1).astype(np.float32)
-    mask = rng.random(E) < 0.5
-    monkeypatch.setenv("F110_FX_ILP", "1")
-    monkeypatch.setenv("F110_FX_REFILL", "0")
-    monkeypatch.setenv("F110_FX_PAD", "0")
-    outs, ctrs = [], []
-    for spec in ("1:0", "2:64", "4:64", "4:8", "2:16"):
-        monkeypatch.setenv("F110_FX_SPEC", spec)
-        sim = _sim(tracks, gpu, n_envs=E, n_agents=A, num_beams=beams, noise_std=0.01, autoreset=True,
-                   spawn_poses=sp, seed=9, keep_f64_scans=True)
-        sim.reset(poses)
-        sim.reset_counters()
-        rec = []
-        for t in range(25):
-            o = sim.reset(poses[::-1].copy(), env_mask=mask) if t == 12 else sim.step(acts[t])
-            rec.append((o.scans_f64.clone(), o.obs.clone(), o.collisions.clone(), sim.agent_states().clone()))
-        torch.cuda.synchronize()
-        outs.append(rec)
-        ctrs.append(sim.read_counters())
-        sim.close()
-    for k in range(1, len(outs)):
-        assert ctrs[0] == ctrs[k]
-        for t, (a, b) in enumerate(zip(outs[0], outs[k])):
-            for x, y in zip(a, b):
-                assert torch.equal(x, y), f"step {t}"
-
-
-@pytest.mark.parametrize("A,beams", [(1, 1080), (2, 1080), (1, 333), (1, 64)])
-def test_pool_kernel_identical(tracks, gpu, monkeypatch, A, beams):
-    """k_rays_fxp (F110_FX_POOL = 1 or 2 cars per wave: two ray slots per
-    lane, a slot whose ray has ended takes the pool's next ray, the pool's
-    chunks queued by the previous step's per-chunk cost) against k_rays_fxn:
-    scans, obs, collisions and states bit-identical over 25 noisy steps with
-    autoreset and a masked reset (which runs k_rays_fxn), an odd car count
-    (the last wave's pool is short), refill thresholds 1, 80 and 128; the
-    counters (lookups, rays) equal k_rays_fxn's."""
-    E = 203
-    sp = _spawns(A)
-    rng = np.random.default_rng(beams + A + 7)
-    poses = sp[rng.integers(0, sp.shape[0], E)]
-    acts = np.stack([rng.uniform(-0.4189, 0.4189, (25, E, A)), rng.uniform(0, 20, (25, E, A))], -1).astype(np.float32)
-    mask = rng.random(E) < 0.5
-    monkeypatch.setenv("F110_FX_ILP", "2")
-    monkeypatch.setenv("F110_HEAVY_T", "0")
-    monkeypatch.setenv("F110_FX_REFILL", "0")
-    outs, ctrs = [], []
-    for pool, T, pad in (("0", "80", "0"), ("1", "80", "1"), ("2", "80", "1"), ("2", "1", "1"), ("2", "128", "1")):
-        monkeypatch.setenv("F110_FX_POOL", pool)
-        monkeypatch.setenv("F110_FX_POOL_T", T)
-        monkeypatch.setenv("F110_FX_PAD", pad)
-        sim = _sim(tracks, gpu, n_envs=E, n_agents=A, num_beams=beams, noise_std=0.01, autoreset=True,
-                   spawn_poses=sp, seed=6, keep_f64_scans=True)
-        assert sim.ray_pool == int(pool)
-        sim.reset(poses)
-        sim.reset_counters()
-        rec = []
-        for t in range(25):
-            o = sim.reset(poses[::-1].copy(), env_mask=mask) if t == 12 else sim.step(acts[t])
-            rec.append((o.scans_f64.clone(), o.obs.clone(), o.collisions.clone(), sim.agent_states().clone()))
-        torch.cuda.synchronize()
-        outs.append(rec)
-        ctrs.append(sim.read_counters())
-        sim.close()
-    for k in range(1, len(outs)):
-        assert ctrs[0] == ctrs[k], k
-        for t, (a, b) in enumerate(zip(outs[0], outs[k])):
-            for x, y in zip(a, b):
-                assert torch.equal(x, y), f"variant {k} step {t}"
-
-
-@pytest.mark.parametrize("beams,dtype,cpw", [(1080, "f32", 8), (333, "f64", 3), (64, "f32", 1), (1080, "f64", 5)])
-def test_step1_matches_three_launch_step(tracks, gpu, beams, dtype, cpw, monkeypatch):
-    """k_step1 (f110_set_fused: the single-agent step -- dynamics, rays, post
-    stage -- in one launch per call, or n steps in one launch via
-    f110_step_n) against the three-launch step: obs, f64 / f32 scans,
-    collisions, terminated, was_reset, lap times / counts, sim time, states
-    and lookup counters bit-identical over 40 noisy random-action steps with
-    autoreset (crashes and respawns happen), a masked reset in the middle
-    (which runs the three-launch path in both) and float32 / float64 actions;
-    f110_step_n over 9 / 11 / 9 steps equals single calls.  cpw cars per
-    workgroup (F110_FUSED_CPW); 203 envs leave a ragged last workgroup."""
-    monkeypatch.setenv("F110_FUSED_CPW", str(cpw))
-    E = 203
-    sp = _spawns(1)
-    rng = np.random.default_rng(beams)
-    poses = sp[rng.integers(0, sp.shape[0], E)]
-    T = 40
-    acts = np.stack([rng.uniform(-0.4189, 0.4189, (T, E, 1)), rng.uniform(0, 20, (T, E, 1))], -1)
-    acts = torch.from_numpy(acts.astype(np.float32 if dtype == "f32" else np.float64)).to(gpu)
-    mask = rng.random(E) < 0.5
-    runs = []
-    for mode in ("three", "fused", "fused_n"):
-        sim = _sim(tracks, gpu, n_envs=E, n_agents=1, num_beams=beams, noise_std=0.01, autoreset=True,
-                   spawn_poses=sp, seed=9, keep_f64_scans=True)
-        sim.set_fused(mode != "three")
-        assert sim.fused == (mode != "three")
-        sim.reset(poses)
-        sim.reset_counters()
-        snaps = {}
-        t = 0
-        while t < T:
-            if t == 20:
-                sim.reset(poses[::-1].copy(), env_mask=mask)
-            n = {0: 9, 20: 11, 31: 9}.get(t, 1) if mode == "fused_n" else 1
-            o = sim.step_n(acts[t:t + n]) if n > 1 else sim.step(acts[t])
-            t += n
-            if t in (9, 31, 40):
-                torch.cuda.synchronize()
-                snaps[t] = (o.obs.clone(), o.scans.clone(), o.scans_f64.clone(), o.collisions.clone(),
-                            o.terminated.clone(), o.was_reset.clone(), o.lap_times.clone(), o.lap_counts.clone(),
-                            o.sim_time.clone(), sim.agent_states().clone())
-        runs.append((snaps, sim.read_counters()))
-        sim.close()
-    ref_snaps, ref_ctr = runs[0]
-    for k in (1, 2):
-        snaps, ctr = runs[k]
-        assert ctr == ref_ctr, k
-        assert sorted(snaps) == sorted(ref_snaps) == [9, 31, 40]
-        for t in ref_snaps:
-            for j, (x, y) in enumerate(zip(ref_snaps[t], snaps[t])):
-                assert torch.equal(x, y), f"mode {k} after step {t} field {j}"
+    acts = np.stack([rng.uniform(-0.4189, 0.4189, (T, E, A)), rng.uniform(0, 20, (T, E, A))], -1)
+    for dt in (np.float32, np.float64):
+        a = torch.from_numpy(acts.astype(dt)).to(gpu)
+        runs = []
+        for n_call in (False, True):
+            sim = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=9,
+                       keep_f64_scans=True)
+            sim.reset(poses)
+            sim.reset_counters()
+            if n_call:
+                o = sim.step_n(a)
+            else:
+                for t in range(T):
+                    o = sim.step(a[t])
+            torch.cuda.synchronize()
+            runs.append((o.obs.clone(), o.scans_f64.clone(), sim.agent_states().clone(), sim.read_counters()))
+            sim.close()
+        for x, y in zip(runs[0][:3], runs[1][:3]):
+            assert torch.equal(x, y)
+        assert runs[0][3] == runs[1][3]

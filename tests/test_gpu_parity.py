@@ -61,8 +61,8 @@ def test_scan_batch_rotated_origin_golden(rotated, gpu):
 
 @pytest.mark.parametrize("A", [1, 2])
 def test_step_rotated_origin_vs_oracle(rotated, gpu, oracle_mod, monkeypatch, A):
-    """Steps on the rotated map through every ray-kernel dispatch (row-major,
-    tiled flat, tiled chunked: the ROT=true instantiations): each step's
+    """Steps on the rotated map through every ray-kernel dispatch (tiled flat,
+    tiled chunked: the ROT=true instantiations): each step's
     scans equal the oracle scanner's at the poses the step produced."""
     from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
     import os
@@ -77,7 +77,7 @@ def test_step_rotated_origin_vs_oracle(rotated, gpu, oracle_mod, monkeypatch, A)
     poses[:, 1:, 0] += 0.8  # the other car 0.8 m along x
     acts = np.stack([rng.uniform(-0.4189, 0.4189, (6, E, A)), rng.uniform(0, 8, (6, E, A))], -1).astype(np.float32)
     outs = []
-    for k in ("0", "1", "2", "3"):  # 3 (k_rays_fx) falls back to 2 on a rotated map
+    for k in ("1", "2", "3"):  # 3 (the fixed-point kernels) falls back to 2 on a rotated map
         monkeypatch.setenv("F110_RAY_KERNEL", k)
         sim = BatchSim(tm, n_envs=E, n_agents=A, device=gpu, noise_std=0.0, keep_f64_scans=True)
         sim.reset(poses.reshape(E, A, 3))
@@ -296,50 +296,27 @@ def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A, nonexact
     nonexact_budget(f"ray_cast_adversarial_A{A}", nonexact)
 
 
-@pytest.mark.parametrize("kernel,ilp,table,pad,refill,pool,lean", [
-    ("2", "1", "rm", "1", "0", "0", "1"), ("3", "1", "rm", "1", "0", "0", "1"), ("3", "2", "rm", "0", "0", "0", "1"),
-    ("3", "2", "rm", "1", "0", "0", "1"), ("3", "3", "rm", "1", "0", "0", "1"), ("3", "1", "tiled", "1", "0", "0", "1"),
-    ("3", "2", "rm", "0", "1", "0", "1"), ("3", "2", "rm", "1", "1", "0", "1"), ("3", "2", "rm", "1", "1", "0", "0"),
-    ("3", "2", "rm", "1", "1", "0", "q"), ("3", "2", "rm", "1", "1", "0", "m"), ("3", "2", "rm", "1", "1", "0", "x"), ("3", "2", "rm", "1", "1", "0", "j"), ("3", "2", "rm", "1", "1", "0", "p"), ("3", "1", "rm", "0", "0", "0", "s2"), ("3", "1", "rm", "0", "0", "0", "s4"),
-    ("3", "2", "rm", "1", "0", "1", "1"), ("3", "2", "rm", "1", "0", "2", "1")])
-def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanners, monkeypatch, kernel, ilp, table,
-                                                      pad, refill, pool, lean):
-    """k_rays_fx's fixed-point cell index (F110_RAY_KERNEL=3, the default;
-    on the row-major EDT with 1 or 2 rays per lane, k_rays_fxn for 2, and on
-    the 4x4-tiled EDT) against the oracle's IEEE xy_2_rc
-    (laser_models.py:55-104) where it is hardest: scan origins exactly on
-    cell edges and corners with the beam whose table direction is exactly
-    (1, 0) (every lookup of that ray then sits on a row edge: the guard-band
-    path), origins just inside / outside the map edges looking out (clamped
-    into the row-major padding), and origins far off the map (dt[-1, -1]
-    steps; the cars whose rays could leave t's binade take fx_step).  Scans
-    must be bit-exact; every kernel must agree.  With 2 or 3 rays per lane
-    k_rays_fxn runs on the padded table (F110_FX_PAD=1, opt-in: 2^24
-    binade, u24 offsets, no clamp) or the clamped one (0, the default); origins 1-20
-    cells outside the map edges straddle its per-car test (fast loop up to
-    6 cells out, the IEEE loop beyond); with F110_FX_REFILL=1 the same
-    through k_rays_fxr (k_rays_fxs on the padded table, F110_FXR_LEAN=0 the
-    round-3 pass), with F110_FX_POOL=1/2 through k_rays_fxp (lane-level
-    refill over a pool of cars; a pool holding an off-map origin takes the
-    IEEE loop for all its cars); with F110_FX_SPEC=K:64 through k_rays_fx's
-    speculative step (K positions gathered per round, kept while the EDT
-    value repeats)."""
+@pytest.mark.parametrize("kernel,lanes,pad,refill", [
+    ("2", 1, "1", 0), ("3", 1, "1", 0), ("3", 2, "0", 0), ("3", 2, "1", 0), ("3", 2, "1", 1), ("3", 2, "1", 3)])
+def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanners, monkeypatch, kernel, lanes, pad,
+                                                      refill):
+    """The fixed-point cell index (F110_RAY_KERNEL=3, the default) against
+    the oracle's IEEE xy_2_rc (laser_models.py:55-104) where it is hardest:
+    scan origins exactly on cell edges and corners with the beam whose table
+    direction is exactly (1, 0) (every lookup of that ray then sits on a row
+    edge: the guard-band path), origins just inside / outside the map edges
+    looking out (clamped into the row-major padding), and origins far off the
+    map (dt[-1, -1] steps; the cars whose rays could leave t's binade take
+    fx_step).  Scans must be bit-exact for every kernel: k_rays_tiled
+    (kernel 2), k_rays_fx (1 ray per lane), k_rays_fxn (2, on the clamped
+    table or, F110_FX_PAD=1, the padded one: 2^24 binade, u24 offsets, no
+    clamp; origins 1-20 cells outside the map edges straddle its per-car
+    test, the fast loop up to 6 cells out, the IEEE loop beyond) and
+    k_rays_fxs (f110_set_ray_refill: 1 or 3 waves per car, kFxsBase
+    offsets on the padded table)."""
     from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
     monkeypatch.setenv("F110_RAY_KERNEL", kernel)
-    monkeypatch.setenv("F110_FX_ILP", ilp)
-    monkeypatch.setenv("F110_FX_TABLE", table)
     monkeypatch.setenv("F110_FX_PAD", pad)
-    monkeypatch.setenv("F110_FX_REFILL", refill)  # k_rays_fxr (one wave per car, chunk slots with refill)
-    monkeypatch.setenv("F110_FX_POOL", pool)  # k_rays_fxp (lane-level refill over a pool of cars)
-    # k_rays_fxs's range-checked gathers (m) / no gathers for ended lanes (x)
-    monkeypatch.setenv("F110_FXS_MASKLD", {"m": "1", "x": "2", "j": "3"}.get(lean, "0"))
-    monkeypatch.setenv("F110_FXS_PIPE", "0" if lean == "j" else "1")  # j: lock-step slots sharing a gather
-    monkeypatch.setenv("F110_FXS_PACK", "1" if lean == "p" else "0")  # p: interleaved trig / beam tables
-    monkeypatch.setenv("F110_FXR_LEAN", "0" if lean == "0" else "1")  # padded k_rays_fxr: k_rays_fxs (1), round 3's (0)
-    monkeypatch.setenv("F110_FX_LPOOL", "1" if lean == "q" else "0")  # k_rays_fxq: lane-level refill (q)
-    # k_rays_fx with its speculative step on every iteration (s2 / s4: 2 / 4 guessed steps per lookup round)
-    monkeypatch.setenv("F110_FX_SPEC", f"{lean[1]}:64" if lean.startswith("s") else "1:0")
-    monkeypatch.setenv("F110_HEAVY_T", "0" if refill == "1" or pool != "0" else "16")
     tm = tracks("Spielberg_map")
     ox, oy, _ = tm.origin
     res = tm.resolution
@@ -387,8 +364,10 @@ def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanne
     E = poses.shape[0]
     sim = BatchSim(tm, n_envs=E, n_agents=1, device=gpu, noise_std=0.0, keep_f64_scans=True)
     assert sim.ray_kernel == int(kernel)  # no silent fallback on this axis-aligned map
-    assert sim.ray_refill == int(refill)
-    assert sim.ray_pool == int(pool)
+    if kernel == "3":
+        sim.set_ray_lanes(lanes)
+        sim.set_ray_refill(refill)
+    assert sim.ray_refill == refill
     out = sim.reset(poses[:, None, :])
     torch.cuda.synchronize()
     st = sim.agent_states().cpu().numpy().reshape(E, 7)
