@@ -99,6 +99,7 @@ struct f110_ctx {
     bool fx_pad = false;    // the padded table is wanted (from 32768 cars or with refill; F110_FX_PAD=0: never)
     int32_t fx_refill = 0;   // waves per car of k_rays_fxs (0 = k_rays_fxn; f110_set_ray_refill)
     int32_t fxs_variant = 0;  // f110_set_ray_variant (A/B)
+    uint8_t *ccost = nullptr;  // [EA][nch] k_rays_fxs's per-chunk trip counts (its chunk order, ORD)
     bool count_slots = false;  // f110_set_simt: lane-slot counter of the fixed-point loops (f110_read_simt)
     int fx_ilp = 1;         // rays per lane (f110_set_ray_lanes; default by car count)
 
@@ -429,28 +430,80 @@ static hipError_t upload(T **p, const std::vector<T> &h) {
 
 // k_rays_fxn / k_rays_fxs's padded table (PAD, see kFxpBase): cell (r, c) at
 // row r + P, column c + P; every other cell holds dt[-1,-1] (the reference's
-// off-map read), and a 0.0 after the last row is the zero cell.  Built only
-// where its byte offsets stay 32-bit and a row stride stays a 24-bit
-// multiplier (else t->rmp stays null and the clamped table is used).
-static hipError_t build_padded_table(MapTables *t, int32_t pad, const std::vector<double> &d) {
-    const int32_t H = t->H, W = t->W;
-    const size_t N = (size_t)H * W;
-    // rows of Wp = 511 mod 512 cells: the row stride Wp * 8 is 8 bytes short of a multiple of
-    // 4096, which k_rays_fxs's offset arithmetic needs (kFxsBase); any width serves the others
-    const size_t P = (size_t)pad, Wp = ((size_t)W + 2 * P + 1 + 511) / 512 * 512 - 1, Hp = (size_t)H + 2 * P;
-    if ((Wp * Hp + 16) * 8 >= (1ull << 32) || Wp * 8 >= (1u << 24)) return hipSuccess;
+// off-map read), and a 0.0 after the last row is the zero cell.  Rows of Wp =
+// 511 mod 512 cells: the row stride Wp * 8 is 8 bytes short of a multiple of
+// 4096, which k_rays_fxs's offset arithmetic needs (kFxsBase); any width
+// serves the others.  Built only where its byte offsets stay 32-bit and a row
+// stride stays a 24-bit multiplier (else empty: the clamped table is used).
+// Host-only (f110_host_map_table tests it on the CPU, under ASan / UBSan too).
+static std::vector<double> host_padded_table(int32_t H, int32_t W, int32_t pad, const std::vector<double> &d,
+                                             size_t &Wp, size_t &Hp) {
+    const size_t N = (size_t)H * W, P = (size_t)pad;
+    Wp = ((size_t)W + 2 * P + 1 + 511) / 512 * 512 - 1;
+    Hp = (size_t)H + 2 * P;
+    if (pad <= 0 || d.size() != N || (Wp * Hp + 16) * 8 >= (1ull << 32) || Wp * 8 >= (1u << 24)) return {};
     std::vector<double> rmp(Wp * Hp + 16, d[N - 1]);
-    for (int r = 0; r < H; ++r)
-        for (int q = 0; q < W; ++q) rmp[((size_t)r + P) * Wp + q + P] = d[(size_t)r * W + q];
+    for (size_t r = 0; r < (size_t)H; ++r)
+        for (size_t q = 0; q < (size_t)W; ++q) rmp[(r + P) * Wp + q + P] = d[r * W + q];
     rmp[Wp * Hp] = 0.0;
+    return rmp;
+}
+
+// k_rays_fx / k_rays_fxn's row-major EDT: rows of Wp cells (W + 1 rounded up
+// to 16: 128-B aligned), the padding columns and row H hold dt[-1,-1] (a
+// clamped index then reads the reference's off-map value), and a 0.0 after
+// the last row is the zero cell of rays that have ended.  Host-only.
+static std::vector<double> host_rowmajor_table(int32_t H, int32_t W, const std::vector<double> &d, size_t &Wp,
+                                               size_t &Hp) {
+    const size_t N = (size_t)H * W;
+    Wp = ((size_t)W + 1 + 15) / 16 * 16;
+    Hp = (size_t)H + 1;
+    if (d.size() != N) return {};
+    std::vector<double> rm(Wp * Hp + 16, d[N - 1]);
+    for (size_t r = 0; r < (size_t)H; ++r)
+        for (size_t q = 0; q < (size_t)W; ++q) rm[r * Wp + q] = d[r * W + q];
+    rm[Wp * Hp] = 0.0;
+    return rm;
+}
+
+// dt = res * EDT (get_dt, laser_models.py:52) -- bit-exact from the integer k
+static std::vector<double> host_dt(const uint32_t *edt_k, size_t N, double res) {
+    std::vector<double> dt(N);
+    for (size_t i = 0; i < N; ++i) dt[i] = res * std::sqrt((double)edt_k[i]);
+    return dt;
+}
+
+static hipError_t build_padded_table(MapTables *t, int32_t pad, const std::vector<double> &d) {
+    size_t Wp = 0, Hp = 0;
+    const std::vector<double> rmp = host_padded_table(t->H, t->W, pad, d, Wp, Hp);
+    if (rmp.empty()) return hipSuccess;
     const hipError_t e = upload(&t->rmp, rmp);
-    if (e == hipSuccess) {
+    if (e == hipSuccess) {  // the metadata only with the table it describes
         t->rmp_w = (int32_t)Wp;
         t->rmp_h = (int32_t)Hp;
-        t->rmp_P = (int32_t)P;
+        t->rmp_P = pad;
         t->rmp_zero = (uint32_t)(Wp * Hp * 8);
     }
     return e;
+}
+
+// Test hook: the padded (kind 1) or row-major (kind 0) table f110_create
+// would upload for this EDT, on the host.  Returns the table's length in
+// doubles (0 when it is not built: the padded table's limits), fills out when
+// out_len is enough, and meta = {rows, cols, zero-cell byte offset}.
+extern "C" int64_t f110_host_map_table(const uint32_t *edt_k, int32_t H, int32_t W, double res, int32_t kind,
+                                       int32_t pad, double *out, int64_t out_len, int64_t meta[3]) {
+    if (!edt_k || H <= 0 || W <= 0 || !(res > 0)) return fail(F110_E_INVALID, "f110_host_map_table: bad arguments");
+    const std::vector<double> d = host_dt(edt_k, (size_t)H * W, res);
+    size_t Wp = 0, Hp = 0;
+    const std::vector<double> t = kind == 1 ? host_padded_table(H, W, pad, d, Wp, Hp) : host_rowmajor_table(H, W, d, Wp, Hp);
+    if (meta) {
+        meta[0] = (int64_t)Hp;
+        meta[1] = (int64_t)Wp;
+        meta[2] = t.empty() ? -1 : (int64_t)(Wp * Hp * 8);
+    }
+    if (out && out_len >= (int64_t)t.size()) std::copy(t.begin(), t.end(), out);
+    return (int64_t)t.size();
 }
 
 // The tables of (device, map), built and uploaded on first use; `want_rm`
@@ -486,10 +539,7 @@ static hipError_t acquire_map_tables(int device, const uint32_t *edt_k, int32_t 
     hipError_t e = hipSuccess;
     std::vector<double> dt;
     auto dt_host = [&]() -> const std::vector<double> & {
-        if (dt.empty()) {  // dt = res * EDT (get_dt, laser_models.py:52) -- bit-exact from the integer k
-            dt.resize(N);
-            for (size_t i = 0; i < N; ++i) dt[i] = res * std::sqrt((double)edt_k[i]);
-        }
+        if (dt.empty()) dt = host_dt(edt_k, N, res);
         return dt;
     };
     if (fresh) {
@@ -502,17 +552,8 @@ static hipError_t acquire_map_tables(int device, const uint32_t *edt_k, int32_t 
         }
     }
     if (e == hipSuccess && want_rm && !t->rm) {
-        // k_rays_fx / k_rays_fxn's row-major EDT: rows of rm_w cells (128-B
-        // aligned), the padding columns and row H hold dt[-1,-1] (a clamped
-        // index then reads the reference's off-map value), and a 0.0 after the
-        // last row is the zero cell of rays that have ended
-        const std::vector<double> &d = dt_host();
-        const size_t Wp = ((size_t)W + 1 + 15) / 16 * 16, Hp = (size_t)H + 1;
-        std::vector<double> rm(Wp * Hp + 16, d[N - 1]);
-        for (int r = 0; r < H; ++r)
-            for (int q = 0; q < W; ++q) rm[(size_t)r * Wp + q] = d[(size_t)r * W + q];
-        rm[Wp * Hp] = 0.0;
-        e = upload(&t->rm, rm);
+        size_t Wp = 0, Hp = 0;
+        e = upload(&t->rm, host_rowmajor_table(H, W, dt_host(), Wp, Hp));
         if (e == hipSuccess) {  // the metadata only with the table it describes
             t->rm_w = (int32_t)Wp;
             t->rm_oob = (uint32_t)(((size_t)(H - 1) * Wp + (W - 1)) * 8);
@@ -715,6 +756,10 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     // 65536 envs as 2 x 32768 67.1 vs 63.0 M env-steps/s; at 16384 cars its long waves
     // leave a tail (0.324 vs 0.289 ms); it runs only without heavy-first and masks
     c->fx_refill = EA >= 32768 ? 1 : 0;
+    if (fx_ok) {  // zeroed: the first order is the descending one
+        const hipError_t ea = c->alloc(&c->ccost, EA * (size_t)c->nch);
+        if (ea != hipSuccess) return cleanup(F110_E_ALLOC, std::string("hipMalloc ccost: ") + hipGetErrorString(ea));
+    }
     const double pad_q = std::ceil(C.max_range / resolution) + 8.0;
     const int32_t fx_pad_cells = pad_q > 0.0 && pad_q < 65536.0 ? (int32_t)pad_q : 0;  // else no padded table
     if (e == hipSuccess)
@@ -833,6 +878,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.count_slots = c->count_slots ? 1 : 0;
     a.fx_refill = c->fx_refill;
     a.fxs_variant = c->fxs_variant;
+    a.ccost = c->ccost;
     a.fx_ilp = c->fx_ilp;
     a.gate_wait = c->gate_wait;
     a.gate_record = c->gate_record;
@@ -938,11 +984,9 @@ static int ensure_padded_table(f110_ctx *ctx) {
         std::lock_guard<std::mutex> g(g_maps_mu);
         MapTables *t = ctx->maps;
         if (!t->rmp) {
-            std::vector<double> d((size_t)t->H * t->W);
             double res;
             std::memcpy(&res, &t->res_bits, 8);
-            for (size_t i = 0; i < d.size(); ++i) d[i] = res * std::sqrt((double)t->k[i]);
-            HIP_TRY(build_padded_table(t, (int32_t)pad_q, d));
+            HIP_TRY(build_padded_table(t, (int32_t)pad_q, host_dt(t->k.data(), t->k.size(), res)));
         }
     }
     if (ctx->maps->rmp) {
@@ -986,7 +1030,7 @@ extern "C" int f110_set_ray_lanes(f110_ctx *ctx, int32_t n) {
 
 extern "C" int f110_set_ray_variant(f110_ctx *ctx, int32_t variant) {
     if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_variant: null context");
-    if (variant < 0 || variant > 7) return fail(F110_E_INVALID, "f110_set_ray_variant: variant must be in 0..7");
+    if (variant < 0 || variant > 1) return fail(F110_E_INVALID, "f110_set_ray_variant: variant must be 0 or 1");
     ctx->fxs_variant = variant;
     return F110_OK;
 }

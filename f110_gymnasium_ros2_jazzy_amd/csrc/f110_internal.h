@@ -60,6 +60,7 @@ struct StepArgs {
     int32_t fxs_ok;     // the padded table's rows and columns are below 2^20 (kFxsBase's offsets)
     int32_t fx_refill;  // waves per car of k_rays_fxs (two chunk slots with refill; 0 = off)
     int32_t fxs_variant;  // f110_set_ray_variant (A/B of k_rays_fxs variants; 0 = the default)
+    uint8_t *ccost;       // [EA][nch] k_rays_fxs (ORD): each chunk's trip count in the previous launch
     int32_t count_slots;  // f110_set_simt: lane-slot counter of the fixed-point loops
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2: k_rays_fxn / k_rays_fxs)
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
@@ -160,6 +161,7 @@ struct RayArgs {
     int32_t fxp_P;
     double fxs_cx, fxs_cy;  // k_rays_fxs: 2^20 + P + 2^-26 - origin / res (see kFxsBase)
     int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_read_simt)
+    uint8_t *ccost;       // [EA][nch] k_rays_fxs (ORD): per-chunk trip counts, read and rewritten
     const double *cs2, *bs2;  // k_rays_fxs: interleaved (cos, sin) / (side, beam_cos) tables
 };
 

@@ -23,7 +23,6 @@
 
 #include <algorithm>
 #include <cmath>
-#include <type_traits>
 
 #include "f110_internal.h"
 
@@ -1063,15 +1062,23 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
 
 // ------------------------------------------------------------------------
 // k_rays_fxs: one wave per car (a.G4 waves per car: wave j takes the car's
-// chunks nch-1-j, nch-1-j-G4, ...; car-minor block order puts car g's waves on
-// XCD g % 8 when EA % 8 == 0).  Its 64-beam chunks are traced two at a time
-// in two slots; a slot whose rays have all ended writes its chunk's outputs
-// and takes the car's next chunk at once, so both slots keep gathers in
-// flight until the car's last chunk (offline model over oracle trip counts,
-// scripts/pair_model.py: 146.7k wave-iterations for adjacent pairs vs 109.1k).
-// Padded EDT (kFxsBase offsets), no heavy-first, no masked reset; cars whose
-// origin lies off the map trace their chunks one after the other with the
-// IEEE cell.  Per ray the arithmetic is k_rays_fxn's, so bit-identical.
+// chunks at positions j, j+G4, ... of its chunk order; car-minor block order
+// puts car g's waves on XCD g % 8 when EA % 8 == 0).  Its 64-beam chunks are
+// traced two at a time in two slots; a slot whose rays have all ended writes
+// its chunk's outputs and takes the car's next chunk at once, so both slots
+// keep gathers in flight until the car's last chunk (offline model over oracle
+// trip counts, scripts/pair_model.py: 146.7k wave-iterations for adjacent
+// pairs vs 109.1k).  Padded EDT (kFxsBase offsets), no heavy-first, no masked
+// reset; cars whose origin lies off the map trace their chunks one after the
+// other with the IEEE cell.  Per ray the arithmetic is k_rays_fxn's, so
+// bit-identical.
+//
+// Chunk order: descending chunk index (the scan's left edge first), or (ORD)
+// longest pair first: the previous launch's per-chunk trip counts
+// (RayArgs::ccost, written by every ORD launch) rank the car's 128-beam
+// chunk pairs by their longer chunk, ties by descending index, so the long
+// grazing-beam chunks start first and the short ones fill in behind them
+// (offline model: 103.1 -> 98.0 trips per car, scripts/slot_merge_model.py).
 //
 // The refill pass keeps nothing in SGPRs across the loop: kernel arguments
 // are re-read at the use through kernarg_here, the scan origin and first
@@ -1087,7 +1094,7 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
 // gather every trip, a closed slot on the zero cell).  Per slot and trip: the
 // total (:141), the activity test (:133), the refill when the slot's chunk has
 // ended, the step (:135-136) and its gather.
-template <bool HANDOFF, int TAIL = 0, int SM = 0>
+template <bool HANDOFF, bool ORD = false>
 __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
     constexpr int NS = 2;
     const int wj = (int)blockIdx.x / a.EA;
@@ -1110,9 +1117,13 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
     // slot r traces chunk kk[r] (-1: closed); lane l owns beam kk[r] * 64 + l
     double x[NS], y[NS], d[NS], tot[NS], c[NS], sn[NS];
     int kk[NS];
-    int next = nch - 1 - wj;
-    int vlo = 0;  // lane k < nch: the run holding beam 64 k (one divergent search per car)
-    uint32_t srch = 0;  // the search's vector loads (lane-divergent: their wave-level count is the max)
+    int kpar[NS];         // the noise cache entry of the slot's chunk pair
+    uint32_t karm[NS];    // ORD: the trip at which the slot's chunk was armed
+    int pnext = wj;       // position of this wave's next chunk in the car's chunk order
+    // lane k < nch, packed in one VGPR: bits 0-7 the run holding beam 64 k (one divergent
+    // search per car), 8-15 (ORD) chunk k's position in the order, 16-23 its pair's rank
+    int kinfo = 0;
+    uint32_t srch = 0;    // the search's vector loads (lane-divergent: their wave-level count is the max)
     if (lane < nch) {
         const BeamRun *R = a.runs + (size_t)g * kMaxSeg;
         int lo = 0, hi = ld_const(a.nruns + g) - 1;
@@ -1122,19 +1133,45 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
             else hi = mid - 1;
             ++srch;
         }
-        vlo = lo;
+        kinfo = lo;
+    }
+    if (ORD) {
+        // pair q = chunks (2q, 2q+1), keyed by its longer chunk's previous trip count, ties by index
+        uint32_t ck = lane < nch ? (uint32_t)a.ccost[(size_t)g * nch + lane] : 0u;
+        const uint32_t pc = max(ck, (uint32_t)__shfl_xor((int)ck, 1, 64));
+        const uint32_t key = pc * 64u + (uint32_t)(lane >> 1);
+        const int npair = (nch + 1) >> 1;
+        int kpos = 0, krank = 0;
+        for (int q = 0; q < npair; ++q) {  // pairs ranked ahead of this lane's pair and their chunks
+            const uint32_t kq = __builtin_amdgcn_readlane(key, 2 * q);
+            const bool ahead = kq > key;
+            krank += ahead ? 1 : 0;
+            kpos += ahead ? (2 * q + 1 < nch ? 2 : 1) : 0;
+        }
+        kpos += ((lane & 1) == 0 && lane + 1 < nch) ? 1 : 0;  // inside a pair the higher chunk goes first
+        kinfo |= (kpos << 8) | (krank << 16);
+        ++srch;
     }
     // wave-level vector loads other than the slot gathers (SIMT / TA accounting, counter 3):
     // the arms' and finishes' table loads, the guard-band re-gathers (wave-uniform, scalar)
     uint32_t loads = 0;
+    uint32_t trips = 0;
     // in_loop: the slot's next `tot += d` completes tot = d (:130)
     auto arm = [&](int r, bool in_loop) {
         const RayArgs &K = kernarg_here();
-        const int k = next;
-        next -= wstride;
+        int k;
+        if (ORD) {
+            k = __builtin_ctzll(__builtin_amdgcn_ballot_w64(lane < nch && ((kinfo >> 8) & 255) == pnext));
+            kpar[r] = (__builtin_amdgcn_readlane(kinfo, k) >> 16) & 1;
+            karm[r] = trips;
+        } else {
+            k = nch - 1 - pnext;
+            kpar[r] = (k >> 1) & 1;
+        }
+        pnext += wstride;
         kk[r] = k;
         const int b = k * 64 + lane, bc = b < B ? b : B - 1;
-        const int lo = __builtin_amdgcn_readlane(vlo, k);
+        const int lo = __builtin_amdgcn_readlane(kinfo, k) & 255;
         int ti = (int)beam_theta(K.runs + (size_t)g * kMaxSeg, ld_const(K.nruns + g), lo, k * 64, bc);  // :124
         if (ti >= K.theta_dis) ti = 0;
         const double2 t2 = ld_off(reinterpret_cast<const double2 *>(K.cs2), (uint32_t)ti * 16u);
@@ -1149,8 +1186,9 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
     uint32_t lanes = 0;
     // device noise: chunks 2p and 2p + 1 (beams b and b + 64 of a 128-beam block) share one
     // Philox draw (beam_normal_pair_k); the half a finished chunk does not use is kept for its
-    // partner in a two-entry cache indexed by p & 1 (the open pairs are p and p - 1: the
-    // slots take the car's chunks in descending order), so most pairs are drawn once
+    // partner in a two-entry cache whose entry alternates from pair to pair in the chunk order
+    // (the open pairs are two consecutive ones: the slots take a pair's chunks one after the
+    // other), so most pairs are drawn once
     float cval[2] = {0.0f, 0.0f};
     int ctag[2] = {-1, -1};
     auto finish = [&](int r) {  // the ended chunk's outputs (fx_epilogue, noise after the clamp)
@@ -1163,7 +1201,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
             nz = K.noise_ext[(size_t)e * B + bc];
             ++loads;
         } else if (K.noise_std > 0.0) {
-            const int pp = kk[r] >> 1, ci = pp & 1;
+            const int pp = kk[r] >> 1, ci = kpar[r];
             float nv;
             if (ctag[ci] == pp) {
                 nv = cval[ci];
@@ -1199,10 +1237,14 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
             if (K.scans_f64) *reinterpret_cast<double *>(reinterpret_cast<char *>(K.scans_f64 + row) + (uint32_t)b * 8u) = range;
             if (HANDOFF) *reinterpret_cast<double *>(reinterpret_cast<char *>(K.scan + row) + (uint32_t)b * 8u) = range;
         }
+        if (ORD && lane == 0) {  // this chunk's trips, the next launch's order key
+            const uint32_t t = trips - karm[r];
+            K.ccost[(size_t)g * nch + kk[r]] = (uint8_t)(t < 255u ? t : 255u);
+        }
         lanes += (uint32_t)min(64, B - kk[r] * 64);  // the chunk's beams (scalar)
     };
 
-    uint32_t lane_iters = 0, slot_gathers = 0, smem_loads = 0;
+    uint32_t lane_iters = 0, slot_gathers = 0;
     const double ux = fma(ld_const(a.ray0 + g), L.ir, L.cxk) - kFxpBase;
     const double uy = fma(ld_const(a.ray0 + a.EA + g), L.ir, L.cyk) - kFxpBase;
     // q + P of the scan origin inside [fxp_lo, fxp_h*): its rays stay in the padded table (false for NaN)
@@ -1215,105 +1257,49 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
         }
 #pragma unroll
         for (int r = 0; r < NS; ++r)
-            if (next >= 0) arm(r, true);  // tot = 0: the first trip's total completes tot = d00
+            if (pnext < nch) arm(r, true);  // tot = 0: the first trip's total completes tot = d00
         __builtin_amdgcn_s_waitcnt(0);
-        uint32_t steps = 0, scalar_steps = 0, skipped = 0;  // slot steps; those without a vector gather
-        // slot r's step (:135-136) and its gather: a vector gather, or (SM) scalar loads for the
-        // <= SM active lanes of a slot in its chunk's tail and none for a slot without one
-        auto step_slot = [&](auto R, bool act, uint64_t m) {
-            constexpr int r = decltype(R)::value;
-            bool near;
-            const uint32_t off = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act,
-                                               zero_v, near);
-            const uint32_t cnt = SM ? (uint32_t)__popcll(m) : 64u;
-            if (SM == 0 || cnt > (uint32_t)SM) {
-                d[r] = ld_off(dt, off);
-            } else {  // wave-uniform: an ended lane reads 0.0, as from the zero cell
-                double v = 0.0;
-                uint64_t mm = m;
+        for (;;) {
 #pragma unroll
-                for (int j = 0; j < SM; ++j) {
-                    if (mm) {
-                        const int l = __builtin_ctzll(mm);
-                        mm &= mm - 1;
-                        const uint32_t o = __builtin_amdgcn_readlane(off, l);
-                        const double sv = ld_const(reinterpret_cast<const double *>(reinterpret_cast<const char *>(dt) + o));
-                        v = lane == l ? sv : v;
+            for (int r = 0; r < NS; ++r) {
+                tot[r] += d[r];  // :141 (d00 for a freshly armed slot: tot = d00, :130)
+                bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+                uint64_t m = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+                if (!m && kk[r] >= 0) {  // wave-uniform, rare: the slot's chunk has ended; refill it
+                    finish(r);
+                    if (pnext < nch) {
+                        arm(r, false);  // tot = d = d00
+                        act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+                        m = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+                    } else {
+                        kk[r] = -1;
                     }
+                    // the refill's own loads (tables) land here, so that the common path's wait
+                    // before the step stays vmcnt(1) (the other slot's gather may be in flight)
+                    __builtin_amdgcn_s_waitcnt(0);
                 }
-                d[r] = v;
-                scalar_steps += cnt ? 1u : 0u;
-                skipped += cnt ? 0u : 1u;
-            }
-            const uint64_t nb = __builtin_amdgcn_ballot_w64(near) & m;
-            if (nb) {  // rare: lanes within the guard band re-gather from the IEEE cell
-                const RayArgs &K = kernarg_here();
-                if (lane_in(nb)) d[r] = ld_off(dt, exact_offset_pad(K.m, x[r], y[r], (uint32_t)K.fxp_P));
-                ++loads;
-            }
-        };
-        // one trip of slot r: the total (:141), the activity test (:133), the refill when the
-        // slot's chunk has ended, the step and its gather.  Returns true (TAIL) when the slot has
-        // just closed: the other slot then runs alone
-        auto trip = [&](auto R) -> bool {
-            constexpr int r = decltype(R)::value;
-            tot[r] += d[r];  // :141 (d00 for a freshly armed slot: tot = d00, :130)
-            bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
-            uint64_t m = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
-            if (!m && kk[r] >= 0) {  // wave-uniform, rare: the slot's chunk has ended; refill it
-                finish(r);
-                if (next >= 0) {
-                    arm(r, false);  // tot = d = d00
-                    act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
-                    m = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
-                } else {
-                    kk[r] = -1;
-                    if (TAIL) return true;
+                lane_iters += (uint32_t)__popcll(m);
+                bool near;
+                const uint32_t off = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act,
+                                                   zero_v, near);
+                d[r] = ld_off(dt, off);
+                const uint64_t nb = __builtin_amdgcn_ballot_w64(near) & m;
+                if (nb) {  // rare: lanes within the guard band re-gather from the IEEE cell
+                    const RayArgs &K = kernarg_here();
+                    if (lane_in(nb)) d[r] = ld_off(dt, exact_offset_pad(K.m, x[r], y[r], (uint32_t)K.fxp_P));
+                    ++loads;
                 }
-                // the refill's own loads (tables) land here, so that the common path's wait
-                // before the step stays vmcnt(1) (the other slot's gather may be in flight)
-                __builtin_amdgcn_s_waitcnt(0);
             }
-            lane_iters += (uint32_t)__popcll(m);
-            step_slot(R, act, m);
-            return false;
-        };
-        const std::integral_constant<int, 0> I0;
-        const std::integral_constant<int, 1> I1;
-        int alone = TAIL && kk[1] < 0 ? 0 : -1;  // TAIL: the slot left running alone
-        uint32_t trips = 0;
-        if (alone < 0) {
-            for (;;) {
-                if (trip(I0)) {
-                    alone = 1;
-                    break;
-                }
-                if (trip(I1)) {
-                    alone = 0;
-                    break;
-                }
-                ++trips;
-                if (!TAIL && kk[0] < 0 && kk[1] < 0) break;
-            }
+            ++trips;
+            bool open = false;
+#pragma unroll
+            for (int r = 0; r < NS; ++r) open |= kk[r] >= 0;
+            if (!open) break;
         }
-        steps = trips * NS;
-        if (TAIL) {  // the last open slot alone: one gather per trip
-            auto tail = [&](auto R) {
-                for (;;) {
-                    ++steps;
-                    if (trip(R)) break;
-                }
-                --steps;  // the closing trip gathers nothing
-            };
-            if (alone == 0) tail(I0);
-            else if (alone == 1) tail(I1);
-            steps += alone == 0 ? trips : 0u;  // slot 0 stepped in the main loop's last, partial trip
-        }
-        slot_gathers = steps - scalar_steps - skipped;
-        smem_loads = scalar_steps;
+        slot_gathers = trips * NS;  // every trip gathers in both slots (a closed slot on the zero cell)
     } else {  // an origin off the map: the IEEE cell of every lookup, chunk after chunk
         uint32_t cnt = 0;
-        while (next >= 0) {
+        while (pnext < nch) {
             arm(0, false);
             const RayArgs &K = kernarg_here();
             uint32_t cc = 0;
@@ -1325,10 +1311,11 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
                 ++cc;
             }
             cnt += cc;
-            if (K.count_slots) slot_gathers += wave_max(cc);  // the chunk's wave-level gathers
+            trips += wave_max(cc);  // the chunk's wave-level gathers (its trip count for ORD)
             finish(0);
         }
         lane_iters = wave_sum(cnt);
+        slot_gathers = trips;
     }
     if (lane == 0) {
         const RayArgs &K = kernarg_here();
@@ -1340,10 +1327,9 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
         if (K.count_slots) {
             atomicAdd(cs + 2, (unsigned long long)slot_gathers * 64ull);
             atomicAdd(cs + 3, (unsigned long long)loads);
-            if (SM) atomicAdd(cs + 4, (unsigned long long)smem_loads);  // slot steps on scalar loads
         }
     }
-    if (a.count_slots) {  // the run search's wave-level loads (counter 3)
+    if (a.count_slots) {  // the run search's (and ORD's cost read's) wave-level loads (counter 3)
         const uint32_t ws = wave_max(srch);
         if (lane == 0) atomicAdd(a.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride + 3, (unsigned long long)ws);
     }
@@ -1797,14 +1783,14 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                 ra.fxs_cy = std::fma(-a.tmap.oy, a.tmap.inv_res, kFxsBase + P + kFxsShift);
                 if (a.fx_refill > 0 && a.fxs_ok && !mask && ra.HB == 0 && !ra.wcost) {
                     // one wave per car, two chunk slots with refill (k_rays_fxs; no heavy-first)
-                    // f110_set_ray_variant (A/B): bit 0 the lone slot's tail loop, bits 1-2 scalar
-                    // gathers for slots with <= 1 / 2 / 4 active lanes
-#define F110_FXS(T, S) {reinterpret_cast<const void *>(&k_rays_fxs<false, T, S>), \
-                        reinterpret_cast<const void *>(&k_rays_fxs<true, T, S>)}
-                    const void *fs[8][2] = {F110_FXS(0, 0), F110_FXS(1, 0), F110_FXS(0, 1), F110_FXS(1, 1),
-                                            F110_FXS(0, 2), F110_FXS(1, 2), F110_FXS(0, 4), F110_FXS(1, 4)};
-#undef F110_FXS
-                    f = fs[a.fxs_variant & 7][single ? 0 : 1];
+                    // f110_set_ray_variant (A/B): 1 = longest chunk pair first (ORD)
+                    const void *fs[2][2] = {{reinterpret_cast<const void *>(&k_rays_fxs<false, false>),
+                                             reinterpret_cast<const void *>(&k_rays_fxs<true, false>)},
+                                            {reinterpret_cast<const void *>(&k_rays_fxs<false, true>),
+                                             reinterpret_cast<const void *>(&k_rays_fxs<true, true>)}};
+                    const int ord = a.fxs_variant == 1 && a.ccost ? 1 : 0;
+                    ra.ccost = a.ccost;
+                    f = fs[ord][single ? 0 : 1];
                     ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
                     g2 = dim3((unsigned)(ra.EA * ra.G4));
                 }

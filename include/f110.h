@@ -314,11 +314,11 @@ F110_API int f110_ray_refill(const f110_ctx *ctx);
  * once, not one context's.  Any time.  Scheduling only: results are unchanged. */
 F110_API int f110_set_ray_refill(f110_ctx *ctx, int32_t waves);
 
-/* A/B of k_rays_fxs's variants for the following steps (0 = the default;
- * bit 0: the slot left alone once the other has closed runs a one-slot loop;
- * bits 1-2 = 1 / 2 / 3: slots with at most 1 / 2 / 4 active lanes gather by
- * scalar loads).  Scheduling only: results are bit-identical.  Measurement
- * hook (scripts/ray_ab.py), no reference counterpart. */
+/* A/B of k_rays_fxs's variants for the following steps (0 = the default,
+ * chunks in descending order; 1 = the car's chunk pairs longest first by the
+ * previous launch's per-chunk trip counts).  Scheduling only: results are
+ * bit-identical.  Measurement hook (scripts/ray_ab.py), no reference
+ * counterpart. */
 F110_API int f110_set_ray_variant(f110_ctx *ctx, int32_t variant);
 
 /* Sets the rays per lane of the fixed-point ray kernel (1 or 2) before the
@@ -373,6 +373,16 @@ F110_API int f110_host_beam_indices(double yaw, double fov, int32_t theta_dis, i
  * points. */
 F110_API int f110_host_cell_index(int32_t H, int32_t W, double resolution, const double origin[3], const double *xy,
                                   int64_t n, int64_t *lin_out);
+
+/* The EDT table f110_create uploads for the fixed-point ray kernels, built on
+ * the host: kind 0 the row-major table (rows of W + 1 cells rounded up to 16,
+ * dt[-1,-1] in the padding, a 0.0 zero cell after the last row), kind 1 the
+ * table padded by `pad` cells of dt[-1,-1] on every side (rows of 511 mod 512
+ * cells; not built past its 32-bit / 24-bit offset limits: returns 0).
+ * Returns the length in doubles; fills out[] when out_len suffices; meta =
+ * {rows, cols, zero-cell byte offset or -1}.  Host test hook. */
+F110_API int64_t f110_host_map_table(const uint32_t *edt_k, int32_t H, int32_t W, double res, int32_t kind,
+                                     int32_t pad, double *out, int64_t out_len, int64_t meta[3]);
 
 /* The beam-index ranges (r0a..r0b, r1a..r1b; empty when a > b) the agent
  * ray_cast visits for an opponent box whose angular window at the scan

@@ -30,6 +30,32 @@
 
 #define OR_API __attribute__((visibility("default")))
 
+/* Residue attribution (not the reference's arithmetic): the
+ * sin / cos calls whose device counterparts are the correctly rounded
+ * cr_sincos (dynamics, scan pose, get_vertices, ray_cast beam direction,
+ * get_blocked_view_indices' ego bearing) go through or_sin / or_cos.  By
+ * default they are glibc's sin / cos, as NumPy's and Numba's; with a hook set
+ * (or_set_sincos_hook: libf110's f110_host_sincos, the host copy of
+ * cr_sincos) the oracle reproduces the device's trig, so whatever still
+ * differs from the device is not glibc's own last-ulp error.  The lookup
+ * tables (sines / cosines, RaceCar's beam tables) stay glibc's: the device
+ * uses the host's tables too. */
+typedef void (*or_sincos_fn)(const double *x, int64_t n, double *sn, double *cs);
+static or_sincos_fn g_sincos_hook = NULL;
+OR_API void or_set_sincos_hook(or_sincos_fn fn) { g_sincos_hook = fn; }
+static double or_sin(double x) {
+    if (!g_sincos_hook) return sin(x);
+    double s, c;
+    g_sincos_hook(&x, 1, &s, &c);
+    return s;
+}
+static double or_cos(double x) {
+    if (!g_sincos_hook) return cos(x);
+    double s, c;
+    g_sincos_hook(&x, 1, &s, &c);
+    return c;
+}
+
 typedef struct {
     double mu, C_Sf, C_Sr, lf, lr, h, m, I, s_min, s_max, sv_min, sv_max, v_switch, a_max,
         v_min, v_max, width, length;
@@ -272,8 +298,8 @@ OR_API void or_vehicle_dynamics_ks(const double *x, const double *u_init, const 
     double lwb = p->lf + p->lr;
     double u0 = or_steering_constraint(x[2], u_init[0], p->s_min, p->s_max, p->sv_min, p->sv_max);
     double u1 = or_accl_constraints(x[3], u_init[1], p->v_switch, p->a_max, p->v_min, p->v_max);
-    f[0] = x[3] * cos(x[4]);
-    f[1] = x[3] * sin(x[4]);
+    f[0] = x[3] * or_cos(x[4]);
+    f[1] = x[3] * or_sin(x[4]);
     f[2] = u0;
     f[3] = u1;
     f[4] = x[3] / lwb * tan(x[2]);
@@ -291,7 +317,7 @@ OR_API void or_vehicle_dynamics_st(const double *x, const double *u_init, const 
         double lwb = lf + lr;
         double fks[5];
         or_vehicle_dynamics_ks(x, u, p, fks); /* re-applies the (idempotent) constraints */
-        double c2 = cos(x[2]);
+        double c2 = or_cos(x[2]);
         f[0] = fks[0];
         f[1] = fks[1];
         f[2] = fks[2];
@@ -303,8 +329,8 @@ OR_API void or_vehicle_dynamics_st(const double *x, const double *u_init, const 
         double glr_m = g * lr - u[1] * h; /* (g*lr - u[1]*h) */
         double glf_p = g * lf + u[1] * h; /* (g*lf + u[1]*h) */
         double lrlf = lr + lf;
-        f[0] = x[3] * cos(x[6] + x[4]);
-        f[1] = x[3] * sin(x[6] + x[4]);
+        f[0] = x[3] * or_cos(x[6] + x[4]);
+        f[1] = x[3] * or_sin(x[6] + x[4]);
         f[2] = u[0];
         f[3] = u[1];
         f[4] = x[5];
@@ -422,7 +448,7 @@ OR_API int or_check_ttc(const double *scan, int nb, double vel, const double *co
 
 /* get_trmtx + get_vertices, collision_models.py:218-260; out [rl, rr, fr, fl] x (x,y). */
 OR_API void or_get_vertices(const double *pose, double length, double width, double *v) {
-    double c = cos(pose[2]), s = sin(pose[2]);
+    double c = or_cos(pose[2]), s = or_sin(pose[2]);
     const double px[4] = {-length / 2, -length / 2, length / 2, length / 2};
     const double py[4] = {width / 2, -width / 2, -width / 2, width / 2};
     for (int k = 0; k < 4; ++k) {
@@ -531,7 +557,7 @@ static double or_get_range(const double *pose, double beam_theta, const double *
     double o[2] = {pose[0], pose[1]};
     double v1[2] = {o[0] - va[0], o[1] - va[1]};
     double v2[2] = {vb[0] - va[0], vb[1] - va[1]};
-    double v3[2] = {cos(beam_theta + M_PI / 2.), sin(beam_theta + M_PI / 2.)};
+    double v3[2] = {or_cos(beam_theta + M_PI / 2.), or_sin(beam_theta + M_PI / 2.)};
     double denom = dot2(v2, v3);
     double distance = INFINITY;
     if (fabs(denom) > 0.0) {
@@ -554,7 +580,7 @@ static double or_get_range(const double *pose, double beam_theta, const double *
 
 /* get_blocked_view_indices, laser_models.py:282-315 */
 static void or_blocked(const double *pose, const double *v, const double *angles, int nb, int *lo, int *hi) {
-    double ex = cos(pose[2]), ey = sin(pose[2]);
+    double ex = or_cos(pose[2]), ey = or_sin(pose[2]);
     int inds[4];
     for (int i = 0; i < 4; ++i) {
         double vx = v[2 * i] - pose[0], vy = v[2 * i + 1] - pose[1];
@@ -653,7 +679,7 @@ static void or_sim_step_env(const or_sim *S, int64_t env, double *state, double 
     for (int i = 0; i < A; ++i) { /* :581-587 */
         double *st = state + 7 * i;
         or_update_pose(st, buf + 2 * i, cnt + i, act[2 * i], act[2 * i + 1], S->p, S->dt, S->integrator);
-        double scan_pose[3] = {st[0] + S->lidar_dist * cos(st[4]), st[1] + S->lidar_dist * sin(st[4]), st[4]};
+        double scan_pose[3] = {st[0] + S->lidar_dist * or_cos(st[4]), st[1] + S->lidar_dist * or_sin(st[4]), st[4]};
         or_get_scan(S->sc, scan_pose, scans + (size_t)i * B, NULL, NULL);
         if (noisy) /* after the clamp, laser_models.py:450-452 */
             for (int b = 0; b < B; ++b) scans[(size_t)i * B + b] += noise[b];

@@ -94,6 +94,40 @@ def lib():
     return _lib
 
 
+_HOOK_KEEP = []
+
+
+def set_device_trig(on: bool = True):
+    """Residue attribution only: route the oracle's sin / cos at
+    the sites the device evaluates with its correctly rounded cr_sincos
+    through libf110's host copy of it (f110_host_sincos); off restores glibc
+    (the reference's).  The scan tables stay glibc's either way."""
+    L = lib()
+    if not hasattr(L, "_hooked"):
+        L.or_set_sincos_hook.argtypes = [ctypes.c_void_p]
+        L.or_set_sincos_hook.restype = None
+        L._hooked = True
+    if not on:
+        L.or_set_sincos_hook(None)
+        return
+    from f110_gymnasium_ros2_jazzy_amd import _lib as F
+    fn = F.load().f110_host_sincos
+    _HOOK_KEEP[:] = [fn]
+    L.or_set_sincos_hook(ctypes.cast(fn, ctypes.c_void_p))
+
+
+class device_trig:
+    """Context manager: set_device_trig(True) inside, glibc again after."""
+
+    def __enter__(self):
+        set_device_trig(True)
+        return self
+
+    def __exit__(self, *exc):
+        set_device_trig(False)
+        return False
+
+
 def _p(a, t=_D):
     return a.ctypes.data_as(t)
 

@@ -128,18 +128,25 @@ def test_c4_8192x2_lockstep_sample(tracks, gpu, oracle_scanners, nonexact_budget
     poses = np.stack([cl[i0], cl[(i0 + gap) % n]], 1)
     sim = BatchSim(tracks("Spielberg_map"), n_envs=E, n_agents=A, device=gpu, noise_std=0.0, keep_f64_scans=True)
     ref = O.OracleSim(oracle_scanners("Spielberg_map"), S, A)
+    # residue attribution: the oracle with the device's correctly rounded sin / cos
+    refd = O.OracleSim(oracle_scanners("Spielberg_map"), S, A)
     sim.reset(poses)
     ref.reset(poses[:S])
     rs, rc = ref.step(np.zeros((S, A, 2)))
+    with O.device_trig():
+        refd.reset(poses[:S])
+        rd, _ = refd.step(np.zeros((S, A, 2)))
     g = torch.Generator(device=gpu)
     g.manual_seed(44)
-    nonexact = gjk = occluded = 0
+    nonexact = nonexact_d = gjk = occluded = 0
     clean = BatchSim(tracks("Spielberg_map"), n_envs=S, n_agents=1, device=gpu, noise_std=0.0)
     for t in range(T + 1):
         if t:
             act = _actions(g, E, A, gpu)
             out = sim.step(act)
             rs, rc = ref.step(act[:S].double().cpu().numpy())
+            with O.device_trig():
+                rd, _ = refd.step(act[:S].double().cpu().numpy())
         else:
             out = sim.out
         torch.cuda.synchronize()
@@ -148,6 +155,7 @@ def test_c4_8192x2_lockstep_sample(tracks, gpu, oracle_scanners, nonexact_budget
         sc = out.scans_f64[:S].cpu().numpy()
         np.testing.assert_allclose(sc, rs, rtol=1e-9, atol=1e-9)
         nonexact += int(np.sum(sc != rs))
+        nonexact_d += int(np.sum(sc != rd))
         col = out.collisions[:S].cpu().numpy()
         assert np.array_equal(col, rc.astype(np.uint8)), t
         gjk += int(col.all(1).sum())
@@ -157,11 +165,13 @@ def test_c4_8192x2_lockstep_sample(tracks, gpu, oracle_scanners, nonexact_budget
         live = col[:, 0] == 0  # a TTC response zeroes the yaw after the scan
         occluded += int(np.sum(sc[live, 0] < bare[live]))
         ref.state[:] = st[:S].reshape(S * A, 7)
+        refd.state[:] = ref.state
         # the rest of the batch: ranges in [0, 30], obs finite
         full = out.scans_f64
         assert bool(((full >= 0) & (full <= 30)).all()) and bool(torch.isfinite(out.obs).all())
     assert gjk > 0 and occluded > 0, (gjk, occluded)
     nonexact_budget("c4_8192x2_sample256_20steps", nonexact)
+    nonexact_budget("c4_8192x2_sample256_20steps/device_trig_oracle", nonexact_d)
     clean.close()
     sim.close()
 

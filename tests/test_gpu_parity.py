@@ -280,20 +280,31 @@ def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A, nonexact
     poses = _adversarial_poses(rng, E, A, centerline_spawns("Spielberg", 1))
     sim = sims("Spielberg_map", E, A)
     ref = O.OracleSim(oracle_scanners("Spielberg_map"), E, A)
+    # residue attribution: the same oracle with the device's correctly rounded
+    # sin / cos in place of glibc's at the sites the device computes them
+    refd = O.OracleSim(oracle_scanners("Spielberg_map"), E, A)
     sim.reset(poses)
     ref.reset(poses)
     rs, rc = ref.step(np.zeros((E, A, 2)))
-    nonexact = 0
+    with O.device_trig():
+        refd.reset(poses)
+        rd, _ = refd.step(np.zeros((E, A, 2)))
+    nonexact = nonexact_d = 0
     for t in range(4):
         g = sim.out.scans_f64.cpu().numpy()
         np.testing.assert_allclose(g, rs, rtol=1e-9, atol=1e-9)
         nonexact += int(np.sum(g != rs))
+        nonexact_d += int(np.sum(g != rd))
         np.testing.assert_array_equal(sim.out.collisions.cpu().numpy(), rc.astype(np.uint8))
         act = np.stack([rng.uniform(-0.2, 0.2, (E, A)), rng.uniform(0, 3, (E, A))], -1)
         ref.state[:] = sim.agent_states().cpu().numpy().reshape(E * A, 7)
+        refd.state[:] = ref.state
         sim.step(act)
         rs, rc = ref.step(act)
+        with O.device_trig():
+            rd, _ = refd.step(act)
     nonexact_budget(f"ray_cast_adversarial_A{A}", nonexact)
+    nonexact_budget(f"ray_cast_adversarial_A{A}/device_trig_oracle", nonexact_d)
 
 
 @pytest.mark.parametrize("kernel,lanes,pad,refill", [

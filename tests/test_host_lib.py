@@ -312,3 +312,37 @@ def test_cr_sincos_matches_numpy():
     L.f110_host_sincos(xn.ctypes.data_as(ctypes.c_void_p), 2, sn.ctypes.data_as(ctypes.c_void_p),
                        cn.ctypes.data_as(ctypes.c_void_p))
     assert np.isnan(sn).all() and np.isnan(cn).all()
+
+
+@pytest.mark.parametrize("H,W,pad", [(7, 5, 3), (40, 33, 12), (1, 1, 1), (16, 15, 0)])
+def test_host_map_tables(L, H, W, pad):
+    """The fixed-point kernels' EDT tables as f110_create builds them
+    (f110_host_map_table, the same host code): the row-major table (rows of
+    W + 1 rounded up to 16 cells, dt[-1,-1] in the padding column / row, a 0.0
+    zero cell after the last row) and the padded one (pad cells of dt[-1,-1]
+    on every side, rows of 511 mod 512 cells, the zero cell after the last
+    row), checked cell by cell against a NumPy construction."""
+    rng = np.random.default_rng(H * 100 + W)
+    k = rng.integers(0, 50, (H, W)).astype(np.uint32)
+    res = 0.05
+    dt = res * np.sqrt(k.astype(np.float64))
+    meta = np.zeros(3, np.int64)
+    for kind in (0, 1):
+        n = L.f110_host_map_table(k.ctypes.data, H, W, res, kind, pad, None, 0, meta.ctypes.data)
+        rows, cols, zero = (int(v) for v in meta)
+        if kind == 1 and pad == 0:
+            assert n == 0 and zero == -1  # no padded table without padding
+            continue
+        out = np.full(n, np.nan)
+        assert L.f110_host_map_table(k.ctypes.data, H, W, res, kind, pad, out.ctypes.data, n, meta.ctypes.data) == n
+        assert n == rows * cols + 16 and zero == rows * cols * 8
+        ref = np.full(rows * cols + 16, dt[-1, -1])
+        grid = ref[:rows * cols].reshape(rows, cols)
+        if kind == 0:
+            assert cols % 16 == 0 and cols >= W + 1 and rows == H + 1
+            grid[:H, :W] = dt
+        else:
+            assert cols % 512 == 511 and cols >= W + 2 * pad + 1 and rows == H + 2 * pad
+            grid[pad:pad + H, pad:pad + W] = dt
+        ref[rows * cols] = 0.0
+        assert np.array_equal(out, ref)
