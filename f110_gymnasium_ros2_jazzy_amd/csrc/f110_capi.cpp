@@ -1030,7 +1030,7 @@ extern "C" int f110_set_ray_lanes(f110_ctx *ctx, int32_t n) {
 
 extern "C" int f110_set_ray_variant(f110_ctx *ctx, int32_t variant) {
     if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_variant: null context");
-    if (variant < 0 || variant > 1) return fail(F110_E_INVALID, "f110_set_ray_variant: variant must be 0 or 1");
+    if (variant < 0 || variant > 7) return fail(F110_E_INVALID, "f110_set_ray_variant: variant must be in 0..7");
     ctx->fxs_variant = variant;
     return F110_OK;
 }
@@ -1257,7 +1257,9 @@ extern "C" int f110_debug_wave_trace(f110_ctx *ctx, int32_t arm, uint64_t *host_
     if (!ctx) return fail(F110_E_INVALID, "f110_debug_wave_trace: null context");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     const int64_t EA = (int64_t)ctx->cfg.n_envs * ctx->cfg.n_agents;
-    const int64_t waves = ((EA + 3) / 4) * ((ctx->cfg.n_beams + 63) / 64) * (kRayBlock / 64);
+    // an upper bound of any ray launch's waves (one-wave blocks: the chunked grids' EA x nch
+    // plus the heavy-first prefix; k_rays_fxs: EA x waves per car <= EA x nch)
+    const int64_t waves = EA * ((ctx->cfg.n_beams + 63) / 64) + ctx->heavy_cap + 64;
     if (!ctx->wtrace) {
         void *q = nullptr;
         HIP_TRY(hipMalloc(&q, (size_t)waves * 4 * sizeof(uint64_t)));

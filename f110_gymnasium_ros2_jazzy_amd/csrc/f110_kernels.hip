@@ -254,6 +254,20 @@ __device__ __forceinline__ const RayArgs *kernarg_rays() {
 #endif
 }
 
+// The kernarg block behind an opaque copy of its pointer: loads through it
+// stay where they are written (in the refill pass) instead of being hoisted
+// out of the trace loop into SGPRs, which would spill there: an opaque SGPR copy of a pointer to read-only kernel arguments, typed in the
+// constant address space: its field loads are scalar loads placed at the use
+// (a generic pointer out of the asm would make them flat vector loads)
+template <class T>
+__device__ __forceinline__ const T *launder_const(const T *ptr) {
+    const __attribute__((address_space(4))) T *p;
+    asm volatile("s_mov_b64 %0, %1" : "=s"(p) : "s"(ptr));
+    return (const T *)p;
+}
+
+__device__ __forceinline__ const RayArgs &kernarg_here() { return *launder_const(kernarg_rays()); }
+
 // Lookup statistics of one wave's trace, the same in every lane: lookups
 // made, lanes that traced a ray, the longest ray's lookups.
 struct WaveLookups {
@@ -594,6 +608,25 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {  // set bits of
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// Diagnostic wave trace of the one-wave-block ray kernels (f110_debug_wave_trace;
+// the pointer is null in every other launch): lane 0 stores the wave's start
+// time (s_memrealtime, 100 MHz) at entry and its end time, hardware id, XCC and
+// work item (item << 32 | car) at exit, 4 u64 per block, with vector stores.
+__device__ __forceinline__ void wave_stamp_start(uint64_t *wt) {
+    if (wt && threadIdx.x == 0) wt[4 * (size_t)blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+}
+__device__ __forceinline__ void wave_stamp_end(uint64_t *wt, uint32_t item, uint32_t g) {
+    if (wt && threadIdx.x == 0) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        uint64_t *o = wt + 4 * (size_t)blockIdx.x;
+        o[1] = __builtin_amdgcn_s_memrealtime();
+        o[2] = ((uint64_t)xcc << 32) | hw;
+        o[3] = ((uint64_t)item << 32) | g;
+    }
+}
+
 // Every lane runs one ray; lanes whose ray has ended leave the loop (exec
 // mask), each lane counts its own lookups (summed once per wave), and cars
 // whose rays stay in t's binade take fx_step_safe (~36 instead of ~59
@@ -617,6 +650,7 @@ __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
         if (g >= a.EA) return;
         if (a.HB && ((ld_const(a.heavy_mask + g) >> k) & 1u)) return;  // ran in a heavy block
     }
+    wave_stamp_start(a.wtrace);
     const int lane = (int)threadIdx.x;
     const int B = a.B;
     const int b0 = k * 64;
@@ -706,6 +740,7 @@ __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
             K.wcost[(size_t)g * a.nch + k] = (uint8_t)(mx < 255u ? mx : 255u);
         }
     }
+    wave_stamp_end(kernarg_here().wtrace, (uint32_t)k, (uint32_t)g);
 }
 
 
@@ -815,6 +850,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
         grp = ng - 1 - slot;  // descending, as the chunk order of k_rays_fx
         if (a.HB && ((ld_const(a.heavy_mask + g) >> grp) & 1u)) return;  // ran in a heavy block
     }
+    wave_stamp_start(a.wtrace);
     const int lane = (int)threadIdx.x;
     const int B = a.B;
     const int b0 = grp * 64 * N;
@@ -976,6 +1012,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
             K.wcost[(size_t)g * ng + grp] = (uint8_t)(mx < 255u ? mx : 255u);
         }
     }
+    wave_stamp_end(kernarg_here().wtrace, (uint32_t)grp, (uint32_t)g);
 }
 
 // get_scan's theta index of beam bc (laser_models.py:167-184) from the car's runs;
@@ -995,19 +1032,6 @@ __device__ __forceinline__ double beam_theta(const BeamRun *R, int n, int lo, in
     return t0 + (double)(bc - rs) * dl;  // get_scan's theta_index (laser_models.py:167-184)
 }
 
-// The kernarg block behind an opaque copy of its pointer: loads through it
-// stay where they are written (in the refill pass) instead of being hoisted
-// out of the trace loop into SGPRs, which would spill there: an opaque SGPR copy of a pointer to read-only kernel arguments, typed in the
-// constant address space: its field loads are scalar loads placed at the use
-// (a generic pointer out of the asm would make them flat vector loads)
-template <class T>
-__device__ __forceinline__ const T *launder_const(const T *ptr) {
-    const __attribute__((address_space(4))) T *p;
-    asm volatile("s_mov_b64 %0, %1" : "=s"(p) : "s"(ptr));
-    return (const T *)p;
-}
-
-__device__ __forceinline__ const RayArgs &kernarg_here() { return *launder_const(kernarg_rays()); }
 
 __device__ __forceinline__ bool lane_in(uint64_t mask) {
     return (uint32_t)(mask >> (threadIdx.x & 63)) & 1u;
@@ -1097,6 +1121,7 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
 template <bool HANDOFF, bool ORD = false>
 __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
     constexpr int NS = 2;
+    wave_stamp_start(a.wtrace);
     const int wj = (int)blockIdx.x / a.EA;
     const int g = (int)blockIdx.x - wj * a.EA;
     const int lane = (int)threadIdx.x;
@@ -1333,6 +1358,8 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
         const uint32_t ws = wave_max(srch);
         if (lane == 0) atomicAdd(a.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride + 3, (unsigned long long)ws);
     }
+    wave_stamp_end(kernarg_here().wtrace, (uint32_t)(trips < 0xffffu ? trips : 0xffffu) << 8 | (uint32_t)wj,
+                   (uint32_t)g);
 }
 
 // F110Env.step's time + _check_done (f110_env.py:404-406, :310-352) and the
@@ -1641,6 +1668,193 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
     if (tid == 0) env_epilogue(a, e, &sh.stl[0][0], 7, sh.col, sh.do_reset, sh.epe, sh.epi);
 }
 
+// k_post_pair: k_post_multi's work for two-agent envs, EPB envs per wave.
+// k_post_multi's serial phases run on one or two lanes of a 128-thread block
+// per env; here every phase spreads over the EPB envs of one wave: a lane per
+// (env, car) for the loads, the TTC response, the opponent box and the
+// heading, a lane per env for GJK, a lane per (env, car, vertex) for the
+// blocked beams, a lane per (env, car) for the beam windows, then every
+// (env, car, beam) item of the agent ray_cast flattened over the wave.  Same
+// operations on the same operands as k_post_multi: bit-identical results.
+template <int EPB> struct PairSlot {
+    double stl[2][7];   // state after the TTC response
+    double pose0[2][3]; // agent_poses before the TTC response (base_classes.py:587)
+    double rv[2][8];    // pair i: opponent 1-i seen by car i (RaceCar i's params)
+    double phi[2][4];
+    double ego[2];
+    double wcen[2], whalf[2];
+    int32_t rng[2][4];
+    int32_t kq[2][4];
+    int32_t col[2];
+    int32_t valid, do_reset;
+    EpiCar epi[2];
+    EpiEnv epe;
+};
+
+template <int EPB> __global__ void __launch_bounds__(64) k_post_pair(StepArgs a) {
+    static_assert(3 * EPB <= 64 && (EPB & (EPB - 1)) == 0, "EPB: a power of two, three lanes per env");
+    reset_next_heavy(a);
+    __shared__ PairSlot<EPB> sh[EPB];
+    __shared__ int32_t off[2 * EPB];  // first ray_cast item of each (env, car) pass
+    const int lane = threadIdx.x;
+    const int B = a.B;
+    const int EA = a.E * 2;
+    const int e0 = blockIdx.x * EPB;
+    // ---- (env, car) lanes: loads, TTC response (RaceCar.check_ttc, base_classes.py:246-249)
+    if (lane < 2 * EPB) {
+        const int s = lane >> 1, i = lane & 1;
+        const int e = e0 + s;
+        PairSlot<EPB> &q = sh[s];
+        const bool valid = e < a.E && !(a.mode == 1 && a.reset_mask && !a.reset_mask[e]);
+        if (i == 0) q.valid = valid;
+        if (valid) {
+            const int g = e * 2 + i;
+            double st[7];
+#pragma unroll
+            for (int k = 0; k < 7; ++k) st[k] = a.st[(size_t)k * EA + g];
+            const int hit = a.ttc_hit[g];
+            epilogue_load_car(a, g, q.epi[i]);
+            if (i == 0) {
+                q.do_reset = a.reset_flag[e];
+                epilogue_load_env(a, e, q.epe);
+            }
+            q.pose0[i][0] = st[0];
+            q.pose0[i][1] = st[1];
+            q.pose0[i][2] = st[4];
+            q.col[i] = hit;  // Simulator.step :601-602
+            if (hit) {
+#pragma unroll
+                for (int k = 3; k < 7; ++k) {
+                    st[k] = 0.0;
+                    a.st[(size_t)k * EA + g] = 0.0;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 7; ++k) q.stl[i][k] = st[k];
+        }
+    }
+    wave_sync();
+    if (lane < 2 * EPB) {  // opponent box seen by car i, ego heading (post-TTC yaw)
+        const int s = lane >> 1, i = lane & 1;
+        PairSlot<EPB> &q = sh[s];
+        if (q.valid) {
+            const f110_params &pi = a.pa[i];
+            get_vertices(q.pose0[1 - i][0], q.pose0[1 - i][1], q.pose0[1 - i][2], pi.length, pi.width, q.rv[i]);
+            double ys, yc;
+            cr_sincos(q.stl[i][4], ys, yc);
+            q.ego[i] = atan2(ys, yc);
+        }
+    } else if (lane < 3 * EPB) {  // collision_multiple (collision_models.py:184-212) on Simulator.params boxes
+        PairSlot<EPB> &q = sh[lane - 2 * EPB];
+        if (q.valid) {
+            double v0[8], v1[8];
+            get_vertices(q.pose0[0][0], q.pose0[0][1], q.pose0[0][2], a.p.length, a.p.width, v0);
+            get_vertices(q.pose0[1][0], q.pose0[1][1], q.pose0[1][2], a.p.length, a.p.width, v1);
+            if (gjk_collision(v0, v1)) {
+                q.col[0] = 1;
+                q.col[1] = 1;
+            }
+        }
+    }
+    wave_sync();
+    for (int w = lane; w < 8 * EPB; w += 64) {  // get_blocked_view_indices, one (env, car, vertex) per lane
+        PairSlot<EPB> &q = sh[w >> 3];
+        const int i = (w >> 2) & 1, v = w & 3;
+        if (q.valid)
+            q.kq[i][v] = blocked_vertex_beam(q.stl[i][0], q.stl[i][1], q.ego[i], q.rv[i][2 * v], q.rv[i][2 * v + 1], B,
+                                             a.fov, a.beam_incr, q.phi[i][v]);
+    }
+    wave_sync();
+    int cnt = 0;
+    if (lane < 2 * EPB) {  // each pass's beams: window_beam_ranges clipped to the blocked range
+        const int s = lane >> 1, i = lane & 1;
+        PairSlot<EPB> &q = sh[s];
+        if (q.valid) {
+            int lo = q.kq[i][0], hi = q.kq[i][0];
+#pragma unroll
+            for (int v = 1; v < 4; ++v) {
+                lo = q.kq[i][v] < lo ? q.kq[i][v] : lo;
+                hi = q.kq[i][v] > hi ? q.kq[i][v] : hi;
+            }
+            double wc, wh;
+            box_beam_window(q.stl[i][0], q.stl[i][1], q.rv[i], q.phi[i], wc, wh);
+            q.wcen[i] = wc;
+            q.whalf[i] = wh;
+            int r0a, r0b, r1a, r1b;
+            window_beam_ranges(q.stl[i][4], a.fov, a.beam_incr, B, wc, wh, r0a, r0b, r1a, r1b);
+            const int ra = r0a > lo ? r0a : lo, rb = r0b < hi ? r0b : hi;
+            const int rc = r1a > lo ? r1a : lo, rd = r1b < hi ? r1b : hi;
+            q.rng[i][0] = ra;
+            q.rng[i][1] = rb;
+            q.rng[i][2] = rc;
+            q.rng[i][3] = rd;
+            cnt = (rb >= ra ? rb - ra + 1 : 0) + (rd >= rc ? rd - rc + 1 : 0);
+        }
+    }
+    int incl = cnt;  // inclusive prefix over the wave's passes
+#pragma unroll
+    for (int d = 1; d < 2 * EPB; d <<= 1) {
+        const int t = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += t;
+    }
+    const int total = __shfl(incl, 2 * EPB - 1, 64);
+    if (lane < 2 * EPB) off[lane] = incl - cnt;
+    wave_sync();
+    // agent ray_cast (base_classes.py:206-227; laser_models.py:318-346): the
+    // beams of every (env, car) pass, one item per lane
+    for (int item = lane; item < total; item += 64) {
+        int p = 0;
+#pragma unroll
+        for (int d = EPB; d >= 1; d >>= 1)
+            if (off[p + d] <= item) p += d;  // p + d <= 2 * EPB - 1
+        const int s = p >> 1, i = p & 1;
+        const PairSlot<EPB> &q = sh[s];
+        const int k = item - off[p];
+        const int n0 = q.rng[i][1] - q.rng[i][0] + 1;
+        const int b = k < (n0 > 0 ? n0 : 0) ? q.rng[i][0] + k : q.rng[i][2] + k - (n0 > 0 ? n0 : 0);
+        const double ox = q.stl[i][0], oy = q.stl[i][1], oth = q.stl[i][4];
+        const double ang = beam_angle(b, a.fov, a.beam_incr);
+        if (!(fabs(wrap_pm_pi(oth + ang - q.wcen[i])) <= q.whalf[i])) continue;  // box_beam_window
+        const double bt = oth + ang + kPi / 2.;
+        double v31, v30;
+        cr_sincos(bt, v31, v30);
+        const int e = e0 + s;
+        const size_t o = ((size_t)e * 2 + i) * B + b;
+        double cur = a.scan[o];
+        const double cur0 = cur;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int v1 = (v + 1) & 3;
+            const double rr = get_range(ox, oy, v30, v31, q.rv[i][2 * v], q.rv[i][2 * v + 1], q.rv[i][2 * v1],
+                                        q.rv[i][2 * v1 + 1]);
+            if (rr < cur) cur = rr;
+        }
+        if (cur != cur0) {  // patch the ray pass's outputs for this beam
+            a.scan[o] = cur;
+            if (a.out.scans) a.out.scans[o] = (float)cur;
+            if (a.out.scans_f64) a.out.scans_f64[o] = cur;
+            if (i == 0 && a.out.obs) a.out.obs[(size_t)e * obs_row(a) + b] = obs_scan_value(cur, (float)a.p.lidar_max);
+        }
+    }
+    // ---- outputs: pose entries (F110Env._pack_flat_obs, f110_env.py:552-584), collisions, env epilogue
+    if (lane < 2 * EPB) {
+        const int s = lane >> 1, i = lane & 1;
+        const PairSlot<EPB> &q = sh[s];
+        const int e = e0 + s;
+        if (q.valid) {
+            if (a.out.obs) {
+                float *o = a.out.obs + (size_t)e * obs_row(a) + B + 4 * i;
+                o[0] = (float)q.stl[i][0];
+                o[1] = (float)q.stl[i][1];
+                o[2] = (float)wrap_angle(q.stl[i][4]);
+                o[3] = q.col[i] ? 1.0f : 0.0f;
+            }
+            if (a.out.collisions) a.out.collisions[(size_t)e * 2 + i] = (uint8_t)q.col[i];
+            if (i == 0) env_epilogue(a, e, &q.stl[0][0], 7, q.col, q.do_reset, q.epe, q.epi);
+        }
+    }
+}
+
 // One f110_step / f110_reset: k_agents, the ray kernel, the post stage.
 // The ray kernel by context (f110_create's rules):
 //   ray_kernel 1 / 2: k_rays_tiled in flat / chunked order (rotated maps, or
@@ -1788,7 +2002,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                                              reinterpret_cast<const void *>(&k_rays_fxs<true, false>)},
                                             {reinterpret_cast<const void *>(&k_rays_fxs<false, true>),
                                              reinterpret_cast<const void *>(&k_rays_fxs<true, true>)}};
-                    const int ord = a.fxs_variant == 1 && a.ccost ? 1 : 0;
+                    const int ord = (a.fxs_variant & 1) && a.ccost ? 1 : 0;
                     ra.ccost = a.ccost;
                     f = fs[ord][single ? 0 : 1];
                     ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
@@ -1808,7 +2022,12 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     if (a.gate_record && (e = hipEventRecord(a.gate_record, s)) != hipSuccess) return e;
     if (single)
         hipExtLaunchKernelGGL(k_post_single, dim3((a.E + 63) / 64), dim3(64), 0, s, evk(4), evk(5), 0, a);
-    else
+    else if (a.A == 2 && (a.fxs_variant & 6)) {  // f110_set_ray_variant bits 1 / 2 (A/B): k_post_pair<8 / 4>
+        if (a.fxs_variant & 4)
+            hipExtLaunchKernelGGL(k_post_pair<4>, dim3((a.E + 3) / 4), dim3(64), 0, s, evk(4), evk(5), 0, a);
+        else
+            hipExtLaunchKernelGGL(k_post_pair<8>, dim3((a.E + 7) / 8), dim3(64), 0, s, evk(4), evk(5), 0, a);
+    } else
         hipExtLaunchKernelGGL(k_post_multi, dim3(a.E), dim3(kMultiBlock), 0, s, evk(4), evk(5), 0, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return hipSuccess;

@@ -265,11 +265,14 @@ F110_API int f110_profile_begin(f110_ctx *ctx, int32_t max_steps);
 F110_API int f110_profile_end(f110_ctx *ctx, double ms_out[3], int32_t *steps_out);
 
 /* ---- diagnostics -------------------------------------------------------------
- * Wave trace of the ray kernel (chunked dispatch, axis-aligned map, no reset
- * mask): arm != 0 records the next f110_step's ray launch -- per wave
- * {start, end} s_memrealtime ticks (100 MHz), {XCC id << 32 | HW_ID},
- * {chunk slot << 32 | car}.  host_out [max_waves][4] (or NULL) receives the
- * last trace (waits for `stream`); n_waves gets the wave count of a launch. */
+ * Wave trace of the ray kernel (one-wave blocks: k_rays_fx / k_rays_fxn /
+ * k_rays_fxs, or the chunked k_rays_tiled on an axis-aligned map without a
+ * reset mask): arm != 0 records the next f110_step's ray launch -- per wave
+ * (block) {start, end} s_memrealtime ticks (100 MHz), {XCC id << 32 | HW_ID},
+ * {item << 32 | car} (item: the chunk, chunk group, or k_rays_fxs's trips << 8
+ * | wave of the car).  Entries of waves that did not run stay 0.  host_out
+ * [max_waves][4] (or NULL) receives the last trace (waits for `stream`);
+ * n_waves gets the buffer's capacity in waves. */
 F110_API int f110_debug_wave_trace(f110_ctx *ctx, int32_t arm, uint64_t *host_out, int64_t max_waves,
                                    int64_t *n_waves, void *stream);
 
@@ -314,11 +317,12 @@ F110_API int f110_ray_refill(const f110_ctx *ctx);
  * once, not one context's.  Any time.  Scheduling only: results are unchanged. */
 F110_API int f110_set_ray_refill(f110_ctx *ctx, int32_t waves);
 
-/* A/B of k_rays_fxs's variants for the following steps (0 = the default,
- * chunks in descending order; 1 = the car's chunk pairs longest first by the
- * previous launch's per-chunk trip counts).  Scheduling only: results are
- * bit-identical.  Measurement hook (scripts/ray_ab.py), no reference
- * counterpart. */
+/* A/B of kernel variants for the following steps, a bit mask (0 = the
+ * defaults).  Bit 0: k_rays_fxs takes the car's chunk pairs longest first by
+ * the previous launch's per-chunk trip counts.  Bits 1 / 2: two-agent envs
+ * run their post stage as k_post_pair with 8 / 4 envs per wave.  Scheduling
+ * only: results are bit-identical.  Measurement hook (scripts/ray_ab.py), no
+ * reference counterpart. */
 F110_API int f110_set_ray_variant(f110_ctx *ctx, int32_t variant);
 
 /* Sets the rays per lane of the fixed-point ray kernel (1 or 2) before the

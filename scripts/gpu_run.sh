@@ -6,12 +6,15 @@
 # the job (no GPU step runs after a failed / faulted / timed-out one).  Output
 # goes to gpurun_out/TAG/.  Steps:
 #   suite      pytest -m gpu (one process, per-test timeout)
+#   quick      the dispatch-variant tests of tests/test_gpu_batch.py only
 #   smoke      __graft_entry__.smoke()
 #   bench      python bench.py (defaults) -> bench.json
 #   bench20    python bench.py --steps 20 --warmup 5 (the driver's settings) -> bench20.json
 #   prof       rocprofv3 --kernel-trace --stats over bench.py (no cpu leg) -> prof/, kernel_stats.csv
 #   pmc        scripts/profile_round.py TAG (kernel trace + PMC passes of the headline ray kernel)
 #   ab         scripts/ray_ab.py with the caller's AB_* environment -> ab.json
+#   abpost     scripts/ray_ab.py, two-agent post-stage variants at 8192 / 4096 envs -> abpost.json
+#   trace      scripts/wave_trace.py (WT_ENVS), one context and bench's sub-shards -> trace_*.json
 #   c4 / c5    bench.py --agents 2 --global-envs 8192 / --workload ddpg -> c4.json / c5.json
 set -o pipefail
 TAG=${1:?tag}
@@ -37,6 +40,8 @@ run() {  # name seconds cmd...
 for step in "$@"; do
     case $step in
         suite) run suite 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+        quick) run quick 600 python -u -m pytest tests/test_gpu_batch.py -m gpu -x -v --timeout 300 --timeout-method thread \
+                   -p no:cacheprovider -k "variants_identical or step_n or simt or refill_kernel" ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python -u bench.py && cp "$OUT/bench.out" "$OUT/bench.json" ;;
         bench20) run bench20 600 python -u bench.py --steps 20 --warmup 5 && cp "$OUT/bench20.out" "$OUT/bench20.json" ;;
@@ -45,6 +50,12 @@ for step in "$@"; do
               find "$OUT/prof" -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} "$OUT/kernel_stats.csv" ;;
         pmc) run pmc 900 python -u scripts/profile_round.py "$TAG" ;;
         ab) run ab 900 python -u scripts/ray_ab.py && cp "$OUT/ab.out" "$OUT/ab.json" ;;
+        abpost) AB_AGENTS=2 AB_ENVS=8192,4096 AB_STEPS=100 AB_ROUNDS=5 AB_SIMT=0 \
+                AB_VARIANTS="multi:REFILL=1,LANES=2;pair8:REFILL=1,LANES=2,VARIANT=2;pair4:REFILL=1,LANES=2,VARIANT=4;multib:REFILL=1,LANES=2" \
+                run abpost 900 python -u scripts/ray_ab.py && cp "$OUT/abpost.out" "$OUT/abpost.json" ;;
+        trace) WT_MODE=one run trace 600 python -u scripts/wave_trace.py && cp "$OUT/trace.out" "$OUT/trace_one.json" &&
+               WT_MODE=shards run trace_shards 600 python -u scripts/wave_trace.py &&
+               cp "$OUT/trace_shards.out" "$OUT/trace_shards.json" ;;
         c4) run c4 600 python -u bench.py --agents 2 --global-envs 8192 --no-cpu-baseline --no-secondary &&
             cp "$OUT/c4.out" "$OUT/c4.json" ;;
         c5) run c5 600 python -u bench.py --workload ddpg --steps 200 --warmup 20 && cp "$OUT/c5.out" "$OUT/c5.json" ;;

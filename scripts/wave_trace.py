@@ -1,84 +1,118 @@
-"""Wave timeline of one ray launch (diagnostic; GPU box).
+"""Wave timeline of the ray launch of one step (diagnostic; GPU box).
 
-For each chunk order in WT_ORDERS (';'-separated, '' = library default),
-records one traced f110_step of the 8192-env bench workload
-(f110_debug_wave_trace) and prints per-order statistics: launch span, the
-times by which 50/90/99/100 % of the waves had finished, per-XCD spans,
-occupancy (resident waves per CU) over time, and per-chunk wave durations."""
+For each size in WT_ENVS, the bench workload (Spielberg, random actions,
+noise, autoreset) runs 100 warm-up steps, then one traced step
+(f110_debug_wave_trace: per wave start / end s_memrealtime stamps, 100 MHz, on
+one clock for every context of the device).  Modes (WT_MODE):
+  one     one BatchSim context (the ray kernel f110_create picks for the size)
+  shards  streams.StreamShards as bench.py runs it (auto_streams sub-shards,
+          their ray launches traced in the same step, on one common clock)
+Per launch it prints: span, the times by which 50 / 90 / 99 / 100 % of the
+waves had ended, the in-flight wave count over time (40 bins), and the split
+into ramp (until >= 90 % of the peak in-flight waves run), steady state and
+tail (after in-flight drops below 90 % of the peak for good).  One JSON line.
+
+    WT_ENVS=8192,65536 WT_MODE=one python scripts/wave_trace.py
+"""
 import ctypes
 import json
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import numpy as np
-import torch
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
-from f110_gymnasium_ros2_jazzy_amd import _lib
-from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns, load_map
-from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
+from f110_gymnasium_ros2_jazzy_amd import _lib  # noqa: E402
+from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns, load_map  # noqa: E402
+from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim  # noqa: E402
 
-E = int(os.environ.get("WT_ENVS", 8192))
-A = int(os.environ.get("WT_AGENTS", 1))
-orders = os.environ.get("WT_ORDERS", ";0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16").split(";")
-tm = load_map("Spielberg_map")
-sp = centerline_spawns("Spielberg", A)
-rng = np.random.default_rng(12345)
-p0 = sp[rng.integers(0, sp.shape[0], E)]
-g = torch.Generator(device="cuda").manual_seed(0)
-acts = torch.rand(120, E, A, 2, device="cuda", generator=g)
-acts[..., 0] = acts[..., 0] * 0.8378 - 0.4189
-acts[..., 1] *= 20
-res = {}
-for order in orders:
-    if order:
-        os.environ["F110_CHUNK_ORDER"] = order
-    else:
-        os.environ.pop("F110_CHUNK_ORDER", None)
-    sim = BatchSim(tm, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp)
-    L = sim.L
+TICK_US = 0.01  # s_memrealtime: 100 MHz
+
+
+def read_trace(sm, arm):
     nw = ctypes.c_int64()
-    s = sim._stream()
-    sim.reset(p0)
-    for k in range(100):
-        sim.step(acts[k], minimal_outputs=True)
-    traces = []
-    for rep in range(3):
-        _lib.check(L.f110_debug_wave_trace(sim.ctx, 1, None, 0, ctypes.byref(nw), s), "trace arm")
-        sim.step(acts[100 + rep], minimal_outputs=True)
-        buf = np.zeros((nw.value, 4), np.uint64)
-        _lib.check(L.f110_debug_wave_trace(sim.ctx, 0, buf.ctypes.data, nw.value, ctypes.byref(nw), s), "trace read")
-        traces.append(buf)
-    sim.close()
-    out = []
-    for buf in traces:
-        live = buf[:, 1] > 0
-        missing = int(np.sum(~live))
-        t0 = buf[live, 0].astype(np.int64)
-        t1 = buf[live, 1].astype(np.int64)
-        base = t0.min()
-        t0 = (t0 - base) * 10e-3  # us (100 MHz ticks)
-        t1 = (t1 - base) * 10e-3
-        hw = buf[live, 2]
-        xcc = (hw >> np.uint64(32)).astype(np.int64)
-        slot = (buf[live, 3] >> np.uint64(32)).astype(np.int64)
-        dur = t1 - t0
-        span = float(t1.max())
-        fin = np.sort(t1)
-        n = fin.size
-        o = {"span_us": round(span, 2), "waves": int(n), "missing": missing,
-             "t_done_50_90_99_100": [round(float(fin[int(q * (n - 1))]), 2) for q in (0.5, 0.9, 0.99, 1.0)],
-             "last_start_us": round(float(t0.max()), 2),
-             "mean_wave_us": round(float(dur.mean()), 3), "max_wave_us": round(float(dur.max()), 2),
-             "xcc_end_us": [round(float(t1[xcc == x].max()), 1) if np.any(xcc == x) else None for x in range(8)],
-             "xcc_wave_us_sum": [round(float(dur[xcc == x].sum()), 0) for x in range(8)]}
-        bins = np.arange(0.0, span + 10, 10.0)  # resident waves per CU over time (10 us bins)
-        o["resident_waves_per_cu_10us"] = [round(float(np.sum((t0 < b0 + 10) & (t1 > b0))) / 256, 2)
-                                           for b0 in bins[:-1]]
-        slots = np.unique(slot)
-        o["slot_mean_wave_us"] = [round(float(dur[slot == q].mean()), 2) for q in slots]
-        o["slot_end_us"] = [round(float(t1[slot == q].max()), 1) for q in slots]
-        o["slot_start_us"] = [round(float(t0[slot == q].min()), 1) for q in slots]
-        out.append(o)
-    res[order or "default"] = out
-print(json.dumps(res))
+    s = sm._stream()
+    if arm:
+        _lib.check(sm.L.f110_debug_wave_trace(sm.ctx, 1, None, 0, ctypes.byref(nw), s), "trace arm")
+        return None
+    _lib.check(sm.L.f110_debug_wave_trace(sm.ctx, 0, None, 0, ctypes.byref(nw), s), "trace size")
+    buf = np.zeros((nw.value, 4), np.uint64)
+    _lib.check(sm.L.f110_debug_wave_trace(sm.ctx, 0, buf.ctypes.data, nw.value, ctypes.byref(nw), s), "trace read")
+    return buf[buf[:, 1] > 0]
+
+
+def summarize(t0, t1, bins=40):
+    base = t0.min()
+    s = (t0 - base).astype(np.float64) * TICK_US
+    e = (t1 - base).astype(np.float64) * TICK_US
+    span = float(e.max())
+    grid = np.linspace(0.0, span, 400)
+    inflight = np.array([np.sum((s <= t) & (e > t)) for t in grid])
+    peak = int(inflight.max())
+    hi = np.flatnonzero(inflight >= 0.9 * peak)
+    ramp_end = float(grid[hi[0]]) if hi.size else 0.0
+    tail_start = float(grid[hi[-1]]) if hi.size else span
+    dur = e - s
+    edges = np.linspace(0.0, span, bins + 1)
+    hist = [int(np.sum((s <= (a + b) / 2) & (e > (a + b) / 2))) for a, b in zip(edges[:-1], edges[1:])]
+    return {"waves": int(s.size), "span_us": span,
+            "end_quantiles_us": {q: float(np.quantile(e, f)) for q, f in (("p50", .5), ("p90", .9), ("p99", .99),
+                                                                            ("max", 1.0))},
+            "wave_us": {"mean": float(dur.mean()), "p50": float(np.median(dur)), "p99": float(np.quantile(dur, .99)),
+                        "max": float(dur.max())},
+            "peak_inflight": peak, "ramp_us": ramp_end, "steady_us": tail_start - ramp_end,
+            "tail_us": span - tail_start, "inflight_bins": hist}
+
+
+def main():
+    envs = [int(x) for x in os.environ.get("WT_ENVS", "8192").split(",")]
+    mode = os.environ.get("WT_MODE", "one")
+    reps = int(os.environ.get("WT_REPS", 3))
+    tm = load_map("Spielberg_map")
+    sp = centerline_spawns("Spielberg", 1)
+    res = {"mode": mode, "by_envs": {}}
+    for E in envs:
+        rng = np.random.default_rng(12345)
+        p0 = sp[rng.integers(0, sp.shape[0], E)]
+        g = torch.Generator(device="cuda")
+        g.manual_seed(0)
+        acts = torch.rand(100 + reps, E, 1, 2, device="cuda", generator=g)
+        acts[..., 0] = acts[..., 0] * 0.8378 - 0.4189
+        acts[..., 1] *= 20
+        kw = dict(n_agents=1, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=7)
+        if mode == "shards":
+            import bench
+            from f110_gymnasium_ros2_jazzy_amd.streams import StreamShards
+            S = bench.auto_streams(E, 1)
+            runner = StreamShards(tm, n_envs=E, n_streams=S, **kw)
+            sims = runner.sims
+        else:
+            runner = BatchSim(tm, n_envs=E, **kw)
+            sims = [runner]
+        runner.reset(p0)
+        for k in range(100):
+            runner.step(acts[k], minimal_outputs=True)
+        torch.cuda.synchronize()
+        out = []
+        for rep in range(reps):
+            for sm in sims:
+                read_trace(sm, True)
+            runner.step(acts[100 + rep], minimal_outputs=True)
+            torch.cuda.synchronize()
+            bufs = [read_trace(sm, False) for sm in sims]
+            allw = np.concatenate(bufs)
+            line = summarize(allw[:, 0], allw[:, 1])
+            if len(bufs) > 1:
+                line["per_shard_span_us"] = [float((b[:, 1].max() - b[:, 0].min()) * TICK_US) for b in bufs]
+            out.append(line)
+        kinds = {"ray_kernel": sims[0].ray_kernel, "lanes": sims[0].ray_lanes, "refill": sims[0].ray_refill,
+                 "contexts": len(sims)}
+        res["by_envs"][str(E)] = {"kernel": kinds, "reps": out}
+        runner.close()
+        torch.cuda.empty_cache()
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
