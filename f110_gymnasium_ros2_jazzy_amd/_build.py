@@ -13,7 +13,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libf110.so")
-SOURCES = ["f110_kernels.hip", "f110_opponent.hip", "f110_reward.hip", "f110_replay.hip", "f110_adam.hip", "f110_ddpg.hip",
+SOURCES = ["f110_kernels.hip", "f110_opponent.hip", "f110_reward.hip", "f110_replay.hip", "f110_adam.hip", "f110_ddpg.hip", "f110_gemm.hip",
            "f110_capi.cpp",
            "f110_replay_capi.cpp"]
 HEADERS = ["f110_device.h", "f110_internal.h"]

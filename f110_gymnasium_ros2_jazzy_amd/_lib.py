@@ -47,6 +47,16 @@ class F110RewardParams(ctypes.Structure):
                                              "use_progress")]
 
 
+class F110GemmOp(ctypes.Structure):  # f110_gemm_op
+    _fields_ = [(n, _P) for n in ("A", "B", "bias", "amask", "omask", "x2", "w2", "C")] + \
+               [(n, ctypes.c_int32) for n in ("N", "K", "lda", "ldb", "ldc", "ldx2", "ldw2", "nx2", "relu", "nn")]
+
+
+class F110WgradOp(ctypes.Structure):  # f110_wgrad_op
+    _fields_ = [(n, _P) for n in ("G", "gmask", "X", "dW", "db")] + \
+               [(n, ctypes.c_int32) for n in ("N", "KX", "ldg", "ldx", "ldw")]
+
+
 REWARD_STATE_BYTES = 8 * 12 + 4 * 4   # f110_reward_state
 
 F32 = 0
@@ -67,6 +77,7 @@ EXPORTS = [
     "f110_dynamics_ks_batch", "f110_collision_batch", "f110_collision_multiple", "f110_adam_step", "f110_ddpg_scratch_floats", "f110_ddpg_actor_head",
     "f110_ddpg_actor_head_bwd", "f110_ddpg_td_target", "f110_ddpg_critic_loss", "f110_ddpg_critic_loss_bwd",
     "f110_ddpg_q_mean", "f110_ddpg_q_mean_bwd", "f110_ddpg_relu_bwd_scratch_floats", "f110_ddpg_relu_bwd", "f110_ddpg_linear_relu",
+    "f110_learner_gemm", "f110_learner_wgrad_scratch_floats", "f110_learner_wgrad",
 ]
 
 _lib = None
@@ -172,24 +183,28 @@ def load(build_if_missing: bool = True):
     f32 = ctypes.c_float
     L.f110_ddpg_scratch_floats.argtypes = [i32, i32, i32]
     L.f110_ddpg_actor_head.argtypes = [_P] * 5 + [i32] * 3 + [_P] * 3
-    L.f110_ddpg_actor_head_bwd.argtypes = [_P] * 5 + [i32] * 3 + [_P] * 5
+    L.f110_ddpg_actor_head_bwd.argtypes = [_P] * 5 + [i32] * 3 + [_P] * 6
     L.f110_ddpg_td_target.argtypes = [_P] * 5 + [f32, i32, i32, _P, _P]
     L.f110_ddpg_critic_loss.argtypes = [_P] * 5 + [i32] * 2 + [_P] * 4
-    L.f110_ddpg_critic_loss_bwd.argtypes = [_P] * 5 + [i32] * 2 + [_P] * 5
+    L.f110_ddpg_critic_loss_bwd.argtypes = [_P] * 5 + [i32] * 2 + [_P] * 6
     L.f110_ddpg_q_mean.argtypes = [_P] * 3 + [f32, i32, i32] + [_P] * 3
-    L.f110_ddpg_q_mean_bwd.argtypes = [_P] * 3 + [f32, i32, i32] + [_P] * 5
+    L.f110_ddpg_q_mean_bwd.argtypes = [_P] * 3 + [f32, i32, i32] + [_P] * 6
     L.f110_ddpg_relu_bwd_scratch_floats.argtypes = [i32, i32]
     L.f110_ddpg_relu_bwd.argtypes = [_P, _P, i32, i32, _P, _P, _P, _P]
     L.f110_ddpg_linear_relu.argtypes = [_P, _P, _P, i32, i32, i32, _P, _P]
+    L.f110_learner_gemm.argtypes = [ctypes.POINTER(F110GemmOp), i32, i32, _P]
+    L.f110_learner_wgrad_scratch_floats.argtypes = [ctypes.POINTER(F110WgradOp), i32, i32]
+    L.f110_learner_wgrad.argtypes = [ctypes.POINTER(F110WgradOp), i32, i32, _P, _P]
     for name in EXPORTS:
         if name not in ("f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config",
                         "f110_host_np_sincosf", "f110_host_sincos",
                         "f110_host_tables", "f110_host_window_ranges", "f110_track_arrays",
                         "f110_default_reward_params", "f110_ddpg_scratch_floats",
-                        "f110_ddpg_relu_bwd_scratch_floats"):
+                        "f110_ddpg_relu_bwd_scratch_floats", "f110_learner_wgrad_scratch_floats"):
             getattr(L, name).restype = ctypes.c_int
     L.f110_ddpg_scratch_floats.restype = i64
     L.f110_ddpg_relu_bwd_scratch_floats.restype = i64
+    L.f110_learner_wgrad_scratch_floats.restype = i64
     if L.f110_abi_version() != 2:
         raise F110Error("libf110.so ABI version mismatch")
     _lib = L

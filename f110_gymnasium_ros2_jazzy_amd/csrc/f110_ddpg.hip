@@ -43,6 +43,7 @@ struct HeadArgs {
     const float *t, *dout, *g;  // backward: tanh output, upstream grad [B][nout], loss grad (device scalar)
     float *out0, *out1;         // actor: a, t; target: y; loss: td
     float *dh, *dW, *db;
+    const float *dh_mask;       // backward: dh := dh_mask > 0 ? dh : 0 (the ReLU of h), or null
     float *dz;                  // scratch [B][nout]
     float *part;                // scratch [nblk][nout][K + 1] or [nblk] (loss partials)
     float *loss;
@@ -173,7 +174,7 @@ __global__ void __launch_bounds__(kHB) k_head_bwd_rows(HeadArgs a) {
 #pragma unroll
                 for (int j = 0; j < NOUT; ++j)
                     if (k + i < a.K) s = fmaf(dz[j], a.W[(size_t)j * a.K + k + i], s);
-                r4[i] = s;
+                r4[i] = a.dh_mask && k + i < a.K && !(a.dh_mask[row * a.K + k + i] > 0.0f) ? 0.0f : s;
             }
             if ((a.K & 3) == 0) {
                 *reinterpret_cast<float4 *>(o + k) = make_float4(r4[0], r4[1], r4[2], r4[3]);
@@ -558,12 +559,12 @@ extern "C" int f110_ddpg_actor_head(const float *h, const float *W, const float 
 }
 
 extern "C" int f110_ddpg_actor_head_bwd(const float *h, const float *W, const float *t, const float *scale,
-                                        const float *dact, int32_t B, int32_t K, int32_t nout, float *dh, float *dW,
-                                        float *db, float *scratch, void *stream) {
+                                        const float *dact, int32_t B, int32_t K, int32_t nout, float *dh,
+                                        const float *dh_mask, float *dW, float *db, float *scratch, void *stream) {
     if (bad_shape(B, K, nout) || !h || !W || !t || !scale || !dact || !scratch)
         return fail_arg("f110_ddpg_actor_head_bwd");
     HeadArgs a{};
-    a.h = h, a.W = W, a.t = t, a.aux0 = scale, a.dout = dact, a.dh = dh, a.dW = dW, a.db = db;
+    a.h = h, a.W = W, a.t = t, a.aux0 = scale, a.dout = dact, a.dh = dh, a.dh_mask = dh_mask, a.dW = dW, a.db = db;
     a.dz = scratch, a.part = scratch + (int64_t)B * nout;
     a.B = B, a.K = K, a.nout = nout;
     hipError_t e = with_nout(nout, [&](auto N) {
@@ -604,11 +605,12 @@ extern "C" int f110_ddpg_critic_loss(const float *h, const float *W, const float
 }
 
 extern "C" int f110_ddpg_critic_loss_bwd(const float *h, const float *W, const float *td, const float *w,
-                                         const float *g, int32_t B, int32_t K, float *dh, float *dW, float *db,
-                                         float *scratch, void *stream) {
+                                         const float *g, int32_t B, int32_t K, float *dh, const float *dh_mask,
+                                         float *dW, float *db, float *scratch, void *stream) {
     if (bad_shape(B, K, 1) || !h || !W || !td || !w || !g || !scratch) return fail_arg("f110_ddpg_critic_loss_bwd");
     HeadArgs a{};
-    a.h = h, a.W = W, a.out0 = const_cast<float *>(td), a.aux1 = w, a.g = g, a.dh = dh, a.dW = dW, a.db = db;
+    a.h = h, a.W = W, a.out0 = const_cast<float *>(td), a.aux1 = w, a.g = g, a.dh = dh, a.dh_mask = dh_mask, a.dW = dW,
+    a.db = db;
     a.dz = scratch, a.part = scratch + B;
     a.B = B, a.K = K, a.nout = 1;
     hipLaunchKernelGGL((k_head_bwd_rows<kLoss, 1>), dim3(row_blocks(B)), dim3(kHB), 0, (hipStream_t)stream, a);
@@ -633,10 +635,11 @@ extern "C" int f110_ddpg_q_mean(const float *h, const float *W, const float *b, 
 }
 
 extern "C" int f110_ddpg_q_mean_bwd(const float *h, const float *W, const float *g, float sign, int32_t B, int32_t K,
-                                    float *dh, float *dW, float *db, float *scratch, void *stream) {
+                                    float *dh, const float *dh_mask, float *dW, float *db, float *scratch,
+                                    void *stream) {
     if (bad_shape(B, K, 1) || !W || !g || !scratch || ((dW || db) && !h)) return fail_arg("f110_ddpg_q_mean_bwd");
     HeadArgs a{};
-    a.h = h, a.W = W, a.g = g, a.sign = sign, a.dh = dh, a.dW = dW, a.db = db;
+    a.h = h, a.W = W, a.g = g, a.sign = sign, a.dh = dh, a.dh_mask = dh_mask, a.dW = dW, a.db = db;
     a.dz = scratch, a.part = scratch + B;
     a.B = B, a.K = K, a.nout = 1;
     hipLaunchKernelGGL((k_head_bwd_rows<kMean, 1>), dim3(row_blocks(B)), dim3(kHB), 0, (hipStream_t)stream, a);

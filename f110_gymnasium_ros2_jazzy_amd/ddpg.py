@@ -42,6 +42,10 @@ FUSED = os.environ.get("F110_DDPG_FUSED", "1") != "0"
 # batch (20.0 vs 20.6 us, M = 4096, K = 1088) and loses at M = 8192 and at
 # K = 128 (learner).
 MFMA_HIDDEN = os.environ.get("F110_DDPG_MFMA", "0") == "1"
+# The GPU learner's update runs without autograd (learner_fused.py: grouped
+# fp32 matrix-core GEMMs with fused epilogues, gradients written straight into
+# the flat buckets).  F110_DDPG_EXPLICIT=0 keeps the autograd path (A/B runs).
+EXPLICIT = os.environ.get("F110_DDPG_EXPLICIT", "1") != "0"
 
 
 # The learner's GEMM choices at batch 4096 (torch TunableOp, tuned on MI355X
@@ -223,6 +227,7 @@ class GradBucket:
             off += p.numel()
         self.group = group
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.direct = False  # learner_fused writes the gradients into self.flat itself (no .grad tensors)
 
     def zero(self):
         for p in self.params:  # optimizer.zero_grad(set_to_none=True) (agent.py:318, :329)
@@ -231,6 +236,8 @@ class GradBucket:
     # pack / reduce / unpack: in graph mode pack ends one captured phase,
     # reduce runs eagerly (RCCL) and unpack starts the next captured phase
     def pack(self):
+        if self.direct:
+            return
         if self.world > 1 or self.always_pack:
             torch.cat([p.grad.reshape(-1) for p in self.params], out=self.flat)
 
@@ -240,7 +247,7 @@ class GradBucket:
             self.flat.mul_(1.0 / self.world)
 
     def unpack(self):
-        if self.world > 1 and not self.always_pack:
+        if self.world > 1 and not self.always_pack and not self.direct:
             torch._foreach_copy_([p.grad for p in self.params], self.views)
 
     def all_reduce(self):
@@ -374,6 +381,12 @@ class DDPGLearner:
             self.critic_optim = torch.optim.Adam(self.critic.parameters(), lr=critic_lr)
             self._online = list(self.actor.parameters()) + list(self.critic.parameters())
             self._target = list(self.actor_target.parameters()) + list(self.critic_target.parameters())
+        self.explicit = None
+        if self.flat and FUSED and EXPLICIT:
+            from .learner_fused import ExplicitUpdate
+            if ExplicitUpdate.supported(self):
+                self.explicit = ExplicitUpdate(self)
+                self.actor_grads.direct = self.critic_grads.direct = True
         self.memory = None
         if replay == "device":
             from .replay import DeviceReplayBuffer
@@ -413,6 +426,10 @@ class DDPGLearner:
         for name, t in (("states", states), ("actions", actions), ("next_states", next_states), ("rewards", r),
                         ("dones", d)):
             self._finite(name, t)
+        if self.explicit is not None:  # learner_fused.py: the same graph without autograd
+            critic_loss, td = self.explicit.critic(states, actions, r, next_states, d, w)
+            self._finite("td", td)
+            return critic_loss, td
         fused = _fused(states)
         with torch.no_grad():  # :302-308
             a_next = self.actor_target(next_states)
@@ -445,6 +462,8 @@ class DDPGLearner:
     def _phase_actor(self, states):
         """agent.py:321-331: critic step, actor loss through the frozen critic."""
         self._optim_step(self.critic_optim, self.critic_grads)
+        if self.explicit is not None:
+            return self.explicit.actor(states)
         for p in self.critic.parameters():
             p.requires_grad_(False)
         if _fused(states):
@@ -564,7 +583,10 @@ class DDPGLearner:
         decays once per call (GaussianActionNoise.__call__, :520-539)."""
         with torch.no_grad(), TunedGemms(self.tuned_gemms):
             o = torch.as_tensor(obs, device=self.device, dtype=torch.float32)
-            a = self.actor(o)
+            if self.explicit is not None:
+                a = self.explicit.policy(self.actor, o if o.dim() == 2 else o.unsqueeze(0))
+            else:
+                a = self.actor(o)
             if training:
                 noise = torch.randn(a.shape, generator=self._noise_gen, device=self.device) * self.sigma
                 a = torch.clamp(a + noise, self._low, self._high)

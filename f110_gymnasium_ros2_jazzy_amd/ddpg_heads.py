@@ -73,8 +73,8 @@ class _ActorHead(torch.autograd.Function):
         dW = torch.empty_like(W) if nw else None
         db = torch.empty(n, dtype=torch.float32, device=h.device) if nb else None
         dact = dact.contiguous()
-        _lib.check(L.f110_ddpg_actor_head_bwd(_p(h), _p(W), _p(t), _p(scale), _p(dact), B, K, n, _p(dh), _p(dW),
-                                              _p(db), _p(_scratch(L, B, K, n, h)), _stream(h)),
+        _lib.check(L.f110_ddpg_actor_head_bwd(_p(h), _p(W), _p(t), _p(scale), _p(dact), B, K, n, _p(dh), None,
+                                              _p(dW), _p(db), _p(_scratch(L, B, K, n, h)), _stream(h)),
                    "f110_ddpg_actor_head_bwd")
         return dh, dW, db, None, None
 
@@ -105,8 +105,8 @@ class _CriticLoss(torch.autograd.Function):
         dW = torch.empty_like(W) if nw else None
         db = torch.empty(1, dtype=torch.float32, device=h.device) if nb else None
         g = gloss.reshape(()).contiguous()
-        _lib.check(L.f110_ddpg_critic_loss_bwd(_p(h), _p(W), _p(td), _p(w), _p(g), B, K, _p(dh), _p(dW), _p(db),
-                                               _p(_scratch(L, B, K, 1, h)), _stream(h)), "f110_ddpg_critic_loss_bwd")
+        _lib.check(L.f110_ddpg_critic_loss_bwd(_p(h), _p(W), _p(td), _p(w), _p(g), B, K, _p(dh), None, _p(dW),
+                                               _p(db), _p(_scratch(L, B, K, 1, h)), _stream(h)), "f110_ddpg_critic_loss_bwd")
         return dh, dW, db, None, None
 
 
@@ -134,7 +134,7 @@ class _QMean(torch.autograd.Function):
         dW = torch.empty_like(W) if nw else None
         db = torch.empty(1, dtype=torch.float32, device=h.device) if nb else None
         g = gloss.reshape(()).contiguous()
-        _lib.check(L.f110_ddpg_q_mean_bwd(_p(h), _p(W), _p(g), ctx.sign, B, K, _p(dh), _p(dW), _p(db),
+        _lib.check(L.f110_ddpg_q_mean_bwd(_p(h), _p(W), _p(g), ctx.sign, B, K, _p(dh), None, _p(dW), _p(db),
                                           _p(_scratch(L, B, K, 1, h)), _stream(h)), "f110_ddpg_q_mean_bwd")
         return dh, dW, db, None
 

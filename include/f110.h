@@ -542,7 +542,8 @@ F110_API int f110_adam_step(float *param, float *exp_avg, float *exp_avg_sq, con
  * Row-major float32 device buffers: h [B][K] (the last hidden layer), W
  * [nout][K], b [nout]; K <= 255, nout <= 4 (nout = 1 for the critic).
  * scratch: f110_ddpg_scratch_floats(B, K, nout) floats.  dh / dW / db
- * outputs may be null (not wanted).  g: device scalar, the gradient of the
+ * outputs may be null (not wanted); dh_mask [B][K] (may be null) zeroes dh
+ * where dh_mask <= 0 (h's ReLU: threshold_backward fused into the head).  g: device scalar, the gradient of the
  * loss (autograd's grad_output).  Deterministic; async on stream. */
 F110_API int64_t f110_ddpg_scratch_floats(int32_t B, int32_t K, int32_t nout);
 /* t = tanh(h W^T + b); act = scale * t + shift  (act, t: [B][nout]) */
@@ -551,8 +552,8 @@ F110_API int f110_ddpg_actor_head(const float *h, const float *W, const float *b
                                   void *stream);
 /* dz = (dact * scale) * (1 - t*t); dh = dz W; dW = dz^T h; db = sum_rows dz */
 F110_API int f110_ddpg_actor_head_bwd(const float *h, const float *W, const float *t, const float *scale,
-                                      const float *dact, int32_t B, int32_t K, int32_t nout, float *dh, float *dW,
-                                      float *db, float *scratch, void *stream);
+                                      const float *dact, int32_t B, int32_t K, int32_t nout, float *dh,
+                                      const float *dh_mask, float *dW, float *db, float *scratch, void *stream);
 /* y = r + (gamma * (1 - d)) * (h W^T + b) */
 F110_API int f110_ddpg_td_target(const float *h, const float *W, const float *b, const float *r, const float *d,
                                  float gamma, int32_t B, int32_t K, float *y, void *stream);
@@ -561,8 +562,8 @@ F110_API int f110_ddpg_critic_loss(const float *h, const float *W, const float *
                                    int32_t B, int32_t K, float *td, float *loss, float *scratch, void *stream);
 /* dq = -((g / B) * w) * (2 td); dh, dW, db from dq */
 F110_API int f110_ddpg_critic_loss_bwd(const float *h, const float *W, const float *td, const float *w,
-                                       const float *g, int32_t B, int32_t K, float *dh, float *dW, float *db,
-                                       float *scratch, void *stream);
+                                       const float *g, int32_t B, int32_t K, float *dh, const float *dh_mask,
+                                       float *dW, float *db, float *scratch, void *stream);
 /* loss = sign * mean(h W^T + b)  (sign -1: the actor loss) */
 F110_API int f110_ddpg_q_mean(const float *h, const float *W, const float *b, float sign, int32_t B, int32_t K,
                               float *loss, float *scratch, void *stream);
@@ -580,7 +581,48 @@ F110_API int f110_ddpg_relu_bwd(const float *gy, const float *y, int32_t B, int3
                                 float *scratch, void *stream);
 /* dq = sign * (g / B); dh, dW, db from dq (h only needed for dW / db) */
 F110_API int f110_ddpg_q_mean_bwd(const float *h, const float *W, const float *g, float sign, int32_t B, int32_t K,
-                                  float *dh, float *dW, float *db, float *scratch, void *stream);
+                                  float *dh, const float *dh_mask, float *dW, float *db, float *scratch,
+                                  void *stream);
+
+/* ---- learner GEMMs (fp32 matrix cores) -------------------------------------------
+ * The hidden layers of the DDPG networks (agent.py:25-97: fc1 / fc2, fcs1 /
+ * fcs2 and replay()'s backward through them, :302-331), forward and backward,
+ * as grouped fp32 MFMA launches with the layer's epilogue fused.  Replaces
+ * torch.addmm + relu, threshold_backward, torch.cat([z, action]) and the
+ * weight / input gradient GEMMs of autograd.  Row-major float32 device
+ * buffers; every op of one launch shares M (the batch rows).
+ *
+ * f110_learner_gemm: for each op,
+ *   C[m][n] = epi( sum_k A'[m][k] B(k, n)  +  sum_{t < nx2} x2[m][t] w2[n][t]  +  bias[n] )
+ *   A'[m][k] = amask ? (amask[m][k] > 0 ? A[m][k] : 0) : A[m][k]   (amask stride lda)
+ *   B(k, n)  = nn ? B[k * ldb + n] : B[n * ldb + k]   (nn = 0: a Linear's weight
+ *              [N][K] as in x W^T; nn = 1: the weight itself as in g W)
+ *   epi: ReLU when relu != 0 (NaN kept, as torch.relu), then
+ *        C := omask[m][n] > 0 ? C : 0 when omask is set (stride ldc).
+ * bias, amask, omask, x2 / w2 may be null; nx2 <= 2 (the critic's action
+ * columns of fcs2's input, agent.py:94).  All ops of a launch share nn and
+ * whether amask is set.
+ * Deterministic (fixed summation order); async on stream. */
+typedef struct f110_gemm_op {
+    const float *A, *B, *bias, *amask, *omask, *x2, *w2;
+    float *C;
+    int32_t N, K, lda, ldb, ldc, ldx2, ldw2, nx2, relu, nn;
+} f110_gemm_op;
+F110_API int f110_learner_gemm(const f110_gemm_op *ops, int32_t nops, int32_t M, void *stream);
+
+/* f110_learner_wgrad: a Linear's weight and bias gradients, for each op
+ *   dW[n][kx] (stride ldw) = sum_m G'[m][n] X[m][kx],  db[n] = sum_m G'[m][n]
+ *   G'[m][n] = gmask ? (gmask[m][n] > 0 ? G[m][n] : 0) : G[m][n]   (gmask stride ldg)
+ * (autograd's grad_W = gz^T x and grad_b = gz.sum(0) after threshold_backward).
+ * db may be null; all ops of a launch share whether gmask is set.  M is split over blocks; the partial sums go to scratch
+ * (f110_learner_wgrad_scratch_floats floats) and are added in a fixed order. */
+typedef struct f110_wgrad_op {
+    const float *G, *gmask, *X;
+    float *dW, *db;
+    int32_t N, KX, ldg, ldx, ldw;
+} f110_wgrad_op;
+F110_API int64_t f110_learner_wgrad_scratch_floats(const f110_wgrad_op *ops, int32_t nops, int32_t M);
+F110_API int f110_learner_wgrad(const f110_wgrad_op *ops, int32_t nops, int32_t M, float *scratch, void *stream);
 
 #ifdef __cplusplus
 }

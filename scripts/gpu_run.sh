@@ -6,6 +6,8 @@
 # the job (no GPU step runs after a failed / faulted / timed-out one).  Output
 # goes to gpurun_out/TAG/.  Steps:
 #   suite      pytest -m gpu (one process, per-test timeout)
+#   lgemm      tests/test_gpu_learner_gemm.py, scripts/learner_gemm_mb.py (+ its rocprofv3 kernel stats)
+#   learner    tests/test_gpu_replay.py + tests/test_gpu_ddpg_heads.py (the DDPG learner)
 #   quick      the dispatch-variant tests of tests/test_gpu_batch.py only
 #   smoke      __graft_entry__.smoke()
 #   bench      python bench.py (defaults) -> bench.json
@@ -42,6 +44,13 @@ for step in "$@"; do
         suite) run suite 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
         quick) run quick 600 python -u -m pytest tests/test_gpu_batch.py -m gpu -x -v --timeout 300 --timeout-method thread \
                    -p no:cacheprovider -k "variants_identical or step_n or simt or refill_kernel" ;;
+        lgemm) run lgemm 600 python -u -m pytest tests/test_gpu_learner_gemm.py -m gpu -x -v --timeout 120 \
+                   --timeout-method thread -p no:cacheprovider &&
+               run lgemm_mb 300 python -u scripts/learner_gemm_mb.py && cp "$OUT/lgemm_mb.out" "$OUT/lgemm_mb.json" &&
+               run lgemm_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/lgemm_prof" -o run -- \
+                   python3 scripts/learner_gemm_mb.py ;;
+        learner) run learner 600 python -u -m pytest tests/test_gpu_replay.py tests/test_gpu_ddpg_heads.py -m gpu -x -v \
+                     --timeout 200 --timeout-method thread -p no:cacheprovider ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python -u bench.py && cp "$OUT/bench.out" "$OUT/bench.json" ;;
         bench20) run bench20 600 python -u bench.py --steps 20 --warmup 5 && cp "$OUT/bench20.out" "$OUT/bench20.json" ;;

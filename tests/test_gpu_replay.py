@@ -158,6 +158,44 @@ def test_learner_on_gpu_matches_reference(gpu):
                                        err_msg=f"{name}.{k}")
 
 
+@pytest.mark.parametrize("M,D", [(4096, 1088), (333, 64), (64, 12)])
+def test_explicit_update_matches_autograd(gpu, monkeypatch, M, D):
+    """learner_fused.ExplicitUpdate (the learner GEMMs, no autograd) against
+    the autograd learner on the same weights and batch: losses (rtol 1e-4),
+    the critic's and the actor's flat gradient buckets after one update
+    (|diff| <= 1e-4 |g| + 1e-5 max|g|, fp32 summation-order noise) and the
+    policy's actions; then two more updates: losses still within 1e-4."""
+    import f110_gymnasium_ros2_jazzy_amd.ddpg as Dd
+    g = torch.Generator(device="cuda").manual_seed(M + D)
+    S = torch.randn(M, D, device="cuda", generator=g)
+    A = torch.rand(M, 2, device="cuda", generator=g) * torch.tensor([0.8378, 20.0], device="cuda") - \
+        torch.tensor([0.4189, 0.0], device="cuda")
+    R = torch.randn(M, device="cuda", generator=g)
+    S2 = S + 0.1 * torch.randn(M, D, device="cuda", generator=g)
+    Dn = (torch.rand(M, device="cuda", generator=g) < 0.1).float()
+    W = torch.rand(M, device="cuda", generator=g) + 0.5
+    runs = []
+    for explicit in (True, False):
+        monkeypatch.setattr(Dd, "EXPLICIT", explicit)
+        ln = Dd.DDPGLearner(obs_dim=D, act_dim=2, action_low=[-0.4189, 0.0], action_high=[0.4189, 20.0], seed=1,
+                            device="cuda:0", replay=None)
+        assert (ln.explicit is not None) == explicit
+        losses = []
+        st = ln.update(S, A, R, S2, Dn, W)
+        losses.append((float(st["critic_loss"]), float(st["actor_loss"])))
+        grads = (ln.critic_grads.flat.clone(), ln.actor_grads.flat.clone(), st["td"].clone())
+        pol = ln.choose_action(S[:100], training=False).clone()
+        for _ in range(2):
+            st = ln.update(S, A, R, S2, Dn, W)
+            losses.append((float(st["critic_loss"]), float(st["actor_loss"])))
+        runs.append((losses, grads, pol))
+    np.testing.assert_allclose(runs[0][0], runs[1][0], rtol=1e-4)
+    for x, y in zip(runs[0][1], runs[1][1]):
+        tol = 1e-4 * y.abs() + 1e-5 * y.abs().max()
+        assert bool(((x - y).abs() <= tol).all()), float(((x - y).abs() / tol).max())
+    torch.testing.assert_close(runs[0][2], runs[1][2], rtol=1e-5, atol=1e-6)
+
+
 def test_vector_trainer_loop(gpu):
     """The batched train_ddpg loop: 256 two-agent envs, gap-follow opponent,
     device reward, replay, learner updates after a 5-step warm-up."""
