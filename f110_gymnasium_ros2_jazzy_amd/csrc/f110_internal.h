@@ -59,8 +59,11 @@ struct StepArgs {
     int32_t fx_pad;     // the padded table is built (k_rays_fxn on it unless F110_FX_PAD=0; k_rays_fxs)
     int32_t fxs_ok;     // the padded table's rows and columns are below 2^20 (kFxsBase's offsets)
     int32_t fx_refill;  // waves per car of k_rays_fxs (two chunk slots with refill; 0 = off)
-    int32_t fxs_variant;  // f110_set_ray_variant (A/B of k_rays_fxs variants; 0 = the default)
-    uint8_t *ccost;       // [EA][nch] k_rays_fxs (ORD): each chunk's trip count in the previous launch
+    int32_t fxs_variant;  // f110_set_ray_variant (A/B bits; 0 = the defaults)
+    uint16_t *lcost;      // [EA * nch] k_rays_fxs: each wave item's trips in the previous launch (LPT key)
+    uint32_t *lorder;     // [EA * nch] k_lpt_order: wave items, longest first
+    int32_t lpt_items;    // items the order was last built for (0: none yet)
+    int32_t *lpt_items_out;  // host: set to the items of the order this step builds
     int32_t count_slots;  // f110_set_simt: lane-slot counter of the fixed-point loops
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2: k_rays_fxn / k_rays_fxs)
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
@@ -161,7 +164,8 @@ struct RayArgs {
     int32_t fxp_P;
     double fxs_cx, fxs_cy;  // k_rays_fxs: 2^20 + P + 2^-26 - origin / res (see kFxsBase)
     int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_read_simt)
-    uint8_t *ccost;       // [EA][nch] k_rays_fxs (ORD): per-chunk trip counts, read and rewritten
+    uint16_t *lcost;         // k_rays_fxs: each wave item's trips written here (or null)
+    const uint32_t *lorder;  // k_rays_fxs: block p traces item lorder[p] (or null: item p)
     const double *cs2, *bs2;  // k_rays_fxs: interleaved (cos, sin) / (side, beam_cos) tables
 };
 
@@ -277,6 +281,7 @@ struct ReplayView {
     int64_t capacity;
     int32_t obs_dim, act_dim;
     float *obs, *next_obs, *act, *reward, *done, *prio;  // [cap][D], [cap][D], [cap][A], [cap] x3
+    double *wt;          // [cap] sampling weight (prio + eps)^alpha, written with prio (add, update)
     uint32_t *keys;      // [cap] exponential-race keys
     uint32_t *hist;      // [4][256]
     double *den_part;    // [kReplayMaxGrid]

@@ -1097,12 +1097,11 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
 // other with the IEEE cell.  Per ray the arithmetic is k_rays_fxn's, so
 // bit-identical.
 //
-// Chunk order: descending chunk index (the scan's left edge first), or (ORD)
-// longest pair first: the previous launch's per-chunk trip counts
-// (RayArgs::ccost, written by every ORD launch) rank the car's 128-beam
-// chunk pairs by their longer chunk, ties by descending index, so the long
-// grazing-beam chunks start first and the short ones fill in behind them
-// (offline model: 103.1 -> 98.0 trips per car, scripts/slot_merge_model.py).
+// Chunk order: descending chunk index (the scan's left edge first).  (Longest
+// pair first by the previous launch's per-chunk trips, ORD, cut the trips 5 %
+// and lost 1-2 % of time: round 4)  Wave order (LPT): with
+// RayArgs::lorder the block at position p traces wave item lorder[p] (k_lpt_order
+// sorts the previous launch's per-item trip counts, RayArgs::lcost, longest first).
 //
 // The refill pass keeps nothing in SGPRs across the loop: kernel arguments
 // are re-read at the use through kernarg_here, the scan origin and first
@@ -1118,12 +1117,13 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
 // gather every trip, a closed slot on the zero cell).  Per slot and trip: the
 // total (:141), the activity test (:133), the refill when the slot's chunk has
 // ended, the step (:135-136) and its gather.
-template <bool HANDOFF, bool ORD = false>
+template <bool HANDOFF>
 __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
     constexpr int NS = 2;
     wave_stamp_start(a.wtrace);
-    const int wj = (int)blockIdx.x / a.EA;
-    const int g = (int)blockIdx.x - wj * a.EA;
+    const int item = a.lorder ? (int)ld_const(a.lorder + blockIdx.x) : (int)blockIdx.x;  // (wj, g) of this block
+    const int wj = item / a.EA;
+    const int g = item - wj * a.EA;
     const int lane = (int)threadIdx.x;
     const int B = a.B;
     const int e = HANDOFF ? g / a.A : g;
@@ -1143,11 +1143,8 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
     double x[NS], y[NS], d[NS], tot[NS], c[NS], sn[NS];
     int kk[NS];
     int kpar[NS];         // the noise cache entry of the slot's chunk pair
-    uint32_t karm[NS];    // ORD: the trip at which the slot's chunk was armed
     int pnext = wj;       // position of this wave's next chunk in the car's chunk order
-    // lane k < nch, packed in one VGPR: bits 0-7 the run holding beam 64 k (one divergent
-    // search per car), 8-15 (ORD) chunk k's position in the order, 16-23 its pair's rank
-    int kinfo = 0;
+    int kinfo = 0;        // lane k < nch: the run holding beam 64 k (one divergent search per car)
     uint32_t srch = 0;    // the search's vector loads (lane-divergent: their wave-level count is the max)
     if (lane < nch) {
         const BeamRun *R = a.runs + (size_t)g * kMaxSeg;
@@ -1160,23 +1157,6 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
         }
         kinfo = lo;
     }
-    if (ORD) {
-        // pair q = chunks (2q, 2q+1), keyed by its longer chunk's previous trip count, ties by index
-        uint32_t ck = lane < nch ? (uint32_t)a.ccost[(size_t)g * nch + lane] : 0u;
-        const uint32_t pc = max(ck, (uint32_t)__shfl_xor((int)ck, 1, 64));
-        const uint32_t key = pc * 64u + (uint32_t)(lane >> 1);
-        const int npair = (nch + 1) >> 1;
-        int kpos = 0, krank = 0;
-        for (int q = 0; q < npair; ++q) {  // pairs ranked ahead of this lane's pair and their chunks
-            const uint32_t kq = __builtin_amdgcn_readlane(key, 2 * q);
-            const bool ahead = kq > key;
-            krank += ahead ? 1 : 0;
-            kpos += ahead ? (2 * q + 1 < nch ? 2 : 1) : 0;
-        }
-        kpos += ((lane & 1) == 0 && lane + 1 < nch) ? 1 : 0;  // inside a pair the higher chunk goes first
-        kinfo |= (kpos << 8) | (krank << 16);
-        ++srch;
-    }
     // wave-level vector loads other than the slot gathers (SIMT / TA accounting, counter 3):
     // the arms' and finishes' table loads, the guard-band re-gathers (wave-uniform, scalar)
     uint32_t loads = 0;
@@ -1184,19 +1164,12 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
     // in_loop: the slot's next `tot += d` completes tot = d (:130)
     auto arm = [&](int r, bool in_loop) {
         const RayArgs &K = kernarg_here();
-        int k;
-        if (ORD) {
-            k = __builtin_ctzll(__builtin_amdgcn_ballot_w64(lane < nch && ((kinfo >> 8) & 255) == pnext));
-            kpar[r] = (__builtin_amdgcn_readlane(kinfo, k) >> 16) & 1;
-            karm[r] = trips;
-        } else {
-            k = nch - 1 - pnext;
-            kpar[r] = (k >> 1) & 1;
-        }
+        const int k = nch - 1 - pnext;
+        kpar[r] = (k >> 1) & 1;
         pnext += wstride;
         kk[r] = k;
         const int b = k * 64 + lane, bc = b < B ? b : B - 1;
-        const int lo = __builtin_amdgcn_readlane(kinfo, k) & 255;
+        const int lo = __builtin_amdgcn_readlane(kinfo, k);
         int ti = (int)beam_theta(K.runs + (size_t)g * kMaxSeg, ld_const(K.nruns + g), lo, k * 64, bc);  // :124
         if (ti >= K.theta_dis) ti = 0;
         const double2 t2 = ld_off(reinterpret_cast<const double2 *>(K.cs2), (uint32_t)ti * 16u);
@@ -1261,10 +1234,6 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
             if (K.scans_f32) *reinterpret_cast<float *>(reinterpret_cast<char *>(K.scans_f32 + row) + (uint32_t)b * 4u) = (float)range;
             if (K.scans_f64) *reinterpret_cast<double *>(reinterpret_cast<char *>(K.scans_f64 + row) + (uint32_t)b * 8u) = range;
             if (HANDOFF) *reinterpret_cast<double *>(reinterpret_cast<char *>(K.scan + row) + (uint32_t)b * 8u) = range;
-        }
-        if (ORD && lane == 0) {  // this chunk's trips, the next launch's order key
-            const uint32_t t = trips - karm[r];
-            K.ccost[(size_t)g * nch + kk[r]] = (uint8_t)(t < 255u ? t : 255u);
         }
         lanes += (uint32_t)min(64, B - kk[r] * 64);  // the chunk's beams (scalar)
     };
@@ -1344,6 +1313,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
     }
     if (lane == 0) {
         const RayArgs &K = kernarg_here();
+        if (K.lcost) K.lcost[item] = (uint16_t)(trips < 0xffffu ? trips : 0xffffu);  // the next launch's LPT key
         unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
         atomicAdd(cs, (unsigned long long)(lanes + lane_iters));  // the first lookup came from k_agents
         atomicAdd(cs + 1, (unsigned long long)lanes);
@@ -1354,7 +1324,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
             atomicAdd(cs + 3, (unsigned long long)loads);
         }
     }
-    if (a.count_slots) {  // the run search's (and ORD's cost read's) wave-level loads (counter 3)
+    if (a.count_slots) {  // the run search's wave-level loads (counter 3)
         const uint32_t ws = wave_max(srch);
         if (lane == 0) atomicAdd(a.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride + 3, (unsigned long long)ws);
     }
@@ -1855,6 +1825,42 @@ template <int EPB> __global__ void __launch_bounds__(64) k_post_pair(StepArgs a)
     }
 }
 
+// LPT wave order for k_rays_fxs: the n wave items by the previous launch's
+// trips, longest first (a counting sort over 256 cost buckets, one
+// workgroup; order within a bucket is arbitrary: results do not depend on it).
+__device__ __forceinline__ uint32_t lpt_bucket(uint16_t c) { return 255u - (min((uint32_t)c, 511u) >> 1); }
+
+__global__ void __launch_bounds__(1024) k_lpt_order(const uint16_t *cost, int32_t n, uint32_t *order) {
+    __shared__ uint32_t cnt[256];
+    const int t = (int)threadIdx.x;
+    if (t < 256) cnt[t] = 0;
+    __syncthreads();
+    for (int i = t; i < n; i += 1024) atomicAdd(&cnt[lpt_bucket(cost[i])], 1u);
+    __syncthreads();
+    if (t < 64) {  // exclusive scan of the 256 counts: 4 per lane, then a wave scan
+        uint32_t c[4], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            c[k] = cnt[4 * t + k];
+            sum += c[k];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t v = __shfl_up(incl, d, 64);
+            if (t >= d) incl += v;
+        }
+        uint32_t base = incl - sum;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            cnt[4 * t + k] = base;
+            base += c[k];
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < n; i += 1024) order[atomicAdd(&cnt[lpt_bucket(cost[i])], 1u)] = (uint32_t)i;
+}
+
 // One f110_step / f110_reset: k_agents, the ray kernel, the post stage.
 // The ray kernel by context (f110_create's rules):
 //   ray_kernel 1 / 2: k_rays_tiled in flat / chunked order (rotated maps, or
@@ -1871,6 +1877,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (a.gate_wait && (e = hipStreamWaitEvent(s, a.gate_wait, 0)) != hipSuccess) return e;
     const bool single = a.A == 1;
+    int lpt_n = 0;  // wave items of this launch's LPT order (0: off)
     RayArgs ra{};
     ra.m = a.tmap;
     ra.sines = a.sines;
@@ -1997,16 +2004,15 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                 ra.fxs_cy = std::fma(-a.tmap.oy, a.tmap.inv_res, kFxsBase + P + kFxsShift);
                 if (a.fx_refill > 0 && a.fxs_ok && !mask && ra.HB == 0 && !ra.wcost) {
                     // one wave per car, two chunk slots with refill (k_rays_fxs; no heavy-first)
-                    // f110_set_ray_variant (A/B): 1 = longest chunk pair first (ORD)
-                    const void *fs[2][2] = {{reinterpret_cast<const void *>(&k_rays_fxs<false, false>),
-                                             reinterpret_cast<const void *>(&k_rays_fxs<true, false>)},
-                                            {reinterpret_cast<const void *>(&k_rays_fxs<false, true>),
-                                             reinterpret_cast<const void *>(&k_rays_fxs<true, true>)}};
-                    const int ord = (a.fxs_variant & 1) && a.ccost ? 1 : 0;
-                    ra.ccost = a.ccost;
-                    f = fs[ord][single ? 0 : 1];
+                    f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false>)
+                               : reinterpret_cast<const void *>(&k_rays_fxs<true>);
                     ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
                     g2 = dim3((unsigned)(ra.EA * ra.G4));
+                    // f110_set_ray_variant bit 0 (A/B): blocks take the wave items longest first by
+                    // the previous launch's trips (LPT); the order is rebuilt after every launch
+                    lpt_n = (a.fxs_variant & 1) && a.lcost ? ra.EA * ra.G4 : 0;
+                    ra.lcost = lpt_n ? a.lcost : nullptr;
+                    ra.lorder = lpt_n && a.lpt_items == lpt_n ? a.lorder : nullptr;
                 }
             }
         }
@@ -2019,6 +2025,11 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     void *args[] = {&ra};
     if ((e = hipExtLaunchKernel(f, g2, dim3(bdim), args, 0u, s, evk(2), evk(3), 0)) != hipSuccess) return e;
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (lpt_n) {  // the next launch's wave order from this launch's trips
+        hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(1024), 0, s, a.lcost, lpt_n, a.lorder);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (a.lpt_items_out) *a.lpt_items_out = lpt_n;
+    }
     if (a.gate_record && (e = hipEventRecord(a.gate_record, s)) != hipSuccess) return e;
     if (single)
         hipExtLaunchKernelGGL(k_post_single, dim3((a.E + 63) / 64), dim3(64), 0, s, evk(4), evk(5), 0, a);

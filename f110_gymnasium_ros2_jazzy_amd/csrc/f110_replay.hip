@@ -150,6 +150,7 @@ __global__ void __launch_bounds__(kOneBlock) k_add_scan(ReplayView v, const uint
                 p = (float)(q < 1e-8 ? 1e-8 : (q > (double)FLT_MAX ? (double)FLT_MAX : q));
             }
             v.prio[slot] = p;  // replay_buffer.py:65
+            v.wt[slot] = prio_weight(p, v.eps, v.alpha);
             ++rank;
         } else {
             v.pos[i] = -1;
@@ -204,7 +205,7 @@ __global__ void __launch_bounds__(kRB) k_keys(ReplayView v, int32_t batch) {
     __syncthreads();
     double acc = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * kRB + threadIdx.x; i < len; i += (int64_t)gridDim.x * kRB) {
-        const double w = prio_weight(v.prio[i], v.eps, v.alpha);
+        const double w = v.wt[i];  // prio_weight(prio[i]), cached at add / update
         acc += w;
         U4 c = {(uint32_t)i, (uint32_t)((uint64_t)i >> 32), (uint32_t)draw, (uint32_t)(draw >> 32)};
         U4 r = philox(c, (uint32_t)v.seed, (uint32_t)(v.seed >> 32) ^ 0x9E3779B9u);
@@ -346,7 +347,7 @@ __device__ void write_weights(const ReplayView &v, const int64_t *idx, int32_t b
     __shared__ double wm[kOneBlock / 64];
     double m = -INFINITY;
     for (int j = threadIdx.x; j < batch; j += blockDim.x) {
-        const double p = prio_weight(v.prio[idx[j]], v.eps, v.alpha) / den;
+        const double p = v.wt[idx[j]] / den;
         const double w = pow((double)len * p, -beta);
         wsh[j] = w;
         m = fmax(m, w);
@@ -427,7 +428,7 @@ __global__ void __launch_bounds__(kOneBlock) k_sample_replace(ReplayView v, int3
     double *cdf = reinterpret_cast<double *>(smem);  // [batch] (len < batch)
     int64_t *idx = reinterpret_cast<int64_t *>(cdf + batch);
     double *wsh = reinterpret_cast<double *>(idx + batch);
-    for (int64_t i = threadIdx.x; i < len; i += blockDim.x) cdf[i] = prio_weight(v.prio[i], v.eps, v.alpha);
+    for (int64_t i = threadIdx.x; i < len; i += blockDim.x) cdf[i] = v.wt[i];
     __syncthreads();
     if (threadIdx.x == 0) {
         double acc = 0.0;
@@ -507,13 +508,21 @@ __global__ void __launch_bounds__(kRB) k_update(ReplayView v, const int64_t *idx
         if (blockIdx.x == 0 && threadIdx.x == 0)
             for (int64_t j = 0; j < n; ++j) {
                 const int64_t i = idx[j];
-                if (i >= 0 && i < v.capacity) v.prio[i] = pr_of(j);
+                if (i >= 0 && i < v.capacity) {
+                    const float p = pr_of(j);
+                    v.prio[i] = p;
+                    v.wt[i] = prio_weight(p, v.eps, v.alpha);
+                }
             }
         return;
     }
     for (int64_t j = (int64_t)blockIdx.x * kRB + threadIdx.x; j < n; j += (int64_t)gridDim.x * kRB) {
         const int64_t i = idx[j];
-        if (i >= 0 && i < v.capacity) v.prio[i] = pr_of(j);
+        if (i >= 0 && i < v.capacity) {
+            const float p = pr_of(j);
+            v.prio[i] = p;
+            v.wt[i] = prio_weight(p, v.eps, v.alpha);
+        }
     }
 }
 

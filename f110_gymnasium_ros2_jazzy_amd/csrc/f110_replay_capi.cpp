@@ -67,6 +67,7 @@ extern "C" int f110_replay_create(f110_replay **out, int32_t device, int64_t cap
     if (e == hipSuccess) e = rb->alloc(&v.reward, cap);
     if (e == hipSuccess) e = rb->alloc(&v.done, cap);
     if (e == hipSuccess) e = rb->alloc(&v.prio, cap);
+    if (e == hipSuccess) e = rb->alloc(&v.wt, cap);
     if (e == hipSuccess) e = rb->alloc(&v.keys, cap);
     if (e == hipSuccess) e = rb->alloc(&v.hist, 4 * 256);
     if (e == hipSuccess) e = rb->alloc(&v.den_part, kReplayMaxGrid);
@@ -76,6 +77,7 @@ extern "C" int f110_replay_create(f110_replay **out, int32_t device, int64_t cap
     if (e == hipSuccess) e = rb->alloc(&v.pos, (size_t)max_add);
     if (e == hipSuccess) e = hipMemset(v.hdr, 0, sizeof(ReplayHdr));
     if (e == hipSuccess) e = hipMemset(v.prio, 0, cap * sizeof(float));
+    if (e == hipSuccess) e = hipMemset(v.wt, 0, cap * sizeof(double));
     if (e == hipSuccess) e = hipMemset(v.hist, 0, 4 * 256 * sizeof(uint32_t));
     if (e == hipSuccess) e = prepare_replay(max_batch);
     if (e == hipSuccess) e = hipDeviceSynchronize();

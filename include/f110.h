@@ -318,8 +318,9 @@ F110_API int f110_ray_refill(const f110_ctx *ctx);
 F110_API int f110_set_ray_refill(f110_ctx *ctx, int32_t waves);
 
 /* A/B of kernel variants for the following steps, a bit mask (0 = the
- * defaults).  Bit 0: k_rays_fxs takes the car's chunk pairs longest first by
- * the previous launch's per-chunk trip counts.  Bits 1 / 2: two-agent envs
+ * defaults).  Bit 0: k_rays_fxs's blocks take its wave items longest first by
+ * the previous launch's trips per item (LPT order, rebuilt after every launch).
+ * Bits 1 / 2: two-agent envs
  * run their post stage as k_post_pair with 8 / 4 envs per wave.  Scheduling
  * only: results are bit-identical.  Measurement hook (scripts/ray_ab.py), no
  * reference counterpart. */

@@ -7,7 +7,10 @@
 # goes to gpurun_out/TAG/.  Steps:
 #   suite      pytest -m gpu (one process, per-test timeout)
 #   lgemm      tests/test_gpu_learner_gemm.py, scripts/learner_gemm_mb.py (+ its rocprofv3 kernel stats)
+#   lgemmv     scripts/learner_gemm_mb.py under rocprofv3 for each F110_LGEMM_VARIANT (0-3)
+#   lgemmpmc   two PMC passes (SQ wait / MFMA busy; TA busy) over scripts/learner_gemm_mb.py
 #   learner    tests/test_gpu_replay.py + tests/test_gpu_ddpg_heads.py (the DDPG learner)
+#   c5prof     scripts/profile_c5.py TAG (C5 bench + rocprofv3 kernel stats by stage) -> gpurun_out/prof_c5_TAG/
 #   quick      the dispatch-variant tests of tests/test_gpu_batch.py only
 #   smoke      __graft_entry__.smoke()
 #   bench      python bench.py (defaults) -> bench.json
@@ -49,8 +52,19 @@ for step in "$@"; do
                run lgemm_mb 300 python -u scripts/learner_gemm_mb.py && cp "$OUT/lgemm_mb.out" "$OUT/lgemm_mb.json" &&
                run lgemm_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/lgemm_prof" -o run -- \
                    python3 scripts/learner_gemm_mb.py ;;
+        lgemmv) for v in ${LGV:-0 1 2 3}; do
+                    F110_LGEMM_VARIANT=$v run lgemm_v$v 300 rocprofv3 --kernel-trace --stats -d "$OUT/lgemm_v$v" -o run -- \
+                        python3 scripts/learner_gemm_mb.py || exit 1
+                done ;;
+        lgemmpmc) run lgemm_pmc1 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+                      SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
+                      -d "$OUT/lgemm_pmc1" -o run -- python3 scripts/learner_gemm_mb.py &&
+                  run lgemm_pmc2 120 rocprofv3 --pmc TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum SQ_INSTS_VMEM_RD \
+                      GRBM_GUI_ACTIVE --output-format csv -d "$OUT/lgemm_pmc2" -o run -- \
+                      python3 scripts/learner_gemm_mb.py ;;
         learner) run learner 600 python -u -m pytest tests/test_gpu_replay.py tests/test_gpu_ddpg_heads.py -m gpu -x -v \
                      --timeout 200 --timeout-method thread -p no:cacheprovider ;;
+        c5prof) run c5prof 900 python -u scripts/profile_c5.py "$TAG" ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python -u bench.py && cp "$OUT/bench.out" "$OUT/bench.json" ;;
         bench20) run bench20 600 python -u bench.py --steps 20 --warmup 5 && cp "$OUT/bench20.out" "$OUT/bench20.json" ;;

@@ -55,7 +55,7 @@ def main():
                                                                       w2=(Ws2, H), nx2=2, ldx2=2, ldw2=H + 2,
                                                                       relu=True)], M, dev))
         us["torch_dgrad_128"] = timed(lambda: G.mm(Ws2))
-        us["ours_dgrad_128_masked"] = timed(lambda: lg.gemm([lg.op(G, Ws2, y1, H, H, H, H + 2, H, amask=Y, omask=Z,
+        us["ours_dgrad_128_masked"] = timed(lambda: lg.gemm([lg.op(G, Ws2, y1, H, H, H, H + 2, H, omask=Z,
                                                                    nn=True)], M, dev))
         us["torch_wgrad_1088"] = timed(lambda: G.t().mm(S))
         dW = torch.empty(H, D, device="cuda")
@@ -63,8 +63,8 @@ def main():
         us["ours_wgrad_1088"] = timed(lambda: lg.wgrad([lg.wop(G, S, dW, H, D, H, D, D, db=db)], M, dev))
         us["torch_wgrad_128"] = timed(lambda: G.t().mm(Z))
         dW2 = torch.empty(H, H + 2, device="cuda")
-        us["ours_wgrad_128_130_1088"] = timed(lambda: lg.wgrad([lg.wop(G, Z, dW2, H, H, H, H, H + 2, db=db, gmask=Y),
-                                                               lg.wop(G, act, (dW2, H), H, 2, H, 2, H + 2, gmask=Y),
+        us["ours_wgrad_128_130_1088"] = timed(lambda: lg.wgrad([lg.wop(G, Z, dW2, H, H, H, H, H + 2, db=db),
+                                                               lg.wop(G, act, (dW2, H), H, 2, H, 2, H + 2),
                                                                lg.wop(Y, S, dW, H, D, H, D, D, db=db)], M, dev))
     flops = 2.0 * M * D * H
     out["tflops"] = {k: flops * n / (us[k] * 1e-6) / 1e12 for k, n in

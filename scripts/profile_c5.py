@@ -46,8 +46,7 @@ def stage(name):
     n = name
     if "f110::" in n:
         k = n.split("(f110::")[0].split("(float")[0].split("(int")[0].split("<")[0].split("::")[-1]
-        if k in ("k_agents", "k_rays", "k_rays_fx", "k_rays_fx_tail", "k_rays_tiled", "k_post", "k_post_multi",
-                 "k_post_single"):
+        if k.startswith("k_rays") or k in ("k_agents", "k_post_multi", "k_post_pair", "k_post_single"):
             return "env_step"
         if k.startswith("k_gap_follow"):
             return "opponent_gap_follow"
@@ -59,6 +58,8 @@ def stage(name):
             return "learner_adam"
         if k in HEADS:
             return "learner_heads"
+        if k in ("k_lgemm", "k_lwgrad", "k_lwgrad_finish"):  # csrc/f110_gemm.hip
+            return "learner_gemm"
     if n.startswith("Cijk") or "gemm" in n.lower() or "hipblaslt" in n.lower():
         return "learner_gemm"
     return "other_torch"
@@ -83,7 +84,8 @@ summary = {
     "kernel_ms_per_step_total": total / 1e6 / steps,
     "top_kernels": sorted(rows, key=lambda r: -r["total_ms"])[:25],
     "note": "per-step = total kernel time / traced steps (warm-up + timed + phase-split pass); learner GEMMs "
-            "are hipBLASLt (Cijk*), heads / ReLU backward / Adam are libf110 kernels",
+            "are libf110's k_lgemm / k_lwgrad (hipBLASLt Cijk* on the autograd path), heads / Adam are libf110 "
+            "kernels",
 }
 import shutil  # noqa: E402
 if not SUMMARIZE_ONLY:

@@ -78,9 +78,10 @@ def test_input_gradient_nn(gpu, M, K, N, ldb, off):
 
 @pytest.mark.parametrize("M", [4096, 333, 8])
 def test_weight_gradients(gpu, M):
-    """dW = G'^T X and db = sum G' for the three critic-phase ops of one
-    launch: fcs2's [128 x 128] + its 2 action columns (ldw 130) + fcs1's
-    [128 x 1088]; run twice: bit-identical."""
+    """dW = G'^T X and db = sum G' for the critic-phase ops: fcs2's
+    [128 x 128] + its 2 action columns (ldw 130) in one masked launch, fcs1's
+    [128 x 1088] in an unmasked one (grouped with a second op); one op alone
+    (a different slice count: same values); run twice: bit-identical."""
     lg = _lg()
     g = torch.Generator(device="cuda").manual_seed(M)
     G, Y, Z1, A, G1, S = _rand(g, M, 128), _rand(g, M, 128), _rand(g, M, 128), _rand(g, M, 2), _rand(g, M, 128), \
@@ -90,8 +91,10 @@ def test_weight_gradients(gpu, M):
         dWs2, dbs2 = torch.full((128, 130), float("nan"), device="cuda"), torch.empty(128, device="cuda")
         dWs1, dbs1 = torch.empty(128, 1088, device="cuda"), torch.empty(128, device="cuda")
         lg.wgrad([lg.wop(G, Z1, dWs2, 128, 128, 128, 128, 130, db=dbs2, gmask=Y),
-                  lg.wop(G, A, (dWs2, 128), 128, 2, 128, 2, 130, gmask=Y),
-                  lg.wop(G1, S, dWs1, 128, 1088, 128, 1088, 1088, db=dbs1)], M, G.device)
+                  lg.wop(G, A, (dWs2, 128), 128, 2, 128, 2, 130, gmask=Y)], M, G.device)
+        lg.wgrad([lg.wop(G1, S, dWs1, 128, 1088, 128, 1088, 1088, db=dbs1),
+                  lg.wop(G1, Z1, dWs2, 128, 128, 128, 128, 130)], M, G.device)  # overwritten by the next line
+        lg.wgrad([lg.wop(G, Z1, dWs2, 128, 128, 128, 128, 130, db=dbs2, gmask=Y)], M, G.device)
         outs.append((dWs2, dbs2, dWs1, dbs1))
     Gm = torch.where(Y > 0, G, torch.zeros_like(G)).double()
     zc = torch.cat([Z1, A], 1).double()
@@ -115,3 +118,7 @@ def test_rejects_bad_ops(gpu):
         lg.gemm([lg.op(x, x, y, 4, 16, 16, 16, 4, nn=False), lg.op(x, x, y, 4, 16, 16, 16, 4, nn=True)], 8, x.device)
     with pytest.raises((RuntimeError, _lib.F110Error)):
         lg.wgrad([lg.wop(x, x, y, 4, 16, 2, 16, 16)], 8, x.device)  # ldg < N
+    with pytest.raises((RuntimeError, _lib.F110Error)):  # gmask on one op of a launch only
+        lg.wgrad([lg.wop(x, x, y, 4, 16, 16, 16, 16, gmask=x), lg.wop(x, x, y, 4, 16, 16, 16, 16)], 8, x.device)
+    with pytest.raises(RuntimeError):  # amask on one op of a launch only
+        lg.gemm([lg.op(x, x, y, 4, 16, 16, 16, 4, amask=x), lg.op(x, x, y, 4, 16, 16, 16, 4)], 8, x.device)
