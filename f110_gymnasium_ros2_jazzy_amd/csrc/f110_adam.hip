@@ -10,7 +10,10 @@
 //   v = v*b2 + ((1-b2)*g)*g              exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1-beta2)
 //   p = p + (-lr/bc1) * (m / (sqrt(v)/sqrt(bc2) + eps))
 // with bc_i = 1 - beta_i^t from the device step counter t (graph-safe: the
-// last block to finish advances it).
+// last block to finish advances it).  With a target buffer the soft target
+// update of the same network follows in the same pass (agent.py:340-341,
+// target.lerp_(online, tau): t = t + tau * (p - t)): the reference applies it
+// after both networks' steps, and neither network changes in between.
 #include <hip/hip_runtime.h>
 
 #include "f110_internal.h"
@@ -33,9 +36,14 @@ __global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
         v = v * b2;
         v = v + (w2 * g) * g;
         const float denom = sqrtf(v) / bc2_sqrt + eps;
-        a.param[i] = a.param[i] + (-step_size) * (m / denom);
+        const float p = a.param[i] + (-step_size) * (m / denom);
+        a.param[i] = p;
         a.exp_avg[i] = m;
         a.exp_avg_sq[i] = v;
+        if (a.target) {
+            const float t0 = a.target[i];
+            a.target[i] = t0 + a.tau * (p - t0);
+        }
     }
     // the last block to finish advances the step counter
     __syncthreads();

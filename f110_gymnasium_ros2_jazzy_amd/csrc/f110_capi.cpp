@@ -98,10 +98,6 @@ struct f110_ctx {
     uint32_t rmp_zero = 0;
     bool fx_pad = false;    // the padded table is wanted (from 32768 cars or with refill; F110_FX_PAD=0: never)
     int32_t fx_refill = 0;   // waves per car of k_rays_fxs (0 = k_rays_fxn; f110_set_ray_refill)
-    int32_t fxs_variant = 0;  // f110_set_ray_variant (A/B)
-    uint16_t *lcost = nullptr;   // [EA * nch] k_rays_fxs's per-wave-item trips (LPT order keys)
-    uint32_t *lorder = nullptr;  // [EA * nch] the LPT wave order built from them
-    int32_t lpt_items = 0;       // items of the last order built (0: none)
     bool count_slots = false;  // f110_set_simt: lane-slot counter of the fixed-point loops (f110_read_simt)
     int fx_ilp = 1;         // rays per lane (f110_set_ray_lanes; default by car count)
 
@@ -758,11 +754,6 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     // 65536 envs as 2 x 32768 67.1 vs 63.0 M env-steps/s; at 16384 cars its long waves
     // leave a tail (0.324 vs 0.289 ms); it runs only without heavy-first and masks
     c->fx_refill = EA >= 32768 ? 1 : 0;
-    if (fx_ok) {  // LPT wave order of k_rays_fxs (f110_set_ray_variant bit 0)
-        hipError_t ea = c->alloc(&c->lcost, EA * (size_t)c->nch);
-        if (ea == hipSuccess) ea = c->alloc(&c->lorder, EA * (size_t)c->nch);
-        if (ea != hipSuccess) return cleanup(F110_E_ALLOC, std::string("hipMalloc lpt: ") + hipGetErrorString(ea));
-    }
     const double pad_q = std::ceil(C.max_range / resolution) + 8.0;
     const int32_t fx_pad_cells = pad_q > 0.0 && pad_q < 65536.0 ? (int32_t)pad_q : 0;  // else no padded table
     if (e == hipSuccess)
@@ -880,11 +871,6 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.fxs_ok = fxs_ok(c) ? 1 : 0;
     a.count_slots = c->count_slots ? 1 : 0;
     a.fx_refill = c->fx_refill;
-    a.fxs_variant = c->fxs_variant;
-    a.lcost = c->lcost;
-    a.lorder = c->lorder;
-    a.lpt_items = c->lpt_items;
-    a.lpt_items_out = &c->lpt_items;
     a.fx_ilp = c->fx_ilp;
     a.gate_wait = c->gate_wait;
     a.gate_record = c->gate_record;
@@ -1031,13 +1017,6 @@ extern "C" int f110_set_ray_lanes(f110_ctx *ctx, int32_t n) {
     const bool fx = ctx->ray_kernel == 3;
     if (!fx && n != 1) return fail(F110_E_INVALID, "f110_set_ray_lanes: this context's ray kernel traces one ray per lane");
     if (fx) ctx->fx_ilp = n;
-    return F110_OK;
-}
-
-extern "C" int f110_set_ray_variant(f110_ctx *ctx, int32_t variant) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_variant: null context");
-    if (variant < 0 || variant > 7) return fail(F110_E_INVALID, "f110_set_ray_variant: variant must be in 0..7");
-    ctx->fxs_variant = variant;
     return F110_OK;
 }
 

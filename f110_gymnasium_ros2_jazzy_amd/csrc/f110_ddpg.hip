@@ -347,120 +347,6 @@ __global__ void __launch_bounds__(kHB) k_colsum_finish(const float *part, int32_
     if (lane == 0) out[c] = s;
 }
 
-// A hidden layer forward, Y = relu(X W^T + b) (agent.py's F.relu(fc(x))),
-// on the fp32 matrix cores: X [M][K], W [N][K] row-major (both K-contiguous),
-// N a multiple of 32, K of 32.  A block owns a 32 x 32 output tile (2 x 2
-// v_mfma_f32_16x16x4_f32 accumulators per wave) and splits K over its 4
-// waves (M = 4096: 512 blocks; the BLAS tile of 128 rows leaves half the
-// CUs idle at this M); the four partial tiles meet in LDS and are summed in
-// wave order.  Per 32-k chunk a lane loads two float4 of each of its two X
-// rows and two W columns - a whole 128 B line per row per chunk, so L2
-// sends every line once per block - and issues 32 MFMAs, with the next
-// chunk's loads in flight.  k = 32c + 16j + 4h + e for lane quarter h,
-// float4 j, element e: the same permutation on both sides, so each partial
-// is an exact fp32 fma chain of a reordered sum.  The column tiles of one
-// row tile are consecutive on one XCD (blockIdx % 8), so X is fetched into
-// one L2.  Bias and ReLU (NaN kept, as torch's relu) in the epilogue.
-using f32x4 = __attribute__((ext_vector_type(4))) float;
-constexpr int kLRows = 32, kLCols = 32, kLWaves = 4;
-
-struct LinFrag {
-    float4 a[2][2], b[2][2];  // [row / column half][16-k half]
-};
-
-// pins a prefetched float4 in its registers: without it the compiler turns
-// the register double buffer back into loads at the top of each iteration
-__device__ __forceinline__ void pin(float4 &v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
-
-__device__ __forceinline__ f32x4 mfma4(const float4 &a, const float4 &b, f32x4 acc) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
-}
-
-__global__ void __launch_bounds__(256) k_linear_relu(const float *__restrict__ X, const float *__restrict__ W,
-                                                     const float *__restrict__ bias, float *__restrict__ Y, int32_t M,
-                                                     int32_t K, int32_t N) {
-    __shared__ float red[kLWaves * 16 * 64];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ncg = N / kLCols;  // column tiles per row tile
-    const int blk = (int)blockIdx.x;
-    // XCD-aware: the ncg column tiles of a row tile share blockIdx % 8
-    const int grp = blk / (8 * ncg), rem = blk % (8 * ncg);
-    const int rt = grp * 8 + rem % 8, cg = rem / 8;
-    const int64_t row0 = (int64_t)rt * kLRows;
-    const int col0 = cg * kLCols;
-    const int li = lane & 15, lh = lane >> 4;
-    const float *pa[2], *pb[2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        const int64_t ar = row0 + 16 * r + li < M ? row0 + 16 * r + li : M - 1;  // rows past M: computed, not stored
-        pa[r] = X + ar * K + 4 * lh;
-        pb[r] = W + (int64_t)(col0 + 16 * r + li) * K + 4 * lh;
-    }
-    const int C = K >> 5;
-    const int beg = wave * C / kLWaves, end = (wave + 1) * C / kLWaves;
-    // unconditional loads (past this wave's range: its last chunk again,
-    // unused) - no branch around them, so the wait before a chunk's MFMAs
-    // is for that chunk's loads, issued one chunk earlier
-    auto load = [&](int ch, LinFrag &f) {
-        const int o = 32 * max(min(ch, end - 1), 0);
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                f.a[r][j] = *reinterpret_cast<const float4 *>(pa[r] + o + 16 * j);
-                f.b[r][j] = *reinterpret_cast<const float4 *>(pb[r] + o + 16 * j);
-            }
-    };
-    f32x4 acc[2][2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) acc[r][c] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    LinFrag cur;
-    load(beg, cur);
-    for (int ch = beg; ch < end; ++ch) {
-        LinFrag nxt;
-        load(ch + 1, nxt);
-        __builtin_amdgcn_sched_barrier(0);  // the prefetch goes out before this chunk's MFMAs
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 2; ++r)
-#pragma unroll
-                for (int c = 0; c < 2; ++c) acc[r][c] = mfma4(cur.a[r][j], cur.b[c][j], acc[r][c]);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                pin(nxt.a[r][j]);
-                pin(nxt.b[r][j]);
-            }
-        cur = nxt;
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) red[(wave * 16 + t * 4 + q) * 64 + lane] = acc[t >> 1][t & 1][q];
-    __syncthreads();
-    // thread -> (lane, registers 4*wave .. 4*wave+3): the 4 partials in wave order
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int e = wave * 4 + j, t = e >> 2, q = e & 3;
-        float v = red[e * 64 + lane];
-#pragma unroll
-        for (int w = 1; w < kLWaves; ++w) v += red[(w * 16 + e) * 64 + lane];
-        // C/D: column = lane & 15, row = (lane >> 4) * 4 + register
-        const int c = col0 + 16 * (t & 1) + li;
-        const int64_t row = row0 + 16 * (t >> 1) + 4 * lh + q;
-        v += bias[c];
-        if (row < M) Y[row * N + c] = v > 0.0f ? v : (v != v ? v : 0.0f);
-    }
-}
-
 template <class F>
 hipError_t with_nout(int nout, F f) {
     switch (nout) {
@@ -529,18 +415,6 @@ extern "C" int f110_ddpg_relu_bwd(const float *gy, const float *y, int32_t B, in
         e = hipGetLastError();
     }
     return e == hipSuccess ? 0 : fail_hip("f110_ddpg_relu_bwd", e);
-}
-
-extern "C" int f110_ddpg_linear_relu(const float *x, const float *W, const float *b, int32_t M, int32_t K,
-                                     int32_t N, float *y, void *stream) {
-    if (M <= 0 || K <= 0 || N <= 0 || K % 32 || N % kLCols || !x || !W || !b || !y)
-        return fail_arg("f110_ddpg_linear_relu");
-    // row tiles padded to a multiple of 8 (whole XCD groups); padded tiles store nothing
-    const int64_t rts = ((int64_t)(M + kLRows - 1) / kLRows + 7) / 8 * 8;
-    const dim3 grid((unsigned)(rts * (N / kLCols)));
-    hipLaunchKernelGGL(k_linear_relu, grid, dim3(256), 0, (hipStream_t)stream, x, W, b, y, M, K, N);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : fail_hip("f110_ddpg_linear_relu", e);
 }
 
 extern "C" int f110_ddpg_actor_head(const float *h, const float *W, const float *b, const float *scale,

@@ -27,7 +27,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <string>
 
 #include "f110_internal.h"
@@ -93,14 +92,17 @@ struct Frag {
     float4 b[kTN / 32][2];
 };
 
-// VEC: A rows (and amask) 16-B aligned; BV: B rows (nn = 0) loaded as float4 / float2 / floats;
-// NW waves per block split K; NB register buffers (NB - 1 chunks of loads in flight)
-template <bool NN, bool VEC, int BV, bool AMASK, int NW, int NB>
-__global__ void __launch_bounds__(64 * NW) k_lgemm(GemmLaunch L) {
+// VEC: A rows (and amask) 16-B aligned; BV: B rows (nn = 0) loaded as float4 / float2 / floats.
+// NW waves per block split K; NB register buffers (NB - 1 chunks of loads in flight).  Round 4
+// measured 8 waves and 3 buffers (no faster), v_mfma_f32_16x16x4_f32 with 8 accumulators (slower
+// on the grouped launches) and a probe without loads in the loop (the 3-op launch 42 -> 29 us: the
+// operand path, ~14 B/clk/CU of fragment-shaped loads, is the bound)
+template <bool NN, bool VEC, int BV, bool AMASK>
+__global__ void __launch_bounds__(256) k_lgemm(GemmLaunch L) {
+    constexpr int NW = 4, NB = 2;
     constexpr int RI = kTM / 32, RJ = kTN / 32, R = RI * RJ * 16;
-    static_assert(R % NW == 0 && NB >= 1 && (NW == 4 || NW == 8), "tile registers split evenly over the waves");
-    constexpr int NR = NW > 4 ? NW / 2 : NW;  // partial tiles in LDS (<= 32 KB; 8 waves fold in pairs first)
-    __shared__ float red[NR][R][64];
+    static_assert(R % NW == 0, "tile registers split evenly over the waves");
+    __shared__ float red[NW][R][64];
     const int blk = (int)blockIdx.x;
     f110_gemm_op o;
     const int p = select_op(L, blk, o);
@@ -220,14 +222,8 @@ __global__ void __launch_bounds__(64 * NW) k_lgemm(GemmLaunch L) {
     };
     // NB register buffers: while chunk c's MFMAs issue, chunks c+1 .. c+NB-1 are in flight
     const int cf = min(ce, K >> 4);
-    if (NB == 1) {  // measurement probe: one chunk loaded, the MFMAs of all (wrong values, issue ceiling)
-        if (cb < cf) {
-            Frag f0;
-            load_full(cb, f0);
-            for (int c = cb; c < cf; ++c) compute(f0);
-        }
-    } else if (cb < cf) {
-        Frag f[NB > 1 ? NB : 2];
+    if (cb < cf) {
+        Frag f[NB];
 #pragma unroll
         for (int u = 0; u < NB - 1; ++u) load_full(min(cb + u, cf - 1), f[u]);
         int c = cb;
@@ -249,31 +245,12 @@ __global__ void __launch_bounds__(64 * NW) k_lgemm(GemmLaunch L) {
         load_tail(cf, ft);
         compute(ft);
     }
-    if (NW > NR) {  // waves NR.. hand their tiles to waves 0..NR-1
-        if (wave >= NR)
 #pragma unroll
-            for (int i = 0; i < RI; ++i)
+    for (int i = 0; i < RI; ++i)
 #pragma unroll
-                for (int j = 0; j < RJ; ++j)
+        for (int j = 0; j < RJ; ++j)
 #pragma unroll
-                    for (int v = 0; v < 16; ++v) red[wave - NR][(i * RJ + j) * 16 + v][lane] = acc[i][j][v];
-        __syncthreads();
-        if (wave < NR)
-#pragma unroll
-            for (int i = 0; i < RI; ++i)
-#pragma unroll
-                for (int j = 0; j < RJ; ++j)
-#pragma unroll
-                    for (int v = 0; v < 16; ++v) acc[i][j][v] += red[wave][(i * RJ + j) * 16 + v][lane];
-        __syncthreads();
-    }
-    if (wave < NR)
-#pragma unroll
-        for (int i = 0; i < RI; ++i)
-#pragma unroll
-            for (int j = 0; j < RJ; ++j)
-#pragma unroll
-                for (int v = 0; v < 16; ++v) red[wave][(i * RJ + j) * 16 + v][lane] = acc[i][j][v];
+            for (int v = 0; v < 16; ++v) red[wave][(i * RJ + j) * 16 + v][lane] = acc[i][j][v];
     __syncthreads();
     // thread (wave, lane): registers wave*R/NW .. of every partial tile, summed in wave order
 #pragma unroll
@@ -281,134 +258,11 @@ __global__ void __launch_bounds__(64 * NW) k_lgemm(GemmLaunch L) {
         const int v = wave * (R / NW) + u;
         float s = red[0][v][lane];
 #pragma unroll
-        for (int w = 1; w < NR; ++w) s += red[w][v][lane];
+        for (int w = 1; w < NW; ++w) s += red[w][v][lane];
         const int t = v >> 4, vv = v & 15;
         const int i = t / RJ, j = t - i * RJ;
         const int row = m0 + 32 * i + (vv & 3) + 8 * (vv >> 2) + 4 * h;
         const int col = n0 + 32 * j + r;
-        if (row < M && col < N) {
-            for (int x = 0; x < o.nx2; ++x) s = fmaf(o.x2[(size_t)row * o.ldx2 + x], o.w2[(size_t)col * o.ldw2 + x], s);
-            if (o.bias) s += o.bias[col];
-            if (o.relu) s = relu_nan(s);
-            if (o.omask) s = o.omask[(size_t)row * o.ldc + col] > 0.0f ? s : 0.0f;
-            o.C[(size_t)row * o.ldc + col] = s;
-        }
-    }
-}
-
-// k_lgemm16: k_lgemm's tile (32 x 64 per block, K split over 4 waves) on
-// v_mfma_f32_16x16x4_f32: 8 accumulators per wave (2 x 4 blocks of 16 x 16),
-// lane (i, g) = (l & 15, l >> 4) loads float4 at k = 16c + 4g of its row, so
-// one load instruction covers 16 rows x 64 B.  NT, aligned, unmasked only.
-// (NB == 1: the issue-ceiling probe, see k_lgemm.)
-template <int NB>
-__global__ void __launch_bounds__(kGB) k_lgemm16(GemmLaunch L) {
-    constexpr int RI = kTM / 16, RJ = kTN / 16, R = RI * RJ * 4;
-    __shared__ float red[4][R][64];
-    const int blk = (int)blockIdx.x;
-    f110_gemm_op o;
-    const int p = select_op(L, blk, o);
-    int ntn = L.ntn[0], b0 = L.blk0[0];
-#pragma unroll
-    for (int q = 1; q < kMaxOps; ++q)
-        if (p == q) {
-            ntn = L.ntn[q];
-            b0 = L.blk0[q];
-        }
-    const int local = blk - b0;
-    const int grp = local / (8 * ntn), rem = local - grp * 8 * ntn;
-    const int m0 = (grp * 8 + (rem & 7)) * kTM, n0 = (rem >> 3) * kTN;
-    const int M = L.M, N = o.N, K = o.K;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
-    const int nch = (K + 15) >> 4;
-    const int cb = wave * nch / 4, ce = (wave + 1) * nch / 4;
-    const float *pa[RI], *pb[RJ];
-#pragma unroll
-    for (int i = 0; i < RI; ++i) pa[i] = o.A + (size_t)min(m0 + 16 * i + li, M - 1) * o.lda + 4 * lg;
-#pragma unroll
-    for (int j = 0; j < RJ; ++j) pb[j] = o.B + (size_t)min(n0 + 16 * j + li, N - 1) * o.ldb + 4 * lg;
-    struct F16 {
-        float4 a[RI], b[RJ];
-    };
-    auto load_full = [&](int c, F16 &f) {
-#pragma unroll
-        for (int i = 0; i < RI; ++i) f.a[i] = *reinterpret_cast<const float4 *>(pa[i] + 16 * c);
-#pragma unroll
-        for (int j = 0; j < RJ; ++j) f.b[j] = *reinterpret_cast<const float4 *>(pb[j] + 16 * c);
-    };
-    auto load_tail = [&](int c, F16 &f) {
-        const int k = 16 * c + 4 * lg;
-#pragma unroll
-        for (int i = 0; i < RI; ++i)
-            f.a[i] = make_float4(k < K ? pa[i][16 * c] : 0.0f, k + 1 < K ? pa[i][16 * c + 1] : 0.0f,
-                                 k + 2 < K ? pa[i][16 * c + 2] : 0.0f, k + 3 < K ? pa[i][16 * c + 3] : 0.0f);
-#pragma unroll
-        for (int j = 0; j < RJ; ++j)
-            f.b[j] = make_float4(k < K ? pb[j][16 * c] : 0.0f, k + 1 < K ? pb[j][16 * c + 1] : 0.0f,
-                                 k + 2 < K ? pb[j][16 * c + 2] : 0.0f, k + 3 < K ? pb[j][16 * c + 3] : 0.0f);
-    };
-    using f32x4v = __attribute__((ext_vector_type(4))) float;
-    f32x4v acc[RI][RJ];
-#pragma unroll
-    for (int i = 0; i < RI; ++i)
-#pragma unroll
-        for (int j = 0; j < RJ; ++j) acc[i][j] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-    auto compute = [&](const F16 &f) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int i = 0; i < RI; ++i)
-#pragma unroll
-                for (int j = 0; j < RJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(get(f.a[i], e), get(f.b[j], e), acc[i][j], 0, 0, 0);
-    };
-    const int cf = min(ce, K >> 4);
-    if (NB == 1) {
-        if (cb < cf) {
-            F16 f0;
-            load_full(cb, f0);
-            for (int c = cb; c < cf; ++c) compute(f0);
-        }
-    } else if (cb < cf) {
-        F16 f[NB > 1 ? NB : 2];
-#pragma unroll
-        for (int u = 0; u < NB - 1; ++u) load_full(min(cb + u, cf - 1), f[u]);
-        int c = cb;
-        for (; c + NB <= cf; c += NB) {
-#pragma unroll
-            for (int u = 0; u < NB; ++u) {
-                load_full(min(c + u + NB - 1, cf - 1), f[(u + NB - 1) % NB]);
-                __builtin_amdgcn_sched_barrier(0);
-                compute(f[u]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < NB - 1; ++u)
-            if (c + u < cf) compute(f[u]);
-    }
-    if (ce > cf) {
-        F16 ft;
-        load_tail(cf, ft);
-        compute(ft);
-    }
-#pragma unroll
-    for (int i = 0; i < RI; ++i)
-#pragma unroll
-        for (int j = 0; j < RJ; ++j)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) red[wave][(i * RJ + j) * 4 + v][lane] = acc[i][j][v];
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < R / 4; ++u) {
-        const int v = wave * (R / 4) + u;
-        float s = red[0][v][lane];
-#pragma unroll
-        for (int w = 1; w < 4; ++w) s += red[w][v][lane];
-        const int t = v >> 2, q = v & 3;
-        const int i = t / RJ, j = t - i * RJ;
-        const int row = m0 + 16 * i + 4 * lg + q;  // C/D: column = lane & 15, row = (lane >> 4) * 4 + register
-        const int col = n0 + 16 * j + li;
         if (row < M && col < N) {
             for (int x = 0; x < o.nx2; ++x) s = fmaf(o.x2[(size_t)row * o.ldx2 + x], o.w2[(size_t)col * o.ldw2 + x], s);
             if (o.bias) s += o.bias[col];
@@ -653,7 +507,7 @@ extern "C" int f110_learner_gemm(const f110_gemm_op *ops, int32_t nops, int32_t 
     }
     L.blk0[nops] = blk;
     for (int q = nops; q < kMaxOps; ++q) L.blk0[q] = blk;
-#define F110_LG(NN, V, BV, AM) reinterpret_cast<const void *>(&k_lgemm<NN, V, BV, AM, 4, 2>)
+#define F110_LG(NN, V, BV, AM) reinterpret_cast<const void *>(&k_lgemm<NN, V, BV, AM>)
     const void *fs[2][2][3][2] = {  // [nn][vec][bv: 1, 2, 4][amask]
         {{{F110_LG(false, false, 1, false), F110_LG(false, false, 1, true)},
           {F110_LG(false, false, 2, false), F110_LG(false, false, 2, true)},
@@ -670,31 +524,8 @@ extern "C" int f110_learner_gemm(const f110_gemm_op *ops, int32_t nops, int32_t 
 #undef F110_LG
     const int bvi = bv == 4 ? 2 : bv == 2 ? 1 : 0;
     const void *k = fs[nn][vec ? 1 : 0][bvi][am];
-    int nw = 4;
-    // A/B of the pipeline shape (F110_LGEMM_VARIANT, measurement only): 1 = 4 waves x 3
-    // buffers, 2 = 8 waves x 2, 3 = 8 waves x 3 (unmasked, aligned launches)
-    static const int variant = [] {
-        const char *v = std::getenv("F110_LGEMM_VARIANT");
-        return v ? std::atoi(v) : 0;
-    }();
-    if (variant >= 1 && variant <= 3 && vec && !am) {
-#define F110_LGV(NN, BV, NW, NB) reinterpret_cast<const void *>(&k_lgemm<NN, true, BV, false, NW, NB>)
-        const void *vs[3][3] = {  // [variant - 1][nt bv 4, nt bv 2, nn]
-            {F110_LGV(false, 4, 4, 3), F110_LGV(false, 2, 4, 3), F110_LGV(true, 1, 4, 3)},
-            {F110_LGV(false, 4, 8, 2), F110_LGV(false, 2, 8, 2), F110_LGV(true, 1, 8, 2)},
-            {F110_LGV(false, 4, 8, 3), F110_LGV(false, 2, 8, 3), F110_LGV(true, 1, 8, 3)}};
-#undef F110_LGV
-        const int col = nn ? 2 : bv == 4 ? 0 : bv == 2 ? 1 : -1;
-        if (col >= 0) {
-            k = vs[variant - 1][col];
-            nw = variant == 1 ? 4 : 8;
-        }
-    }
-    if (variant == 4 && vec && !am && !nn && bv == 4) k = reinterpret_cast<const void *>(&k_lgemm<false, true, 4, false, 4, 1>);
-    if (variant == 5 && vec && !am && !nn && bv == 4) k = reinterpret_cast<const void *>(&k_lgemm16<2>);
-    if (variant == 6 && vec && !am && !nn && bv == 4) k = reinterpret_cast<const void *>(&k_lgemm16<1>);
     void *args[] = {&L};
-    hipError_t e = hipLaunchKernel(k, dim3((unsigned)blk), dim3(64 * nw), args, 0, (hipStream_t)stream);
+    hipError_t e = hipLaunchKernel(k, dim3((unsigned)blk), dim3(kGB), args, 0, (hipStream_t)stream);
     if (e == hipSuccess) e = hipGetLastError();
     return e == hipSuccess ? 0 : f110_set_error(F110_E_HIP, std::string(fn) + ": " + hipGetErrorString(e));
 }

@@ -59,11 +59,6 @@ struct StepArgs {
     int32_t fx_pad;     // the padded table is built (k_rays_fxn on it unless F110_FX_PAD=0; k_rays_fxs)
     int32_t fxs_ok;     // the padded table's rows and columns are below 2^20 (kFxsBase's offsets)
     int32_t fx_refill;  // waves per car of k_rays_fxs (two chunk slots with refill; 0 = off)
-    int32_t fxs_variant;  // f110_set_ray_variant (A/B bits; 0 = the defaults)
-    uint16_t *lcost;      // [EA * nch] k_rays_fxs: each wave item's trips in the previous launch (LPT key)
-    uint32_t *lorder;     // [EA * nch] k_lpt_order: wave items, longest first
-    int32_t lpt_items;    // items the order was last built for (0: none yet)
-    int32_t *lpt_items_out;  // host: set to the items of the order this step builds
     int32_t count_slots;  // f110_set_simt: lane-slot counter of the fixed-point loops
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2: k_rays_fxn / k_rays_fxs)
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
@@ -164,8 +159,6 @@ struct RayArgs {
     int32_t fxp_P;
     double fxs_cx, fxs_cy;  // k_rays_fxs: 2^20 + P + 2^-26 - origin / res (see kFxsBase)
     int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_read_simt)
-    uint16_t *lcost;         // k_rays_fxs: each wave item's trips written here (or null)
-    const uint32_t *lorder;  // k_rays_fxs: block p traces item lorder[p] (or null: item p)
     const double *cs2, *bs2;  // k_rays_fxs: interleaved (cos, sin) / (side, beam_cos) tables
 };
 
@@ -310,7 +303,7 @@ struct ReplayBatch {     // one sample(): the gathered batch (device, contiguous
 hipError_t launch_replay_add(const ReplayView &v, const ReplayRows &in, const uint8_t *mask, int64_t n,
                              hipStream_t s);
 hipError_t launch_replay_sample(const ReplayView &v, int32_t batch, double beta, int64_t *idx, float *w,
-                                const ReplayBatch &out, hipStream_t s);
+                                const ReplayBatch &out, bool known_full, hipStream_t s);
 hipError_t launch_replay_update(const ReplayView &v, const int64_t *idx, const float *val, int64_t n, float add_eps,
                                 int32_t from_td, int32_t serial, hipStream_t s);
 hipError_t prepare_replay(int32_t max_batch);
@@ -324,6 +317,8 @@ struct AdamArgs {
     double lr, beta1, beta2, eps;
     int64_t *step;     // device step counter
     uint32_t *done;    // device: blocks finished (last one advances step)
+    float *target;     // the target network's flat buffer (soft update after the step) or null
+    float tau;
 };
 hipError_t launch_adam(const AdamArgs &a, hipStream_t s);
 

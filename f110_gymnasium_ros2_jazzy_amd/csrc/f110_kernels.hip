@@ -1097,11 +1097,11 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
 // other with the IEEE cell.  Per ray the arithmetic is k_rays_fxn's, so
 // bit-identical.
 //
-// Chunk order: descending chunk index (the scan's left edge first).  (Longest
-// pair first by the previous launch's per-chunk trips, ORD, cut the trips 5 %
-// and lost 1-2 % of time: round 4)  Wave order (LPT): with
-// RayArgs::lorder the block at position p traces wave item lorder[p] (k_lpt_order
-// sorts the previous launch's per-item trip counts, RayArgs::lcost, longest first).
+// Chunk order: descending chunk index (the scan's left edge first).  Round 4
+// measured two reorderings, both bit-identical and both slower:
+// the car's chunk pairs longest first by the previous launch's trips (5 % fewer
+// trips, 1-2 % slower), and the blocks' wave items longest first (LPT: the
+// indirection costs this 64-VGPR kernel 21 spilled registers).
 //
 // The refill pass keeps nothing in SGPRs across the loop: kernel arguments
 // are re-read at the use through kernarg_here, the scan origin and first
@@ -1121,9 +1121,8 @@ template <bool HANDOFF>
 __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
     constexpr int NS = 2;
     wave_stamp_start(a.wtrace);
-    const int item = a.lorder ? (int)ld_const(a.lorder + blockIdx.x) : (int)blockIdx.x;  // (wj, g) of this block
-    const int wj = item / a.EA;
-    const int g = item - wj * a.EA;
+    const int wj = (int)blockIdx.x / a.EA;
+    const int g = (int)blockIdx.x - wj * a.EA;
     const int lane = (int)threadIdx.x;
     const int B = a.B;
     const int e = HANDOFF ? g / a.A : g;
@@ -1313,7 +1312,6 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
     }
     if (lane == 0) {
         const RayArgs &K = kernarg_here();
-        if (K.lcost) K.lcost[item] = (uint16_t)(trips < 0xffffu ? trips : 0xffffu);  // the next launch's LPT key
         unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
         atomicAdd(cs, (unsigned long long)(lanes + lane_iters));  // the first lookup came from k_agents
         atomicAdd(cs + 1, (unsigned long long)lanes);
@@ -1638,229 +1636,6 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
     if (tid == 0) env_epilogue(a, e, &sh.stl[0][0], 7, sh.col, sh.do_reset, sh.epe, sh.epi);
 }
 
-// k_post_pair: k_post_multi's work for two-agent envs, EPB envs per wave.
-// k_post_multi's serial phases run on one or two lanes of a 128-thread block
-// per env; here every phase spreads over the EPB envs of one wave: a lane per
-// (env, car) for the loads, the TTC response, the opponent box and the
-// heading, a lane per env for GJK, a lane per (env, car, vertex) for the
-// blocked beams, a lane per (env, car) for the beam windows, then every
-// (env, car, beam) item of the agent ray_cast flattened over the wave.  Same
-// operations on the same operands as k_post_multi: bit-identical results.
-template <int EPB> struct PairSlot {
-    double stl[2][7];   // state after the TTC response
-    double pose0[2][3]; // agent_poses before the TTC response (base_classes.py:587)
-    double rv[2][8];    // pair i: opponent 1-i seen by car i (RaceCar i's params)
-    double phi[2][4];
-    double ego[2];
-    double wcen[2], whalf[2];
-    int32_t rng[2][4];
-    int32_t kq[2][4];
-    int32_t col[2];
-    int32_t valid, do_reset;
-    EpiCar epi[2];
-    EpiEnv epe;
-};
-
-template <int EPB> __global__ void __launch_bounds__(64) k_post_pair(StepArgs a) {
-    static_assert(3 * EPB <= 64 && (EPB & (EPB - 1)) == 0, "EPB: a power of two, three lanes per env");
-    reset_next_heavy(a);
-    __shared__ PairSlot<EPB> sh[EPB];
-    __shared__ int32_t off[2 * EPB];  // first ray_cast item of each (env, car) pass
-    const int lane = threadIdx.x;
-    const int B = a.B;
-    const int EA = a.E * 2;
-    const int e0 = blockIdx.x * EPB;
-    // ---- (env, car) lanes: loads, TTC response (RaceCar.check_ttc, base_classes.py:246-249)
-    if (lane < 2 * EPB) {
-        const int s = lane >> 1, i = lane & 1;
-        const int e = e0 + s;
-        PairSlot<EPB> &q = sh[s];
-        const bool valid = e < a.E && !(a.mode == 1 && a.reset_mask && !a.reset_mask[e]);
-        if (i == 0) q.valid = valid;
-        if (valid) {
-            const int g = e * 2 + i;
-            double st[7];
-#pragma unroll
-            for (int k = 0; k < 7; ++k) st[k] = a.st[(size_t)k * EA + g];
-            const int hit = a.ttc_hit[g];
-            epilogue_load_car(a, g, q.epi[i]);
-            if (i == 0) {
-                q.do_reset = a.reset_flag[e];
-                epilogue_load_env(a, e, q.epe);
-            }
-            q.pose0[i][0] = st[0];
-            q.pose0[i][1] = st[1];
-            q.pose0[i][2] = st[4];
-            q.col[i] = hit;  // Simulator.step :601-602
-            if (hit) {
-#pragma unroll
-                for (int k = 3; k < 7; ++k) {
-                    st[k] = 0.0;
-                    a.st[(size_t)k * EA + g] = 0.0;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < 7; ++k) q.stl[i][k] = st[k];
-        }
-    }
-    wave_sync();
-    if (lane < 2 * EPB) {  // opponent box seen by car i, ego heading (post-TTC yaw)
-        const int s = lane >> 1, i = lane & 1;
-        PairSlot<EPB> &q = sh[s];
-        if (q.valid) {
-            const f110_params &pi = a.pa[i];
-            get_vertices(q.pose0[1 - i][0], q.pose0[1 - i][1], q.pose0[1 - i][2], pi.length, pi.width, q.rv[i]);
-            double ys, yc;
-            cr_sincos(q.stl[i][4], ys, yc);
-            q.ego[i] = atan2(ys, yc);
-        }
-    } else if (lane < 3 * EPB) {  // collision_multiple (collision_models.py:184-212) on Simulator.params boxes
-        PairSlot<EPB> &q = sh[lane - 2 * EPB];
-        if (q.valid) {
-            double v0[8], v1[8];
-            get_vertices(q.pose0[0][0], q.pose0[0][1], q.pose0[0][2], a.p.length, a.p.width, v0);
-            get_vertices(q.pose0[1][0], q.pose0[1][1], q.pose0[1][2], a.p.length, a.p.width, v1);
-            if (gjk_collision(v0, v1)) {
-                q.col[0] = 1;
-                q.col[1] = 1;
-            }
-        }
-    }
-    wave_sync();
-    for (int w = lane; w < 8 * EPB; w += 64) {  // get_blocked_view_indices, one (env, car, vertex) per lane
-        PairSlot<EPB> &q = sh[w >> 3];
-        const int i = (w >> 2) & 1, v = w & 3;
-        if (q.valid)
-            q.kq[i][v] = blocked_vertex_beam(q.stl[i][0], q.stl[i][1], q.ego[i], q.rv[i][2 * v], q.rv[i][2 * v + 1], B,
-                                             a.fov, a.beam_incr, q.phi[i][v]);
-    }
-    wave_sync();
-    int cnt = 0;
-    if (lane < 2 * EPB) {  // each pass's beams: window_beam_ranges clipped to the blocked range
-        const int s = lane >> 1, i = lane & 1;
-        PairSlot<EPB> &q = sh[s];
-        if (q.valid) {
-            int lo = q.kq[i][0], hi = q.kq[i][0];
-#pragma unroll
-            for (int v = 1; v < 4; ++v) {
-                lo = q.kq[i][v] < lo ? q.kq[i][v] : lo;
-                hi = q.kq[i][v] > hi ? q.kq[i][v] : hi;
-            }
-            double wc, wh;
-            box_beam_window(q.stl[i][0], q.stl[i][1], q.rv[i], q.phi[i], wc, wh);
-            q.wcen[i] = wc;
-            q.whalf[i] = wh;
-            int r0a, r0b, r1a, r1b;
-            window_beam_ranges(q.stl[i][4], a.fov, a.beam_incr, B, wc, wh, r0a, r0b, r1a, r1b);
-            const int ra = r0a > lo ? r0a : lo, rb = r0b < hi ? r0b : hi;
-            const int rc = r1a > lo ? r1a : lo, rd = r1b < hi ? r1b : hi;
-            q.rng[i][0] = ra;
-            q.rng[i][1] = rb;
-            q.rng[i][2] = rc;
-            q.rng[i][3] = rd;
-            cnt = (rb >= ra ? rb - ra + 1 : 0) + (rd >= rc ? rd - rc + 1 : 0);
-        }
-    }
-    int incl = cnt;  // inclusive prefix over the wave's passes
-#pragma unroll
-    for (int d = 1; d < 2 * EPB; d <<= 1) {
-        const int t = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += t;
-    }
-    const int total = __shfl(incl, 2 * EPB - 1, 64);
-    if (lane < 2 * EPB) off[lane] = incl - cnt;
-    wave_sync();
-    // agent ray_cast (base_classes.py:206-227; laser_models.py:318-346): the
-    // beams of every (env, car) pass, one item per lane
-    for (int item = lane; item < total; item += 64) {
-        int p = 0;
-#pragma unroll
-        for (int d = EPB; d >= 1; d >>= 1)
-            if (off[p + d] <= item) p += d;  // p + d <= 2 * EPB - 1
-        const int s = p >> 1, i = p & 1;
-        const PairSlot<EPB> &q = sh[s];
-        const int k = item - off[p];
-        const int n0 = q.rng[i][1] - q.rng[i][0] + 1;
-        const int b = k < (n0 > 0 ? n0 : 0) ? q.rng[i][0] + k : q.rng[i][2] + k - (n0 > 0 ? n0 : 0);
-        const double ox = q.stl[i][0], oy = q.stl[i][1], oth = q.stl[i][4];
-        const double ang = beam_angle(b, a.fov, a.beam_incr);
-        if (!(fabs(wrap_pm_pi(oth + ang - q.wcen[i])) <= q.whalf[i])) continue;  // box_beam_window
-        const double bt = oth + ang + kPi / 2.;
-        double v31, v30;
-        cr_sincos(bt, v31, v30);
-        const int e = e0 + s;
-        const size_t o = ((size_t)e * 2 + i) * B + b;
-        double cur = a.scan[o];
-        const double cur0 = cur;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            const int v1 = (v + 1) & 3;
-            const double rr = get_range(ox, oy, v30, v31, q.rv[i][2 * v], q.rv[i][2 * v + 1], q.rv[i][2 * v1],
-                                        q.rv[i][2 * v1 + 1]);
-            if (rr < cur) cur = rr;
-        }
-        if (cur != cur0) {  // patch the ray pass's outputs for this beam
-            a.scan[o] = cur;
-            if (a.out.scans) a.out.scans[o] = (float)cur;
-            if (a.out.scans_f64) a.out.scans_f64[o] = cur;
-            if (i == 0 && a.out.obs) a.out.obs[(size_t)e * obs_row(a) + b] = obs_scan_value(cur, (float)a.p.lidar_max);
-        }
-    }
-    // ---- outputs: pose entries (F110Env._pack_flat_obs, f110_env.py:552-584), collisions, env epilogue
-    if (lane < 2 * EPB) {
-        const int s = lane >> 1, i = lane & 1;
-        const PairSlot<EPB> &q = sh[s];
-        const int e = e0 + s;
-        if (q.valid) {
-            if (a.out.obs) {
-                float *o = a.out.obs + (size_t)e * obs_row(a) + B + 4 * i;
-                o[0] = (float)q.stl[i][0];
-                o[1] = (float)q.stl[i][1];
-                o[2] = (float)wrap_angle(q.stl[i][4]);
-                o[3] = q.col[i] ? 1.0f : 0.0f;
-            }
-            if (a.out.collisions) a.out.collisions[(size_t)e * 2 + i] = (uint8_t)q.col[i];
-            if (i == 0) env_epilogue(a, e, &q.stl[0][0], 7, q.col, q.do_reset, q.epe, q.epi);
-        }
-    }
-}
-
-// LPT wave order for k_rays_fxs: the n wave items by the previous launch's
-// trips, longest first (a counting sort over 256 cost buckets, one
-// workgroup; order within a bucket is arbitrary: results do not depend on it).
-__device__ __forceinline__ uint32_t lpt_bucket(uint16_t c) { return 255u - (min((uint32_t)c, 511u) >> 1); }
-
-__global__ void __launch_bounds__(1024) k_lpt_order(const uint16_t *cost, int32_t n, uint32_t *order) {
-    __shared__ uint32_t cnt[256];
-    const int t = (int)threadIdx.x;
-    if (t < 256) cnt[t] = 0;
-    __syncthreads();
-    for (int i = t; i < n; i += 1024) atomicAdd(&cnt[lpt_bucket(cost[i])], 1u);
-    __syncthreads();
-    if (t < 64) {  // exclusive scan of the 256 counts: 4 per lane, then a wave scan
-        uint32_t c[4], sum = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            c[k] = cnt[4 * t + k];
-            sum += c[k];
-        }
-        uint32_t incl = sum;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t v = __shfl_up(incl, d, 64);
-            if (t >= d) incl += v;
-        }
-        uint32_t base = incl - sum;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            cnt[4 * t + k] = base;
-            base += c[k];
-        }
-    }
-    __syncthreads();
-    for (int i = t; i < n; i += 1024) order[atomicAdd(&cnt[lpt_bucket(cost[i])], 1u)] = (uint32_t)i;
-}
-
 // One f110_step / f110_reset: k_agents, the ray kernel, the post stage.
 // The ray kernel by context (f110_create's rules):
 //   ray_kernel 1 / 2: k_rays_tiled in flat / chunked order (rotated maps, or
@@ -1877,7 +1652,6 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (a.gate_wait && (e = hipStreamWaitEvent(s, a.gate_wait, 0)) != hipSuccess) return e;
     const bool single = a.A == 1;
-    int lpt_n = 0;  // wave items of this launch's LPT order (0: off)
     RayArgs ra{};
     ra.m = a.tmap;
     ra.sines = a.sines;
@@ -2008,11 +1782,6 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                                : reinterpret_cast<const void *>(&k_rays_fxs<true>);
                     ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
                     g2 = dim3((unsigned)(ra.EA * ra.G4));
-                    // f110_set_ray_variant bit 0 (A/B): blocks take the wave items longest first by
-                    // the previous launch's trips (LPT); the order is rebuilt after every launch
-                    lpt_n = (a.fxs_variant & 1) && a.lcost ? ra.EA * ra.G4 : 0;
-                    ra.lcost = lpt_n ? a.lcost : nullptr;
-                    ra.lorder = lpt_n && a.lpt_items == lpt_n ? a.lorder : nullptr;
                 }
             }
         }
@@ -2025,20 +1794,10 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     void *args[] = {&ra};
     if ((e = hipExtLaunchKernel(f, g2, dim3(bdim), args, 0u, s, evk(2), evk(3), 0)) != hipSuccess) return e;
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (lpt_n) {  // the next launch's wave order from this launch's trips
-        hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(1024), 0, s, a.lcost, lpt_n, a.lorder);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        if (a.lpt_items_out) *a.lpt_items_out = lpt_n;
-    }
     if (a.gate_record && (e = hipEventRecord(a.gate_record, s)) != hipSuccess) return e;
     if (single)
         hipExtLaunchKernelGGL(k_post_single, dim3((a.E + 63) / 64), dim3(64), 0, s, evk(4), evk(5), 0, a);
-    else if (a.A == 2 && (a.fxs_variant & 6)) {  // f110_set_ray_variant bits 1 / 2 (A/B): k_post_pair<8 / 4>
-        if (a.fxs_variant & 4)
-            hipExtLaunchKernelGGL(k_post_pair<4>, dim3((a.E + 3) / 4), dim3(64), 0, s, evk(4), evk(5), 0, a);
-        else
-            hipExtLaunchKernelGGL(k_post_pair<8>, dim3((a.E + 7) / 8), dim3(64), 0, s, evk(4), evk(5), 0, a);
-    } else
+    else
         hipExtLaunchKernelGGL(k_post_multi, dim3(a.E), dim3(kMultiBlock), 0, s, evk(4), evk(5), 0, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return hipSuccess;

@@ -548,7 +548,7 @@ hipError_t launch_replay_add(const ReplayView &v, const ReplayRows &in, const ui
 }
 
 hipError_t launch_replay_sample(const ReplayView &v, int32_t batch, double beta, int64_t *idx, float *w,
-                                const ReplayBatch &out, hipStream_t s) {
+                                const ReplayBatch &out, bool known_full, hipStream_t s) {
     const int grid = replay_grid(v.capacity);
     // histograms and tie count are cleared by k_select of the previous sample
     // (and at create), so a sample is kernels only
@@ -561,8 +561,9 @@ hipError_t launch_replay_sample(const ReplayView &v, int32_t batch, double beta,
     hipLaunchKernelGGL(k_count, dim3(grid), dim3(kRB), 0, s, v, batch);
     hipLaunchKernelGGL(k_place, dim3(grid), dim3(kRB), 0, s, v, batch);
     hipLaunchKernelGGL(k_finish, dim3(1), dim3(kOneBlock), replay_finish_lds(batch), s, v, batch, beta, idx, w);
-    hipLaunchKernelGGL(k_sample_replace, dim3(1), dim3(kOneBlock), replay_replace_lds(batch), s, v, batch, beta,
-                       idx, w);
+    if (!known_full)  // (f110_replay_length has seen length >= batch: the with-replacement path cannot run)
+        hipLaunchKernelGGL(k_sample_replace, dim3(1), dim3(kOneBlock), replay_replace_lds(batch), s, v, batch, beta,
+                           idx, w);
     if (out.obs) hipLaunchKernelGGL(k_gather, dim3((unsigned)batch), dim3(kRB), 0, s, v, batch, idx, out);
     return hipGetLastError();
 }

@@ -21,6 +21,7 @@ struct f110_replay {
     int device = 0;
     int64_t max_add = 0;
     int32_t max_batch = 0;
+    int64_t known_len = 0;  // a lower bound of the device length seen by f110_replay_length (never shrinks)
     ReplayView v{};
     std::vector<void *> allocs;
 
@@ -144,7 +145,8 @@ extern "C" int f110_replay_sample(f110_replay *rb, int32_t batch, double beta, i
     out.reward = reward;
     out.done = done;
     out.vec4 = (rb->v.obs_dim % 4 == 0 && obs && aligned16(obs) && aligned16(next_obs)) ? 1 : 0;
-    hipError_t e = launch_replay_sample(rb->v, batch, beta, idx, weights, out, (hipStream_t)stream);
+    hipError_t e = launch_replay_sample(rb->v, batch, beta, idx, weights, out, rb->known_len >= batch,
+                                        (hipStream_t)stream);
     if (e != hipSuccess) return fail(F110_E_HIP, std::string("f110_replay_sample: ") + hipGetErrorString(e));
     return F110_OK;
 }
@@ -168,6 +170,7 @@ extern "C" int f110_replay_length(f110_replay *rb, int64_t *length, int64_t *nex
     if (e != hipSuccess) return fail(F110_E_HIP, std::string("f110_replay_length: ") + hipGetErrorString(e));
     if (length) *length = h.length;
     if (next_idx) *next_idx = h.next;
+    if (h.length > rb->known_len) rb->known_len = h.length;  // the ring never shrinks
     return F110_OK;
 }
 
@@ -184,7 +187,8 @@ extern "C" int f110_replay_arrays(f110_replay *rb, float **priority, float **obs
 }
 
 extern "C" int f110_adam_step(float *param, float *exp_avg, float *exp_avg_sq, const float *grad, int64_t n,
-                              double lr, double beta1, double beta2, double eps, void *state, void *stream) {
+                              double lr, double beta1, double beta2, double eps, void *state, float *target,
+                              double tau, void *stream) {
     if (n < 0 || (n > 0 && (!param || !exp_avg || !exp_avg_sq || !grad || !state)))
         return fail(F110_E_INVALID, "f110_adam_step: bad arguments");
     AdamArgs a{};
@@ -198,6 +202,8 @@ extern "C" int f110_adam_step(float *param, float *exp_avg, float *exp_avg_sq, c
     a.beta2 = beta2;
     a.eps = eps;
     a.step = static_cast<int64_t *>(state);
+    a.target = target;
+    a.tau = (float)tau;
     a.done = reinterpret_cast<uint32_t *>(static_cast<int64_t *>(state) + 1);
     hipError_t e = launch_adam(a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(F110_E_HIP, std::string("f110_adam_step: ") + hipGetErrorString(e));

@@ -36,12 +36,6 @@ import torch.nn.functional as F
 # as relu(linear(x))) and their output layers as the fused learner heads of
 # ddpg_heads.py.  F110_DDPG_FUSED=0 keeps the plain torch modules (A/B runs).
 FUSED = os.environ.get("F110_DDPG_FUSED", "1") != "0"
-# F110_DDPG_MFMA=1: hidden layers with K % 32 == 0 and 32-multiple widths
-# (fc1, fc2, fcs1) run forward on csrc/f110_ddpg.hip's fp32 matrix-core
-# kernel instead of BLAS.  Off by default: it ties hipBLASLt at the learner's
-# batch (20.0 vs 20.6 us, M = 4096, K = 1088) and loses at M = 8192 and at
-# K = 128 (learner).
-MFMA_HIDDEN = os.environ.get("F110_DDPG_MFMA", "0") == "1"
 # The GPU learner's update runs without autograd (learner_fused.py: grouped
 # fp32 matrix-core GEMMs with fused epilogues, gradients written straight into
 # the flat buckets).  F110_DDPG_EXPLICIT=0 keeps the autograd path (A/B runs).
@@ -110,11 +104,7 @@ class _LinearReLU(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, W, b):
-        from .ddpg_heads import linear_relu, linear_relu_ok
-        if MFMA_HIDDEN and linear_relu_ok(x, W):
-            y = linear_relu(x, W, b)  # csrc/f110_ddpg.hip k_linear_relu (matrix cores, fp32)
-        else:
-            y = torch._addmm_activation(b, x, W.t())
+        y = torch._addmm_activation(b, x, W.t())
         ctx.save_for_backward(x, W, y)
         return y
 
@@ -286,13 +276,16 @@ class FlatAdam:
         self.exp_avg_sq = torch.zeros_like(flat)
         self.state = torch.zeros(2, dtype=torch.int64, device=flat.device)  # [step, scratch]
 
-    def step(self, flat_grad: torch.Tensor):
+    def step(self, flat_grad: torch.Tensor, target: torch.Tensor | None = None, tau: float = 0.0):
+        """One Adam step; with ``target`` (the target network's flat buffer) its
+        soft update target.lerp_(param, tau) follows in the same launch."""
         import ctypes
         s = torch.cuda.current_stream(self.flat.device).cuda_stream
         vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         self._check(self.L.f110_adam_step(vp(self.flat), vp(self.exp_avg), vp(self.exp_avg_sq), vp(flat_grad),
                                           self.flat.numel(), self.lr, self.betas[0], self.betas[1], self.eps,
-                                          vp(self.state), ctypes.c_void_p(s)), "f110_adam_step")
+                                          vp(self.state), vp(target) if target is not None else None, float(tau),
+                                          ctypes.c_void_p(s)), "f110_adam_step")
 
     def _views(self, flat):
         out, off = [], 0
@@ -453,15 +446,15 @@ class DDPGLearner:
         critic_loss.backward()
         return critic_loss.detach(), td.detach()
 
-    def _optim_step(self, optim, bucket):
-        if self.flat:
-            optim.step(bucket.flat)
+    def _optim_step(self, optim, bucket, target=None):
+        if self.flat:  # the flat path soft-updates the network's target in the same launch (agent.py:340-341)
+            optim.step(bucket.flat, target, self.tau)
         else:
             optim.step()
 
     def _phase_actor(self, states):
         """agent.py:321-331: critic step, actor loss through the frozen critic."""
-        self._optim_step(self.critic_optim, self.critic_grads)
+        self._optim_step(self.critic_optim, self.critic_grads, self._flat["critic_target"] if self.flat else None)
         if self.explicit is not None:
             return self.explicit.actor(states)
         for p in self.critic.parameters():
@@ -480,10 +473,11 @@ class DDPGLearner:
 
     def _phase_finish(self):
         """agent.py:331, :340-341: actor step, soft target update."""
-        self._optim_step(self.actor_optim, self.actor_grads)
-        with torch.no_grad():
-            for tgt, src in zip(self._target, self._online):  # one launch per flat network
-                tgt.lerp_(src, self.tau)
+        self._optim_step(self.actor_optim, self.actor_grads, self._flat["actor_target"] if self.flat else None)
+        if not self.flat:  # (the flat path did both soft updates inside the Adam launches)
+            with torch.no_grad():
+                for tgt, src in zip(self._target, self._online):
+                    tgt.lerp_(src, self.tau)
 
     def update(self, states, actions, rewards, next_states, dones, weights) -> dict:
         """The learning part of replay() (agent.py:302-343) on one batch:

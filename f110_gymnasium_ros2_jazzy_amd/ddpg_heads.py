@@ -183,23 +183,3 @@ def relu_bwd(gy, y, need_db: bool = True):
     _lib.check(L.f110_ddpg_relu_bwd(_p(gy), _p(y), B, K, _p(gz), _p(db), _p(scratch), _stream(y)),
                "f110_ddpg_relu_bwd")
     return gz, db
-
-
-def linear_relu_ok(x, W) -> bool:
-    """Shapes the matrix-core hidden-layer kernel takes (K % 32, N % 32)."""
-    return x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and x.shape[1] % 32 == 0 \
-        and W.shape[0] % 32 == 0 and x.shape[0] > 0
-
-
-def linear_relu(x, W, b):
-    """relu(x W^T + b) on the fp32 matrix cores (no autograd; ddpg._LinearReLU
-    wraps it)."""
-    if not linear_relu_ok(x, W) or W.shape[1] != x.shape[1] or b.numel() != W.shape[0]:
-        raise _lib.F110Error(f"linear_relu shapes: x {tuple(x.shape)} W {tuple(W.shape)}")
-    L = _lib.load()
-    x, W, b = x.contiguous(), W.contiguous(), b.contiguous()
-    M, K = x.shape
-    N = W.shape[0]
-    y = torch.empty(M, N, dtype=torch.float32, device=x.device)
-    _lib.check(L.f110_ddpg_linear_relu(_p(x), _p(W), _p(b), M, K, N, _p(y), _stream(x)), "f110_ddpg_linear_relu")
-    return y

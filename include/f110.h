@@ -317,15 +317,6 @@ F110_API int f110_ray_refill(const f110_ctx *ctx);
  * once, not one context's.  Any time.  Scheduling only: results are unchanged. */
 F110_API int f110_set_ray_refill(f110_ctx *ctx, int32_t waves);
 
-/* A/B of kernel variants for the following steps, a bit mask (0 = the
- * defaults).  Bit 0: k_rays_fxs's blocks take its wave items longest first by
- * the previous launch's trips per item (LPT order, rebuilt after every launch).
- * Bits 1 / 2: two-agent envs
- * run their post stage as k_post_pair with 8 / 4 envs per wave.  Scheduling
- * only: results are bit-identical.  Measurement hook (scripts/ray_ab.py), no
- * reference counterpart. */
-F110_API int f110_set_ray_variant(f110_ctx *ctx, int32_t variant);
-
 /* Sets the rays per lane of the fixed-point ray kernel (1 or 2) before the
  * context's first reset/step.  The size-based default looks at this
  * context's cars only; a caller stepping S contexts concurrently on one GPU
@@ -531,9 +522,12 @@ F110_API int f110_replay_arrays(f110_replay *rb, float **priority, float **obs, 
  * parameters, gradients and moments are flat float32 device buffers of n
  * elements.  state: device int64 step counter followed by a uint32 scratch
  * word (both zero initially); the step is advanced on the device, so the
- * call can be captured in a HIP graph.  Async on stream. */
+ * call can be captured in a HIP graph.  target (may be null): the network's
+ * target copy, soft-updated in the same pass after the step (agent.py:340-341,
+ * target.lerp_(param, tau)).  Async on stream. */
 F110_API int f110_adam_step(float *param, float *exp_avg, float *exp_avg_sq, const float *grad, int64_t n, double lr,
-                            double beta1, double beta2, double eps, void *state, void *stream);
+                            double beta1, double beta2, double eps, void *state, float *target, double tau,
+                            void *stream);
 
 /* ---- learner heads -------------------------------------------------------------
  * The DDPG networks' output layers fused with what follows them
@@ -568,11 +562,6 @@ F110_API int f110_ddpg_critic_loss_bwd(const float *h, const float *W, const flo
 /* loss = sign * mean(h W^T + b)  (sign -1: the actor loss) */
 F110_API int f110_ddpg_q_mean(const float *h, const float *W, const float *b, float sign, int32_t B, int32_t K,
                               float *loss, float *scratch, void *stream);
-/* A hidden layer's forward, y = relu(x W^T + b) on the fp32 matrix cores
- * (replaces F.relu(self.fc1(obs)) etc., rl_training/DDPG/agent.py:55-56, :93, :95):
- * x [M][K], W [N][K], b [N], y [M][N]; K a multiple of 32, N of 32. */
-F110_API int f110_ddpg_linear_relu(const float *x, const float *W, const float *b, int32_t M, int32_t K, int32_t N,
-                                   float *y, void *stream);
 /* A hidden layer's ReLU backward with its bias gradient (agent.py's F.relu(fc(x))
  * under autograd): gz = gy where y > 0 else 0 (torch threshold_backward), db =
  * sum_rows gz (db may be null).  gy, y, gz: [B][K]; K <= 1024; scratch:

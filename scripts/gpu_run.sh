@@ -7,7 +7,6 @@
 # goes to gpurun_out/TAG/.  Steps:
 #   suite      pytest -m gpu (one process, per-test timeout)
 #   lgemm      tests/test_gpu_learner_gemm.py, scripts/learner_gemm_mb.py (+ its rocprofv3 kernel stats)
-#   lgemmv     scripts/learner_gemm_mb.py under rocprofv3 for each F110_LGEMM_VARIANT (0-3)
 #   lgemmpmc   two PMC passes (SQ wait / MFMA busy; TA busy) over scripts/learner_gemm_mb.py
 #   learner    tests/test_gpu_replay.py + tests/test_gpu_ddpg_heads.py (the DDPG learner)
 #   c5prof     scripts/profile_c5.py TAG (C5 bench + rocprofv3 kernel stats by stage) -> gpurun_out/prof_c5_TAG/
@@ -18,7 +17,6 @@
 #   prof       rocprofv3 --kernel-trace --stats over bench.py (no cpu leg) -> prof/, kernel_stats.csv
 #   pmc        scripts/profile_round.py TAG (kernel trace + PMC passes of the headline ray kernel)
 #   ab         scripts/ray_ab.py with the caller's AB_* environment -> ab.json
-#   abpost     scripts/ray_ab.py, two-agent post-stage variants at 8192 / 4096 envs -> abpost.json
 #   trace      scripts/wave_trace.py (WT_ENVS), one context and bench's sub-shards -> trace_*.json
 #   c4 / c5    bench.py --agents 2 --global-envs 8192 / --workload ddpg -> c4.json / c5.json
 set -o pipefail
@@ -46,16 +44,12 @@ for step in "$@"; do
     case $step in
         suite) run suite 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
         quick) run quick 600 python -u -m pytest tests/test_gpu_batch.py -m gpu -x -v --timeout 300 --timeout-method thread \
-                   -p no:cacheprovider -k "variants_identical or step_n or simt or refill_kernel" ;;
+                   -p no:cacheprovider -k "step_n or simt or refill_kernel" ;;
         lgemm) run lgemm 600 python -u -m pytest tests/test_gpu_learner_gemm.py -m gpu -x -v --timeout 120 \
                    --timeout-method thread -p no:cacheprovider &&
                run lgemm_mb 300 python -u scripts/learner_gemm_mb.py && cp "$OUT/lgemm_mb.out" "$OUT/lgemm_mb.json" &&
                run lgemm_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/lgemm_prof" -o run -- \
                    python3 scripts/learner_gemm_mb.py ;;
-        lgemmv) for v in ${LGV:-0 1 2 3}; do
-                    F110_LGEMM_VARIANT=$v run lgemm_v$v 300 rocprofv3 --kernel-trace --stats -d "$OUT/lgemm_v$v" -o run -- \
-                        python3 scripts/learner_gemm_mb.py || exit 1
-                done ;;
         lgemmpmc) run lgemm_pmc1 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
                       SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
                       -d "$OUT/lgemm_pmc1" -o run -- python3 scripts/learner_gemm_mb.py &&
@@ -73,9 +67,6 @@ for step in "$@"; do
               find "$OUT/prof" -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} "$OUT/kernel_stats.csv" ;;
         pmc) run pmc 900 python -u scripts/profile_round.py "$TAG" ;;
         ab) run ab 900 python -u scripts/ray_ab.py && cp "$OUT/ab.out" "$OUT/ab.json" ;;
-        abpost) AB_AGENTS=2 AB_ENVS=8192,4096 AB_STEPS=100 AB_ROUNDS=5 AB_SIMT=0 \
-                AB_VARIANTS="multi:REFILL=1,LANES=2;pair8:REFILL=1,LANES=2,VARIANT=2;pair4:REFILL=1,LANES=2,VARIANT=4;multib:REFILL=1,LANES=2" \
-                run abpost 900 python -u scripts/ray_ab.py && cp "$OUT/abpost.out" "$OUT/abpost.json" ;;
         trace) WT_MODE=one run trace 600 python -u scripts/wave_trace.py && cp "$OUT/trace.out" "$OUT/trace_one.json" &&
                WT_MODE=shards run trace_shards 600 python -u scripts/wave_trace.py &&
                cp "$OUT/trace_shards.out" "$OUT/trace_shards.json" ;;

@@ -46,7 +46,7 @@ def stage(name):
     n = name
     if "f110::" in n:
         k = n.split("(f110::")[0].split("(float")[0].split("(int")[0].split("<")[0].split("::")[-1]
-        if k.startswith("k_rays") or k in ("k_agents", "k_post_multi", "k_post_pair", "k_post_single"):
+        if k.startswith("k_rays") or k in ("k_agents", "k_post_multi", "k_post_single"):
             return "env_step"
         if k.startswith("k_gap_follow"):
             return "opponent_gap_follow"

@@ -5,8 +5,7 @@ scans, states, collisions after the same steps, noise + autoreset on, a masked
 reset in the middle).  Prints one JSON line.
 
 A variant is `name:KEY=V,KEY=V`; keys: F110_RAY_KERNEL / F110_FX_PAD (env at
-create), LANES (f110_set_ray_lanes), REFILL (f110_set_ray_refill), VARIANT
-(f110_set_ray_variant: k_rays_fxs's experimental variants), HEAVY=0
+create), LANES (f110_set_ray_lanes), REFILL (f110_set_ray_refill), HEAVY=0
 (f110_disable_heavy_first), NOISE.
 
     AB_ENVS=8192,65536 AB_VARIANTS='fxn:REFILL=0,LANES=2;fxs:REFILL=1,LANES=2' python scripts/ray_ab.py
@@ -54,8 +53,6 @@ def make(tm, sp, E, A, spec, **kw):
         sm.set_ray_lanes(int(spec["LANES"]))
     if "REFILL" in spec:
         sm.set_ray_refill(int(spec["REFILL"]))
-    if "VARIANT" in spec:
-        _lib.check(sm.L.f110_set_ray_variant(sm.ctx, int(spec["VARIANT"])), "f110_set_ray_variant")
     if spec.get("HEAVY") == "0":
         sm.disable_heavy_first()
     return sm

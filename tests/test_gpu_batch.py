@@ -360,48 +360,6 @@ def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
                 assert torch.equal(x, y), f"step {t}"
 
 
-def test_kernel_variants_identical(tracks, gpu):
-    """f110_set_ray_variant's bits: k_rays_fxs with the chunk pairs longest
-    first (bit 0, ORD) and the two-agent post stage as k_post_pair with 8 or 4
-    envs per wave (bits 1 / 2) against the defaults: every StepOut field and
-    the states bit-identical over 30 noisy steps with autoreset, car-car and
-    wall collisions and a masked reset (E = 203: the last wave's envs are
-    partly past the end)."""
-    from f110_gymnasium_ros2_jazzy_amd import _lib
-    E, A, T = 203, 2, 30
-    sp = _spawns(A)
-    rng = np.random.default_rng(21)
-    poses = sp[rng.integers(0, sp.shape[0], E)]
-    poses[:40, 1] = poses[:40, 0]  # 40 envs start with the cars stacked: GJK collisions
-    poses[:40, 1, 0] += rng.uniform(-0.3, 0.3, 40)
-    acts = np.stack([rng.uniform(-0.4189, 0.4189, (T, E, A)), rng.uniform(0, 20, (T, E, A))], -1).astype(np.float32)
-    mask = rng.random(E) < 0.5
-    outs = []
-    for variant in (0, 1, 2, 4, 3, 5):
-        sim = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=5,
-                   keep_f64_scans=True)
-        sim.set_ray_lanes(2)
-        sim.set_ray_refill(1)
-        _lib.check(sim.L.f110_set_ray_variant(sim.ctx, variant), "f110_set_ray_variant")
-        sim.reset(poses)
-        rec = []
-        for t in range(T):
-            o = sim.reset(poses[::-1].copy(), env_mask=mask) if t == 14 else sim.step(acts[t])
-            rec.append(tuple(getattr(o, f).clone() for f in ("obs", "scans", "scans_f64", "collisions", "terminated",
-                                                               "was_reset", "lap_times", "lap_counts", "sim_time"))
-                       + (sim.agent_states().clone(),))
-        torch.cuda.synchronize()
-        outs.append(rec)
-        with pytest.raises(RuntimeError, match="0..7"):
-            _lib.check(sim.L.f110_set_ray_variant(sim.ctx, 8), "f110_set_ray_variant")
-        sim.close()
-    assert sum(int(r[3].sum()) for r in outs[0]) > 0  # collisions happened
-    for k in range(1, len(outs)):
-        for t, (a, b) in enumerate(zip(outs[0], outs[k])):
-            for x, y in zip(a, b):
-                assert torch.equal(x, y), f"variant index {k} step {t}"
-
-
 def test_step_n_matches_single_steps(tracks, gpu):
     """f110_step_n (n resident steps, no host work in between) equals n
     f110_step calls: obs, scans, states and counters bit-identical, f32 and

@@ -86,47 +86,3 @@ def test_fused_heads_reject_bad_shapes(gpu):
         q_mean(h, torch.zeros(1, 300, device="cuda"), torch.zeros(1, device="cuda"))
     with pytest.raises(_lib.F110Error):
         q_mean(torch.zeros(8, 16), torch.zeros(1, 16), torch.zeros(1))  # CPU tensors
-
-
-@pytest.mark.parametrize("M,K", [(4096, 1088), (333, 1088), (1, 128), (77, 32)])
-def test_linear_relu_matches_torch(gpu, M, K):
-    """The matrix-core hidden layer (csrc/f110_ddpg.hip k_linear_relu) against
-    relu(x W^T + b) in torch fp32: a reordered fp32 sum (rtol 1e-5), ragged
-    row counts (tiles past M are computed, not stored) and NaN kept."""
-    from f110_gymnasium_ros2_jazzy_amd.ddpg_heads import linear_relu
-    g = torch.Generator(device="cuda").manual_seed(M + K)
-    x = torch.rand(M, K, device="cuda", generator=g)
-    W = torch.randn(128, K, device="cuda", generator=g) * (2.0 / K) ** 0.5
-    b = torch.randn(128, device="cuda", generator=g) * 0.1
-    x[0, 3] = float("nan")
-    ref = torch.relu(x @ W.t() + b)
-    got = linear_relu(x, W, b)
-    assert got.shape == ref.shape
-    assert torch.isnan(got[0]).all() and torch.isnan(ref[0]).all()
-    if M > 1:
-        _close(got[1:], ref[1:], f"linear_relu M={M} K={K}")
-
-
-def test_linear_relu_in_learner(gpu, monkeypatch):
-    """F110_DDPG_MFMA=1 routes the actor's hidden layers through the kernel:
-    same actions and gradients as the BLAS path within fp32 rounding."""
-    import f110_gymnasium_ros2_jazzy_amd.ddpg as D
-    s = torch.rand(512, 1088, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5))
-    out = {}
-    for on in (False, True):
-        monkeypatch.setattr(D, "MFMA_HIDDEN", on)
-        a, _ = _nets(4)
-        act = a(s)
-        act.sum().backward()
-        out[on] = (act.detach(), [p.grad.clone() for p in a.parameters()])
-    _close(out[True][0], out[False][0], "actions")
-    for i, (x, y) in enumerate(zip(out[True][1], out[False][1])):
-        _close(x, y, f"actor grad {i}")
-
-
-def test_linear_relu_rejects_bad_shapes(gpu):
-    from f110_gymnasium_ros2_jazzy_amd import _lib
-    from f110_gymnasium_ros2_jazzy_amd.ddpg_heads import linear_relu
-    with pytest.raises(_lib.F110Error):
-        linear_relu(torch.zeros(8, 130, device="cuda"), torch.zeros(128, 130, device="cuda"),
-                    torch.zeros(128, device="cuda"))  # K % 32

@@ -247,7 +247,8 @@ def test_learner_graphs_match_eager(gpu):
 
 def test_flat_adam_matches_torch_adam(gpu):
     """f110_adam_step over a flat buffer == torch.optim.Adam's single-tensor
-    update (agent.py:187-188) on CPU, five steps, float32 tolerance."""
+    update (agent.py:187-188) on CPU, five steps, float32 tolerance; its fused
+    soft target update == target.lerp_(param, tau) after each step."""
     import ctypes
     from f110_gymnasium_ros2_jazzy_amd import _lib
     L = _lib.load()
@@ -259,14 +260,19 @@ def test_flat_adam_matches_torch_adam(gpu):
     dev = p0.cuda()
     m, v = torch.zeros_like(dev), torch.zeros_like(dev)
     state = torch.zeros(2, dtype=torch.int64, device="cuda")
+    tgt_ref = torch.randn(5000, generator=g)
+    tgt = tgt_ref.cuda()
     vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     for gr in grads:
         ref.grad = gr.clone()
         opt.step()
+        with torch.no_grad():
+            tgt_ref.lerp_(ref, 0.005)
         gd = gr.cuda()
         _lib.check(L.f110_adam_step(vp(dev), vp(m), vp(v), vp(gd), dev.numel(), 1e-3, 0.9, 0.999, 1e-8, vp(state),
-                                    ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "adam")
+                                    vp(tgt), 0.005, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "adam")
     torch.cuda.synchronize()
     assert int(state[0]) == 5
+    torch.testing.assert_close(tgt.cpu(), tgt_ref, rtol=2e-6, atol=1e-7)
     torch.testing.assert_close(dev.cpu(), ref.detach(), rtol=2e-6, atol=1e-7)
     torch.testing.assert_close(m.cpu(), opt.state[ref]["exp_avg"], rtol=1e-5, atol=1e-7)  # CPU lerp may fuse (1 ulp)
