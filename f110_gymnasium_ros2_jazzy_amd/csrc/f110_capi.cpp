@@ -689,12 +689,16 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
         const uint64_t rm_bytes = ((uint64_t)W + 16) / 16 * 16 * ((uint64_t)H + 1) * 8 + 128;
         if (rm_bytes >= (1ull << 32)) c->ray_kernel = 2;
     }
+    // two or more agents per env from 8192 cars: k_rays_fxs (refill) with 2 rays per lane, one context
+    // (round 4, profiles/r04_ab/refill_sweep_a2.json: 4096 x 2 0.173 -> 0.165 ms, 8192 x 2 0.298 -> 0.261;
+    // one agent at 16384 cars keeps k_rays_fxn, 0.289 vs 0.324 ms)
+    const bool multi_refill = C.n_agents >= 2 && EA >= 8192;
     if (c->ray_kernel == 3) {
         // rays per lane: 2 keeps 2 gathers in flight per lane where the grid is deep enough
         // (measured; k_rays ms, 1 vs 2 rays per lane: 4096 cars 0.107 / 0.124,
         // 8192 0.165 / 0.175, 16384 0.304 / 0.284, 32768 0.637 / 0.547, 65536 1.190 / 1.054;
         // profiles/r02_ray_ab/)
-        c->fx_ilp = EA >= 12288 ? 2 : 1;
+        c->fx_ilp = (EA >= 12288 || multi_refill) ? 2 : 1;
     }
     // heavy-first pays where one ray grid is a few rounds of waves deep (16384 cars: 0.281 vs 0.287 ms)
     // and costs where it is deep (65536 cars: 1.288 vs 1.251 ms without; profiles/r02_ray_ab/ab_heavy.json)
@@ -702,7 +706,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     // 0.124 vs 0.109 ms without; profiles/r03_ab/small_shards.json); off from 32768 cars, where the
     // refill kernel (which takes no heavy-first list) runs: at exactly 32768 it used to stay on and
     // turn the refill off (one context 57.0 M env-steps/s, profiles/r03_ab/e32768_*.json)
-    if (EA >= 32768 || EA <= 8192) c->heavy_T = 0;
+    if (EA >= 32768 || EA <= 8192 || multi_refill) c->heavy_T = 0;
     if (c->ray_kernel >= 2 && c->heavy_T > 0) {
         // up to 1/6 of the waves (measured: ~7% of the waves have a ray longer
         // than 40 lookups and carry ~46% of the wave-iterations)
@@ -748,12 +752,12 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     // k_rays_fxn, latency-bound, did not gain from them (1.029 vs 1.026 ms), DESIGN §3.3.
     // F110_FX_PAD (A/B): 1 builds the table at any size (k_rays_fxn then runs on it), 0 never.
     const bool fx_ok = c->ray_kernel == 3;
-    c->fx_pad = fx_ok && EA >= 32768;
+    c->fx_pad = fx_ok && (EA >= 32768 || multi_refill);
     if (const char *v = std::getenv("F110_FX_PAD")) c->fx_pad = fx_ok && std::atoi(v) != 0;
     // k_rays_fxs (one wave per car, two chunk slots with refill) where the grid is deep:
     // 65536 envs as 2 x 32768 67.1 vs 63.0 M env-steps/s; at 16384 cars its long waves
     // leave a tail (0.324 vs 0.289 ms); it runs only without heavy-first and masks
-    c->fx_refill = EA >= 32768 ? 1 : 0;
+    c->fx_refill = (EA >= 32768 || multi_refill) ? 1 : 0;
     const double pad_q = std::ceil(C.max_range / resolution) + 8.0;
     const int32_t fx_pad_cells = pad_q > 0.0 && pad_q < 65536.0 ? (int32_t)pad_q : 0;  // else no padded table
     if (e == hipSuccess)
