@@ -61,6 +61,7 @@ struct f110_ctx {
     double *dt = nullptr, *sines = nullptr, *cosines = nullptr, *angles = nullptr, *beam_cos = nullptr,
            *side = nullptr, *spawn = nullptr;
     double *cs2 = nullptr, *bs2 = nullptr;  // interleaved (cos, sin)[theta_dis], (side, beam_cos)[B] (k_rays_fxs)
+    double side_max = 0.0;                  // max of the side table (k_rays_fxs's TTC pre-test)
     double *start_rot = nullptr;
     double *st = nullptr, *sb = nullptr, *start = nullptr, *sim_time = nullptr, *ray0 = nullptr, *scan = nullptr;
     BeamRun *runs = nullptr;
@@ -721,6 +722,8 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
 
     std::vector<double> s(C.theta_dis), co(C.theta_dis), an(C.n_beams), bc(C.n_beams), sd(C.n_beams);
     f110_host_tables(C.theta_dis, C.n_beams, C.fov, params, s.data(), co.data(), an.data(), bc.data(), sd.data());
+    c->side_max = -INFINITY;
+    for (double v : sd) c->side_max = v > c->side_max ? v : c->side_max;  // NaN-free table (f110_host_tables)
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipMemcpy(c->sines, s.data(), s.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->cosines, co.data(), co.size() * sizeof(double), hipMemcpyHostToDevice);
@@ -820,6 +823,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.dt = c->cfg.time_step;
     a.lidar_dist = c->cfg.lidar_dist;
     a.ttc_thresh = c->cfg.ttc_thresh;
+    a.side_max = c->side_max;
     a.noise_std = c->cfg.noise_std;
     a.inc = c->inc;
     a.beam_incr = c->beam_incr;

@@ -62,6 +62,7 @@ struct StepArgs {
     int32_t count_slots;  // f110_set_simt: lane-slot counter of the fixed-point loops
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2: k_rays_fxn / k_rays_fxs)
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
+    double side_max;  // max of the RaceCar side table (the TTC pre-test of k_rays_fxs)
     uint64_t seed;
     int64_t env_offset;
     // persistent per-agent / per-env state (SoA, owned by the context)
@@ -127,6 +128,7 @@ struct RayArgs {
     const double *vel;         // state[3][EA]
     const double *beam_cos, *side;
     double ttc_thresh;
+    double side_max;           // max_b side[b]: a range above side_max + 1.2 thresh |v| cannot fire TTC
     uint8_t *ttc_hit;          // [EA]
     float *obs;                // [E][obs_len] or null
     float *scans_f32;          // [EA][B] or null

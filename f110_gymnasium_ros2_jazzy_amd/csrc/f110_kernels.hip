@@ -78,6 +78,15 @@ __device__ __forceinline__ bool ttc_fires(double range, double side, double proj
     return ttc < thresh && ttc >= 0.0;
 }
 
+// ttc_fires' first test passed for EVERY beam of the car: with side <= side_max
+// and |v beam_cos| <= |v| (rounding is monotonic), range - side_max > 0 and
+// >= (1.2 thresh) |v| make it return false whatever the beam.  The caller
+// loads (side, beam_cos) only for the lanes (and waves) where this is true.
+__device__ __forceinline__ bool ttc_may_fire_lane(double range, double side_max, double v, double thresh) {
+    const double nm = range - side_max;
+    return !(nm > 0.0 && nm >= (1.2 * thresh) * fabs(v));
+}
+
 
 // ------------------------------------------------------------------------
 // k_agents: one thread per car.
@@ -286,7 +295,7 @@ __device__ __forceinline__ WaveLookups trace_wave(const RayArgs &a, bool has, in
     WaveLookups w{0u, (uint32_t)__popcll(hm), 0u};
     if (!hm) return w;
     const int B = a.B;
-    double c = 0.0, s = 0.0, x = 0.0, y = 0.0, d = 0.0, v = 0.0, bcos = 0.0, side = 0.0, noise = 0.0;
+    double c = 0.0, s = 0.0, x = 0.0, y = 0.0, d = 0.0, v = 0.0, noise = 0.0;
     if (has) {
         double t = beam_theta_index(a.runs + (size_t)g * kMaxSeg, a.nruns[g], b);
         int ti = (int)t;  // int(theta_index), laser_models.py:124
@@ -296,11 +305,7 @@ __device__ __forceinline__ WaveLookups trace_wave(const RayArgs &a, bool has, in
         x = a.ray0[g];
         y = a.ray0[a.EA + g];
         d = a.ray0[2 * a.EA + g];  // :129
-        // the TTC operands are loaded before the loop, which hides their
-        // latency (the epilogue would otherwise wait on them)
         v = a.vel[g];
-        bcos = a.beam_cos[b];
-        side = a.side[b];
         // the ray's scan noise does not depend on the trace: drawn (or
         // loaded) here, it overlaps the set-up loads above
         const RayArgs &K = *kernarg_rays();
@@ -338,7 +343,10 @@ __device__ __forceinline__ WaveLookups trace_wave(const RayArgs &a, bool has, in
     if (K.noise_ext || K.noise_std > 0.0) range += noise;  // noise after the clamp (see store_ray)
     // state[3] after update_pose; check_ttc_jit on the noisy scan, before the
     // agent ray_cast (base_classes.py:597-599)
-    if (v != 0.0 && ttc_fires(range, side, v * bcos, K.ttc_thresh)) K.ttc_hit[g] = 1;
+    if (v != 0.0 && ttc_may_fire_lane(range, K.side_max, v, K.ttc_thresh)) {
+        const double bcos = K.beam_cos[b], side = K.side[b];
+        if (ttc_fires(range, side, v * bcos, K.ttc_thresh)) K.ttc_hit[g] = 1;
+    }
     // outputs straight from the ray; with other cars in the env (HANDOFF)
     // k_post_multi patches the beams its ray_cast shortens
     if (K.obs && g == e * a.A) K.obs[(size_t)e * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
@@ -593,11 +601,14 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // k_post_multi, whose agent ray_cast re-writes the entries it shortens.
 template <bool HANDOFF>
 __device__ __forceinline__ void fx_epilogue(const RayArgs &K, int g, int e, int b, double tot, double mr,
-                                            double noise, double v, double bcos, double side) {
+                                            double noise, double v) {
     const int64_t r = (int64_t)g * K.B + b;
     double range = tot > mr ? mr : tot;
     if (K.noise_ext || K.noise_std > 0.0) range += noise;
-    if (v != 0.0 && ttc_fires(range, side, v * bcos, K.ttc_thresh)) K.ttc_hit[g] = 1;
+    if (v != 0.0 && ttc_may_fire_lane(range, K.side_max, v, K.ttc_thresh)) {  // (side, beam_cos) loaded only where TTC can fire
+        const double bcos = K.beam_cos[b], side = K.side[b];
+        if (ttc_fires(range, side, v * bcos, K.ttc_thresh)) K.ttc_hit[g] = 1;
+    }
     if (K.obs && g == e * K.A) K.obs[(size_t)e * K.obs_len + b] = obs_scan_value(range, K.lidar_max);
     if (K.scans_f32) K.scans_f32[r] = (float)range;
     if (K.scans_f64) K.scans_f64[r] = range;
@@ -691,7 +702,6 @@ __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
     int ti = (int)t;  // int(theta_index), laser_models.py:124
     if (ti >= a.theta_dis) ti = 0;
     const double c = a.cosines[ti], s = a.sines[ti];
-    const double bcos = a.beam_cos[bc], side = a.side[bc];
     double x = x00, y = y00, d = has ? d00 : 0.0;
     double noise = 0.0;
     {
@@ -726,7 +736,7 @@ __global__ void __launch_bounds__(64) k_rays_fx(RayArgs a) {
 
     // ---- epilogue ----
     const uint32_t lanes = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(has));
-    if (has) fx_epilogue<HANDOFF>(*kernarg_rays(), g, e, b, tot, L.mr, noise, v, bcos, side);
+    if (has) fx_epilogue<HANDOFF>(*kernarg_rays(), g, e, b, tot, L.mr, noise, v);
     if (lane == 0) {
         const RayArgs &K = *kernarg_rays();
         if (lanes) {  // one (lookups, rays) atomic pair per wave; the first lookup came from k_agents
@@ -995,7 +1005,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxn(RayArgs a) {  // 8 waves per
         if (K.noise_ext) nz = K.noise_ext[(size_t)e * B + bc[r]];
         else if (K.noise_std > 0.0) nz = K.noise_std * (double)pn[r];
         if (has[r])
-            fx_epilogue<HANDOFF>(K, g, e, b0 + 64 * r + lane, tot[r], L.mr, nz, v, a.beam_cos[bc[r]], a.side[bc[r]]);
+            fx_epilogue<HANDOFF>(K, g, e, b0 + 64 * r + lane, tot[r], L.mr, nz, v);
         lanes += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(has[r]));
     }
     if (lane == 0) {
@@ -1220,9 +1230,13 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
             const double v = ld_const(K.vel + g);
             const uint32_t boff = (uint32_t)bc * 8u;
             if (v != 0.0) {
-                const double2 t2 = ld_off(reinterpret_cast<const double2 *>(K.bs2), boff * 2u);  // (side, beam_cos)
-                ++loads;
-                if (ttc_fires(range, t2.x, v * t2.y, K.ttc_thresh)) K.ttc_hit[g] = 1;
+                // the wave loads (side, beam_cos) only when a lane may fire (ttc_may_fire_lane)
+                const bool may = ttc_may_fire_lane(range, K.side_max, v, K.ttc_thresh);
+                if (__builtin_amdgcn_ballot_w64(may)) {
+                    const double2 t2 = ld_off(reinterpret_cast<const double2 *>(K.bs2), boff * 2u);  // (side, beam_cos)
+                    ++loads;
+                    if (may && ttc_fires(range, t2.x, v * t2.y, K.ttc_thresh)) K.ttc_hit[g] = 1;
+                }
             }
             if (K.obs && (!HANDOFF || g == e * K.A)) {
                 float *orow = K.obs + (size_t)e * K.obs_len;
@@ -1680,6 +1694,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     ra.cs2 = a.cs2;
     ra.bs2 = a.bs2;
     ra.ttc_thresh = a.ttc_thresh;
+    ra.side_max = a.side_max;
     ra.ttc_hit = a.ttc_hit;
     ra.obs = a.out.obs;
     ra.obs_len = (int32_t)obs_row(a);
