@@ -19,9 +19,9 @@
 //     columns of fcs2's input (no torch.cat), an output mask (the next
 //     layer's threshold_backward) and an input mask (this layer's).
 //   * k_lwgrad: dW = G'^T X over M split across blocks (4 waves x S slices),
-//     64 x 64 tiles of 32x32x2 MFMAs whose operands are plain row loads (a
-//     lane's G / X element per row pair: 128-B coalesced, no transpose); db
-//     from the same G' loads; k_lwgrad_finish adds the S partials in order.
+//     64 x 64 tiles of 32x32x2 MFMAs; each wave stages its 16-row chunks of
+//     G' and X through LDS (float4 row loads, fragments by ds_read_b32); db
+//     from the same G' fragments; k_lwgrad_finish adds the S partials in order.
 // The C/D layout of the 32x32 f32 MFMA: column = lane & 31, row = (reg & 3)
 // + 8 (reg >> 2) + 4 (lane >> 5).
 #include <hip/hip_runtime.h>
@@ -54,6 +54,7 @@ struct WgradLaunch {
     int64_t poff[kMaxOps + 1];  // each op's partials in the scratch: [S][N][KX] then [S][N]
     int32_t blk0[kMaxOps + 1];
     int32_t ntk[kMaxOps];       // kx tiles of each op
+    int32_t vec[kMaxOps];       // k_lwgrad: G / X / gmask rows loadable as float4
     int32_t nops, M, S;
     float *part;
 };
@@ -68,6 +69,11 @@ __device__ __forceinline__ void pin(float4 &v) { asm volatile("" : "+v"(v.x), "+
 __device__ __forceinline__ void pin(float &v) { asm volatile("" : "+v"(v)); }
 
 __device__ __forceinline__ float relu_nan(float v) { return v > 0.0f ? v : (v != v ? v : 0.0f); }
+
+__device__ __forceinline__ float4 keep(float4 v, uint32_t m) {  // v where m = ~0, +0 where m = 0
+    return make_float4(__uint_as_float(__float_as_uint(v.x) & m), __uint_as_float(__float_as_uint(v.y) & m),
+                       __uint_as_float(__float_as_uint(v.z) & m), __uint_as_float(__float_as_uint(v.w) & m));
+}
 
 __device__ __forceinline__ float get(const float4 &v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; }
 
@@ -87,6 +93,51 @@ __device__ __forceinline__ int select_op(const Launch &L, int blk, Op &o) {
 }
 
 // ---------------------------------------------------------------- k_lgemm --
+// the partial tiles red[w][v][lane] (w = the NW K-split waves, v = accumulator
+// register (i, j, reg) of the 32 x 32 tiles) summed in wave order, then the
+// layer's epilogue; thread (wave, lane) owns registers wave*R/NW .. +R/NW
+template <int NW, int RJ, int R>
+__device__ __forceinline__ void lgemm_epilogue(const f110_gemm_op &o, const float (*red)[R][64], int wave, int lane,
+                                               int m0, int n0, int M) {
+    const int r = lane & 31, h = lane >> 5, N = o.N;
+#pragma unroll
+    for (int u = 0; u < R / NW; ++u) {
+        const int v = wave * (R / NW) + u;
+        float s = red[0][v][lane];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) s += red[w][v][lane];
+        const int t = v >> 4, vv = v & 15;
+        const int i = t / RJ, j = t - i * RJ;
+        const int row = m0 + 32 * i + (vv & 3) + 8 * (vv >> 2) + 4 * h;
+        const int col = n0 + 32 * j + r;
+        if (row < M && col < N) {
+            for (int x = 0; x < o.nx2; ++x) s = fmaf(o.x2[(size_t)row * o.ldx2 + x], o.w2[(size_t)col * o.ldw2 + x], s);
+            if (o.bias) s += o.bias[col];
+            if (o.relu) s = relu_nan(s);
+            if (o.omask) s = o.omask[(size_t)row * o.ldc + col] > 0.0f ? s : 0.0f;
+            o.C[(size_t)row * o.ldc + col] = s;
+        }
+    }
+}
+
+// the block's op and output tile: (p, m0, n0), XCD-aware (the column tiles of
+// one row tile share blockIdx % 8, so one L2 holds A's rows)
+__device__ __forceinline__ void lgemm_tile(const GemmLaunch &L, f110_gemm_op &o, int &m0, int &n0) {
+    const int blk = (int)blockIdx.x;
+    const int p = select_op(L, blk, o);
+    int ntn = L.ntn[0], b0 = L.blk0[0];
+#pragma unroll
+    for (int q = 1; q < kMaxOps; ++q)
+        if (p == q) {
+            ntn = L.ntn[q];
+            b0 = L.blk0[q];
+        }
+    const int local = blk - b0;
+    const int grp = local / (8 * ntn), rem = local - grp * 8 * ntn;
+    m0 = (grp * 8 + (rem & 7)) * kTM;
+    n0 = (rem >> 3) * kTN;
+}
+
 struct Frag {
     float4 a[kTM / 32][2];
     float4 b[kTN / 32][2];
@@ -95,29 +146,19 @@ struct Frag {
 // VEC: A rows (and amask) 16-B aligned; BV: B rows (nn = 0) loaded as float4 / float2 / floats.
 // NW waves per block split K; NB register buffers (NB - 1 chunks of loads in flight).  Round 4
 // measured 8 waves and 3 buffers (no faster), v_mfma_f32_16x16x4_f32 with 8 accumulators (slower
-// on the grouped launches) and a probe without loads in the loop (the 3-op launch 42 -> 29 us: the
-// operand path, ~14 B/clk/CU of fragment-shaped loads, is the bound)
+// on the grouped launches), a probe without loads in the loop (the 3-op launch 42 -> 29 us) and
+// both operands staged through LDS in whole 128-B lines (8-row pieces, XOR-swizzled images,
+// ds_read_b128 fragments; 1 / 2 / 3 ops 16.9 / 29.5 / 40.8 -> 17.6 / 28.8 / 41.5 us: no gain, so
+// the fragment-shaped loads are not what bounds it)
 template <bool NN, bool VEC, int BV, bool AMASK>
 __global__ void __launch_bounds__(256) k_lgemm(GemmLaunch L) {
     constexpr int NW = 4, NB = 2;
     constexpr int RI = kTM / 32, RJ = kTN / 32, R = RI * RJ * 16;
     static_assert(R % NW == 0, "tile registers split evenly over the waves");
     __shared__ float red[NW][R][64];
-    const int blk = (int)blockIdx.x;
     f110_gemm_op o;
-    const int p = select_op(L, blk, o);
-    int ntn = L.ntn[0];
-#pragma unroll
-    for (int q = 1; q < kMaxOps; ++q)
-        if (p == q) ntn = L.ntn[q];
-    int b0 = L.blk0[0];
-#pragma unroll
-    for (int q = 1; q < kMaxOps; ++q)
-        if (p == q) b0 = L.blk0[q];
-    // XCD-aware: the column tiles of one row tile share blockIdx % 8 (one L2 holds A's rows)
-    const int local = blk - b0;
-    const int grp = local / (8 * ntn), rem = local - grp * 8 * ntn;
-    const int m0 = (grp * 8 + (rem & 7)) * kTM, n0 = (rem >> 3) * kTN;
+    int m0, n0;
+    lgemm_tile(L, o, m0, n0);
     const int M = L.M, N = o.N, K = o.K;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     const int nch = (K + 15) >> 4;
@@ -252,36 +293,118 @@ __global__ void __launch_bounds__(256) k_lgemm(GemmLaunch L) {
 #pragma unroll
             for (int v = 0; v < 16; ++v) red[wave][(i * RJ + j) * 16 + v][lane] = acc[i][j][v];
     __syncthreads();
-    // thread (wave, lane): registers wave*R/NW .. of every partial tile, summed in wave order
+    lgemm_epilogue<NW, RJ, R>(o, red, wave, lane, m0, n0, M);
+}
+
+// --------------------------------------------------------------- k_lwgrad --
+// A 64 x 64 tile of dW per block, M split over S slices x 4 waves: per
+// 16-row chunk a wave loads its G' and X rows (64 columns each) as 4 rows x
+// 256 B per dwordx4 instruction (4 + 4, + 4 for the mask; round 4's first
+// form loaded the fragments directly, 32 single-dword loads per chunk, 6 %
+// slower on the 128 x 1088 gradient), writes them to its own LDS image and
+// reads the MFMA fragments (lane = column, lane half = row parity) with
+// ds_read_b32.
+// Image rows are 96 floats apart, so the two lane halves (rows 2t and 2t+1)
+// read opposite halves of the 64 banks.  Ops whose rows are not float4-able
+// (the critic's two action columns) take the same loop with per-element
+// loads (a block-uniform choice outside the loop).  Columns past N / KX are
+// loaded from clamped addresses (their outputs are not stored); rows past M
+// load row M-1 with G' = 0.  Sum order: per lane the chunk rows in order, as
+// k_lwgrad's 8-row chunks.
+template <bool VEC, bool GMASK>
+__device__ __forceinline__ void lwgrad_loop(const f110_wgrad_op &o, float *img, int M, int cb, int ce, int n0,
+                                                int k0, f32x16 (&acc)[2][2], float (&dsum)[2]) {
+    constexpr int CM = 16, PITCH = 96;
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    const int rl = lane >> 4, sg = lane & 15;  // load row (of 4), 16-B segment
+    const int N = o.N, KX = o.KX;
+    const size_t ldg = o.ldg, ldx = o.ldx;
+    // column offsets of this lane's segment (clamped in range)
+    const int cg = min(n0 + 4 * sg, N - 4 < 0 ? 0 : N - 4), cx = min(k0 + 4 * sg, KX - 4 < 0 ? 0 : KX - 4);
+    int eg[4], ex[4];  // per-element columns for the !VEC loads
 #pragma unroll
-    for (int u = 0; u < R / NW; ++u) {
-        const int v = wave * (R / NW) + u;
-        float s = red[0][v][lane];
+    for (int e = 0; e < 4; ++e) {
+        eg[e] = min(n0 + 4 * sg + e, N - 1);
+        ex[e] = min(k0 + 4 * sg + e, KX - 1);
+    }
+    float4 gg[4], gx[4], gk[4];
+    uint32_t rin[4];
+    auto ld4 = [&](const float *base, size_t row, size_t ld, int cv, const int *ce4) -> float4 {
+        const float *p = base + row * ld;
+        if (VEC) return *reinterpret_cast<const float4 *>(p + cv);
+        return make_float4(p[ce4[0]], p[ce4[1]], p[ce4[2]], p[ce4[3]]);
+    };
+    auto gload = [&](int c) {
 #pragma unroll
-        for (int w = 1; w < NW; ++w) s += red[w][v][lane];
-        const int t = v >> 4, vv = v & 15;
-        const int i = t / RJ, j = t - i * RJ;
-        const int row = m0 + 32 * i + (vv & 3) + 8 * (vv >> 2) + 4 * h;
-        const int col = n0 + 32 * j + r;
-        if (row < M && col < N) {
-            for (int x = 0; x < o.nx2; ++x) s = fmaf(o.x2[(size_t)row * o.ldx2 + x], o.w2[(size_t)col * o.ldw2 + x], s);
-            if (o.bias) s += o.bias[col];
-            if (o.relu) s = relu_nan(s);
-            if (o.omask) s = o.omask[(size_t)row * o.ldc + col] > 0.0f ? s : 0.0f;
-            o.C[(size_t)row * o.ldc + col] = s;
+        for (int i = 0; i < 4; ++i) {
+            const int m = CM * c + 4 * i + rl;
+            rin[i] = m < M ? ~0u : 0u;
+            const size_t mr = (size_t)min(m, M - 1);
+            gg[i] = ld4(o.G, mr, ldg, cg, eg);
+            if (GMASK) gk[i] = ld4(o.gmask, mr, ldg, cg, eg);
+            gx[i] = ld4(o.X, mr, ldx, cx, ex);
+        }
+    };
+    auto swrite = [&]() {  // G rows at image rows 0..15, X rows at 16..31
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float4 g = gg[i];
+            if (GMASK) {
+                pin(g);  // the mask select stays here, after the MFMAs
+                pin(gk[i]);
+                g.x = gk[i].x > 0.0f ? g.x : 0.0f;
+                g.y = gk[i].y > 0.0f ? g.y : 0.0f;
+                g.z = gk[i].z > 0.0f ? g.z : 0.0f;
+                g.w = gk[i].w > 0.0f ? g.w : 0.0f;
+            }
+            const int q = 4 * i + rl;
+            uint32_t m = rin[i];
+            asm volatile("" : "+v"(m));  // opaque: the zeroing stays here, after the MFMAs (not a select at the load)
+            *reinterpret_cast<float4 *>(img + q * PITCH + 4 * sg) = keep(g, m);
+            *reinterpret_cast<float4 *>(img + (CM + q) * PITCH + 4 * sg) = gx[i];
+        }
+    };
+    auto compute = [&]() {  // every fragment read issued first: the MFMAs wait on them in order
+        float g[CM / 2][2], x[CM / 2][2];
+#pragma unroll
+        for (int t = 0; t < CM / 2; ++t)
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                g[t][a] = img[(2 * t + h) * PITCH + 32 * a + r];
+                x[t][a] = img[(CM + 2 * t + h) * PITCH + 32 * a + r];
+            }
+#pragma unroll
+        for (int t = 0; t < CM / 2; ++t) {
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[a][b] = mfma(g[t][a], x[t][b], acc[a][b]);
+            dsum[0] += g[t][0];
+            dsum[1] += g[t][1];
+        }
+    };
+    if (cb < ce) {
+        gload(cb);
+        swrite();
+        for (int c = cb; c < ce; ++c) {
+            gload(min(c + 1, ce - 1));  // the next chunk in flight (past the end: reloaded, unused)
+            __builtin_amdgcn_sched_barrier(0);
+            compute();
+            __builtin_amdgcn_sched_barrier(0);
+            swrite();
         }
     }
 }
 
-// --------------------------------------------------------------- k_lwgrad --
-template <bool FINAL, bool GMASK>  // FINAL: S == 1, write dW / db directly
+template <bool FINAL, bool GMASK>
 __global__ void __launch_bounds__(kGB) k_lwgrad(WgradLaunch L) {
-    __shared__ float red[4][64][64];
-    __shared__ float dred[4][2][64];
+    constexpr int CM = 16, PITCH = 96;
+    static_assert(4 * 2 * CM * PITCH <= 4 * 64 * 64, "the staging images fit in the reduction buffer");
+    __shared__ float lds[4 * 64 * 64 + 4 * 2 * 64];  // red[4][64][64], dred[4][2][64]; images alias red
     const int blk = (int)blockIdx.x;
     f110_wgrad_op o;
     const int p = select_op(L, blk, o);
-    int ntk = L.ntk[0], b0 = L.blk0[0];
+    int ntk = L.ntk[0], b0 = L.blk0[0], vec = L.vec[0];
     int64_t poff = L.poff[0];
 #pragma unroll
     for (int q = 1; q < kMaxOps; ++q)
@@ -289,45 +412,17 @@ __global__ void __launch_bounds__(kGB) k_lwgrad(WgradLaunch L) {
             ntk = L.ntk[q];
             b0 = L.blk0[q];
             poff = L.poff[q];
+            vec = L.vec[q];
         }
     const int S = L.S, M = L.M, N = o.N, KX = o.KX;
     const int local = blk - b0;
     const int s = local % S, tile = local / S;
     const int n0 = (tile / ntk) * kWN, k0 = (tile % ntk) * kWK;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-    // 8-row chunks: slice s of S, then wave of 4
-    const int mch = (M + 7) >> 3;
+    const int mch = (M + CM - 1) / CM;
     const int sb = s * mch / S, se = (s + 1) * mch / S;
     const int cb = sb + wave * (se - sb) / 4, ce = sb + (wave + 1) * (se - sb) / 4;
     const bool want_db = o.db != nullptr && k0 == 0;
-    const float *pg[2], *pmk[2], *px[2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-        const int n = min(n0 + 32 * a + r, N - 1);
-        pg[a] = o.G + n;
-        pmk[a] = GMASK ? o.gmask + n : nullptr;
-        const int kx = min(k0 + 32 * a + r, KX - 1);
-        px[a] = o.X + kx;
-    }
-    struct WFrag {
-        float g[2][4], x[2][4];
-    };
-    const size_t ldg = o.ldg, ldx = o.ldx;
-    auto load = [&](int c, WFrag &f) {  // rows past M: row M-1 loaded, G' = 0 (no branch)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int m = 8 * c + 2 * t + h;
-            const bool in = m < M;
-            const size_t mr = (size_t)(in ? m : M - 1);
-#pragma unroll
-            for (int a = 0; a < 2; ++a) {
-                float g = pg[a][mr * ldg];
-                if (GMASK) g = pmk[a][mr * ldg] > 0.0f ? g : 0.0f;
-                f.g[a][t] = in ? g : 0.0f;
-                f.x[a][t] = px[a][mr * ldx];
-            }
-        }
-    };
     f32x16 acc[2][2];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -335,35 +430,13 @@ __global__ void __launch_bounds__(kGB) k_lwgrad(WgradLaunch L) {
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.0f;
-    float dsum[2] = {0.0f, 0.0f};  // always summed (cheap), stored only for db
-    auto compute = [&](const WFrag &f) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int a = 0; a < 2; ++a)
-#pragma unroll
-                for (int b = 0; b < 2; ++b) acc[a][b] = mfma(f.g[a][t], f.x[b][t], acc[a][b]);
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int a = 0; a < 2; ++a) dsum[a] += f.g[a][t];
-    };
-    if (cb < ce) {  // two register buffers (see k_lgemm)
-        WFrag f0, f1;
-        load(cb, f0);
-        int c = cb;
-        for (; c + 1 < ce; c += 2) {
-            load(c + 1, f1);
-            __builtin_amdgcn_sched_barrier(0);
-            compute(f0);
-            __builtin_amdgcn_sched_barrier(0);
-            load(min(c + 2, ce - 1), f0);
-            __builtin_amdgcn_sched_barrier(0);
-            compute(f1);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (c < ce) compute(f0);
-    }
+    float dsum[2] = {0.0f, 0.0f};
+    float *img = lds + wave * (2 * CM * PITCH);
+    if (vec) lwgrad_loop<true, GMASK>(o, img, M, cb, ce, n0, k0, acc, dsum);
+    else lwgrad_loop<false, GMASK>(o, img, M, cb, ce, n0, k0, acc, dsum);
+    __syncthreads();  // the reduction reuses the images
+    float(*red)[64][64] = reinterpret_cast<float(*)[64][64]>(lds);
+    float(*dred)[2][64] = reinterpret_cast<float(*)[2][64]>(lds + 4 * 64 * 64);
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -391,7 +464,7 @@ __global__ void __launch_bounds__(kGB) k_lwgrad(WgradLaunch L) {
             else part[(size_t)s * nk + (size_t)n * KX + kx] = sum;
         }
     }
-    if (want_db && wave == 0 && h == 0) {  // n = n0 + 32a + r: both lane halves (rows m even / odd), 4 waves
+    if (want_db && wave == 0 && h == 0) {
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
             float sum = 0.0f;
@@ -551,7 +624,10 @@ extern "C" int f110_learner_wgrad(const f110_wgrad_op *ops, int32_t nops, int32_
     int32_t blk = 0;
     int64_t off = 0, total = 0;
     for (int q = 0; q < nops; ++q) {
-        L.op[q] = ops[q];
+        const f110_wgrad_op &o = ops[q];
+        L.op[q] = o;
+        L.vec[q] = o.N % 4 == 0 && o.KX % 4 == 0 && o.ldg % 4 == 0 && o.ldx % 4 == 0 && aligned16(o.G) &&
+                   aligned16(o.X) && (!o.gmask || aligned16(o.gmask));
         L.blk0[q] = blk;
         L.poff[q] = off;
         L.ntk[q] = (ops[q].KX + kWK - 1) / kWK;
@@ -566,12 +642,15 @@ extern "C" int f110_learner_wgrad(const f110_wgrad_op *ops, int32_t nops, int32_
     for (int q = nops; q < kMaxOps; ++q) L.blk0[q] = blk;
     hipStream_t s = (hipStream_t)stream;
     const bool gm = ops[0].gmask != nullptr;
-    if (L.S == 1) {
-        if (gm) hipLaunchKernelGGL((k_lwgrad<true, true>), dim3((unsigned)blk), dim3(kGB), 0, s, L);
-        else hipLaunchKernelGGL((k_lwgrad<true, false>), dim3((unsigned)blk), dim3(kGB), 0, s, L);
-    } else {
-        if (gm) hipLaunchKernelGGL((k_lwgrad<false, true>), dim3((unsigned)blk), dim3(kGB), 0, s, L);
-        else hipLaunchKernelGGL((k_lwgrad<false, false>), dim3((unsigned)blk), dim3(kGB), 0, s, L);
+    const void *kf[2][2] = {  // [final][gmask]
+        {reinterpret_cast<const void *>(&k_lwgrad<false, false>), reinterpret_cast<const void *>(&k_lwgrad<false, true>)},
+        {reinterpret_cast<const void *>(&k_lwgrad<true, false>), reinterpret_cast<const void *>(&k_lwgrad<true, true>)}};
+    void *args[] = {&L};
+    {
+        hipError_t e = hipLaunchKernel(kf[L.S == 1][gm], dim3((unsigned)blk), dim3(kGB), args, 0, s);
+        if (e != hipSuccess) return f110_set_error(F110_E_HIP, std::string(fn) + ": " + hipGetErrorString(e));
+    }
+    if (L.S > 1) {
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return f110_set_error(F110_E_HIP, std::string(fn) + ": " + hipGetErrorString(e));
         hipLaunchKernelGGL(k_lwgrad_finish, dim3((unsigned)((total + kGB - 1) / kGB)), dim3(kGB), 0, s, L, total);

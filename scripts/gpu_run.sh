@@ -8,6 +8,7 @@
 #   suite      pytest -m gpu (one process, per-test timeout)
 #   lgemm      tests/test_gpu_learner_gemm.py, scripts/learner_gemm_mb.py (+ its rocprofv3 kernel stats)
 #   lgemmpmc   two PMC passes (SQ wait / MFMA busy; TA busy) over scripts/learner_gemm_mb.py
+#   lgab       scripts/learner_gemm_mb.py once per alternate build ab_libs/*.so (F110_LIB)
 #   learner    tests/test_gpu_replay.py + tests/test_gpu_ddpg_heads.py (the DDPG learner)
 #   c5prof     scripts/profile_c5.py TAG (C5 bench + rocprofv3 kernel stats by stage) -> gpurun_out/prof_c5_TAG/
 #   quick      the dispatch-variant tests of tests/test_gpu_batch.py only
@@ -58,6 +59,10 @@ for step in "$@"; do
                       python3 scripts/learner_gemm_mb.py ;;
         learner) run learner 600 python -u -m pytest tests/test_gpu_replay.py tests/test_gpu_ddpg_heads.py -m gpu -x -v \
                      --timeout 200 --timeout-method thread -p no:cacheprovider ;;
+        lgab) for lib in ab_libs/*.so; do  # the microbench per alternate build (F110_LIB)
+                  n=$(basename "$lib" .so)
+                  F110_LIB=$R/$lib run "lgab_$n" 300 python -u scripts/learner_gemm_mb.py || exit $?
+              done ;;
         c5prof) run c5prof 900 python -u scripts/profile_c5.py "$TAG" ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python -u bench.py && cp "$OUT/bench.out" "$OUT/bench.json" ;;

@@ -26,7 +26,8 @@ def _rand(g, *shape):
     return torch.randn(*shape, device="cuda", generator=g, dtype=torch.float32)
 
 
-@pytest.mark.parametrize("M,K,N", [(4096, 1088, 128), (333, 12, 128), (200, 130, 200), (64, 64, 2), (1, 48, 40)])
+@pytest.mark.parametrize("M,K,N", [(4096, 1088, 128), (333, 12, 128), (200, 130, 200), (64, 64, 2), (1, 48, 40),
+                                   (257, 1060, 72), (40, 36, 129)])
 def test_forward_layers(gpu, M, K, N):
     lg = _lg()
     g = torch.Generator(device="cuda").manual_seed(M + K + N)
@@ -59,6 +60,26 @@ def test_grouped_forward_with_action_columns_and_masks(gpu):
     _close(y2, p, a)
     _close(y3, torch.where(om.double() > 0, torch.relu(p + bs2.double()), torch.zeros_like(p)), a + bs2.double().abs())
 
+
+def test_grouped_lds_path_with_input_mask(gpu):
+    """Rows of A and B 16-B aligned with K % 4 == 0 take the LDS-staged kernel
+    (k_lgemm_lds): a grouped launch of two ops with an input mask (amask) on
+    both, K with a partial last 32-k chunk, ragged M and N."""
+    lg = _lg()
+    g = torch.Generator(device="cuda").manual_seed(11)
+    M, K = 301, 1092
+    X1, X2, Am1, Am2 = _rand(g, M, K), _rand(g, M, K), _rand(g, M, K), _rand(g, M, K)
+    W1, W2, b1 = _rand(g, 96, K), _rand(g, 128, K), _rand(g, 96)
+    y1, y2 = torch.empty(M, 96, device="cuda"), torch.empty(M, 128, device="cuda")
+    lg.gemm([lg.op(X1, W1, y1, 96, K, K, K, 96, bias=b1, relu=True, amask=Am1),
+             lg.op(X2, W2, y2, 128, K, K, K, 128, amask=Am2)], M, X1.device)
+    for X, Am, W, y, b, relu in ((X1, Am1, W1, y1, b1, True), (X2, Am2, W2, y2, None, False)):
+        Xm = torch.where(Am > 0, X, torch.zeros_like(X)).double()
+        ref = Xm @ W.double().t()
+        absref = Xm.abs() @ W.double().abs().t()
+        if b is not None:
+            ref, absref = ref + b.double(), absref + b.double().abs()
+        _close(y, torch.relu(ref) if relu else ref, absref)
 
 @pytest.mark.parametrize("M,K,N,ldb,off", [(4096, 128, 128, 130, 0), (4096, 128, 2, 130, 128), (77, 128, 128, 128, 0),
                                            (50, 20, 33, 40, 3)])
