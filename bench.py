@@ -126,11 +126,11 @@ def bench_ddpg(args):
     KP = min(K, 100)
     ph = {"env_step_reward_ms": 0.0, "replay_add_ms": 0.0, "learner_update_ms": 0.0}
     for _ in range(KP):
-        act = tr.agent.choose_action(tr.obs, training=True)
+        act = tr.agent.choose_action(tr.obs, training=True, out=tr.env.agent_actions())  # as VectorTrainer.step
         ev[0].record(stream)
-        nxt, rew, term, _, info = tr.env.step(act)
+        nxt, rew, term, was_reset = tr.env.step_transition(act)
         ev[1].record(stream)
-        tr.agent.remember(tr.obs, act, rew.to(torch.float32), nxt, term, mask=~info["reset"])
+        tr.agent.remember_env(tr.obs, act, rew, nxt, term, was_reset)
         ev[2].record(stream)
         tr.last = tr.agent.replay()
         ev[3].record(stream)

@@ -71,10 +71,10 @@ EXPORTS = [
     "f110_profile_begin", "f110_profile_end", "f110_host_tables", "f110_host_beam_indices",
     "f110_set_scan_noise", "f110_set_params", "f110_host_cell_index", "f110_gap_follow",
     "f110_host_window_ranges", "f110_track_create", "f110_track_destroy", "f110_track_arrays",
-    "f110_default_reward_params", "f110_reward", "f110_replay_create", "f110_replay_destroy", "f110_replay_add",
+    "f110_default_reward_params", "f110_reward", "f110_replay_create", "f110_replay_destroy", "f110_replay_add", "f110_replay_add_env",
     "f110_replay_sample", "f110_replay_update_priorities", "f110_replay_length", "f110_replay_arrays",
     "f110_debug_wave_trace", "f110_set_ray_gate", "f110_disable_heavy_first", "f110_ray_kernel", "f110_ray_lanes", "f110_ray_refill", "f110_set_ray_refill", "f110_read_counter", "f110_step_n", "f110_set_ray_lanes", "f110_set_reset_dtype", "f110_host_np_sincosf", "f110_host_sincos", "f110_host_map_table", "f110_get_lap_state",
-    "f110_dynamics_ks_batch", "f110_collision_batch", "f110_collision_multiple", "f110_adam_step", "f110_ddpg_scratch_floats", "f110_ddpg_actor_head",
+    "f110_dynamics_ks_batch", "f110_collision_batch", "f110_collision_multiple", "f110_adam_step", "f110_ddpg_scratch_floats", "f110_ddpg_actor_head", "f110_ddpg_actor_explore",
     "f110_ddpg_actor_head_bwd", "f110_ddpg_td_target", "f110_ddpg_critic_loss", "f110_ddpg_critic_loss_bwd",
     "f110_ddpg_q_mean", "f110_ddpg_q_mean_bwd", "f110_ddpg_relu_bwd_scratch_floats", "f110_ddpg_relu_bwd",
     "f110_learner_gemm", "f110_learner_wgrad_scratch_floats", "f110_learner_wgrad",
@@ -155,6 +155,7 @@ def load(build_if_missing: bool = True):
                                      ctypes.c_double, u64]
     L.f110_replay_destroy.argtypes = [_P]
     L.f110_replay_add.argtypes = [_P, _P, i64, _P, i64, _P, _P, i64, _P, _P, _P, i64, _P]
+    L.f110_replay_add_env.argtypes = [_P, _P, i64, _P, i64, _P, _P, i64, _P, _P, i64, _P]
     L.f110_replay_sample.argtypes = [_P, i32, ctypes.c_double, _P, _P, _P, _P, _P, _P, _P, _P]
     L.f110_replay_update_priorities.argtypes = [_P, _P, _P, i64, i32, ctypes.c_float, _P]
     L.f110_replay_length.argtypes = [_P, ctypes.POINTER(i64), ctypes.POINTER(i64), _P]
@@ -182,6 +183,8 @@ def load(build_if_missing: bool = True):
     f32 = ctypes.c_float
     L.f110_ddpg_scratch_floats.argtypes = [i32, i32, i32]
     L.f110_ddpg_actor_head.argtypes = [_P] * 5 + [i32] * 3 + [_P] * 3
+    L.f110_ddpg_actor_explore.argtypes = [_P] * 5 + [i32] * 3 + [f32, _P, _P, ctypes.c_uint64, ctypes.c_uint64, _P,
+                                                                  i64, _P]
     L.f110_ddpg_actor_head_bwd.argtypes = [_P] * 5 + [i32] * 3 + [_P] * 6
     L.f110_ddpg_td_target.argtypes = [_P] * 5 + [f32, i32, i32, _P, _P]
     L.f110_ddpg_critic_loss.argtypes = [_P] * 5 + [i32] * 2 + [_P] * 4

@@ -35,7 +35,7 @@ constexpr int kWRows = 64;    // rows per block of the weight-gradient pass
 constexpr int kMaxOut = 4;    // head outputs (act_dim <= 4)
 constexpr int kMaxK = 255;    // hidden width (the weight pass keeps >= 3 row lanes of column quads)
 
-enum HeadMode { kActor = 0, kTarget = 1, kLoss = 2, kMean = 3 };
+enum HeadMode { kActor = 0, kTarget = 1, kLoss = 2, kMean = 3, kExplore = 4 };
 
 struct HeadArgs {
     const float *h, *W, *b;
@@ -49,7 +49,28 @@ struct HeadArgs {
     float *loss;
     float gamma, sign;
     int32_t B, K, nout, nblk;
+    // kExplore: out0[row * out_stride + j] = clamp(act + sigma N(0,1), lo[j], hi[j])
+    const float *lo, *hi;
+    float sigma;
+    int64_t out_stride;
+    uint64_t seed, step;
 };
+
+// choose_action's exploration noise (agent.py:350-370, GaussianActionNoise
+// :520-539, np.random.normal(0, sigma)): N(0,1) pairs by Box-Muller on one
+// Philox2x32-10 block per (call, row, output pair), counter (step, row pair
+// index), key from the seed; f32 log / sqrt / sincospi on 24-bit uniforms
+// (u1 in (0, 1]).  Independent across rows, outputs and calls.
+__device__ __forceinline__ float2 explore_normals(uint64_t seed, uint64_t step, int64_t row, int pair) {
+    const uint32_t key = (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x85EBCA6Bu) ^ ((uint32_t)(step >> 32) * 0xC2B2AE35u);
+    const U2 r = philox2x32((uint32_t)step, (uint32_t)(row * 2 + pair), key);
+    const float u1 = ((float)(r.x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+    const float u2 = (float)(r.y >> 8) * (1.0f / 16777216.0f);
+    const float rad = sqrtf(-2.0f * logf(u1));
+    float sn, cs;
+    sincospif(2.0f * u2, &sn, &cs);
+    return make_float2(rad * cs, rad * sn);
+}
 
 // sum over the 32 lanes of a half-wave (fixed tree); every lane gets it
 __device__ __forceinline__ float half_sum(float v) {
@@ -113,6 +134,20 @@ __global__ void __launch_bounds__(kHB) k_head_fwd(HeadArgs a) {
                     const float t = tanhf(z[j]);
                     a.out1[row * NOUT + j] = t;
                     a.out0[row * NOUT + j] = a.aux0[j] * t + a.aux1[j];
+                }
+            } else if (MODE == kExplore) {  // the action, + sigma N(0,1), clipped to [low, high] (NaN kept)
+#pragma unroll
+                for (int j = 0; j < NOUT; j += 2) {
+                    const float2 nz = explore_normals(a.seed, a.step, row, j >> 1);
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        if (j + q >= NOUT) break;
+                        const float act = a.aux0[j + q] * tanhf(z[j + q]) + a.aux1[j + q];
+                        float v = act + a.sigma * (q == 0 ? nz.x : nz.y);
+                        v = v < a.lo[j + q] ? a.lo[j + q] : v;
+                        v = v > a.hi[j + q] ? a.hi[j + q] : v;
+                        a.out0[row * a.out_stride + j + q] = v;
+                    }
                 }
             } else if (MODE == kTarget) {  // r + gamma * (1.0 - d) * q_next (agent.py:306)
                 const float gd = a.gamma * (1.0f - a.aux1[row]);
@@ -430,6 +465,24 @@ extern "C" int f110_ddpg_actor_head(const float *h, const float *W, const float 
         return hipGetLastError();
     });
     return e == hipSuccess ? 0 : fail_hip("f110_ddpg_actor_head", e);
+}
+
+extern "C" int f110_ddpg_actor_explore(const float *h, const float *W, const float *b, const float *scale,
+                                       const float *shift, int32_t B, int32_t K, int32_t nout, float sigma,
+                                       const float *low, const float *high, uint64_t seed, uint64_t step, float *out,
+                                       int64_t out_stride, void *stream) {
+    if (bad_shape(B, K, nout) || !h || !W || !b || !scale || !shift || !low || !high || !out || out_stride < nout)
+        return fail_arg("f110_ddpg_actor_explore");
+    HeadArgs a{};
+    a.h = h, a.W = W, a.b = b, a.aux0 = scale, a.aux1 = shift, a.out0 = out;
+    a.lo = low, a.hi = high, a.sigma = sigma, a.out_stride = out_stride, a.seed = seed, a.step = step;
+    a.B = B, a.K = K, a.nout = nout;
+    hipError_t e = with_nout(nout, [&](auto N) {
+        hipLaunchKernelGGL((k_head_fwd<kExplore, decltype(N)::value>), dim3(row_blocks(B)), dim3(kHB), 0,
+                           (hipStream_t)stream, a);
+        return hipGetLastError();
+    });
+    return e == hipSuccess ? 0 : fail_hip("f110_ddpg_actor_explore", e);
 }
 
 extern "C" int f110_ddpg_actor_head_bwd(const float *h, const float *W, const float *t, const float *scale,

@@ -291,6 +291,7 @@ struct ReplayView {
 
 struct ReplayRows {      // one add(): n transitions (device, f32 rows with strides in floats)
     const float *obs, *next_obs, *act, *reward;
+    const double *reward64; // [n] f64 rewards instead of reward (rounded to f32 as .to(torch.float32))
     const float *priority;  // [n] explicit priorities or null (= the max priority)
     const uint8_t *done;
     int64_t obs_stride, next_stride, act_stride;
@@ -302,8 +303,8 @@ struct ReplayBatch {     // one sample(): the gathered batch (device, contiguous
     int32_t vec4;
 };
 
-hipError_t launch_replay_add(const ReplayView &v, const ReplayRows &in, const uint8_t *mask, int64_t n,
-                             hipStream_t s);
+hipError_t launch_replay_add(const ReplayView &v, const ReplayRows &in, const uint8_t *mask, int mask_skip,
+                             int64_t n, hipStream_t s);
 hipError_t launch_replay_sample(const ReplayView &v, int32_t batch, double beta, int64_t *idx, float *w,
                                 const ReplayBatch &out, bool known_full, hipStream_t s);
 hipError_t launch_replay_update(const ReplayView &v, const int64_t *idx, const float *val, int64_t n, float add_eps,

@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(kRB) k_prio_max(ReplayView v) {
 // Ring slots of the rows to store (mask[i] != 0, or all) in row order, as the
 // reference's one add() per transition (agent.remember) would fill them.
 __global__ void __launch_bounds__(kOneBlock) k_add_scan(ReplayView v, const uint8_t *mask, const float *priority,
-                                                        int64_t n, int n_part) {
+                                                        int64_t n, int n_part, int mask_skip) {
     __shared__ int64_t part[kOneBlock];
     __shared__ uint32_t wmx[kOneBlock / 64];
     __shared__ uint32_t mx;
@@ -127,7 +127,9 @@ __global__ void __launch_bounds__(kOneBlock) k_add_scan(ReplayView v, const uint
     const int64_t chunk = (n + kOneBlock - 1) / kOneBlock;
     const int64_t r0 = min((int64_t)t * chunk, n), r1 = min(r0 + chunk, n);
     int64_t cnt = 0;
-    for (int64_t i = r0; i < r1; ++i) cnt += (!mask || mask[i]) ? 1 : 0;
+    // stored rows: mask[i] != 0, or (mask_skip) mask[i] == 0, or all rows without a mask
+    auto keep = [&](int64_t i) { return !mask || ((mask[i] != 0) != (mask_skip != 0)); };
+    for (int64_t i = r0; i < r1; ++i) cnt += keep(i) ? 1 : 0;
     part[t] = cnt;
     __syncthreads();
     for (int o = 1; o < kOneBlock; o <<= 1) {  // inclusive scan
@@ -141,7 +143,7 @@ __global__ void __launch_bounds__(kOneBlock) k_add_scan(ReplayView v, const uint
     const int64_t cap = v.capacity, next = v.hdr->next;
     const float p0 = add_priority(v.hdr->length, mx);
     for (int64_t i = r0; i < r1; ++i) {
-        if (!mask || mask[i]) {
+        if (keep(i)) {
             const int64_t slot = (next + rank) % cap;
             v.pos[i] = slot;
             float p = p0;
@@ -187,7 +189,7 @@ __global__ void __launch_bounds__(kRB) k_add_copy(ReplayView v, ReplayRows in, i
     }
     if (threadIdx.x < v.act_dim) v.act[slot * v.act_dim + threadIdx.x] = in.act[i * in.act_stride + threadIdx.x];
     if (threadIdx.x == 0) {
-        v.reward[slot] = in.reward[i];
+        v.reward[slot] = in.reward64 ? (float)in.reward64[i] : in.reward[i];
         v.done[slot] = in.done ? (in.done[i] ? 1.0f : 0.0f) : 0.0f;
     }
 }
@@ -537,12 +539,12 @@ size_t replay_finish_lds(int32_t batch) { return (size_t)batch * 16; }
 
 size_t replay_replace_lds(int32_t batch) { return (size_t)batch * 24; }
 
-hipError_t launch_replay_add(const ReplayView &v, const ReplayRows &in, const uint8_t *mask, int64_t n,
-                             hipStream_t s) {
+hipError_t launch_replay_add(const ReplayView &v, const ReplayRows &in, const uint8_t *mask, int mask_skip,
+                             int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int grid = replay_grid(v.capacity);
     hipLaunchKernelGGL(k_prio_max, dim3(grid), dim3(kRB), 0, s, v);
-    hipLaunchKernelGGL(k_add_scan, dim3(1), dim3(kOneBlock), 0, s, v, mask, in.priority, n, grid);
+    hipLaunchKernelGGL(k_add_scan, dim3(1), dim3(kOneBlock), 0, s, v, mask, in.priority, n, grid, mask_skip);
     hipLaunchKernelGGL(k_add_copy, dim3((unsigned)n), dim3(kRB), 0, s, v, in, n);
     return hipGetLastError();
 }

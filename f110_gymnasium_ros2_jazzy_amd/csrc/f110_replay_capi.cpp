@@ -101,23 +101,25 @@ extern "C" int f110_replay_destroy(f110_replay *rb) {
 
 static bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 
-extern "C" int f110_replay_add(f110_replay *rb, const float *obs, int64_t obs_stride, const float *act,
-                               int64_t act_stride, const float *reward, const float *next_obs, int64_t next_stride,
-                               const uint8_t *done, const float *priority, const uint8_t *mask, int64_t n,
-                               void *stream) {
-    if (!rb) return fail(F110_E_INVALID, "f110_replay_add: null buffer");
-    if (n < 0 || n > rb->max_add) return fail(F110_E_INVALID, "f110_replay_add: n must be in [0, max_add]");
+namespace {
+int replay_add(f110_replay *rb, const char *fn, const float *obs, int64_t obs_stride, const float *act,
+               int64_t act_stride, const float *reward, const double *reward64, const float *next_obs,
+               int64_t next_stride, const uint8_t *done, const float *priority, const uint8_t *mask, int mask_skip,
+               int64_t n, void *stream) {
+    if (!rb) return fail(F110_E_INVALID, std::string(fn) + ": null buffer");
+    if (n < 0 || n > rb->max_add) return fail(F110_E_INVALID, std::string(fn) + ": n must be in [0, max_add]");
     if (n == 0) return F110_OK;
     const ReplayView &v = rb->v;
-    if (!obs || !act || !reward || !next_obs || obs_stride < v.obs_dim || next_stride < v.obs_dim ||
+    if (!obs || !act || (!reward && !reward64) || !next_obs || obs_stride < v.obs_dim || next_stride < v.obs_dim ||
         act_stride < v.act_dim)
-        return fail(F110_E_INVALID, "f110_replay_add: null row pointer or stride below the row length");
-    if (hipSetDevice(rb->device) != hipSuccess) return fail(F110_E_HIP, "f110_replay_add: hipSetDevice");
+        return fail(F110_E_INVALID, std::string(fn) + ": null row pointer or stride below the row length");
+    if (hipSetDevice(rb->device) != hipSuccess) return fail(F110_E_HIP, std::string(fn) + ": hipSetDevice");
     ReplayRows in{};
     in.obs = obs;
     in.next_obs = next_obs;
     in.act = act;
     in.reward = reward;
+    in.reward64 = reward64;
     in.done = done;
     in.priority = priority;
     in.obs_stride = obs_stride;
@@ -125,9 +127,27 @@ extern "C" int f110_replay_add(f110_replay *rb, const float *obs, int64_t obs_st
     in.act_stride = act_stride;
     in.vec4 = (v.obs_dim % 4 == 0 && obs_stride % 4 == 0 && next_stride % 4 == 0 && aligned16(obs) &&
                aligned16(next_obs)) ? 1 : 0;
-    hipError_t e = launch_replay_add(v, in, mask, n, (hipStream_t)stream);
-    if (e != hipSuccess) return fail(F110_E_HIP, std::string("f110_replay_add: ") + hipGetErrorString(e));
+    hipError_t e = launch_replay_add(v, in, mask, mask_skip, n, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(F110_E_HIP, std::string(fn) + ": " + hipGetErrorString(e));
     return F110_OK;
+}
+}  // namespace
+
+extern "C" int f110_replay_add(f110_replay *rb, const float *obs, int64_t obs_stride, const float *act,
+                               int64_t act_stride, const float *reward, const float *next_obs, int64_t next_stride,
+                               const uint8_t *done, const float *priority, const uint8_t *mask, int64_t n,
+                               void *stream) {
+    return replay_add(rb, "f110_replay_add", obs, obs_stride, act, act_stride, reward, nullptr, next_obs, next_stride,
+                      done, priority, mask, 0, n, stream);
+}
+
+extern "C" int f110_replay_add_env(f110_replay *rb, const float *obs, int64_t obs_stride, const float *act,
+                                   int64_t act_stride, const double *reward, const float *next_obs,
+                                   int64_t next_stride, const uint8_t *terminated, const uint8_t *was_reset,
+                                   int64_t n, void *stream) {
+    if (!reward) return fail(F110_E_INVALID, "f110_replay_add_env: null reward");
+    return replay_add(rb, "f110_replay_add_env", obs, obs_stride, act, act_stride, nullptr, reward, next_obs,
+                      next_stride, terminated, nullptr, was_reset, 1, n, stream);
 }
 
 extern "C" int f110_replay_sample(f110_replay *rb, int32_t batch, double beta, int64_t *idx, float *weights,

@@ -396,6 +396,12 @@ class DDPGLearner:
         self._noise_gen.manual_seed(seed)
         self._low = torch.as_tensor(self.action_low, device=self.device)
         self._high = torch.as_tensor(self.action_high, device=self.device)
+        # the explicit path draws the noise inside its head launch (f110_ddpg_actor_explore): per rank a
+        # key, per call a counter
+        self._low32 = self._low.to(torch.float32).contiguous()
+        self._high32 = self._high.to(torch.float32).contiguous()
+        self._noise_key = (int(seed) * 1000003 + (dist.get_rank() if self.distributed else 0)) & ((1 << 64) - 1)
+        self._noise_calls = 0
         self._ready = False
         self.global_step = 0
 
@@ -403,6 +409,12 @@ class DDPGLearner:
     def remember(self, state, action, reward, next_state, done, mask=None):
         """agent.py:223-237 for a batch of transitions (rows with mask == 0 skipped)."""
         self.memory.add(state, action, reward, next_state, done, mask=mask)
+
+    def remember_env(self, state, action, reward, next_state, terminated, was_reset):
+        """remember() of a vector env's raw outputs (float64 rewards, uint8
+        terminated / was_reset flags; reset rows skipped) without torch-side
+        conversions (DeviceReplayBuffer.add_env)."""
+        self.memory.add_env(state, action, reward, next_state, terminated, was_reset)
 
     def _finite(self, name, x):  # agent.py:291-296 (host sync; only with check_finite)
         if self.check_finite and not bool(torch.isfinite(x).all()):
@@ -571,12 +583,21 @@ class DDPGLearner:
         self.global_step += 1
         return self._graph_out
 
-    def choose_action(self, obs, training: bool = True) -> torch.Tensor:
+    def choose_action(self, obs, training: bool = True, out: torch.Tensor | None = None) -> torch.Tensor:
         """agent.py:350-370 for obs [N, obs_dim] (or [obs_dim]): actor output,
         plus N(0, sigma^2) noise clipped to [low, high] when training; sigma
-        decays once per call (GaussianActionNoise.__call__, :520-539)."""
+        decays once per call (GaussianActionNoise.__call__, :520-539).  On the
+        explicit path a training call is one launch after the hidden layers
+        (the head draws the noise and clips) and may write into out, a
+        [N, act_dim] float32 view with unit column stride (e.g. the env's action rows)."""
         with torch.no_grad(), TunedGemms(self.tuned_gemms):
             o = torch.as_tensor(obs, device=self.device, dtype=torch.float32)
+            if self.explicit is not None and training and o.dim() == 2:
+                a = self.explicit.policy(self.actor, o, explore=(self.sigma, self._low32, self._high32,
+                                                                 self._noise_key, self._noise_calls, out))
+                self._noise_calls += 1
+                self.sigma = max(self.sigma * self.noise_decay, self.sigma_min)
+                return a
             if self.explicit is not None:
                 a = self.explicit.policy(self.actor, o if o.dim() == 2 else o.unsqueeze(0))
             else:
@@ -585,6 +606,9 @@ class DDPGLearner:
                 noise = torch.randn(a.shape, generator=self._noise_gen, device=self.device) * self.sigma
                 a = torch.clamp(a + noise, self._low, self._high)
                 self.sigma = max(self.sigma * self.noise_decay, self.sigma_min)
+        if out is not None:
+            out.copy_(a)
+            return out
         return a
 
     def hard_update(self):

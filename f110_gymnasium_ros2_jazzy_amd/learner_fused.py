@@ -148,11 +148,27 @@ class ExplicitUpdate:
                          db=ga["fc1.bias"])], M, dev)
         return loss
 
-    def policy(self, actor, obs):
-        """Actor.forward without autograd (choose_action): fc1, fc2, head."""
+    def policy(self, actor, obs, explore=None):
+        """Actor.forward without autograd (choose_action): fc1, fc2, head.
+        explore = (sigma, low, high, seed, step, out): the head adds
+        sigma * N(0, 1) and clips to [low, high] (f110_ddpg_actor_explore), writing
+        the actions into out (rows may be strided), which is returned."""
         obs = obs.contiguous()
         M = obs.shape[0]
         h1, h2 = self._e(M), self._e(M)
         lg.gemm([self._fwd(obs, actor.fc1, h1)], M, obs.device)
         lg.gemm([self._fwd(h1, actor.fc2, h2)], M, obs.device)
-        return self._actor_head(actor, h2)[0]
+        if explore is None:
+            return self._actor_head(actor, h2)[0]
+        sigma, low, high, seed, step, out = explore
+        W, b = actor.fc3.weight, actor.fc3.bias
+        scale, shift = actor._affine()
+        n = W.shape[0]
+        if out is None:
+            out = self._e(M, n)
+        if out.shape != (M, n) or out.stride(1) != 1 or out.dtype != torch.float32:
+            raise ValueError("policy: out must be [M, act_dim] float32 with unit column stride")
+        _lib.check(self.L.f110_ddpg_actor_explore(_p(h2), _p(W), _p(b), _p(scale), _p(shift), M, h2.shape[1], n,
+                                                  float(sigma), _p(low), _p(high), int(seed), int(step), _p(out),
+                                                  out.stride(0), _stream(h2)), "f110_ddpg_actor_explore")
+        return out

@@ -109,6 +109,30 @@ class DeviceReplayBuffer:
                 self._stream()), "f110_replay_add")
         self._added += n
 
+    def add_env(self, states, actions, rewards, next_states, terminated, was_reset):
+        """add() of a vector env's raw step outputs (f110_replay_add_env): rewards
+        float64, terminated / was_reset uint8 device tensors as the simulator
+        writes them; rows with was_reset != 0 are not stored.  No dtype
+        conversions on the torch side."""
+        s = self._rows(states, self.obs_dim)
+        ns = self._rows(next_states, self.obs_dim)
+        a = self._rows(actions, self.act_dim)
+        n = s.shape[0]
+        r, d, m = rewards.reshape(-1), terminated.reshape(-1), was_reset.reshape(-1)
+        if r.dtype != torch.float64 or d.dtype != torch.uint8 or m.dtype != torch.uint8:
+            raise TypeError("add_env: rewards float64, terminated and was_reset uint8")
+        if not (r.is_contiguous() and d.is_contiguous() and m.is_contiguous()):
+            raise ValueError("add_env: contiguous rewards / flags")
+        if ns.shape[0] != n or a.shape[0] != n or r.shape[0] != n or d.shape[0] != n or m.shape[0] != n:
+            raise ValueError("add_env: every input needs the same number of rows")
+        self._keep = (s, ns, a, r, d, m)  # alive until the stream has consumed them
+        for lo in range(0, n, self.max_add):
+            hi = min(n, lo + self.max_add)
+            _lib.check(self.L.f110_replay_add_env(
+                self.handle, _p(s[lo:hi]), s.stride(0), _p(a[lo:hi]), a.stride(0), _p(r[lo:hi]), _p(ns[lo:hi]),
+                ns.stride(0), _p(d[lo:hi]), _p(m[lo:hi]), hi - lo, self._stream()), "f110_replay_add_env")
+        self._added += n
+
     def _rows(self, x, width):
         t = torch.as_tensor(x, device=self.device)
         if t.dtype != torch.float32:

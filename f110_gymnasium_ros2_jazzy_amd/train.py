@@ -70,17 +70,19 @@ class VectorTrainer:
         self.last = None
 
     def step(self):
-        """One vector step of the loop (train_ddpg.py:160-192)."""
+        """One vector step of the loop (train_ddpg.py:160-192).  Returns the
+        step's rewards (float64) and terminated flags (uint8): device buffers
+        valid until the next step()."""
         if self.global_step < self.warmup:  # :162-163
             u = torch.rand(self.N, 2, generator=self._gen, device=self.device)
             act = self._low + u * (self._high - self._low)
-        else:
-            act = self.agent.choose_action(self.obs, training=True)
-        next_obs, rew, term, trunc, info = self.env.step(act)
+        else:  # the actions land in the env's action rows (no copy in the step)
+            act = self.agent.choose_action(self.obs, training=True, out=self.env.agent_actions())
+        next_obs, rew, term, was_reset = self.env.step_transition(act)
         # NEXT_STEP autoreset: a reset row's obs is the previous episode's last
         # observation and its next_obs the new episode's first -- not a transition
-        keep = ~info["reset"]
-        self.agent.remember(self.obs, act, rew.to(torch.float32), next_obs, term, mask=keep)
+        # (remember_env skips the rows with was_reset != 0)
+        self.agent.remember_env(self.obs, act, rew, next_obs, term, was_reset)
         if self.global_step >= self.warmup:
             for _ in range(self.updates_per_step):
                 self.last = self.agent.replay()

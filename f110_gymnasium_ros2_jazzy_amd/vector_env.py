@@ -167,6 +167,39 @@ class F110VectorEnv:
                     self._infos(out))
         return obs, rewards, term, trunc, self._infos(out)
 
+    def agent_actions(self):
+        """The learning agent's rows of the action buffer the next step reads
+        ([N, 2] view), or None (no opponent, or several learning agents): a
+        policy may write its actions here (DDPGLearner.choose_action(out=...))
+        and pass the same view to step_transition(), which then copies nothing."""
+        if self.opponent is None or len(self._others) != 1:
+            return None
+        return self._act[:, self._others[0]]
+
+    def step_transition(self, actions):
+        """step() for a trainer on the device: (next_obs copy [N, obs_dim],
+        rewards float64 [N], terminated uint8 [N], was_reset uint8 [N]).  The
+        rewards and flags are the simulator's / reward function's own buffers
+        (no clone, no dtype conversion): valid until the next step."""
+        if self.as_numpy:
+            raise ValueError("step_transition: device tensors only (as_numpy=False)")
+        a = torch.as_tensor(actions, device=self.device)
+        if self.opponent is not None:
+            dst = self.agent_actions()
+            if dst is None or a.data_ptr() != dst.data_ptr() or a.stride() != dst.stride():
+                self._act[:, self._others_sl] = a.reshape(self.num_envs, len(self._others), 2)
+            a = self._act
+        elif a.dim() == 2 and self.num_agents == 1:
+            a = a.unsqueeze(1)
+        out = self.sim.step(a)
+        self._opponent_next(out)
+        if self.reward_fn is not None:
+            rewards = self.reward_fn(out.obs, reset_mask=out.was_reset)
+        else:
+            rewards = torch.where(out.was_reset.bool(), torch.zeros((), dtype=torch.float64, device=self.device),
+                                  torch.full((), self.timestep, dtype=torch.float64, device=self.device))
+        return out.obs.clone(), rewards, out.terminated, out.was_reset
+
     def close(self):
         if getattr(self, "sim", None) is not None:
             self.sim.close()

@@ -487,6 +487,16 @@ F110_API int f110_replay_add(f110_replay *rb, const float *obs, int64_t obs_stri
                              const uint8_t *done, const float *priority, const uint8_t *mask, int64_t n,
                              void *stream);
 
+/* f110_replay_add for a vector env's raw step outputs (train_ddpg.py:177-183,
+ * agent.remember per transition): reward [n] f64 (stored rounded to f32),
+ * terminated [n] u8 (the done flag), was_reset [n] u8 -- rows with
+ * was_reset != 0 (NEXT_STEP autoreset: obs is the finished episode's, next_obs
+ * the new one's) are not stored.  No torch dtype conversions on the caller's side. */
+F110_API int f110_replay_add_env(f110_replay *rb, const float *obs, int64_t obs_stride, const float *act,
+                                 int64_t act_stride, const double *reward, const float *next_obs,
+                                 int64_t next_stride, const uint8_t *terminated, const uint8_t *was_reset,
+                                 int64_t n, void *stream);
+
 /* sample(beta) (:76-116) of `batch` rows: without replacement when the buffer
  * holds at least `batch` rows (distributed like numpy's
  * Generator.choice(replace=False, p=...): successive draws, in draw order),
@@ -545,6 +555,15 @@ F110_API int64_t f110_ddpg_scratch_floats(int32_t B, int32_t K, int32_t nout);
 F110_API int f110_ddpg_actor_head(const float *h, const float *W, const float *b, const float *scale,
                                   const float *shift, int32_t B, int32_t K, int32_t nout, float *act, float *t,
                                   void *stream);
+/* choose_action(training=True) after the hidden layers (agent.py:350-370 with
+ * GaussianActionNoise :520-539): out[row * out_stride + j] = clip(scale * tanh(h W^T + b) + shift
+ * + sigma * n, low[j], high[j]), n ~ N(0, 1) independent per (row, j) and per call (Philox2x32
+ * keyed by seed, counter step: a new step per call); NaN actions stay NaN.  out may be a strided
+ * view (e.g. the vector env's action rows). */
+F110_API int f110_ddpg_actor_explore(const float *h, const float *W, const float *b, const float *scale,
+                                     const float *shift, int32_t B, int32_t K, int32_t nout, float sigma,
+                                     const float *low, const float *high, uint64_t seed, uint64_t step, float *out,
+                                     int64_t out_stride, void *stream);
 /* dz = (dact * scale) * (1 - t*t); dh = dz W; dW = dz^T h; db = sum_rows dz */
 F110_API int f110_ddpg_actor_head_bwd(const float *h, const float *W, const float *t, const float *scale,
                                       const float *dact, int32_t B, int32_t K, int32_t nout, float *dh,

@@ -32,15 +32,16 @@ RAYPMC = [sys.executable, os.path.join(REPO, "scripts", "ray_pmc.py")]
 env["MB_ENVS"] = str(ENVS)
 
 
-def run(name, extra, timeout=400, bench_extra=(), target=None):
+def run(name, extra, timeout=400, bench_extra=(), target=None, env_extra=None):
     d = os.path.join(OUT, name)
     if COLLECT:
         return d
     shutil.rmtree(d, ignore_errors=True)
+    run_env = dict(env, **(env_extra or {}))
     cmd = ["rocprofv3"] + extra + ["--output-format", "csv", "-d", d, "-o", "run", "--"] + (target or BENCH + list(bench_extra))
     print(" ".join(cmd), flush=True)
     with open(os.path.join(OUT, f"{name}.log"), "w") as log:
-        subprocess.run(["timeout", "-k", "10", str(timeout)] + cmd, cwd="/tmp", env=env, stdout=log,
+        subprocess.run(["timeout", "-k", "10", str(timeout)] + cmd, cwd="/tmp", env=run_env, stdout=log,
                        stderr=subprocess.STDOUT, check=True)
     return d
 
@@ -154,8 +155,15 @@ except Exception as exc:
 #    busy cycles (TA_BUSY_avr: per TA instance, one per CU), the bound of the gather loop
 grp = ["SQ_INSTS_VMEM_RD", "SQ_WAVES", "TA_BUSY_avr", "TA_FLAT_READ_WAVEFRONTS_sum", "GRBM_GUI_ACTIVE"]
 try:
-    dd = run("pmc_ta", ["--pmc"] + grp, target=RAYPMC)
+    counts_path = os.path.join(OUT, "ray_counts_pmc_ta.json")
+    dd = run("pmc_ta", ["--pmc"] + grp, target=RAYPMC, env_extra={"RAY_PMC_COUNTS": counts_path})
     ta = counters(dd, os.path.join(PROF, f"{tag}_pmc_ta.csv"))
+    if os.path.exists(counts_path):  # the kernel's own count of its wave-level loads, same launches
+        kc = json.load(open(counts_path))
+        busy["kernel_counted_loads_per_launch"] = kc["vmem_loads_per_launch"]
+        busy["kernel_counted_slot_gathers_per_launch"] = kc["slot_gathers_per_launch"]
+        busy["kernel_counted_other_loads_per_launch"] = kc["other_loads_per_launch"]
+        busy["vmem_rd_vs_kernel_counted"] = ta["SQ_INSTS_VMEM_RD"] / max(1.0, kc["vmem_loads_per_launch"])
     cyc = ta["GRBM_GUI_ACTIVE"] / 8.0
     busy["vmem_rd_per_launch"] = ta["SQ_INSTS_VMEM_RD"]
     busy["ta_flat_read_wavefronts"] = ta["TA_FLAT_READ_WAVEFRONTS_sum"]

@@ -19,7 +19,22 @@ sim.reset(sp[rng.integers(0, sp.shape[0], E)])
 g = torch.Generator(device="cuda"); g.manual_seed(0)
 acts = torch.rand(100, E, A, 2, device="cuda", generator=g)
 acts[..., 0] = acts[..., 0] * 0.8378 - 0.4189; acts[..., 1] *= 20
+# RAY_PMC_COUNTS=<path>: the same launches also keep the kernel's own load counters (lane slots of
+# the loop's gathers, counter 3 = its other wave-level loads; returnless lane-0 atomics, no reads),
+# written to <path> beside the PMC pass that counts SQ_INSTS_VMEM_RD on them
+counts = os.environ.get("RAY_PMC_COUNTS")
+if counts:
+    sim.set_simt(True)
+    sim.reset_counters()
 for k in range(100):
     sim.step(acts[k], minimal_outputs=True)
 torch.cuda.synchronize()
+if counts:
+    import json
+    _, slots = sim.read_simt()
+    other = sim.read_counter(3)
+    with open(counts, "w") as f:
+        json.dump({"envs": E, "agents": A, "launches": 100, "slot_gathers_per_launch": slots / 64.0 / 100,
+                   "other_loads_per_launch": other / 100.0, "vmem_loads_per_launch": (slots / 64.0 + other) / 100},
+                  f)
 print("done")

@@ -276,3 +276,69 @@ def test_flat_adam_matches_torch_adam(gpu):
     torch.testing.assert_close(tgt.cpu(), tgt_ref, rtol=2e-6, atol=1e-7)
     torch.testing.assert_close(dev.cpu(), ref.detach(), rtol=2e-6, atol=1e-7)
     torch.testing.assert_close(m.cpu(), opt.state[ref]["exp_avg"], rtol=1e-5, atol=1e-7)  # CPU lerp may fuse (1 ulp)
+
+
+def test_replay_add_env_matches_add(gpu):
+    """add_env (f110_replay_add_env: float64 rewards, uint8 terminated and
+    was_reset as the simulator writes them, reset rows skipped) stores the
+    same rows, in the same ring slots, as add() with the torch conversions
+    train_ddpg used (rew.to(float32), mask = ~reset); strided action rows."""
+    D, A = 1088, 2
+    g = torch.Generator(device="cuda").manual_seed(4)
+    S = torch.rand(90, D, device="cuda", generator=g)
+    S2 = torch.rand(90, D, device="cuda", generator=g)
+    act_rows = torch.rand(90, 2, A, device="cuda", generator=g)  # [env, agent, 2]: agent 1's rows are strided
+    Ac = act_rows[:, 1]
+    R64 = torch.randn(90, device="cuda", generator=g, dtype=torch.float64) * 3.0
+    term = (torch.rand(90, device="cuda", generator=g) < 0.3).to(torch.uint8)
+    reset = (torch.rand(90, device="cuda", generator=g) < 0.25).to(torch.uint8)
+    ra, rb = _rb(128, 32, D=D, A=A, max_add=64), _rb(128, 32, D=D, A=A, max_add=64)
+    for _ in range(2):  # the second pass wraps the ring
+        ra.add(S, Ac, R64.to(torch.float32), S2, term.bool(), mask=~reset.bool())
+        rb.add_env(S, Ac, R64, S2, term, reset)
+    assert len(ra) == len(rb)
+    xa, xb = ra.arrays(), rb.arrays()
+    for k in xa:
+        torch.testing.assert_close(xb[k], xa[k], rtol=0, atol=0, msg=k)
+    ra.close()
+    rb.close()
+
+
+def test_actor_explore_head(gpu):
+    """f110_ddpg_actor_explore (choose_action(training=True) on the explicit
+    path): sigma = 0 gives the actor head's actions clipped to the bounds;
+    sigma > 0 adds N(0, sigma^2) noise (mean / std of act - actor over 65536
+    x 2 draws within 4 standard errors, the two outputs uncorrelated), the
+    result inside [low, high], written into a strided view; the same (seed,
+    step) repeats, the next step draws anew."""
+    from f110_gymnasium_ros2_jazzy_amd.ddpg import DDPGLearner
+    ln = DDPGLearner(obs_dim=64, act_dim=2, action_low=[-0.4189, 0.0], action_high=[0.4189, 20.0], seed=9,
+                     device="cuda:0", replay=None)
+    if ln.explicit is None:
+        pytest.skip("explicit learner path not supported here")
+    M = 65536
+    g = torch.Generator(device="cuda").manual_seed(2)
+    S = torch.randn(M, 64, device="cuda", generator=g) * 0.1
+    base = ln.choose_action(S, training=False).clone()
+    lo, hi = ln._low32, ln._high32
+    buf = torch.full((M, 3, 2), float("nan"), device="cuda")
+    out = buf[:, 1]
+    ex = ln.explicit
+    a0 = ex.policy(ln.actor, S, explore=(0.0, lo, hi, 7, 0, out))
+    assert a0.data_ptr() == out.data_ptr()
+    torch.testing.assert_close(a0, torch.minimum(torch.maximum(base, lo), hi), rtol=0, atol=0)
+    assert bool(torch.isnan(buf[:, 0]).all()) and bool(torch.isnan(buf[:, 2]).all())  # nothing else written
+    sigma = 1e-3  # small enough that almost no row reaches a bound
+    a1 = ex.policy(ln.actor, S, explore=(sigma, lo, hi, 7, 5, None)).clone()
+    a1b = ex.policy(ln.actor, S, explore=(sigma, lo, hi, 7, 5, None)).clone()
+    a2 = ex.policy(ln.actor, S, explore=(sigma, lo, hi, 7, 6, None)).clone()
+    torch.testing.assert_close(a1, a1b, rtol=0, atol=0)
+    assert not torch.equal(a1, a2)
+    assert bool(((a1 >= lo) & (a1 <= hi)).all())
+    inside = ((base > lo + 10 * sigma) & (base < hi - 10 * sigma)).all(1)
+    n = (a1 - base)[inside].double() / sigma
+    assert n.shape[0] > M // 2
+    se = 1.0 / n.shape[0] ** 0.5
+    assert float(n.mean(0).abs().max()) < 4 * se
+    assert float((n.std(0) - 1.0).abs().max()) < 4 * se * 0.75 + 0.01
+    assert abs(float((n[:, 0] * n[:, 1]).mean())) < 4 * se
