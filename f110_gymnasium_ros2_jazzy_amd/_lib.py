@@ -183,8 +183,8 @@ def load(build_if_missing: bool = True):
     f32 = ctypes.c_float
     L.f110_ddpg_scratch_floats.argtypes = [i32, i32, i32]
     L.f110_ddpg_actor_head.argtypes = [_P] * 5 + [i32] * 3 + [_P] * 3
-    L.f110_ddpg_actor_explore.argtypes = [_P] * 5 + [i32] * 3 + [f32, _P, _P, ctypes.c_uint64, ctypes.c_uint64, _P,
-                                                                  i64, _P]
+    L.f110_ddpg_actor_explore.argtypes = [_P] * 5 + [i32] * 3 + [_P, _P, ctypes.c_double, ctypes.c_double, _P, _P,
+                                                                  ctypes.c_uint64, _P, i64, _P]
     L.f110_ddpg_actor_head_bwd.argtypes = [_P] * 5 + [i32] * 3 + [_P] * 6
     L.f110_ddpg_td_target.argtypes = [_P] * 5 + [f32, i32, i32, _P, _P]
     L.f110_ddpg_critic_loss.argtypes = [_P] * 5 + [i32] * 2 + [_P] * 4

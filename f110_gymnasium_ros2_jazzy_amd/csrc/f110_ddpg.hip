@@ -49,11 +49,14 @@ struct HeadArgs {
     float *loss;
     float gamma, sign;
     int32_t B, K, nout, nblk;
-    // kExplore: out0[row * out_stride + j] = clamp(act + sigma N(0,1), lo[j], hi[j])
+    // kExplore: out0[row * out_stride + j] = clamp(act + sigma N(0,1), lo[j], hi[j]); (sigma, call) from
+    // nstate_in, the decayed pair to nstate_out (block 0, thread 0)
     const float *lo, *hi;
-    float sigma;
+    const double *nstate_in;
+    double *nstate_out;
+    double decay, sigma_min;
     int64_t out_stride;
-    uint64_t seed, step;
+    uint64_t seed;
 };
 
 // choose_action's exploration noise (agent.py:350-370, GaussianActionNoise
@@ -136,14 +139,16 @@ __global__ void __launch_bounds__(kHB) k_head_fwd(HeadArgs a) {
                     a.out0[row * NOUT + j] = a.aux0[j] * t + a.aux1[j];
                 }
             } else if (MODE == kExplore) {  // the action, + sigma N(0,1), clipped to [low, high] (NaN kept)
+                const float sigma = (float)a.nstate_in[0];
+                const uint64_t step = (uint64_t)a.nstate_in[1];
 #pragma unroll
                 for (int j = 0; j < NOUT; j += 2) {
-                    const float2 nz = explore_normals(a.seed, a.step, row, j >> 1);
+                    const float2 nz = explore_normals(a.seed, step, row, j >> 1);
 #pragma unroll
                     for (int q = 0; q < 2; ++q) {
                         if (j + q >= NOUT) break;
                         const float act = a.aux0[j + q] * tanhf(z[j + q]) + a.aux1[j + q];
-                        float v = act + a.sigma * (q == 0 ? nz.x : nz.y);
+                        float v = act + sigma * (q == 0 ? nz.x : nz.y);
                         v = v < a.lo[j + q] ? a.lo[j + q] : v;
                         v = v > a.hi[j + q] ? a.hi[j + q] : v;
                         a.out0[row * a.out_stride + j + q] = v;
@@ -164,6 +169,11 @@ __global__ void __launch_bounds__(kHB) k_head_fwd(HeadArgs a) {
     if (MODE == kLoss || MODE == kMean) {
         const float s = block_sum(v);
         if (threadIdx.x == 0) a.part[blockIdx.x] = s;
+    }
+    if (MODE == kExplore && blockIdx.x == 0 && threadIdx.x == 0) {  // GaussianActionNoise.__call__'s decay
+        const double sg = a.nstate_in[0] * a.decay;
+        a.nstate_out[0] = sg > a.sigma_min ? sg : a.sigma_min;  // max(sigma * decay, sigma_min)
+        a.nstate_out[1] = a.nstate_in[1] + 1.0;
     }
 }
 
@@ -468,14 +478,17 @@ extern "C" int f110_ddpg_actor_head(const float *h, const float *W, const float 
 }
 
 extern "C" int f110_ddpg_actor_explore(const float *h, const float *W, const float *b, const float *scale,
-                                       const float *shift, int32_t B, int32_t K, int32_t nout, float sigma,
-                                       const float *low, const float *high, uint64_t seed, uint64_t step, float *out,
+                                       const float *shift, int32_t B, int32_t K, int32_t nout,
+                                       const double *state_in, double *state_out, double decay, double sigma_min,
+                                       const float *low, const float *high, uint64_t seed, float *out,
                                        int64_t out_stride, void *stream) {
-    if (bad_shape(B, K, nout) || !h || !W || !b || !scale || !shift || !low || !high || !out || out_stride < nout)
+    if (bad_shape(B, K, nout) || !h || !W || !b || !scale || !shift || !state_in || !state_out ||
+        state_in == state_out || !low || !high || !out || out_stride < nout)
         return fail_arg("f110_ddpg_actor_explore");
     HeadArgs a{};
     a.h = h, a.W = W, a.b = b, a.aux0 = scale, a.aux1 = shift, a.out0 = out;
-    a.lo = low, a.hi = high, a.sigma = sigma, a.out_stride = out_stride, a.seed = seed, a.step = step;
+    a.lo = low, a.hi = high, a.nstate_in = state_in, a.nstate_out = state_out, a.decay = decay;
+    a.sigma_min = sigma_min, a.out_stride = out_stride, a.seed = seed;
     a.B = B, a.K = K, a.nout = nout;
     hipError_t e = with_nout(nout, [&](auto N) {
         hipLaunchKernelGGL((k_head_fwd<kExplore, decltype(N)::value>), dim3(row_blocks(B)), dim3(kHB), 0,

@@ -402,6 +402,12 @@ class DDPGLearner:
         self._high32 = self._high.to(torch.float32).contiguous()
         self._noise_key = (int(seed) * 1000003 + (dist.get_rank() if self.distributed else 0)) & ((1 << 64) - 1)
         self._noise_calls = 0
+        # (sigma, call index) on the device in two f64 slots: a call reads slot _noise_slot and writes
+        # the decayed pair to the other (so a captured step graph can replay it); the host mirrors the
+        # same double arithmetic in self.sigma / self._noise_calls
+        self._noise_state = torch.tensor([[self.sigma, 0.0]] * 2, dtype=torch.float64, device=self.device)
+        self._noise_slot = 0
+        self._noise_dev = (self.sigma, 0)  # what the current slot holds
         self._ready = False
         self.global_step = 0
 
@@ -593,10 +599,14 @@ class DDPGLearner:
         with torch.no_grad(), TunedGemms(self.tuned_gemms):
             o = torch.as_tensor(obs, device=self.device, dtype=torch.float32)
             if self.explicit is not None and training and o.dim() == 2:
-                a = self.explicit.policy(self.actor, o, explore=(self.sigma, self._low32, self._high32,
-                                                                 self._noise_key, self._noise_calls, out))
-                self._noise_calls += 1
-                self.sigma = max(self.sigma * self.noise_decay, self.sigma_min)
+                s = self._noise_slot
+                if self._noise_dev != (self.sigma, self._noise_calls):  # the host changed sigma: upload it
+                    self._noise_state[s, 0] = self.sigma
+                    self._noise_state[s, 1] = float(self._noise_calls)
+                a = self.explicit.policy(self.actor, o, explore=(
+                    self._noise_state[s], self._noise_state[1 - s], self.noise_decay, self.sigma_min, self._low32,
+                    self._high32, self._noise_key, out))
+                self.noise_advance()
                 return a
             if self.explicit is not None:
                 a = self.explicit.policy(self.actor, o if o.dim() == 2 else o.unsqueeze(0))
@@ -610,6 +620,15 @@ class DDPGLearner:
             out.copy_(a)
             return out
         return a
+
+    def noise_advance(self):
+        """The host mirror of one explicit training choose_action: the device
+        slot flips and the pair decays as f110_ddpg_actor_explore decays it (a
+        replayed step graph calls this per replay)."""
+        self._noise_calls += 1
+        self.sigma = max(self.sigma * self.noise_decay, self.sigma_min)
+        self._noise_slot ^= 1
+        self._noise_dev = (self.sigma, self._noise_calls)
 
     def hard_update(self):
         self.actor_target.load_state_dict(self.actor.state_dict())

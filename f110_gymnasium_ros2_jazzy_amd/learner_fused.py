@@ -150,9 +150,12 @@ class ExplicitUpdate:
 
     def policy(self, actor, obs, explore=None):
         """Actor.forward without autograd (choose_action): fc1, fc2, head.
-        explore = (sigma, low, high, seed, step, out): the head adds
-        sigma * N(0, 1) and clips to [low, high] (f110_ddpg_actor_explore), writing
-        the actions into out (rows may be strided), which is returned."""
+        explore = (state_in, state_out, decay, sigma_min, low, high, seed, out):
+        the head adds sigma * N(0, 1) and clips to [low, high]
+        (f110_ddpg_actor_explore; sigma and the call index from the f64 device
+        pair state_in, the decayed pair written to state_out), writing the
+        actions into out (rows may be strided; None: a new tensor), which is
+        returned."""
         obs = obs.contiguous()
         M = obs.shape[0]
         h1, h2 = self._e(M), self._e(M)
@@ -160,7 +163,7 @@ class ExplicitUpdate:
         lg.gemm([self._fwd(h1, actor.fc2, h2)], M, obs.device)
         if explore is None:
             return self._actor_head(actor, h2)[0]
-        sigma, low, high, seed, step, out = explore
+        st_in, st_out, decay, sigma_min, low, high, seed, out = explore
         W, b = actor.fc3.weight, actor.fc3.bias
         scale, shift = actor._affine()
         n = W.shape[0]
@@ -169,6 +172,7 @@ class ExplicitUpdate:
         if out.shape != (M, n) or out.stride(1) != 1 or out.dtype != torch.float32:
             raise ValueError("policy: out must be [M, act_dim] float32 with unit column stride")
         _lib.check(self.L.f110_ddpg_actor_explore(_p(h2), _p(W), _p(b), _p(scale), _p(shift), M, h2.shape[1], n,
-                                                  float(sigma), _p(low), _p(high), int(seed), int(step), _p(out),
-                                                  out.stride(0), _stream(h2)), "f110_ddpg_actor_explore")
+                                                  _p(st_in), _p(st_out), float(decay), float(sigma_min), _p(low),
+                                                  _p(high), int(seed), _p(out), out.stride(0), _stream(h2)),
+                   "f110_ddpg_actor_explore")
         return out

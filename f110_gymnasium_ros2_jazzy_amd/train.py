@@ -61,6 +61,13 @@ class VectorTrainer:
                                  max_add=self.N, graphs=graphs)
         self.warmup = int(warmup_steps)
         self.updates_per_step = int(updates_per_step)
+        # one HIP graph per vector step once the learner's eager warm-up updates are done (one rank,
+        # explicit learner, one update per step): two graphs, even / odd steps, which swap the two
+        # fixed observation buffers and the learner's two noise-state slots
+        self.step_graphs = bool(graphs) and os.environ.get("F110_STEP_GRAPH", "1") != "0"
+        self._sg = [None, None]
+        self._sg_parity = 0
+        self._sg_obs = None
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(seed * 1000003 + rank_seed)
         self._low = torch.tensor(ACTION_LOW, device=self.device)
@@ -76,6 +83,8 @@ class VectorTrainer:
         if self.global_step < self.warmup:  # :162-163
             u = torch.rand(self.N, 2, generator=self._gen, device=self.device)
             act = self._low + u * (self._high - self._low)
+        elif self._graph_ready():
+            return self._step_graphed()
         else:  # the actions land in the env's action rows (no copy in the step)
             act = self.agent.choose_action(self.obs, training=True, out=self.env.agent_actions())
         next_obs, rew, term, was_reset = self.env.step_transition(act)
@@ -89,6 +98,56 @@ class VectorTrainer:
         self.obs = next_obs
         self.global_step += 1
         return rew, term
+
+    def _graph_ready(self) -> bool:
+        ag = self.agent
+        return (self.step_graphs and not ag.distributed and ag.explicit is not None and ag.graphs and
+                self.updates_per_step == 1 and ag._ready and ag._eager_left == 0 and ag._graphs is None and
+                self.env.agent_actions() is not None)
+
+    def _body(self, obs_in, obs_out):
+        """One vector step after the warm-up, as captured: choose_action (noise in
+        the head launch), env step + reward, replay add, the learner update's
+        three phases (one rank: no all-reduce between them)."""
+        ag = self.agent
+        act = ag.choose_action(obs_in, training=True, out=self.env.agent_actions())
+        nxt, rew, term, was_reset = self.env.step_transition(act, obs_out=obs_out)
+        ag.remember_env(obs_in, act, rew, nxt, term, was_reset)
+        for ph in self._sg_phases:
+            ph()
+        return rew, term
+
+    def _step_graphed(self):
+        """step() as a replay of the parity's captured graph (captured on its
+        first use; the capture runs the Python side once, which is this step's
+        host bookkeeping; later replays repeat that bookkeeping here)."""
+        ag = self.agent
+        p = self._sg_parity
+        if self._sg_obs is None:
+            self._sg_obs = [torch.empty_like(self.obs), torch.empty_like(self.obs)]
+            self._sg_pool = torch.cuda.graph_pool_handle()
+            self._sg_phases, self._sg_out = ag._graph_phases()
+        bufs = self._sg_obs
+        if self.obs.data_ptr() != bufs[p].data_ptr():
+            bufs[p].copy_(self.obs)
+        if self._sg[p] is None:
+            g = torch.cuda.CUDAGraph()
+            cur = torch.cuda.current_stream(self.device)
+            ag._side.wait_stream(cur)
+            with torch.cuda.graph(g, pool=self._sg_pool, stream=ag._side):
+                self._sg_ret = self._body(bufs[p], bufs[1 - p])
+            cur.wait_stream(ag._side)
+            self._sg[p] = g
+        else:  # what the capture's Python side did once
+            ag.noise_advance()
+            ag.memory._added += self.N
+        self._sg[p].replay()
+        ag.global_step += 1
+        self.last = self._sg_out
+        self.obs = bufs[1 - p]
+        self._sg_parity ^= 1
+        self.global_step += 1
+        return self._sg_ret
 
     def close(self):
         self.env.close()

@@ -176,11 +176,13 @@ class F110VectorEnv:
             return None
         return self._act[:, self._others[0]]
 
-    def step_transition(self, actions):
+    def step_transition(self, actions, obs_out=None):
         """step() for a trainer on the device: (next_obs copy [N, obs_dim],
         rewards float64 [N], terminated uint8 [N], was_reset uint8 [N]).  The
         rewards and flags are the simulator's / reward function's own buffers
-        (no clone, no dtype conversion): valid until the next step."""
+        (no clone, no dtype conversion): valid until the next step.  obs_out:
+        a preallocated [N, obs_dim] float32 tensor to copy next_obs into (a
+        captured step graph's fixed buffer) instead of a new one."""
         if self.as_numpy:
             raise ValueError("step_transition: device tensors only (as_numpy=False)")
         a = torch.as_tensor(actions, device=self.device)
@@ -198,7 +200,11 @@ class F110VectorEnv:
         else:
             rewards = torch.where(out.was_reset.bool(), torch.zeros((), dtype=torch.float64, device=self.device),
                                   torch.full((), self.timestep, dtype=torch.float64, device=self.device))
-        return out.obs.clone(), rewards, out.terminated, out.was_reset
+        if obs_out is None:
+            obs_out = out.obs.clone()
+        else:
+            obs_out.copy_(out.obs)
+        return obs_out, rewards, out.terminated, out.was_reset
 
     def close(self):
         if getattr(self, "sim", None) is not None:

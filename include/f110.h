@@ -558,12 +558,15 @@ F110_API int f110_ddpg_actor_head(const float *h, const float *W, const float *b
 /* choose_action(training=True) after the hidden layers (agent.py:350-370 with
  * GaussianActionNoise :520-539): out[row * out_stride + j] = clip(scale * tanh(h W^T + b) + shift
  * + sigma * n, low[j], high[j]), n ~ N(0, 1) independent per (row, j) and per call (Philox2x32
- * keyed by seed, counter step: a new step per call); NaN actions stay NaN.  out may be a strided
- * view (e.g. the vector env's action rows). */
+ * keyed by seed, counter = the call index); NaN actions stay NaN.  The noise state lives on the
+ * device so a captured graph can replay the call: state_in = {sigma, call index} (f64), and the
+ * launch writes state_out = {max(sigma * decay, sigma_min), call index + 1} (state_out !=
+ * state_in: callers alternate two slots).  out may be a strided view (e.g. the vector env's
+ * action rows). */
 F110_API int f110_ddpg_actor_explore(const float *h, const float *W, const float *b, const float *scale,
-                                     const float *shift, int32_t B, int32_t K, int32_t nout, float sigma,
-                                     const float *low, const float *high, uint64_t seed, uint64_t step, float *out,
-                                     int64_t out_stride, void *stream);
+                                     const float *shift, int32_t B, int32_t K, int32_t nout, const double *state_in,
+                                     double *state_out, double decay, double sigma_min, const float *low,
+                                     const float *high, uint64_t seed, float *out, int64_t out_stride, void *stream);
 /* dz = (dact * scale) * (1 - t*t); dh = dz W; dW = dz^T h; db = sum_rows dz */
 F110_API int f110_ddpg_actor_head_bwd(const float *h, const float *W, const float *t, const float *scale,
                                       const float *dact, int32_t B, int32_t K, int32_t nout, float *dh,

@@ -309,11 +309,12 @@ def test_actor_explore_head(gpu):
     path): sigma = 0 gives the actor head's actions clipped to the bounds;
     sigma > 0 adds N(0, sigma^2) noise (mean / std of act - actor over 65536
     x 2 draws within 4 standard errors, the two outputs uncorrelated), the
-    result inside [low, high], written into a strided view; the same (seed,
-    step) repeats, the next step draws anew."""
+    result inside [low, high], written into a strided view; the same (sigma,
+    call index) repeats, the next call index draws anew; the launch writes the
+    decayed (sigma, call + 1) pair, and choose_action's host mirror follows it."""
     from f110_gymnasium_ros2_jazzy_amd.ddpg import DDPGLearner
     ln = DDPGLearner(obs_dim=64, act_dim=2, action_low=[-0.4189, 0.0], action_high=[0.4189, 20.0], seed=9,
-                     device="cuda:0", replay=None)
+                     device="cuda:0", replay=None, noise_sigma_start=0.2, noise_sigma_min=0.02, noise_decay=0.9)
     if ln.explicit is None:
         pytest.skip("explicit learner path not supported here")
     M = 65536
@@ -324,14 +325,21 @@ def test_actor_explore_head(gpu):
     buf = torch.full((M, 3, 2), float("nan"), device="cuda")
     out = buf[:, 1]
     ex = ln.explicit
-    a0 = ex.policy(ln.actor, S, explore=(0.0, lo, hi, 7, 0, out))
+
+    def st(sigma, call):
+        return torch.tensor([sigma, float(call)], dtype=torch.float64, device="cuda")
+
+    nxt = torch.zeros(2, dtype=torch.float64, device="cuda")
+    a0 = ex.policy(ln.actor, S, explore=(st(0.0, 0), nxt, 0.5, 0.01, lo, hi, 7, out))
     assert a0.data_ptr() == out.data_ptr()
     torch.testing.assert_close(a0, torch.minimum(torch.maximum(base, lo), hi), rtol=0, atol=0)
     assert bool(torch.isnan(buf[:, 0]).all()) and bool(torch.isnan(buf[:, 2]).all())  # nothing else written
+    assert nxt.tolist() == [0.01, 1.0]  # max(0 * 0.5, 0.01), call + 1
     sigma = 1e-3  # small enough that almost no row reaches a bound
-    a1 = ex.policy(ln.actor, S, explore=(sigma, lo, hi, 7, 5, None)).clone()
-    a1b = ex.policy(ln.actor, S, explore=(sigma, lo, hi, 7, 5, None)).clone()
-    a2 = ex.policy(ln.actor, S, explore=(sigma, lo, hi, 7, 6, None)).clone()
+    a1 = ex.policy(ln.actor, S, explore=(st(sigma, 5), nxt, 0.5, 0.0, lo, hi, 7, None)).clone()
+    assert nxt.tolist() == [sigma * 0.5, 6.0]
+    a1b = ex.policy(ln.actor, S, explore=(st(sigma, 5), nxt, 0.5, 0.0, lo, hi, 7, None)).clone()
+    a2 = ex.policy(ln.actor, S, explore=(st(sigma, 6), nxt, 0.5, 0.0, lo, hi, 7, None)).clone()
     torch.testing.assert_close(a1, a1b, rtol=0, atol=0)
     assert not torch.equal(a1, a2)
     assert bool(((a1 >= lo) & (a1 <= hi)).all())
@@ -342,3 +350,43 @@ def test_actor_explore_head(gpu):
     assert float(n.mean(0).abs().max()) < 4 * se
     assert float((n.std(0) - 1.0).abs().max()) < 4 * se * 0.75 + 0.01
     assert abs(float((n[:, 0] * n[:, 1]).mean())) < 4 * se
+    # choose_action: the device pair and the host mirror decay together
+    for k in range(3):
+        ln.choose_action(S[:256], training=True)
+        torch.cuda.synchronize()
+        dev = ln._noise_state[ln._noise_slot].tolist()
+        assert dev == [ln.sigma, float(ln._noise_calls)] and ln._noise_calls == k + 1
+    sg = 0.2
+    for _ in range(3):
+        sg = max(sg * 0.9, 0.02)
+    assert ln.sigma == sg
+
+
+def test_trainer_step_graphs_match_eager(gpu, monkeypatch):
+    """VectorTrainer's whole-step graphs (two captured vector steps, even / odd,
+    replayed after the learner's eager warm-up updates) against the same loop
+    run eagerly (F110_STEP_GRAPH=0): after 14 steps the actor / critic weights,
+    the replay ring, the noise state and the last losses are bit-identical."""
+    from f110_gymnasium_ros2_jazzy_amd.train import VectorTrainer
+    runs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("F110_STEP_GRAPH", flag)
+        tr = VectorTrainer(256, batch_size=256, memory_size=4096, warmup_steps=3, seed=11)
+        for _ in range(14):
+            tr.step()
+        torch.cuda.synchronize()
+        assert (tr._sg[0] is not None and tr._sg[1] is not None) == (flag == "1")
+        ag = tr.agent
+        params = [p.detach().clone() for p in list(ag.actor.parameters()) + list(ag.critic.parameters())]
+        n = len(ag.memory)  # rows past the length were never written
+        ring = {k: v[:n].clone() for k, v in ag.memory.arrays().items()}
+        runs.append((params, ring, float(tr.last["critic_loss"]), float(tr.last["actor_loss"]), ag.sigma,
+                     ag._noise_calls, tr.obs.clone(), len(ag.memory), ag.global_step))
+        tr.close()
+    (pa, ra, ca, aa, sa, na, oa, la, ga), (pb, rb_, cb, ab, sb, nb, ob, lb, gb) = runs
+    for x, y in zip(pa, pb):
+        assert torch.equal(x, y)
+    for k in ra:
+        assert torch.equal(ra[k], rb_[k]), k
+    assert (ca, aa, sa, na, la, ga) == (cb, ab, sb, nb, lb, gb)
+    assert torch.equal(oa, ob)
