@@ -77,7 +77,8 @@ EXPORTS = [
     "f110_dynamics_ks_batch", "f110_collision_batch", "f110_collision_multiple", "f110_adam_step", "f110_ddpg_scratch_floats", "f110_ddpg_actor_head", "f110_ddpg_actor_explore",
     "f110_ddpg_actor_head_bwd", "f110_ddpg_td_target", "f110_ddpg_critic_loss", "f110_ddpg_critic_loss_bwd",
     "f110_ddpg_q_mean", "f110_ddpg_q_mean_bwd", "f110_ddpg_relu_bwd_scratch_floats", "f110_ddpg_relu_bwd",
-    "f110_learner_gemm", "f110_learner_wgrad_scratch_floats", "f110_learner_wgrad",
+    "f110_learner_gemm", "f110_learner_wgrad_scratch_floats", "f110_learner_wgrad", "f110_learner_wgrad_loss",
+    "f110_ddpg_critic_step", "f110_ddpg_q_mean_step", "f110_ddpg_row_blocks",
 ]
 
 _lib = None
@@ -196,6 +197,11 @@ def load(build_if_missing: bool = True):
     L.f110_learner_gemm.argtypes = [ctypes.POINTER(F110GemmOp), i32, i32, _P]
     L.f110_learner_wgrad_scratch_floats.argtypes = [ctypes.POINTER(F110WgradOp), i32, i32]
     L.f110_learner_wgrad.argtypes = [ctypes.POINTER(F110WgradOp), i32, i32, _P, _P]
+    L.f110_learner_wgrad_loss.argtypes = [ctypes.POINTER(F110WgradOp), i32, i32, _P, _P, i32, f32, _P, _P]
+    L.f110_ddpg_critic_step.argtypes = [_P] * 5 + [f32] + [_P] * 5 + [i32, i32] + [_P] * 6
+    L.f110_ddpg_q_mean_step.argtypes = [_P] * 4 + [f32, i32, i32] + [_P] * 4
+    L.f110_ddpg_row_blocks.argtypes = [i32]
+    L.f110_ddpg_row_blocks.restype = i32
     for name in EXPORTS:
         if name not in ("f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config",
                         "f110_host_np_sincosf", "f110_host_sincos",

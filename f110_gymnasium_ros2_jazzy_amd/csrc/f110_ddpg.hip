@@ -39,6 +39,7 @@ enum HeadMode { kActor = 0, kTarget = 1, kLoss = 2, kMean = 3, kExplore = 4 };
 
 struct HeadArgs {
     const float *h, *W, *b;
+    const float *ht, *Wt, *bt;  // k_critic_step: the target critic's last hidden layer and head
     const float *aux0, *aux1;  // actor: scale, shift; target: r, d; loss: y, w
     const float *t, *dout, *g;  // backward: tanh output, upstream grad [B][nout], loss grad (device scalar)
     float *out0, *out1;         // actor: a, t; target: y; loss: td
@@ -85,27 +86,57 @@ __device__ __forceinline__ float half_sum(float v) {
 // z[j] = b[j] + sum_k h[k] W[j][k] for the row of this half-wave: lane l
 // takes columns 4l..4l+3 (+128, +256 ...), then a half-wave sum
 template <int NOUT>
-__device__ __forceinline__ void row_dot(const HeadArgs &a, int64_t row, int l, float (&z)[NOUT]) {
-    const float *hr = a.h + row * a.K;
+__device__ __forceinline__ void row_dot_of(const float *h, const float *W, const float *b, int32_t K, int64_t row,
+                                           int l, float (&z)[NOUT]) {
+    const float *hr = h + row * K;
 #pragma unroll
     for (int j = 0; j < NOUT; ++j) z[j] = 0.0f;
-    for (int k = 4 * l; k < a.K; k += 4 * kRowLanes) {
+    for (int k = 4 * l; k < K; k += 4 * kRowLanes) {
         float x[4];
-        if ((a.K & 3) == 0) {
+        if ((K & 3) == 0) {
             const float4 v = *reinterpret_cast<const float4 *>(hr + k);
             x[0] = v.x, x[1] = v.y, x[2] = v.z, x[3] = v.w;
         } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) x[i] = k + i < a.K ? hr[k + i] : 0.0f;
+            for (int i = 0; i < 4; ++i) x[i] = k + i < K ? hr[k + i] : 0.0f;
         }
 #pragma unroll
         for (int j = 0; j < NOUT; ++j)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-                if (k + i < a.K) z[j] = fmaf(x[i], a.W[(size_t)j * a.K + k + i], z[j]);
+                if (k + i < K) z[j] = fmaf(x[i], W[(size_t)j * K + k + i], z[j]);
     }
 #pragma unroll
-    for (int j = 0; j < NOUT; ++j) z[j] = half_sum(z[j]) + a.b[j];  // addmm: bias added to the product
+    for (int j = 0; j < NOUT; ++j) z[j] = half_sum(z[j]) + b[j];  // addmm: bias added to the product
+}
+
+template <int NOUT>
+__device__ __forceinline__ void row_dot(const HeadArgs &a, int64_t row, int l, float (&z)[NOUT]) {
+    row_dot_of<NOUT>(a.h, a.W, a.b, a.K, row, l, z);
+}
+
+// dh[row] = dz W (lane l: columns 4l..4l+3, +128 ...), zero where dh_mask <= 0
+template <int NOUT>
+__device__ __forceinline__ void write_dh(const HeadArgs &a, int64_t row, int l, const float (&dz)[NOUT]) {
+    float *o = a.dh + row * a.K;
+    for (int k = 4 * l; k < a.K; k += 4 * kRowLanes) {
+        float r4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float s = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NOUT; ++j)
+                if (k + i < a.K) s = fmaf(dz[j], a.W[(size_t)j * a.K + k + i], s);
+            r4[i] = a.dh_mask && k + i < a.K && !(a.dh_mask[row * a.K + k + i] > 0.0f) ? 0.0f : s;
+        }
+        if ((a.K & 3) == 0) {
+            *reinterpret_cast<float4 *>(o + k) = make_float4(r4[0], r4[1], r4[2], r4[3]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (k + i < a.K) o[k + i] = r4[i];
+        }
+    }
 }
 
 // deterministic block sum (fixed shuffle tree per wave, waves in order); thread 0 gets it
@@ -177,6 +208,55 @@ __global__ void __launch_bounds__(kHB) k_head_fwd(HeadArgs a) {
     }
 }
 
+// The critic update's head in one launch (agent.py:302-319): per row (one
+// half-wave) the TD target y = r + gamma (1 - d) (ht Wt^T + bt) (k_head_fwd
+// kTarget), td = y - (h W^T + b) and w td^2 (kLoss: block partials for the
+// loss), and its backward (k_head_bwd_rows kLoss): dq = -((g / B) w) (2 td),
+// dh = dq W where dh_mask > 0.  The same float operations in the same order as
+// the three separate launches.  aux0 = r, aux1 = d, aux2 (w) in `dout`.
+__global__ void __launch_bounds__(kHB) k_critic_step(HeadArgs a) {
+    const int l = threadIdx.x & (kRowLanes - 1);
+    const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x / kRowLanes);
+    float v = 0.0f;
+    if (row < a.B) {
+        float zt[1], z[1];
+        row_dot_of<1>(a.ht, a.Wt, a.bt, a.K, row, l, zt);
+        row_dot<1>(a, row, l, z);
+        const float gd = a.gamma * (1.0f - a.aux1[row]);
+        const float y = a.aux0[row] + gd * zt[0];
+        const float td = y - z[0];
+        const float w = a.dout[row];
+        if (l == 0) {
+            a.out0[row] = td;
+            v = w * (td * td);
+        }
+        const float gb = *a.g / (float)a.B;
+        const float dz[1] = {-((gb * w) * (2.0f * td))};
+        if (a.dz && l == 0) a.dz[row] = dz[0];
+        if (a.dh) write_dh<1>(a, row, l, dz);
+    }
+    const float s = block_sum(v);
+    if (threadIdx.x == 0) a.part[blockIdx.x] = s;
+}
+
+// The actor update's loss head (agent.py:321-326): q = h W^T + b, block
+// partials of q (k_head_fwd kMean) and the backward through the frozen
+// critic (k_head_bwd_rows kMean): dq = sign g / B, dh = dq W where dh_mask > 0.
+__global__ void __launch_bounds__(kHB) k_q_mean_step(HeadArgs a) {
+    const int l = threadIdx.x & (kRowLanes - 1);
+    const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x / kRowLanes);
+    float v = 0.0f;
+    if (row < a.B) {
+        float z[1];
+        row_dot<1>(a, row, l, z);
+        if (l == 0) v = z[0];
+        const float dz[1] = {a.sign * (*a.g / (float)a.B)};
+        if (a.dh) write_dh<1>(a, row, l, dz);
+    }
+    const float s = block_sum(v);
+    if (threadIdx.x == 0) a.part[blockIdx.x] = s;
+}
+
 // loss = sign * (sum of the block partials, in block order) / B
 __global__ void __launch_bounds__(kHB) k_loss_finish(HeadArgs a) {
     float v = 0.0f;
@@ -209,27 +289,7 @@ __global__ void __launch_bounds__(kHB) k_head_bwd_rows(HeadArgs a) {
 #pragma unroll
         for (int j = 0; j < NOUT; ++j) a.dz[row * NOUT + j] = dz[j];
     }
-    if (a.dh) {
-        float *o = a.dh + row * a.K;
-        for (int k = 4 * l; k < a.K; k += 4 * kRowLanes) {
-            float r4[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float s = 0.0f;
-#pragma unroll
-                for (int j = 0; j < NOUT; ++j)
-                    if (k + i < a.K) s = fmaf(dz[j], a.W[(size_t)j * a.K + k + i], s);
-                r4[i] = a.dh_mask && k + i < a.K && !(a.dh_mask[row * a.K + k + i] > 0.0f) ? 0.0f : s;
-            }
-            if ((a.K & 3) == 0) {
-                *reinterpret_cast<float4 *>(o + k) = make_float4(r4[0], r4[1], r4[2], r4[3]);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (k + i < a.K) o[k + i] = r4[i];
-            }
-        }
-    }
+    if (a.dh) write_dh<NOUT>(a, row, l, dz);
 }
 
 // dW[j][c] = sum_rows dz[j] h[c], db[j] = sum_rows dz[j]: per-block partials
@@ -587,3 +647,33 @@ extern "C" int f110_ddpg_q_mean_bwd(const float *h, const float *W, const float 
     if (e == hipSuccess) e = wgrad(a, (hipStream_t)stream);
     return e == hipSuccess ? 0 : fail_hip("f110_ddpg_q_mean_bwd", e);
 }
+
+extern "C" int f110_ddpg_critic_step(const float *ht, const float *Wt, const float *bt, const float *r, const float *d,
+                                     float gamma, const float *h, const float *W, const float *b, const float *w,
+                                     const float *g, int32_t B, int32_t K, float *td, float *dh, const float *dh_mask,
+                                     float *dq, float *part, void *stream) {
+    if (bad_shape(B, K, 1) || !ht || !Wt || !bt || !r || !d || !h || !W || !b || !w || !g || !td || !part)
+        return fail_arg("f110_ddpg_critic_step");
+    HeadArgs a{};
+    a.ht = ht, a.Wt = Wt, a.bt = bt, a.aux0 = r, a.aux1 = d, a.gamma = gamma;
+    a.h = h, a.W = W, a.b = b, a.dout = w, a.g = g, a.out0 = td, a.dh = dh, a.dh_mask = dh_mask, a.dz = dq;
+    a.part = part;
+    a.B = B, a.K = K, a.nout = 1;
+    hipLaunchKernelGGL(k_critic_step, dim3(row_blocks(B)), dim3(kHB), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail_hip("f110_ddpg_critic_step", e);
+}
+
+extern "C" int f110_ddpg_q_mean_step(const float *h, const float *W, const float *b, const float *g, float sign,
+                                     int32_t B, int32_t K, float *dh, const float *dh_mask, float *part,
+                                     void *stream) {
+    if (bad_shape(B, K, 1) || !h || !W || !b || !g || !part) return fail_arg("f110_ddpg_q_mean_step");
+    HeadArgs a{};
+    a.h = h, a.W = W, a.b = b, a.g = g, a.sign = sign, a.dh = dh, a.dh_mask = dh_mask, a.part = part;
+    a.B = B, a.K = K, a.nout = 1;
+    hipLaunchKernelGGL(k_q_mean_step, dim3(row_blocks(B)), dim3(kHB), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail_hip("f110_ddpg_q_mean_step", e);
+}
+
+extern "C" int32_t f110_ddpg_row_blocks(int32_t B) { return B > 0 ? (int32_t)row_blocks(B) : -1; }

@@ -54,9 +54,14 @@ struct WgradLaunch {
     int64_t poff[kMaxOps + 1];  // each op's partials in the scratch: [S][N][KX] then [S][N]
     int32_t blk0[kMaxOps + 1];
     int32_t ntk[kMaxOps];       // kx tiles of each op
-    int32_t vec[kMaxOps];       // k_lwgrad: G / X / gmask rows loadable as float4
+    int32_t vec[kMaxOps];       // G / X / gmask rows loadable as float4
     int32_t nops, M, S;
     float *part;
+    // f110_learner_wgrad_loss: *loss = loss_sign * sum(loss_part[0 .. loss_n)) / M (the finishing launch's last block)
+    const float *loss_part;
+    float *loss;
+    float loss_sign;
+    int32_t loss_n;
 };
 
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
@@ -479,8 +484,25 @@ __global__ void __launch_bounds__(kGB) k_lwgrad(WgradLaunch L) {
     }
 }
 
-// dW / db = the S partials added in slice order; one thread per output
+// dW / db = the S partials added in slice order; one thread per output.  With
+// a loss, the last block instead sums its partials as k_loss_finish does
+// (per-thread strided sums, a shuffle tree per wave, waves in order).
 __global__ void __launch_bounds__(kGB) k_lwgrad_finish(WgradLaunch L, int64_t total) {
+    if (L.loss && blockIdx.x == gridDim.x - 1) {  // block-uniform
+        __shared__ float ws[kGB / 64];
+        float v = 0.0f;
+        for (int i = threadIdx.x; i < L.loss_n; i += kGB) v += L.loss_part[i];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float t = 0.0f;
+            for (int w = 0; w < kGB / 64; ++w) t += ws[w];
+            *L.loss = L.loss_sign * (t / (float)L.M);
+        }
+        return;
+    }
     const int64_t idx = (int64_t)blockIdx.x * kGB + threadIdx.x;
     if (idx >= total) return;
     int p = 0;
@@ -612,8 +634,8 @@ extern "C" int64_t f110_learner_wgrad_scratch_floats(const f110_wgrad_op *ops, i
     return n;
 }
 
-extern "C" int f110_learner_wgrad(const f110_wgrad_op *ops, int32_t nops, int32_t M, float *scratch, void *stream) {
-    const char *fn = "f110_learner_wgrad";
+static int learner_wgrad(const char *fn, const f110_wgrad_op *ops, int32_t nops, int32_t M, float *scratch,
+                         const float *loss_part, int32_t loss_n, float loss_sign, float *loss, void *stream) {
     if (!wgrad_ok(ops, nops, M)) return fail(fn, "bad arguments");
     WgradLaunch L{};
     L.nops = nops;
@@ -621,6 +643,8 @@ extern "C" int f110_learner_wgrad(const f110_wgrad_op *ops, int32_t nops, int32_
     L.S = wgrad_slices(ops, nops, M);
     if (L.S > 1 && !scratch) return fail(fn, "scratch required");
     L.part = scratch;
+    if (loss && (!loss_part || loss_n <= 0)) return fail(fn, "loss partials required");
+    L.loss = loss, L.loss_part = loss_part, L.loss_n = loss_n, L.loss_sign = loss_sign;
     int32_t blk = 0;
     int64_t off = 0, total = 0;
     for (int q = 0; q < nops; ++q) {
@@ -650,11 +674,21 @@ extern "C" int f110_learner_wgrad(const f110_wgrad_op *ops, int32_t nops, int32_
         hipError_t e = hipLaunchKernel(kf[L.S == 1][gm], dim3((unsigned)blk), dim3(kGB), args, 0, s);
         if (e != hipSuccess) return f110_set_error(F110_E_HIP, std::string(fn) + ": " + hipGetErrorString(e));
     }
-    if (L.S > 1) {
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return f110_set_error(F110_E_HIP, std::string(fn) + ": " + hipGetErrorString(e));
-        hipLaunchKernelGGL(k_lwgrad_finish, dim3((unsigned)((total + kGB - 1) / kGB)), dim3(kGB), 0, s, L, total);
+    if (L.S > 1 || loss) {  // the partials added (S > 1) and / or the loss (one more block)
+        const int64_t outs = L.S > 1 ? total : 0;
+        hipLaunchKernelGGL(k_lwgrad_finish, dim3((unsigned)((outs + kGB - 1) / kGB + (loss ? 1 : 0))), dim3(kGB), 0,
+                           s, L, outs);
     }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : f110_set_error(F110_E_HIP, std::string(fn) + ": " + hipGetErrorString(e));
+}
+
+extern "C" int f110_learner_wgrad(const f110_wgrad_op *ops, int32_t nops, int32_t M, float *scratch, void *stream) {
+    return learner_wgrad("f110_learner_wgrad", ops, nops, M, scratch, nullptr, 0, 0.0f, nullptr, stream);
+}
+
+extern "C" int f110_learner_wgrad_loss(const f110_wgrad_op *ops, int32_t nops, int32_t M, float *scratch,
+                                       const float *loss_part, int32_t n_part, float sign, float *loss, void *stream) {
+    if (!loss) return fail("f110_learner_wgrad_loss", "null loss");
+    return learner_wgrad("f110_learner_wgrad_loss", ops, nops, M, scratch, loss_part, n_part, sign, loss, stream);
 }

@@ -25,7 +25,7 @@ import torch
 
 from . import _lib
 from . import learner_gemm as lg
-from .ddpg_heads import _p, _scratch, _stream, td_target
+from .ddpg_heads import _p, _scratch, _stream
 
 
 class ExplicitUpdate:
@@ -85,26 +85,30 @@ class ExplicitUpdate:
         a_next, _ = self._actor_head(at, h2t)
         z2t = self._e(M)
         lg.gemm([self._fwd(z1t, ct.fcs2, z2t, x2=a_next)], M, dev)
-        y = td_target(z2t, ct.q.weight, ct.q.bias, r, d, ln.gamma)
+        # one launch: TD target (critic_target's head), td / w td^2 partials (critic's head) and the
+        # head's backward: dq and g2 = dq Wq where z2 > 0 (d loss / d fcs2's pre-activation)
         td = self._e(M, 1)
         loss = torch.empty((), dtype=torch.float32, device=dev)
-        sc = _scratch(L, M, H, 1, s)
-        st = _stream(s)
-        _lib.check(L.f110_ddpg_critic_loss(_p(z2), _p(cr.q.weight), _p(cr.q.bias), _p(y), _p(w), M, H, _p(td),
-                                           _p(loss), _p(sc), st), "f110_ddpg_critic_loss")
+        part = torch.empty(L.f110_ddpg_row_blocks(M), dtype=torch.float32, device=dev)
+        dq = self._e(M, 1)
+        g2 = self._e(M)
+        _lib.check(L.f110_ddpg_critic_step(_p(z2t), _p(ct.q.weight), _p(ct.q.bias), _p(r), _p(d), ln.gamma,
+                                           _p(z2), _p(cr.q.weight), _p(cr.q.bias), _p(w), _p(self.one), M, H,
+                                           _p(td), _p(g2), _p(z2), _p(dq), _p(part), _stream(s)),
+                   "f110_ddpg_critic_step")
         gc = self.gc
-        g2 = self._e(M)  # d loss / d fcs2's pre-activation (the head's dh with z2's ReLU applied)
-        _lib.check(L.f110_ddpg_critic_loss_bwd(_p(z2), _p(cr.q.weight), _p(td), _p(w), _p(self.one), M, H, _p(g2),
-                                               _p(z2), _p(gc["q.weight"]), _p(gc["q.bias"]), _p(sc), st),
-                   "f110_ddpg_critic_loss_bwd")
         Ws2 = cr.fcs2.weight
         ld2 = Ws2.stride(0)
         g1 = self._e(M)  # d loss / d fcs1's pre-activation: g2 Ws2[:, :H] where z1 > 0
         lg.gemm([lg.op(g2, Ws2, g1, H, H, H, ld2, H, omask=z1, nn=True)], M, dev)
+        # the four weight gradients (q, fcs2 and its action columns, fcs1) in one launch; its
+        # finishing launch also writes the loss
         lg.wgrad([lg.wop(g2, z1, gc["fcs2.weight"], H, H, H, H, ld2, db=gc["fcs2.bias"]),
                   lg.wop(g2, a, (gc["fcs2.weight"], H), H, nA, H, a.stride(0), ld2),
                   lg.wop(g1, s, gc["fcs1.weight"], H, D, H, s.stride(0), gc["fcs1.weight"].stride(0),
-                         db=gc["fcs1.bias"])], M, dev)
+                         db=gc["fcs1.bias"]),
+                  lg.wop(dq, z2, gc["q.weight"], 1, H, 1, H, gc["q.weight"].stride(0), db=gc["q.bias"])], M, dev,
+                 loss=(part, 1.0, loss))
         return loss, td
 
     def actor(self, s):
@@ -123,29 +127,31 @@ class ExplicitUpdate:
         nA = act.shape[1]
         z2 = self._e(M)
         lg.gemm([self._fwd(z1, cr.fcs2, z2, x2=act)], M, dev)
-        sc = _scratch(L, M, H, nA, s)
         st = _stream(s)
         loss = torch.empty((), dtype=torch.float32, device=dev)
-        _lib.check(L.f110_ddpg_q_mean(_p(z2), _p(cr.q.weight), _p(cr.q.bias), -1.0, M, H, _p(loss), _p(sc), st),
-                   "f110_ddpg_q_mean")
-        g2 = self._e(M)  # d loss / d fcs2's pre-activation
-        _lib.check(L.f110_ddpg_q_mean_bwd(None, _p(cr.q.weight), _p(self.one), -1.0, M, H, _p(g2), _p(z2), None,
-                                          None, _p(sc), st), "f110_ddpg_q_mean_bwd")
+        part = torch.empty(L.f110_ddpg_row_blocks(M), dtype=torch.float32, device=dev)
+        g2 = self._e(M)  # d loss / d fcs2's pre-activation: (-1 / M) Wq where z2 > 0, with the q partials
+        _lib.check(L.f110_ddpg_q_mean_step(_p(z2), _p(cr.q.weight), _p(cr.q.bias), _p(self.one), -1.0, M, H,
+                                           _p(g2), _p(z2), _p(part), st), "f110_ddpg_q_mean_step")
         Ws2 = cr.fcs2.weight
         da = self._e(M, nA)  # g2 Ws2[:, H:]
         lg.gemm([lg.op(g2, (Ws2, H), da, nA, H, H, Ws2.stride(0), nA, nn=True)], M, dev)
         ga = self.ga
         scale, _ = ac._affine()
         gh2 = self._e(M)  # d loss / d fc2's pre-activation
+        sc = _scratch(L, M, H, nA, s)  # its first M * nA floats: the actor head's dz
         _lib.check(L.f110_ddpg_actor_head_bwd(_p(h2), _p(ac.fc3.weight), _p(t), _p(scale), _p(da), M, H, nA, _p(gh2),
-                                              _p(h2), _p(ga["fc3.weight"]), _p(ga["fc3.bias"]), _p(sc), st),
-                   "f110_ddpg_actor_head_bwd")
+                                              _p(h2), None, None, _p(sc), st), "f110_ddpg_actor_head_bwd")
         gh1 = self._e(M)  # gh2 W2 where h1 > 0
         W2 = ac.fc2.weight
         lg.gemm([lg.op(gh2, W2, gh1, H, H, H, W2.stride(0), H, omask=h1, nn=True)], M, dev)
+        dz = sc[:M * nA].view(M, nA)
+        # fc2, fc1 and the head's fc3 in one launch; its finishing launch also writes the loss
         lg.wgrad([lg.wop(gh2, h1, ga["fc2.weight"], H, H, H, H, ga["fc2.weight"].stride(0), db=ga["fc2.bias"]),
                   lg.wop(gh1, s, ga["fc1.weight"], H, D, H, s.stride(0), ga["fc1.weight"].stride(0),
-                         db=ga["fc1.bias"])], M, dev)
+                         db=ga["fc1.bias"]),
+                  lg.wop(dz, h2, ga["fc3.weight"], nA, H, nA, H, ga["fc3.weight"].stride(0), db=ga["fc3.bias"])],
+                 M, dev, loss=(part, -1.0, loss))
         return loss
 
     def policy(self, actor, obs, explore=None):

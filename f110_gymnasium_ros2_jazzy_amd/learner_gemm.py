@@ -51,15 +51,24 @@ def gemm(ops, M: int, device) -> None:
     _lib.check(L.f110_learner_gemm(arr, len(ops), int(M), _stream(device)), "f110_learner_gemm")
 
 
-def wgrad(ops, M: int, device) -> None:
+def wgrad(ops, M: int, device, loss=None) -> None:
+    """f110_learner_wgrad; loss = (partials, sign, out): also *out = sign *
+    sum(partials) / M in the finishing launch (f110_learner_wgrad_loss)."""
     L = _lib.load()
     arr = (_lib.F110WgradOp * len(ops))(*ops)
     n = L.f110_learner_wgrad_scratch_floats(arr, len(ops), int(M))
     if n < 0:
         raise _lib.F110Error("f110_learner_wgrad: unsupported shapes")
     scratch = torch.empty(max(int(n), 1), dtype=torch.float32, device=device)
-    _lib.check(L.f110_learner_wgrad(arr, len(ops), int(M), ctypes.c_void_p(scratch.data_ptr()), _stream(device)),
-               "f110_learner_wgrad")
+    if loss is None:
+        _lib.check(L.f110_learner_wgrad(arr, len(ops), int(M), ctypes.c_void_p(scratch.data_ptr()), _stream(device)),
+                   "f110_learner_wgrad")
+        return
+    part, sign, out = loss
+    _lib.check(L.f110_learner_wgrad_loss(arr, len(ops), int(M), ctypes.c_void_p(scratch.data_ptr()),
+                                         ctypes.c_void_p(part.data_ptr()), int(part.numel()), float(sign),
+                                         ctypes.c_void_p(out.data_ptr()), _stream(device)),
+               "f110_learner_wgrad_loss")
 
 
 def linear(x, W, b=None, relu: bool = True, x2=None, W2=None, omask=None, out=None):

@@ -567,6 +567,21 @@ F110_API int f110_ddpg_actor_explore(const float *h, const float *W, const float
                                      const float *shift, int32_t B, int32_t K, int32_t nout, const double *state_in,
                                      double *state_out, double decay, double sigma_min, const float *low,
                                      const float *high, uint64_t seed, float *out, int64_t out_stride, void *stream);
+/* The critic update's head in one launch: y = r + gamma (1 - d) (ht Wt^T + bt) (the target critic),
+ * td = y - (h W^T + b), part[blk] = block sums of w td^2 (f110_ddpg_row_blocks(B) floats; the loss
+ * is sum(part) / B: f110_learner_wgrad_loss), dq = -((g / B) w) (2 td) (may be null), dh = dq W where
+ * dh_mask > 0 (dh may be null).  = f110_ddpg_td_target + f110_ddpg_critic_loss + the row part of
+ * f110_ddpg_critic_loss_bwd, same float operations. */
+F110_API int f110_ddpg_critic_step(const float *ht, const float *Wt, const float *bt, const float *r, const float *d,
+                                   float gamma, const float *h, const float *W, const float *b, const float *w,
+                                   const float *g, int32_t B, int32_t K, float *td, float *dh, const float *dh_mask,
+                                   float *dq, float *part, void *stream);
+/* The actor update's loss head: part[blk] = block sums of q = h W^T + b (the loss is sign sum(part) / B),
+ * dh = (sign g / B) W where dh_mask > 0.  = f110_ddpg_q_mean + the row part of f110_ddpg_q_mean_bwd. */
+F110_API int f110_ddpg_q_mean_step(const float *h, const float *W, const float *b, const float *g, float sign,
+                                   int32_t B, int32_t K, float *dh, const float *dh_mask, float *part, void *stream);
+/* blocks of the row-per-half-wave head launches for B rows (their partial-sum counts) */
+F110_API int32_t f110_ddpg_row_blocks(int32_t B);
 /* dz = (dact * scale) * (1 - t*t); dh = dz W; dW = dz^T h; db = sum_rows dz */
 F110_API int f110_ddpg_actor_head_bwd(const float *h, const float *W, const float *t, const float *scale,
                                       const float *dact, int32_t B, int32_t K, int32_t nout, float *dh,
@@ -635,6 +650,11 @@ typedef struct f110_wgrad_op {
 } f110_wgrad_op;
 F110_API int64_t f110_learner_wgrad_scratch_floats(const f110_wgrad_op *ops, int32_t nops, int32_t M);
 F110_API int f110_learner_wgrad(const f110_wgrad_op *ops, int32_t nops, int32_t M, float *scratch, void *stream);
+/* f110_learner_wgrad, and in its finishing launch *loss = sign * (sum of loss_part[0 .. n_part), in
+ * order) / M: the loss of a fused head (f110_ddpg_critic_step / f110_ddpg_q_mean_step) without a
+ * launch of its own. */
+F110_API int f110_learner_wgrad_loss(const f110_wgrad_op *ops, int32_t nops, int32_t M, float *scratch,
+                                     const float *loss_part, int32_t n_part, float sign, float *loss, void *stream);
 
 #ifdef __cplusplus
 }
