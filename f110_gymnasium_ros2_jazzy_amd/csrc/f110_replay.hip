@@ -17,7 +17,7 @@
 //           numpy's Generator.choice(replace=False, p=...) returns (it draws,
 //           drops repeats in draw order and redraws the rest from the
 //           renormalised p).  The B smallest 32-bit key patterns are found by
-//           a 4-pass radix select (8-bit digits, LDS histograms); ties at the
+//           a 4-pass radix select (8-bit digits, LDS histograms; each pass's blocks pick the digits so far from the global histograms themselves); ties at the
 //           threshold go to the lowest indices; the selection is compacted in
 //           index order (two passes, no sort) and one workgroup computes the
 //           IS weights.  As a set the batch has the distribution of the
@@ -222,6 +222,38 @@ __global__ void __launch_bounds__(kRB) k_keys(ReplayView v, int32_t batch) {
     if (hist[threadIdx.x]) atomicAdd(&v.hist[threadIdx.x], hist[threadIdx.x]);
 }
 
+// The digits of the batch-th smallest key from the histograms of passes
+// 0 .. npass-1 (every block of a consumer computes them itself: no one-block
+// select launch between the passes).  Per pass an inclusive scan of its 256
+// bins; the digit is the bin where the running count reaches kleft.
+__device__ void select_digits(const ReplayView &v, int32_t batch, int npass, uint32_t &prefix, uint32_t &kleft) {
+    __shared__ uint32_t inc[256];
+    __shared__ uint32_t res[2];
+    const int t = threadIdx.x;  // blockDim.x == 256
+    prefix = 0u;
+    kleft = (uint32_t)batch;
+    for (int p = 0; p < npass; ++p) {
+        const int shift = 24 - 8 * p;
+        inc[t] = v.hist[p * 256 + t];
+        __syncthreads();
+        for (int o = 1; o < 256; o <<= 1) {
+            const uint32_t add = t >= o ? inc[t - o] : 0u;
+            __syncthreads();
+            inc[t] += add;
+            __syncthreads();
+        }
+        const uint32_t below = t ? inc[t - 1] : 0u;
+        if (inc[t] >= kleft && below < kleft) {
+            res[0] = prefix | ((uint32_t)t << shift);
+            res[1] = kleft - below;
+        }
+        __syncthreads();
+        prefix = res[0];
+        kleft = res[1];
+        __syncthreads();
+    }
+}
+
 // Passes 1..3: histogram of digit `pass` over the keys whose higher digits
 // equal the prefix selected so far.
 __global__ void __launch_bounds__(kRB) k_hist(ReplayView v, int32_t batch, int pass) {
@@ -229,7 +261,9 @@ __global__ void __launch_bounds__(kRB) k_hist(ReplayView v, int32_t batch, int p
     const int64_t len = v.hdr->length;
     if (len < batch) return;
     const int shift = 24 - 8 * pass;
-    const uint32_t want = v.hdr->prefix >> (shift + 8);
+    uint32_t prefix, kleft;
+    select_digits(v, batch, pass, prefix, kleft);
+    const uint32_t want = prefix >> (shift + 8);
     hist[threadIdx.x] = 0;
     __syncthreads();
     for (int64_t i = (int64_t)blockIdx.x * kRB + threadIdx.x; i < len; i += (int64_t)gridDim.x * kRB) {
@@ -238,39 +272,6 @@ __global__ void __launch_bounds__(kRB) k_hist(ReplayView v, int32_t batch, int p
     }
     __syncthreads();
     if (hist[threadIdx.x]) atomicAdd(&v.hist[pass * 256 + threadIdx.x], hist[threadIdx.x]);
-}
-
-// The digit holding the batch-th smallest key (one workgroup).  Pass 0 also
-// adds the partial dens in a fixed order.
-__global__ void __launch_bounds__(256) k_select(ReplayView v, int32_t batch, int pass, int n_part) {
-    __shared__ uint32_t inc[256];
-    __shared__ double sh[4];
-    const int64_t len = v.hdr->length;
-    if (len < batch) return;
-    const int t = threadIdx.x;
-    const int shift = 24 - 8 * pass;
-    if (pass == 0) {
-        double acc = 0.0;
-        for (int k = t; k < n_part; k += 256) acc += v.den_part[k];
-        const double den = block_sum_f64(acc, sh);
-        if (t == 0) v.hdr->den = den;
-    }
-    const uint32_t kleft = pass == 0 ? (uint32_t)batch : v.hdr->kleft;
-    const uint32_t prefix = pass == 0 ? 0u : v.hdr->prefix;
-    inc[t] = v.hist[pass * 256 + t];
-    v.hist[pass * 256 + t] = 0;  // consumed: zero for the next sample
-    __syncthreads();
-    for (int o = 1; o < 256; o <<= 1) {
-        const uint32_t add = t >= o ? inc[t - o] : 0u;
-        __syncthreads();
-        inc[t] += add;
-        __syncthreads();
-    }
-    const uint32_t below = t ? inc[t - 1] : 0u;
-    if (inc[t] >= kleft && below < kleft) {
-        v.hdr->prefix = prefix | ((uint32_t)t << shift);
-        v.hdr->kleft = kleft - below;
-    }
 }
 
 // The selection: every key below the threshold key T, plus the lowest-index
@@ -282,11 +283,23 @@ __device__ __forceinline__ int64_t block_chunk(int64_t len) {
     return (len + gridDim.x - 1) / gridDim.x;
 }
 
-__global__ void __launch_bounds__(kRB) k_count(ReplayView v, int32_t batch) {
+__global__ void __launch_bounds__(kRB) k_count(ReplayView v, int32_t batch, int n_part) {
     __shared__ uint32_t wc[kRB / 64];
+    __shared__ double sh[kRB / 64];
     const int64_t len = v.hdr->length;
     if (len < batch) return;
-    const uint32_t T = v.hdr->prefix;
+    uint32_t T, kleft;
+    select_digits(v, batch, 4, T, kleft);
+    if (blockIdx.x == 0) {  // for k_place / k_finish: the threshold, and den (k_keys' partials, fixed order)
+        double acc = 0.0;
+        for (int k = threadIdx.x; k < n_part; k += kRB) acc += v.den_part[k];
+        const double den = block_sum_f64(acc, sh);
+        if (threadIdx.x == 0) {
+            v.hdr->prefix = T;
+            v.hdr->kleft = kleft;
+            v.hdr->den = den;
+        }
+    }
     const int64_t chunk = block_chunk(len);
     const int64_t i0 = (int64_t)blockIdx.x * chunk, i1 = min(i0 + chunk, len);
     uint32_t c = 0;
@@ -310,6 +323,8 @@ __global__ void __launch_bounds__(kRB) k_place(ReplayView v, int32_t batch) {
     const int64_t len = v.hdr->length;
     if (len < batch) return;
     const uint32_t T = v.hdr->prefix;
+    if (blockIdx.x == 0)  // the four passes' histograms, consumed: zero for the next sample
+        for (int k = threadIdx.x; k < 4 * 256; k += kRB) v.hist[k] = 0u;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     {  // this block's offset: the counts of the blocks before it
         uint32_t acc = 0;
@@ -552,15 +567,12 @@ hipError_t launch_replay_add(const ReplayView &v, const ReplayRows &in, const ui
 hipError_t launch_replay_sample(const ReplayView &v, int32_t batch, double beta, int64_t *idx, float *w,
                                 const ReplayBatch &out, bool known_full, hipStream_t s) {
     const int grid = replay_grid(v.capacity);
-    // histograms and tie count are cleared by k_select of the previous sample
+    // histograms and tie count are cleared by k_place / k_finish of the previous sample
     // (and at create), so a sample is kernels only
     hipLaunchKernelGGL(k_keys, dim3(grid), dim3(kRB), 0, s, v, batch);
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(256), 0, s, v, batch, 0, grid);
-    for (int pass = 1; pass < 4; ++pass) {
+    for (int pass = 1; pass < 4; ++pass)  // each block selects the digits so far from the histograms itself
         hipLaunchKernelGGL(k_hist, dim3(grid), dim3(kRB), 0, s, v, batch, pass);
-        hipLaunchKernelGGL(k_select, dim3(1), dim3(256), 0, s, v, batch, pass, grid);
-    }
-    hipLaunchKernelGGL(k_count, dim3(grid), dim3(kRB), 0, s, v, batch);
+    hipLaunchKernelGGL(k_count, dim3(grid), dim3(kRB), 0, s, v, batch, grid);
     hipLaunchKernelGGL(k_place, dim3(grid), dim3(kRB), 0, s, v, batch);
     hipLaunchKernelGGL(k_finish, dim3(1), dim3(kOneBlock), replay_finish_lds(batch), s, v, batch, beta, idx, w);
     if (!known_full)  // (f110_replay_length has seen length >= batch: the with-replacement path cannot run)
