@@ -141,9 +141,12 @@ class BatchSim:
                    "f110_reset")
         return self.out
 
-    def step(self, actions, minimal_outputs: bool = False) -> StepOut:
+    def step(self, actions, minimal_outputs: bool = False, obs_out=None) -> StepOut:
         """actions: [E, A, 2] (steer, velocity); float32 or float64 tensor/array
-        (float64 keeps Simulator.step's full-precision control inputs)."""
+        (float64 keeps Simulator.step's full-precision control inputs).
+        obs_out: a float32 [E, n_beams + 4A] tensor (unit column stride) that
+        receives this step's observations instead of ``out.obs`` (which then
+        keeps the previous ones): a trainer's own next_obs buffer, no copy."""
         a = torch.as_tensor(actions, device=self.device)
         if a.dtype not in (torch.float32, torch.float64):
             a = a.to(torch.float32)
@@ -154,6 +157,15 @@ class BatchSim:
         a = a.contiguous()
         self._keep_a = a
         outs = self._outs_min if minimal_outputs else self._outs
+        if obs_out is not None:
+            B = self.out.obs.shape[1]
+            if (obs_out.dtype != torch.float32 or obs_out.device != self.device or tuple(obs_out.shape) != (self.E, B)
+                    or obs_out.stride(1) != 1 or obs_out.stride(0) < B):
+                raise ValueError(f"obs_out must be a float32 [{self.E}, {B}] tensor on {self.device}, unit column stride")
+            o = _lib.F110Outputs()
+            ctypes.pointer(o)[0] = outs
+            o.obs, o.obs_stride = obs_out.data_ptr(), obs_out.stride(0)
+            outs = o
         dt = _lib.F64 if a.dtype == torch.float64 else _lib.F32
         _lib.check(self.L.f110_step(self.ctx, _ptr(a), dt, ctypes.byref(outs), self._stream()), "f110_step")
         return self.out

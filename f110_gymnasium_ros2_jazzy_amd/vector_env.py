@@ -193,18 +193,15 @@ class F110VectorEnv:
             a = self._act
         elif a.dim() == 2 and self.num_agents == 1:
             a = a.unsqueeze(1)
-        out = self.sim.step(a)
+        out = self.sim.step(a, obs_out=obs_out)  # the simulator writes obs_out itself (no copy)
+        obs = out.obs if obs_out is None else obs_out
         self._opponent_next(out)
         if self.reward_fn is not None:
-            rewards = self.reward_fn(out.obs, reset_mask=out.was_reset)
+            rewards = self.reward_fn(obs, reset_mask=out.was_reset)
         else:
             rewards = torch.where(out.was_reset.bool(), torch.zeros((), dtype=torch.float64, device=self.device),
                                   torch.full((), self.timestep, dtype=torch.float64, device=self.device))
-        if obs_out is None:
-            obs_out = out.obs.clone()
-        else:
-            obs_out.copy_(out.obs)
-        return obs_out, rewards, out.terminated, out.was_reset
+        return (obs.clone() if obs_out is None else obs_out), rewards, out.terminated, out.was_reset
 
     def close(self):
         if getattr(self, "sim", None) is not None:
