@@ -207,43 +207,40 @@ F110_HD void vehicle_dynamics_st(const double x[7], double u0_in, double u1_in, 
     const double mu = p.mu, C_Sf = p.C_Sf, C_Sr = p.C_Sr, lf = p.lf, lr = p.lr, h = p.h, m = p.m, I = p.I;
     double u0 = steering_constraint(x[2], u0_in, p.s_min, p.s_max, p.sv_min, p.sv_max);
     double u1 = accl_constraints(x[3], u1_in, p.v_switch, p.a_max, p.v_min, p.v_max);
-    if (fabs(x[3]) < 0.5) {
-        double lwb = lf + lr;
-        // vehicle_dynamics_ks re-applies the (idempotent) constraints to u
-        double k0 = steering_constraint(x[2], u0, p.s_min, p.s_max, p.sv_min, p.sv_max);
-        double k1 = accl_constraints(x[3], u1, p.v_switch, p.a_max, p.v_min, p.v_max);
-        double tn = tan(x[2]);
-        double c2 = cr_cos(x[2]);
-        double s4, c4;
-        cr_sincos(x[4], s4, c4);
-        f[0] = x[3] * c4;
-        f[1] = x[3] * s4;
-        f[2] = k0;
-        f[3] = k1;
-        f[4] = x[3] / lwb * tn;
-        f[5] = u1 / lwb * tn + x[3] / (lwb * (c2 * c2)) * u0;
-        f[6] = 0.0;
-    } else {
-        const double glr_m = kG * lr - u1 * h;
-        const double glf_p = kG * lf + u1 * h;
-        const double lrlf = lr + lf;
-        const double a = x[6] + x[4];
-        double sa, ca;
-        cr_sincos(a, sa, ca);
-        f[0] = x[3] * ca;
-        f[1] = x[3] * sa;
-        f[2] = u0;
-        f[3] = u1;
-        f[4] = x[5];
-        double t1 = -mu * m / (x[3] * I * lrlf) * (lf * lf * C_Sf * glr_m + lr * lr * C_Sr * glf_p) * x[5];
-        double t2 = mu * m / (I * lrlf) * (lr * C_Sr * glf_p - lf * C_Sf * glr_m) * x[6];
-        double t3 = mu * m / (I * lrlf) * lf * C_Sf * glr_m * x[2];
-        f[5] = t1 + t2 + t3;
-        double s1 = (mu / (x[3] * x[3] * lrlf) * (C_Sr * glf_p * lr - C_Sf * glr_m * lf) - 1) * x[5];
-        double s2 = mu / (x[3] * lrlf) * (C_Sr * glf_p + C_Sf * glr_m) * x[6];
-        double s3 = mu / (x[3] * lrlf) * (C_Sf * glr_m) * x[2];
-        f[6] = s1 - s2 + s3;
-    }
+    // Both models are evaluated for every car and the car's own is selected
+    // (dynamic_models.py:263-283: the kinematic model below |v| = 0.5): the
+    // transcendentals and divisions of the two are independent chains, so a
+    // wave holding both kinds of car waits for the longer one instead of the
+    // sum (this launch is latency-bound: one wave per SIMD).  f[0], f[1] take
+    // one sincos of the car's own angle (the yaw, or yaw + slip).
+    const bool kinematic = fabs(x[3]) < 0.5;
+    double sy, cy;
+    cr_sincos(kinematic ? x[4] : x[6] + x[4], sy, cy);
+    // kinematic (vehicle_dynamics_ks re-applies the (idempotent) constraints to u)
+    const double lwb = lf + lr;
+    const double k0 = steering_constraint(x[2], u0, p.s_min, p.s_max, p.sv_min, p.sv_max);
+    const double k1 = accl_constraints(x[3], u1, p.v_switch, p.a_max, p.v_min, p.v_max);
+    const double tn = tan(x[2]);
+    const double c2 = cr_cos(x[2]);
+    const double kf4 = x[3] / lwb * tn;
+    const double kf5 = u1 / lwb * tn + x[3] / (lwb * (c2 * c2)) * u0;
+    // single track
+    const double glr_m = kG * lr - u1 * h;
+    const double glf_p = kG * lf + u1 * h;
+    const double lrlf = lr + lf;
+    const double t1 = -mu * m / (x[3] * I * lrlf) * (lf * lf * C_Sf * glr_m + lr * lr * C_Sr * glf_p) * x[5];
+    const double t2 = mu * m / (I * lrlf) * (lr * C_Sr * glf_p - lf * C_Sf * glr_m) * x[6];
+    const double t3 = mu * m / (I * lrlf) * lf * C_Sf * glr_m * x[2];
+    const double s1 = (mu / (x[3] * x[3] * lrlf) * (C_Sr * glf_p * lr - C_Sf * glr_m * lf) - 1) * x[5];
+    const double s2 = mu / (x[3] * lrlf) * (C_Sr * glf_p + C_Sf * glr_m) * x[6];
+    const double s3 = mu / (x[3] * lrlf) * (C_Sf * glr_m) * x[2];
+    f[0] = x[3] * cy;
+    f[1] = x[3] * sy;
+    f[2] = kinematic ? k0 : u0;
+    f[3] = kinematic ? k1 : u1;
+    f[4] = kinematic ? kf4 : x[5];
+    f[5] = kinematic ? kf5 : t1 + t2 + t3;
+    f[6] = kinematic ? 0.0 : s1 - s2 + s3;
 }
 
 // pid, dynamic_models.py:178-221 (v_min = 1e-8 braking quirk included).

@@ -19,6 +19,7 @@
 #   pmc        scripts/profile_round.py TAG (kernel trace + PMC passes of the headline ray kernel)
 #   ab         scripts/ray_ab.py with the caller's AB_* environment -> ab.json
 #   trace      scripts/wave_trace.py (WT_ENVS), one context and bench's sub-shards -> trace_*.json
+#   agents     scripts/agents_probe.py (k_agents per launch: car counts, RK4 / Euler) -> agents.json
 #   c4one      bench.py --agents 2 --global-envs 8192 --runner one (one context) -> c4one.json
 #   c4 / c5    bench.py --agents 2 --global-envs 8192 / --workload ddpg -> c4.json / c5.json
 set -o pipefail
@@ -78,6 +79,7 @@ for step in "$@"; do
                cp "$OUT/trace_shards.out" "$OUT/trace_shards.json" ;;
         c4) run c4 600 python -u bench.py --agents 2 --global-envs 8192 --no-cpu-baseline --no-secondary &&
             cp "$OUT/c4.out" "$OUT/c4.json" ;;
+        agents) run agents 300 python -u scripts/agents_probe.py && cp "$OUT/agents.out" "$OUT/agents.json" ;;
         c4one) run c4one 600 python -u bench.py --agents 2 --global-envs 8192 --no-cpu-baseline --no-secondary \
                    --runner one && cp "$OUT/c4one.out" "$OUT/c4one.json" ;;
         c5) run c5 600 python -u bench.py --workload ddpg --steps 200 --warmup 20 && cp "$OUT/c5.out" "$OUT/c5.json" ;;
