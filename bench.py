@@ -140,7 +140,7 @@ def bench_ddpg(args):
         ph["replay_add_ms"] += ev[1].elapsed_time(ev[2]) / KP
         ph["learner_update_ms"] += ev[2].elapsed_time(ev[3]) / KP
     # data-parallel consistency: every rank must hold the same weights
-    wsum = float(sum(float(p.double().sum()) for p in tr.agent.actor.parameters()))
+    wsum = float(sum(float(p.detach().double().sum()) for p in tr.agent.actor.parameters()))
     in_sync = D.max_over_ranks(wsum) == -D.max_over_ranks(-wsum)
     result = {
         "metric": "env-steps/sec, end-to-end DDPG (BASELINE config 5)", "value": total / elapsed,

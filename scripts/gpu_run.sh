@@ -21,6 +21,7 @@
 #   trace      scripts/wave_trace.py (WT_ENVS), one context and bench's sub-shards -> trace_*.json
 #   agents     scripts/agents_probe.py (k_agents per launch: car counts, RK4 / Euler) -> agents.json
 #   c4one      bench.py --agents 2 --global-envs 8192 --runner one (one context) -> c4one.json
+#   c5x2       the DDPG bench as 2 ranks on the one GPU over gloo (the data-parallel path, no step graphs)
 #   c4 / c5    bench.py --agents 2 --global-envs 8192 / --workload ddpg -> c4.json / c5.json
 set -o pipefail
 TAG=${1:?tag}
@@ -82,6 +83,9 @@ for step in "$@"; do
         agents) run agents 300 python -u scripts/agents_probe.py && cp "$OUT/agents.out" "$OUT/agents.json" ;;
         c4one) run c4one 600 python -u bench.py --agents 2 --global-envs 8192 --no-cpu-baseline --no-secondary \
                    --runner one && cp "$OUT/c4one.out" "$OUT/c4one.json" ;;
+        c5x2) F110_SAME_DEVICE=1 F110_DIST_BACKEND=gloo run c5x2 600 python -m torch.distributed.run --nnodes=1 \
+                  --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --workload ddpg --steps 50 \
+                  --warmup 20 && cp "$OUT/c5x2.out" "$OUT/c5x2.json" ;;
         c5) run c5 600 python -u bench.py --workload ddpg --steps 200 --warmup 20 && cp "$OUT/c5.out" "$OUT/c5.json" ;;
         *) echo "unknown step $step" >&2; exit 2 ;;
     esac
