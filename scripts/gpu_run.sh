@@ -20,6 +20,7 @@
 #   ab         scripts/ray_ab.py with the caller's AB_* environment -> ab.json
 #   trace      scripts/wave_trace.py (WT_ENVS), one context and bench's sub-shards -> trace_*.json
 #   agents     scripts/agents_probe.py (k_agents per launch: car counts, RK4 / Euler) -> agents.json
+#   post       scripts/post_probe.py (k_post_multi per launch at 4096 / 8192 two-agent envs) -> post.json
 #   c4one      bench.py --agents 2 --global-envs 8192 --runner one (one context) -> c4one.json
 #   c5x2       the DDPG bench as 2 ranks on the one GPU over gloo (the data-parallel path, no step graphs)
 #   c4 / c5    bench.py --agents 2 --global-envs 8192 / --workload ddpg -> c4.json / c5.json
@@ -81,6 +82,7 @@ for step in "$@"; do
         c4) run c4 600 python -u bench.py --agents 2 --global-envs 8192 --no-cpu-baseline --no-secondary &&
             cp "$OUT/c4.out" "$OUT/c4.json" ;;
         agents) run agents 300 python -u scripts/agents_probe.py && cp "$OUT/agents.out" "$OUT/agents.json" ;;
+        post) run post 300 python -u scripts/post_probe.py && cp "$OUT/post.out" "$OUT/post.json" ;;
         c4one) run c4one 600 python -u bench.py --agents 2 --global-envs 8192 --no-cpu-baseline --no-secondary \
                    --runner one && cp "$OUT/c4one.out" "$OUT/c4one.json" ;;
         c5x2) F110_SAME_DEVICE=1 F110_DIST_BACKEND=gloo run c5x2 600 python -m torch.distributed.run --nnodes=1 \
