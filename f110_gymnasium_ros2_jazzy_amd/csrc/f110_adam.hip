@@ -20,6 +20,8 @@
 
 namespace f110 {
 
+constexpr int kAdamPer = 4;
+
 __global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
     const double t = (double)(*a.step + 1);
     const float w1 = (float)(1.0 - a.beta1);                        // lerp weight (< 0.5)
@@ -28,27 +30,41 @@ __global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
     const float step_size = (float)(a.lr / bc1);
     const float bc2_sqrt = (float)sqrt(bc2);
     const float eps = (float)a.eps;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * 256) {
-        const float g = a.grad[i];
-        float m = a.exp_avg[i];
-        m = m + w1 * (g - m);
-        float v = a.exp_avg_sq[i];
-        v = v * b2;
-        v = v + (w2 * g) * g;
-        const float denom = sqrtf(v) / bc2_sqrt + eps;
-        const float p = a.param[i] + (-step_size) * (m / denom);
-        a.param[i] = p;
-        a.exp_avg[i] = m;
-        a.exp_avg_sq[i] = v;
-        if (a.target) {
-            const float t0 = a.target[i];
-            a.target[i] = t0 + a.tau * (p - t0);
+    // kAdamPer elements per thread, their loads issued together (one memory round trip), then the
+    // updates; a grid-stride loop over such groups
+    for (int64_t base = (int64_t)blockIdx.x * 256 * kAdamPer + threadIdx.x; base < a.n;
+         base += (int64_t)gridDim.x * 256 * kAdamPer) {
+        float g[kAdamPer], m[kAdamPer], v[kAdamPer], p[kAdamPer], q[kAdamPer];
+#pragma unroll
+        for (int u = 0; u < kAdamPer; ++u) {
+            const int64_t i = base + (int64_t)u * 256;
+            const bool in = i < a.n;
+            g[u] = in ? a.grad[i] : 0.0f;
+            m[u] = in ? a.exp_avg[i] : 0.0f;
+            v[u] = in ? a.exp_avg_sq[i] : 0.0f;
+            p[u] = in ? a.param[i] : 0.0f;
+            q[u] = in && a.target ? a.target[i] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < kAdamPer; ++u) {
+            const int64_t i = base + (int64_t)u * 256;
+            if (i >= a.n) break;
+            float mm = m[u] + w1 * (g[u] - m[u]);
+            float vv = v[u] * b2;
+            vv = vv + (w2 * g[u]) * g[u];
+            const float denom = sqrtf(vv) / bc2_sqrt + eps;
+            const float pp = p[u] + (-step_size) * (mm / denom);
+            a.param[i] = pp;
+            a.exp_avg[i] = mm;
+            a.exp_avg_sq[i] = vv;
+            if (a.target) a.target[i] = q[u] + a.tau * (pp - q[u]);
         }
     }
-    // the last block to finish advances the step counter
+    // the last block to finish advances the step counter.  No fence: the last
+    // block hands no data over, and every block's read of the counter has
+    // returned (its value fed the bias corrections) before its ticket
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence();
         const uint32_t done = atomicAdd(a.done, 1u);
         if (done == gridDim.x - 1) {
             *a.step += 1;
@@ -59,7 +75,9 @@ __global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
 
 hipError_t launch_adam(const AdamArgs &a, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;
-    int64_t g = (a.n + 1023) / 1024;
+    // kAdamPer elements per thread (one memory round trip), at most 1024 blocks: few last-block
+    // tickets on the one counter
+    int64_t g = (a.n + 256 * kAdamPer - 1) / (256 * kAdamPer);
     g = g < 1 ? 1 : (g > 1024 ? 1024 : g);
     hipLaunchKernelGGL(k_adam, dim3((unsigned)g), dim3(256), 0, s, a);
     return hipGetLastError();
