@@ -175,11 +175,23 @@ __global__ void __launch_bounds__(kRB) k_add_copy(ReplayView v, ReplayRows in, i
     const int D = v.obs_dim;
     const float *so = in.obs + i * in.obs_stride, *sn = in.next_obs + i * in.next_stride;
     float *dobs = v.obs + slot * D, *dnext = v.next_obs + slot * D;
-    if (in.vec4) {
+    if (in.vec4) {  // pairs of float4 per thread: both rows' loads issued before the stores
         const int D4 = D >> 2;
-        for (int k = threadIdx.x; k < D4; k += kRB) {
-            reinterpret_cast<float4 *>(dobs)[k] = reinterpret_cast<const float4 *>(so)[k];
-            reinterpret_cast<float4 *>(dnext)[k] = reinterpret_cast<const float4 *>(sn)[k];
+        for (int k0 = threadIdx.x; k0 < D4; k0 += 2 * kRB) {
+            const int k1 = k0 + kRB;
+            const float4 a0 = reinterpret_cast<const float4 *>(so)[k0];
+            const float4 b0 = reinterpret_cast<const float4 *>(sn)[k0];
+            float4 a1, b1;
+            if (k1 < D4) {
+                a1 = reinterpret_cast<const float4 *>(so)[k1];
+                b1 = reinterpret_cast<const float4 *>(sn)[k1];
+            }
+            reinterpret_cast<float4 *>(dobs)[k0] = a0;
+            reinterpret_cast<float4 *>(dnext)[k0] = b0;
+            if (k1 < D4) {
+                reinterpret_cast<float4 *>(dobs)[k1] = a1;
+                reinterpret_cast<float4 *>(dnext)[k1] = b1;
+            }
         }
     } else {
         for (int k = threadIdx.x; k < D; k += kRB) {
@@ -485,11 +497,23 @@ __global__ void __launch_bounds__(kRB) k_gather(ReplayView v, int32_t batch, con
     const int D = v.obs_dim;
     const float *so = v.obs + i * D, *sn = v.next_obs + i * D;
     float *dobs = out.obs + (int64_t)j * D, *dnext = out.next_obs + (int64_t)j * D;
-    if (out.vec4) {
+    if (out.vec4) {  // pairs of float4 per thread: both rows' loads issued before the stores
         const int D4 = D >> 2;
-        for (int k = threadIdx.x; k < D4; k += kRB) {
-            reinterpret_cast<float4 *>(dobs)[k] = reinterpret_cast<const float4 *>(so)[k];
-            reinterpret_cast<float4 *>(dnext)[k] = reinterpret_cast<const float4 *>(sn)[k];
+        for (int k0 = threadIdx.x; k0 < D4; k0 += 2 * kRB) {
+            const int k1 = k0 + kRB;
+            const float4 a0 = reinterpret_cast<const float4 *>(so)[k0];
+            const float4 b0 = reinterpret_cast<const float4 *>(sn)[k0];
+            float4 a1, b1;
+            if (k1 < D4) {
+                a1 = reinterpret_cast<const float4 *>(so)[k1];
+                b1 = reinterpret_cast<const float4 *>(sn)[k1];
+            }
+            reinterpret_cast<float4 *>(dobs)[k0] = a0;
+            reinterpret_cast<float4 *>(dnext)[k0] = b0;
+            if (k1 < D4) {
+                reinterpret_cast<float4 *>(dobs)[k1] = a1;
+                reinterpret_cast<float4 *>(dnext)[k1] = b1;
+            }
         }
     } else {
         for (int k = threadIdx.x; k < D; k += kRB) {
