@@ -139,12 +139,13 @@ __global__ void __launch_bounds__(kOneBlock) k_add_scan(ReplayView v, const uint
         __syncthreads();
     }
     const int64_t total = part[kOneBlock - 1];
-    int64_t rank = part[t] - cnt;
+    const int64_t rank = part[t] - cnt;
     const int64_t cap = v.capacity, next = v.hdr->next;
     const float p0 = add_priority(v.hdr->length, mx);
+    const double w0 = prio_weight(p0, v.eps, v.alpha);  // every new row's weight without explicit priorities
+    int64_t slot = (next + rank) % cap;  // the thread's first ring slot, then consecutive ones
     for (int64_t i = r0; i < r1; ++i) {
         if (keep(i)) {
-            const int64_t slot = (next + rank) % cap;
             v.pos[i] = slot;
             float p = p0;
             if (priority) {  // add(exp, priority): np.clip(p, 1e-8, f32 max).astype(f32) (:59-63)
@@ -152,8 +153,8 @@ __global__ void __launch_bounds__(kOneBlock) k_add_scan(ReplayView v, const uint
                 p = (float)(q < 1e-8 ? 1e-8 : (q > (double)FLT_MAX ? (double)FLT_MAX : q));
             }
             v.prio[slot] = p;  // replay_buffer.py:65
-            v.wt[slot] = prio_weight(p, v.eps, v.alpha);
-            ++rank;
+            v.wt[slot] = priority ? prio_weight(p, v.eps, v.alpha) : w0;
+            slot = slot + 1 == cap ? 0 : slot + 1;
         } else {
             v.pos[i] = -1;
         }
