@@ -17,7 +17,7 @@ for f in $SAN; do HOSTSAN="$HOSTSAN -Xarch_host $f"; done
 /opt/rocm/bin/hipcc -O1 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math --offload-arch=gfx950 \
     -fvisibility=hidden -shared-libsan $HOSTSAN \
     $C/f110_kernels.hip $C/f110_opponent.hip $C/f110_reward.hip $C/f110_replay.hip $C/f110_adam.hip \
-    $C/f110_ddpg.hip $C/f110_capi.cpp $C/f110_replay_capi.cpp -o "$OUT/libf110.so"
+    $C/f110_ddpg.hip $C/f110_gemm.hip $C/f110_capi.cpp $C/f110_replay_capi.cpp -o "$OUT/libf110.so"
 # the oracle with the same (clang) sanitizer runtime; OpenMP pragmas ignored (serial)
 $LLVM/bin/clang -O1 -fPIC -std=c11 -ffp-contract=off -fno-fast-math -fno-builtin-sin -fno-builtin-cos \
     -fno-builtin-sincos -Wno-unknown-pragmas -D_GNU_SOURCE -shared -shared-libsan $SAN \
