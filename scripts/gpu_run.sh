@@ -22,6 +22,7 @@
 #   agents     scripts/agents_probe.py (k_agents per launch: car counts, RK4 / Euler) -> agents.json
 #   post       scripts/post_probe.py (k_post_multi per launch at 4096 / 8192 two-agent envs) -> post.json
 #   c4one      bench.py --agents 2 --global-envs 8192 --runner one (one context) -> c4one.json
+#   x2         the headline bench as 2 ranks on the one GPU over gloo (the multi-rank path of the driver's scaling runs)
 #   c5x2       the DDPG bench as 2 ranks on the one GPU over gloo (the data-parallel path, no step graphs)
 #   c4 / c5    bench.py --agents 2 --global-envs 8192 / --workload ddpg -> c4.json / c5.json
 set -o pipefail
@@ -85,6 +86,9 @@ for step in "$@"; do
         post) run post 300 python -u scripts/post_probe.py && cp "$OUT/post.out" "$OUT/post.json" ;;
         c4one) run c4one 600 python -u bench.py --agents 2 --global-envs 8192 --no-cpu-baseline --no-secondary \
                    --runner one && cp "$OUT/c4one.out" "$OUT/c4one.json" ;;
+        x2) F110_SAME_DEVICE=1 F110_DIST_BACKEND=gloo run x2 600 python -m torch.distributed.run --nnodes=1 \
+                --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 20 \
+                --warmup 5 && cp "$OUT/x2.out" "$OUT/x2.json" ;;
         c5x2) F110_SAME_DEVICE=1 F110_DIST_BACKEND=gloo run c5x2 600 python -m torch.distributed.run --nnodes=1 \
                   --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --workload ddpg --steps 50 \
                   --warmup 20 && cp "$OUT/c5x2.out" "$OUT/c5x2.json" ;;
