@@ -143,3 +143,23 @@ def test_rejects_bad_ops(gpu):
         lg.wgrad([lg.wop(x, x, y, 4, 16, 16, 16, 16, gmask=x), lg.wop(x, x, y, 4, 16, 16, 16, 16)], 8, x.device)
     with pytest.raises(RuntimeError):  # amask on one op of a launch only
         lg.gemm([lg.op(x, x, y, 4, 16, 16, 16, 4, amask=x), lg.op(x, x, y, 4, 16, 16, 16, 4)], 8, x.device)
+
+
+@pytest.mark.parametrize("M", [8, 4096])
+def test_weight_gradients_with_loss(gpu, M):
+    """f110_learner_wgrad_loss: the gradients as f110_learner_wgrad writes
+    them, and *loss = sign * sum(partials) / M from the finishing launch --
+    with S == 1 (M = 8: the finishing launch holds only the loss block) and
+    S > 1 (M = 4096)."""
+    lg = _lg()
+    g = torch.Generator(device="cuda").manual_seed(21 + M)
+    G, X = _rand(g, M, 128), _rand(g, M, 96)
+    dW1, db1 = torch.empty(128, 96, device="cuda"), torch.empty(128, device="cuda")
+    dW2, db2 = torch.empty(128, 96, device="cuda"), torch.empty(128, device="cuda")
+    part = _rand(g, 37)
+    loss = torch.full((), float("nan"), device="cuda")
+    lg.wgrad([lg.wop(G, X, dW1, 128, 96, 128, 96, 96, db=db1)], M, G.device)
+    lg.wgrad([lg.wop(G, X, dW2, 128, 96, 128, 96, 96, db=db2)], M, G.device, loss=(part, -1.0, loss))
+    assert torch.equal(dW1, dW2) and torch.equal(db1, db2)
+    ref = -float(part.double().sum()) / M
+    assert abs(float(loss) - ref) <= 1e-6 * (float(part.double().abs().sum()) / M) + 1e-12
