@@ -43,8 +43,10 @@ def metric_name(global_envs: int, agents: int) -> str:
     who = "parallel envs" if agents == 1 else f"parallel {agents}-agent envs"
     return f"env-steps/sec at {global_envs} {who}, 1080-beam lidar; scan L2 vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# texture-address cycles per wave-level 8-byte load whatever its lanes do: a MEASURED constant
-# (rocprofv3 TA_BUSY / SQ_INSTS_VMEM_RD at 65536 cars), not a datasheet figure
+# texture-address cycles per wave-level 8-byte load whatever its lanes do: MEASURED (rocprofv3
+# TA_BUSY / SQ_INSTS_VMEM_RD), not a datasheet figure.  The roofline takes it from the
+# committed PMC pass of the same configuration (profiles/pmc_busy_E<E>_A<A>.json, its
+# ta_cycles_per_vmem_rd); this is the fallback when no such file exists (round 3's 65536-car value)
 TA_CYCLES_PER_LOAD = 20.1
 N_CU, CLOCK_GHZ = 256, 2.4  # MI355X_MICROARCH.md
 
@@ -67,9 +69,11 @@ def parse():
                          "would mix into the ray kernel's average)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the C3-shard (8192) / C2 (4096) secondary lines at N=1")
-    ap.add_argument("--cpu-envs", type=int, default=4096)
-    ap.add_argument("--cpu-steps", type=int, default=1000)
-    ap.add_argument("--cpu-warmup", type=int, default=100)
+    ap.add_argument("--cpu-envs", type=int, default=GLOBAL_ENVS,
+                    help="envs of the CPU baseline (default: the metric's 65536, all on the host)")
+    ap.add_argument("--cpu-steps", type=int, default=30,
+                    help="timed CPU steps (30 x 65536 envs: ~13 s on 16 threads)")
+    ap.add_argument("--cpu-warmup", type=int, default=3)
     ap.add_argument("--seed", type=int, default=12345)
     ap.add_argument("--ramp-s", type=float, default=1.0,
                     help="untimed steps for at least this long before the W warm-up steps (the idle GPU "
@@ -86,6 +90,18 @@ def parse():
     ap.add_argument("--ddpg-batch", type=int, default=4096)
     ap.add_argument("--ddpg-memory", type=int, default=1 << 20)
     return ap.parse_args()
+
+
+def learner_roofline(M: int, obs: int, update_ms: float) -> dict:
+    """The learner update against the fp32 MFMA peak (its GEMMs run on
+    v_mfma_f32_32x32x2_f32, csrc/f110_gemm.hip): GEMM FLOPs per update / the
+    update's measured time (phases_ms.learner_update_ms, events around
+    replay(): sampling, heads, Adam and the all-reduces included)."""
+    fl = learner_flops_per_update(M, obs)
+    tf = fl / (update_ms * 1e-3) / 1e12 if update_ms > 0 else None
+    return {"bound": "mfma", "flops_per_update": fl, "update_ms": update_ms, "achieved": tf,
+            "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP32_MFMA_PEAK_TFLOPS if tf else None,
+            "note": "GEMM FLOPs of the update (bench.learner_flops_per_update) / the whole update's time"}
 
 
 def bench_ddpg(args):
@@ -153,6 +169,7 @@ def bench_ddpg(args):
                    "batch_per_rank": args.ddpg_batch, "memory_per_rank": args.ddpg_memory,
                    "parallelism": f"env-shard x{world}, DDPG data-parallel (RCCL all-reduce of grads)"},
         "phases_ms": ph,
+        "learner_roofline": learner_roofline(args.ddpg_batch, tr.agent.obs_dim, ph["learner_update_ms"]),
         "learner": {"critic_loss": float(tr.last["critic_loss"]), "actor_loss": float(tr.last["actor_loss"]),
                     "updates": tr.agent.global_step, "ranks_in_sync": in_sync},
     }
@@ -160,6 +177,34 @@ def bench_ddpg(args):
         print(json.dumps(result), flush=True)
     tr.close()
     D.shutdown()
+
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (exact f32), dense
+
+
+def learner_flops_per_update(M: int, obs: int, act: int = 2, hid: int = 128) -> float:
+    """GEMM FLOPs of one DDPG learner update (agent.py:302-331) on M rows, as
+    the explicit learner runs it (learner_fused.py): critic phase = actor_target
+    and critic_target forward on next_states, critic forward on states, critic
+    backward (q, fcs2 weight + input gradients, fcs1 weight gradient; no
+    gradient into obs); actor phase = actor forward, the updated critic forward
+    on (states, actions), backward through q / fcs2 to the action columns, then
+    the actor's weight and input gradients (fc3, fc2; fc1 weight only).  2 M K N
+    per [M x K] x [K x N] product; the heads' N = 1-2 GEMVs included."""
+    def mm(k, n):
+        return 2.0 * M * k * n
+    actor_fwd = mm(obs, hid) + mm(hid, hid) + mm(hid, act)
+    critic_fwd = mm(obs, hid) + mm(hid + act, hid) + mm(hid, 1)
+    critic_bwd = (mm(1, hid) + mm(hid, 1)          # q: dh, dW
+                  + mm(hid + act, hid) + mm(hid, hid)  # fcs2: dW, dX (the fcs1 columns)
+                  + mm(obs, hid))                  # fcs1: dW
+    actor_bwd = (mm(1, hid) + mm(hid, act)          # critic q dh, fcs2 dX (action columns)
+                 + mm(hid, act) + mm(act, hid)      # fc3: dW, dX
+                 + mm(hid, hid) + mm(hid, hid)      # fc2: dW, dX
+                 + mm(obs, hid))                    # fc1: dW
+    critic_phase = actor_fwd + critic_fwd + critic_fwd + critic_bwd  # targets on next_states, critic on states
+    actor_phase = actor_fwd + critic_fwd + actor_bwd
+    return critic_phase + actor_phase
 
 
 def algorithmic_bytes_per_env_step(B: int, A: int, mean_lookups: float) -> float:
@@ -224,8 +269,10 @@ def auto_streams(envs, agents=1):
 
 def cpu_baseline(O, scanner, poses, acts_np, args):
     """The C oracle (oracle/f110_oracle.c, OpenMP over envs) on the host cores:
-    BASELINE.md §3's plan -- cpu_envs envs, cpu_warmup + cpu_steps steps, the
-    GPU run's seeded spawn poses and actions, scan noise on (a host draw)."""
+    BASELINE.md §3's plan -- cpu_envs envs (default the metric's 65536, the
+    GPU run's own spawn poses and actions), cpu_warmup + cpu_steps steps, scan
+    noise on (a host draw).  The sample is bounded by steps, not envs: every
+    env of the configuration is stepped."""
     threads = cpu_threads()
     E = min(args.cpu_envs, poses.shape[0])
     A = args.agents
@@ -247,6 +294,7 @@ def cpu_baseline(O, scanner, poses, acts_np, args):
                        "(the machine's CPUs are shared by its GPUs' jobs)" if omp and int(omp) < affinity_cpus()
                        else "every CPU of the process's affinity set"),
         "kind": "port",
+        "threads": threads, "envs": E, "steps": args.cpu_steps,
         "sample": f"{E} envs x {args.cpu_steps} steps after {args.cpu_warmup} warm-up ({A} agent, {args.map}, RK4, "
                   f"noise {'off' if args.no_noise else 'on'}, the GPU run's spawn poses and actions), C oracle "
                   f"oracle/f110_oracle.c, OpenMP over envs on {threads} threads, {dt:.1f} s timed",
@@ -541,6 +589,8 @@ def main():
     steps(prof, acts, W, simt_steps, True)
     loop_lookups, lane_slots = prof.read_simt()
     other_loads = prof.read_counter(3)  # the loop's other wave-level vector loads (tables, re-gathers)
+    scalar_looks = prof.read_counter(4)  # k_rays_fxs: lookups of one-ray slots gathered by scalar loads
+    closed_trips = prof.read_counter(5)  # k_rays_fxs: slot-trips of a closed slot (no gather issued)
     prof.set_simt(False)
     full_outputs = None
     if not args.no_full_outputs:
@@ -570,8 +620,8 @@ def main():
         "kernel": "k_rays",
         "profiled_steps": KP,
         "profiled_launches": per_kernel["steps"],
-        "bound": ("the texture-address path, per wave-level load (~20 TA cycles each whatever its lanes do; HBM is "
-                  "not the limit: see hbm_traffic_frac; DESIGN.md 3.9)" if prof.ray_kernel == 3 and prof.ray_refill > 0
+        "bound": ("the texture-address path, per wave-level vector load (gather_roofline.ta_cycles_per_load TA cycles "
+                  "each whatever its lanes do; HBM is not the limit: see hbm_traffic_frac; DESIGN.md 3.9)" if prof.ray_kernel == 3 and prof.ray_refill > 0
                   else "latency of the dependent EDT gather chain (HBM is not the limit: see hbm_traffic_frac; capping "
                   "occupancy at 6/4/2 waves per SIMD costs 1.31x/1.62x/2.9x, DESIGN.md 3.2)"),
         "ray_kernel": ray_kernel_name(prof),
@@ -581,9 +631,12 @@ def main():
         "mean_lookups_per_ray": mean_look,
         "step_kernels_ms": {"k_agents": per_kernel["k_agents_ms"], "k_rays": k_ms, "k_post": per_kernel["k_post_ms"]},
         "step_algorithmic_bytes_per_env": algorithmic_bytes_per_env_step(B, A, mean_look),
-        # lookups made in the loop / (64 x the wave-level gathers the loop issued, an ended or closed
-        # slot's zero-cell gathers included), from the kernel's own counters
-        "simt_efficiency": loop_lookups / lane_slots if lane_slots else None,
+        # vector-gathered lookups of the loop / (64 x the wave-level vector gathers it issued, the ended
+        # lanes' zero-cell reads included), from the kernel's own counters; lookups a k_rays_fxs slot
+        # gathered by scalar loads (one ray left) are counted apart
+        "simt_efficiency": (loop_lookups - scalar_looks) / lane_slots if lane_slots else None,
+        "scalar_gathered_lookups_per_launch": scalar_looks / max(1, simt_steps),
+        "closed_slot_trips_per_launch": closed_trips / max(1, simt_steps),
     }
     # the gather bound, per instruction, the form the counters show: the texture-address
     # unit spends ~20.1 cycles (measured) on every wave-level load whatever its lanes do, so the
@@ -591,12 +644,18 @@ def main():
     # kernel's own counters: the loop's gathers (lane slots / 64) + its table loads and guard-band
     # re-gathers (counter 3); compare with SQ_INSTS_VMEM_RD in profiles/
     look_launch = E * A * B * (mean_look - 1.0)  # the kernel's own lookups (the first is k_agents')
-    roof["gather_roofline"] = {"bound": "texture-address cycles per wave-level vector load (measured constant)",
-                               "lookups_per_launch": look_launch, "ta_cycles_per_load": TA_CYCLES_PER_LOAD}
+    ta_cyc = TA_CYCLES_PER_LOAD
+    ta_src = "fallback constant (round 3, 65536 cars)"
+    if busy and busy.get("ta_cycles_per_vmem_rd"):
+        ta_cyc = float(busy["ta_cycles_per_vmem_rd"])
+        ta_src = busy["file"]
+    roof["gather_roofline"] = {"bound": "texture-address cycles per wave-level vector load (measured)",
+                               "lookups_per_launch": look_launch, "ta_cycles_per_load": ta_cyc,
+                               "ta_cycles_source": ta_src}
     if lane_slots:
         gathers = lane_slots / 64.0 / max(1, simt_steps)  # per launch
         loads = gathers + other_loads / max(1, simt_steps)
-        min_ms = loads * TA_CYCLES_PER_LOAD / N_CU / (CLOCK_GHZ * 1e9) * 1e3
+        min_ms = loads * ta_cyc / N_CU / (CLOCK_GHZ * 1e9) * 1e3
         roof["gather_roofline"].update({"slot_gathers_per_launch": gathers, "vmem_loads_per_launch": loads,
                                         "ta_min_ms": min_ms, "ta_frac": min_ms / k_ms})
     # consistency: the kernel runs inside the step it is timed in (the one-context runner's own wall time

@@ -99,6 +99,7 @@ struct f110_ctx {
     uint32_t rmp_zero = 0;
     bool fx_pad = false;    // the padded table is wanted (from 32768 cars or with refill; F110_FX_PAD=0: never)
     int32_t fx_refill = 0;   // waves per car of k_rays_fxs (0 = k_rays_fxn; f110_set_ray_refill)
+    int32_t fxs_sg = 1;      // k_rays_fxs's scalar gathers for slots with <= fxs_sg rays left (F110_FXS_SG, A/B)
     bool count_slots = false;  // f110_set_simt: lane-slot counter of the fixed-point loops (f110_read_simt)
     int fx_ilp = 1;         // rays per lane (f110_set_ray_lanes; default by car count)
 
@@ -761,6 +762,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     // 65536 envs as 2 x 32768 67.1 vs 63.0 M env-steps/s; at 16384 cars its long waves
     // leave a tail (0.324 vs 0.289 ms); it runs only without heavy-first and masks
     c->fx_refill = (EA >= 32768 || multi_refill) ? 1 : 0;
+    if (const char *v = std::getenv("F110_FXS_SG")) c->fxs_sg = std::min(2, std::max(0, std::atoi(v)));
     const double pad_q = std::ceil(C.max_range / resolution) + 8.0;
     const int32_t fx_pad_cells = pad_q > 0.0 && pad_q < 65536.0 ? (int32_t)pad_q : 0;  // else no padded table
     if (e == hipSuccess)
@@ -879,6 +881,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.fxs_ok = fxs_ok(c) ? 1 : 0;
     a.count_slots = c->count_slots ? 1 : 0;
     a.fx_refill = c->fx_refill;
+    a.fxs_sg = c->fxs_sg;
     a.fx_ilp = c->fx_ilp;
     a.gate_wait = c->gate_wait;
     a.gate_record = c->gate_record;

@@ -59,6 +59,7 @@ struct StepArgs {
     int32_t fx_pad;     // the padded table is built (k_rays_fxn on it unless F110_FX_PAD=0; k_rays_fxs)
     int32_t fxs_ok;     // the padded table's rows and columns are below 2^20 (kFxsBase's offsets)
     int32_t fx_refill;  // waves per car of k_rays_fxs (two chunk slots with refill; 0 = off)
+    int32_t fxs_sg;     // k_rays_fxs: a slot with <= fxs_sg rays left gathers them with scalar loads (0, 1, 2)
     int32_t count_slots;  // f110_set_simt: lane-slot counter of the fixed-point loops
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2: k_rays_fxn / k_rays_fxs)
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;

@@ -1127,7 +1127,7 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
 // gather every trip, a closed slot on the zero cell).  Per slot and trip: the
 // total (:141), the activity test (:133), the refill when the slot's chunk has
 // ended, the step (:135-136) and its gather.
-template <bool HANDOFF>
+template <bool HANDOFF, int SG>
 __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
     constexpr int NS = 2;
     wave_stamp_start(a.wtrace);
@@ -1252,44 +1252,90 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
     };
 
     uint32_t lane_iters = 0, slot_gathers = 0;
+    uint32_t scalar_gathers = 0, closed_trips = 0;
     const double ux = fma(ld_const(a.ray0 + g), L.ir, L.cxk) - kFxpBase;
     const double uy = fma(ld_const(a.ray0 + a.EA + g), L.ir, L.cyk) - kFxpBase;
     // q + P of the scan origin inside [fxp_lo, fxp_h*): its rays stay in the padded table (false for NaN)
     const bool fast_car = (ux >= a.fxp_lo) & (ux < a.fxp_hx) & (uy >= a.fxp_lo) & (uy < a.fxp_hy);
     if (fast_car) {
+        // SG > 0: a slot with at most SG rays still tracing gathers their cells with scalar loads
+        // (readlane of the lane's offset, s_load_dwordx2 through the scalar cache) instead of a
+        // 64-lane vector gather: the texture-address unit, the kernel's bound, costs the same ~23
+        // cycles per vector load whatever its active lanes, and 9.5 % of fxs's slot
+        // gathers carry one ray (scripts/slot_merge_model.py's schedule).  The scalar result
+        // lands in the slot's d at its next step.  A closed slot (no chunk left) neither steps
+        // nor gathers (it used to gather the zero cell every trip: 7.9 % of the slot gathers).
+        bool sm[NS];
+        int sl0[NS], sl1[NS];
+        double sv0[NS], sv1[NS];
 #pragma unroll
         for (int r = 0; r < NS; ++r) {
             kk[r] = -1;
             d[r] = tot[r] = x[r] = y[r] = c[r] = sn[r] = 0.0;
+            sm[r] = false;
+            sl0[r] = sl1[r] = 64;
+            sv0[r] = sv1[r] = 0.0;
         }
 #pragma unroll
         for (int r = 0; r < NS; ++r)
             if (pnext < nch) arm(r, true);  // tot = 0: the first trip's total completes tot = d00
         __builtin_amdgcn_s_waitcnt(0);
-        for (;;) {
-#pragma unroll
-            for (int r = 0; r < NS; ++r) {
-                tot[r] += d[r];  // :141 (d00 for a freshly armed slot: tot = d00, :130)
-                bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
-                uint64_t m = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
-                if (!m && kk[r] >= 0) {  // wave-uniform, rare: the slot's chunk has ended; refill it
-                    finish(r);
-                    if (pnext < nch) {
-                        arm(r, false);  // tot = d = d00
-                        act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
-                        m = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
-                    } else {
-                        kk[r] = -1;
-                    }
-                    // the refill's own loads (tables) land here, so that the common path's wait
-                    // before the step stays vmcnt(1) (the other slot's gather may be in flight)
-                    __builtin_amdgcn_s_waitcnt(0);
+        // one step of slot r (:133-141): the total, the activity test, the refill when the slot's
+        // chunk has ended (a slot with no chunk left to arm closes: kk = -1, m = 0), the step
+        // and its gather
+        auto slot_step = [&](int r) {
+            if (SG && sm[r]) {  // the scalar gather of the slot's last ray(s) lands
+                double dv = lane == sl0[r] ? sv0[r] : 0.0;
+                if (SG > 1 && lane == sl1[r]) dv = sv1[r];
+                d[r] = dv;
+            }
+            tot[r] += d[r];  // :141 (d00 for a freshly armed slot: tot = d00, :130)
+            bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+            uint64_t m = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+            if (!m && kk[r] >= 0) {  // wave-uniform, rare: the slot's chunk has ended; refill it
+                finish(r);
+                if (pnext < nch) {
+                    arm(r, false);  // tot = d = d00
+                    act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
+                    m = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
+                } else {
+                    kk[r] = -1;
                 }
-                lane_iters += (uint32_t)__popcll(m);
-                bool near;
-                const uint32_t off = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act,
-                                                   zero_v, near);
+                // the refill's own loads (tables) land here, so that the common path's wait
+                // before the step stays vmcnt(1) (the other slot's gather may be in flight)
+                __builtin_amdgcn_s_waitcnt(0);
+            }
+            lane_iters += (uint32_t)__popcll(m);
+            bool near;
+            const uint32_t off = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act,
+                                               zero_v, near);
+            const uint32_t na = (uint32_t)__popcll(m);
+            if (SG && na - 1u < (uint32_t)SG) {  // wave-uniform: one (two) ray(s) left in the slot
+                uint32_t o = off;
+                const uint64_t nb = __builtin_amdgcn_ballot_w64(near) & m;
+                if (nb) {  // rare: the IEEE cell of a lane within the guard band
+                    const RayArgs &K = kernarg_here();
+                    if (lane_in(nb)) o = exact_offset_pad(K.m, x[r], y[r], (uint32_t)K.fxp_P);
+                    ++loads;
+                }
+                const int l0 = (int)__builtin_ctzll(m);
+                const uint32_t o0 = (uint32_t)__builtin_amdgcn_readlane((int)o, l0);
+                sv0[r] = ld_const(reinterpret_cast<const double *>(reinterpret_cast<const char *>(dt) + o0));
+                sl0[r] = l0;
+                if (SG > 1) {
+                    const int l1 = na > 1u ? 63 - (int)__builtin_clzll(m) : 64;
+                    if (na > 1u) {
+                        const uint32_t o1 = (uint32_t)__builtin_amdgcn_readlane((int)o, l1);
+                        sv1[r] = ld_const(reinterpret_cast<const double *>(reinterpret_cast<const char *>(dt) + o1));
+                    }
+                    sl1[r] = l1;
+                }
+                sm[r] = true;
+                scalar_gathers += na;
+            } else {
+                if (SG) sm[r] = false;
                 d[r] = ld_off(dt, off);
+                ++slot_gathers;
                 const uint64_t nb = __builtin_amdgcn_ballot_w64(near) & m;
                 if (nb) {  // rare: lanes within the guard band re-gather from the IEEE cell
                     const RayArgs &K = kernarg_here();
@@ -1297,13 +1343,40 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
                     ++loads;
                 }
             }
-            ++trips;
-            bool open = false;
+        };
+        // both slots open: two gathers in flight per trip until a slot closes (its chunk ended
+        // with none left to arm; in that trip it gathers the zero cell once more)
+        if (kk[1] >= 0) {
+            for (;;) {
 #pragma unroll
-            for (int r = 0; r < NS; ++r) open |= kk[r] >= 0;
-            if (!open) break;
+                for (int r = 0; r < NS; ++r) slot_step(r);
+                ++trips;
+                if ((kk[0] < 0) | (kk[1] < 0)) break;
+            }
+            if (kk[0] < 0) {  // the open slot moves into slot 0 (wave-uniform copies)
+                x[0] = x[1];
+                y[0] = y[1];
+                d[0] = d[1];
+                tot[0] = tot[1];
+                c[0] = c[1];
+                sn[0] = sn[1];
+                kk[0] = kk[1];
+                kpar[0] = kpar[1];
+                if (SG) {
+                    sm[0] = sm[1];
+                    sl0[0] = sl0[1];
+                    sl1[0] = sl1[1];
+                    sv0[0] = sv0[1];
+                    sv1[0] = sv1[1];
+                }
+            }
         }
-        slot_gathers = trips * NS;  // every trip gathers in both slots (a closed slot on the zero cell)
+        // one slot left: the closed one no longer gathers
+        while (kk[0] >= 0) {
+            slot_step(0);
+            ++trips;
+            ++closed_trips;
+        }
     } else {  // an origin off the map: the IEEE cell of every lookup, chunk after chunk
         uint32_t cnt = 0;
         while (pnext < nch) {
@@ -1329,11 +1402,14 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
         unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
         atomicAdd(cs, (unsigned long long)(lanes + lane_iters));  // the first lookup came from k_agents
         atomicAdd(cs + 1, (unsigned long long)lanes);
-        // lane slots of the gathers the loop issued: 64 per wave-level gather, the ended and
-        // closed slots' zero-cell gathers included (SIMT = loop lookups / lane slots)
+        // lane slots of the vector gathers the loop issued: 64 per wave-level gather, the ended
+        // lanes' zero-cell reads included (SIMT = vector-gathered lookups / lane slots); counter 4:
+        // the lookups gathered by scalar loads; counter 5: slot-trips of a closed slot (no gather)
         if (K.count_slots) {
             atomicAdd(cs + 2, (unsigned long long)slot_gathers * 64ull);
             atomicAdd(cs + 3, (unsigned long long)loads);
+            atomicAdd(cs + 4, (unsigned long long)scalar_gathers);
+            atomicAdd(cs + 5, (unsigned long long)closed_trips);
         }
     }
     if (a.count_slots) {  // the run search's wave-level loads (counter 3)
@@ -1793,8 +1869,13 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                 ra.fxs_cy = std::fma(-a.tmap.oy, a.tmap.inv_res, kFxsBase + P + kFxsShift);
                 if (a.fx_refill > 0 && a.fxs_ok && !mask && ra.HB == 0 && !ra.wcost) {
                     // one wave per car, two chunk slots with refill (k_rays_fxs; no heavy-first)
-                    f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false>)
-                               : reinterpret_cast<const void *>(&k_rays_fxs<true>);
+                    const void *fn_s[2][3] = {{reinterpret_cast<const void *>(&k_rays_fxs<false, 0>),
+                                               reinterpret_cast<const void *>(&k_rays_fxs<false, 1>),
+                                               reinterpret_cast<const void *>(&k_rays_fxs<false, 2>)},
+                                              {reinterpret_cast<const void *>(&k_rays_fxs<true, 0>),
+                                               reinterpret_cast<const void *>(&k_rays_fxs<true, 1>),
+                                               reinterpret_cast<const void *>(&k_rays_fxs<true, 2>)}};
+                    f = fn_s[single ? 0 : 1][std::min(2, std::max(0, a.fxs_sg))];
                     ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
                     g2 = dim3((unsigned)(ra.EA * ra.G4));
                 }

@@ -610,6 +610,8 @@ class DDPGLearner:
                 return a
             if self.explicit is not None:
                 a = self.explicit.policy(self.actor, o if o.dim() == 2 else o.unsqueeze(0))
+                if o.dim() == 1:  # a single observation keeps agent.py's [act_dim] shape (:368-370)
+                    a = a.squeeze(0)
             else:
                 a = self.actor(o)
             if training:

@@ -61,9 +61,10 @@ class VectorTrainer:
                                  max_add=self.N, graphs=graphs)
         self.warmup = int(warmup_steps)
         self.updates_per_step = int(updates_per_step)
-        # one HIP graph per vector step once the learner's eager warm-up updates are done (one rank,
-        # explicit learner, one update per step): two graphs, even / odd steps, which swap the two
-        # fixed observation buffers and the learner's two noise-state slots
+        # HIP graphs per vector step once the learner's eager warm-up updates are done (explicit
+        # learner, one update per step): even / odd steps have their own captures, which swap the two
+        # fixed observation buffers and the learner's two noise-state slots; one graph per step on
+        # one rank, three (split at the gradient all-reduces) on several
         self.step_graphs = bool(graphs) and os.environ.get("F110_STEP_GRAPH", "1") != "0"
         self._sg = [None, None]
         self._sg_parity = 0
@@ -101,53 +102,84 @@ class VectorTrainer:
 
     def _graph_ready(self) -> bool:
         ag = self.agent
-        return (self.step_graphs and not ag.distributed and ag.explicit is not None and ag.graphs and
-                self.updates_per_step == 1 and ag._ready and ag._eager_left == 0 and ag._graphs is None and
-                self.env.agent_actions() is not None)
+        return (self.step_graphs and ag.explicit is not None and ag.graphs and self.updates_per_step == 1 and
+                ag._ready and ag._eager_left == 0 and ag._graphs is None and self.env.agent_actions() is not None)
 
-    def _body(self, obs_in, obs_out):
-        """One vector step after the warm-up, as captured: choose_action (noise in
-        the head launch), env step + reward, replay add, the learner update's
-        three phases (one rank: no all-reduce between them)."""
+    def _head(self, obs_in, obs_out, phase_a):
+        """A vector step after the warm-up up to the first all-reduce, as captured:
+        choose_action (noise in the head launch), env step + reward, replay add,
+        the learner update's first phase (sample, critic loss and gradients)."""
         ag = self.agent
         act = ag.choose_action(obs_in, training=True, out=self.env.agent_actions())
         nxt, rew, term, was_reset = self.env.step_transition(act, obs_out=obs_out)
         ag.remember_env(obs_in, act, rew, nxt, term, was_reset)
-        for ph in self._sg_phases:
-            ph()
+        phase_a()
         return rew, term
 
+    def _capture(self, p):
+        """The parity's step graphs: its own learner phases and loss outputs
+        (ddpg._graph_phases per parity: the two captures share a memory pool,
+        so one parity's outputs must not be the other's scratch).  One rank: the
+        whole step is one graph.  Several ranks: three graphs split at the two
+        gradient-bucket all-reduces, which run eagerly (RCCL) between the replays."""
+        ag = self.agent
+        bufs = self._sg_obs
+        phases, out = ag._graph_phases()
+        ret = {}
+
+        def head():
+            ret["v"] = self._head(bufs[p], bufs[1 - p], phases[0])
+
+        def whole():
+            head()
+            phases[1]()
+            phases[2]()
+        segs = [head, phases[1], phases[2]] if ag.distributed else [whole]
+        cur = torch.cuda.current_stream(self.device)
+        graphs = []
+        for seg in segs:  # capture records, it does not run
+            g = torch.cuda.CUDAGraph()
+            ag._side.wait_stream(cur)
+            with torch.cuda.graph(g, pool=self._sg_pool, stream=ag._side):
+                seg()
+            cur.wait_stream(ag._side)
+            graphs.append(g)
+        return graphs, out, ret["v"]
+
     def _step_graphed(self):
-        """step() as a replay of the parity's captured graph (captured on its
-        first use; the capture runs the Python side once, which is this step's
+        """step() as replays of the parity's captured graphs (captured on its
+        first use: the capture runs the Python side once, which is this step's
         host bookkeeping; later replays repeat that bookkeeping here)."""
         ag = self.agent
         p = self._sg_parity
         if self._sg_obs is None:
             self._sg_obs = [torch.empty_like(self.obs), torch.empty_like(self.obs)]
             self._sg_pool = torch.cuda.graph_pool_handle()
-            self._sg_phases, self._sg_out = ag._graph_phases()
         bufs = self._sg_obs
         if self.obs.data_ptr() != bufs[p].data_ptr():
             bufs[p].copy_(self.obs)
         if self._sg[p] is None:
-            g = torch.cuda.CUDAGraph()
-            cur = torch.cuda.current_stream(self.device)
-            ag._side.wait_stream(cur)
-            with torch.cuda.graph(g, pool=self._sg_pool, stream=ag._side):
-                self._sg_ret = self._body(bufs[p], bufs[1 - p])
-            cur.wait_stream(ag._side)
-            self._sg[p] = g
+            self._sg[p] = self._capture(p)
         else:  # what the capture's Python side did once
+            s = ag._noise_slot
+            if ag._noise_dev != (ag.sigma, ag._noise_calls):  # the host changed sigma: the slot the graph reads
+                ag._noise_state[s, 0] = ag.sigma
+                ag._noise_state[s, 1] = float(ag._noise_calls)
             ag.noise_advance()
             ag.memory._added += self.N
-        self._sg[p].replay()
+        graphs, out, ret = self._sg[p]
+        graphs[0].replay()
+        if len(graphs) > 1:  # several ranks: the bucket all-reduces between the learner's phases
+            ag.critic_grads.reduce()
+            graphs[1].replay()
+            ag.actor_grads.reduce()
+            graphs[2].replay()
         ag.global_step += 1
-        self.last = self._sg_out
+        self.last = out
         self.obs = bufs[1 - p]
         self._sg_parity ^= 1
         self.global_step += 1
-        return self._sg_ret
+        return ret
 
     def close(self):
         self.env.close()

@@ -10,6 +10,7 @@
 #   lgemmpmc   two PMC passes (SQ wait / MFMA busy; TA busy) over scripts/learner_gemm_mb.py
 #   lgab       scripts/learner_gemm_mb.py once per alternate build ab_libs/*.so (F110_LIB)
 #   learner    tests/test_gpu_replay.py + tests/test_gpu_ddpg_heads.py (the DDPG learner)
+#   dpgraph    tests/test_gpu_dp_graphs.py (two gloo ranks on the GPU: step graphs vs eager)
 #   c5prof     scripts/profile_c5.py TAG (C5 bench + rocprofv3 kernel stats by stage) -> gpurun_out/prof_c5_TAG/
 #   quick      the dispatch-variant tests of tests/test_gpu_batch.py only
 #   smoke      __graft_entry__.smoke()
@@ -18,6 +19,8 @@
 #   prof       rocprofv3 --kernel-trace --stats over bench.py (no cpu leg) -> prof/, kernel_stats.csv
 #   pmc        scripts/profile_round.py TAG (kernel trace + PMC passes of the headline ray kernel)
 #   ab         scripts/ray_ab.py with the caller's AB_* environment -> ab.json
+#   abhead     the same A/B with ab_libs/head.so (F110_LIB: the previous commit's build) -> abhead.json
+#   pmcsmall   PMC passes (no kernel trace) at 8192 and 4096 cars, the default ray kernel and k_rays_fxs
 #   trace      scripts/wave_trace.py (WT_ENVS), one context and bench's sub-shards -> trace_*.json
 #   agents     scripts/agents_probe.py (k_agents per launch: car counts, RK4 / Euler) -> agents.json
 #   post       scripts/post_probe.py (k_post_multi per launch at 4096 / 8192 two-agent envs) -> post.json
@@ -68,6 +71,8 @@ for step in "$@"; do
                   n=$(basename "$lib" .so)
                   F110_LIB=$R/$lib run "lgab_$n" 300 python -u scripts/learner_gemm_mb.py || exit $?
               done ;;
+        dpgraph) run dpgraph 600 python -u -m pytest tests/test_gpu_dp_graphs.py -m gpu -x -v --timeout 400 \
+                     --timeout-method thread -p no:cacheprovider ;;
         c5prof) run c5prof 900 python -u scripts/profile_c5.py "$TAG" ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python -u bench.py && cp "$OUT/bench.out" "$OUT/bench.json" ;;
@@ -77,6 +82,13 @@ for step in "$@"; do
               find "$OUT/prof" -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} "$OUT/kernel_stats.csv" ;;
         pmc) run pmc 900 python -u scripts/profile_round.py "$TAG" ;;
         ab) run ab 900 python -u scripts/ray_ab.py && cp "$OUT/ab.out" "$OUT/ab.json" ;;
+        abhead) F110_LIB=$R/ab_libs/head.so run abhead 900 python -u scripts/ray_ab.py &&
+                cp "$OUT/abhead.out" "$OUT/abhead.json" ;;
+        pmcsmall) for e in 8192 4096; do
+                      PROFILE_NO_TRACE=1 PROFILE_ENVS=$e run "pmc_$e" 600 python -u scripts/profile_round.py "$TAG" &&
+                      PROFILE_NO_TRACE=1 PROFILE_ENVS=$e PROFILE_REFILL=1 run "pmc_${e}_fxs" 600 \
+                          python -u scripts/profile_round.py "$TAG" || exit $?
+                  done ;;
         trace) WT_MODE=one run trace 600 python -u scripts/wave_trace.py && cp "$OUT/trace.out" "$OUT/trace_one.json" &&
                WT_MODE=shards run trace_shards 600 python -u scripts/wave_trace.py &&
                cp "$OUT/trace_shards.out" "$OUT/trace_shards.json" ;;

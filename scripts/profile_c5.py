@@ -38,7 +38,7 @@ else:
 
 REPLAY = ("k_add_copy", "k_add_scan", "k_count", "k_finish", "k_gather", "k_hist", "k_keys", "k_place",
           "k_prio_max", "k_sample_replace", "k_select", "k_update")
-HEADS = ("k_colsum_finish", "k_head_bwd_rows", "k_head_fwd", "k_head_wgrad", "k_linear_relu", "k_loss_finish",
+HEADS = ("k_colsum_finish", "k_head_bwd_rows", "k_head_fwd", "k_head_wgrad", "k_loss_finish",
          "k_relu_bwd", "k_wgrad_finish")
 
 

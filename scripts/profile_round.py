@@ -21,6 +21,11 @@ COLLECT = "--collect" in sys.argv
 # only gpurun_out/ comes back from the box: write there, copy into profiles/ locally
 PROF = os.path.join(REPO, "profiles") if COLLECT else os.path.join(OUT, "summary")
 ENVS = int(os.environ.get("PROFILE_ENVS", "65536"))  # the headline configuration (bench.py default)
+# PROFILE_REFILL=<waves per car>: the PMC passes run k_rays_fxs (2 rays per lane) instead of the size's
+# default ray kernel (files suffixed _fxs); PROFILE_NO_TRACE=1 skips the bench kernel trace (step 1)
+REFILL = os.environ.get("PROFILE_REFILL")
+SUFFIX = "_fxs" if REFILL else ""
+NO_TRACE = os.environ.get("PROFILE_NO_TRACE") == "1"
 BENCH = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "300", "--warmup", "50", "--no-cpu-baseline",
          "--no-secondary", "--no-full-outputs", "--global-envs", str(ENVS)]
 env = dict(os.environ, TMPDIR="/tmp")
@@ -30,17 +35,19 @@ env = dict(os.environ, TMPDIR="/tmp")
 # the bench also runs full-output passes whose extra scan writes would mix into the averages
 RAYPMC = [sys.executable, os.path.join(REPO, "scripts", "ray_pmc.py")]
 env["MB_ENVS"] = str(ENVS)
+if REFILL:
+    env["MB_REFILL"] = REFILL
 
 
 def run(name, extra, timeout=400, bench_extra=(), target=None, env_extra=None):
-    d = os.path.join(OUT, name)
+    d = os.path.join(OUT, f"{name}_E{ENVS}{SUFFIX}")
     if COLLECT:
         return d
     shutil.rmtree(d, ignore_errors=True)
     run_env = dict(env, **(env_extra or {}))
     cmd = ["rocprofv3"] + extra + ["--output-format", "csv", "-d", d, "-o", "run", "--"] + (target or BENCH + list(bench_extra))
     print(" ".join(cmd), flush=True)
-    with open(os.path.join(OUT, f"{name}.log"), "w") as log:
+    with open(d + ".log", "w") as log:
         subprocess.run(["timeout", "-k", "10", str(timeout)] + cmd, cwd="/tmp", env=run_env, stdout=log,
                        stderr=subprocess.STDOUT, check=True)
     return d
@@ -70,38 +77,39 @@ def counters(d, dst, kernel="k_rays"):
 
 os.makedirs(OUT, exist_ok=True)
 os.makedirs(PROF, exist_ok=True)
-d = run("trace", ["--kernel-trace", "--stats"])
-stats = find(d, "kernel_stats.csv")
-shutil.copy(stats, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
-summary = {}
-with open(stats) as f:
-    for row in csv.DictReader(f):
-        summary[row["Name"][:80]] = {k: row[k] for k in ("Calls", "TotalDurationNs", "AverageNs", "Percentage")
-                                     if k in row}
-# the default bench launches k_rays at two grid sizes: the timed region's
-# sub-shards (E/S cars each, concurrent streams) and the isolated full-shard
-# roofline pass (E cars, one stream).  Split the averages by grid size so the
-# roofline's kernel_ms can be matched against the E-car launches.
-trace = find(d, "kernel_trace.csv")
-by_grid = {}
-with open(trace) as f:
-    for row in csv.DictReader(f):
-        if "k_rays" not in row.get("Kernel_Name", ""):
-            continue
-        g = next((row[k] for k in ("Grid_Size_X", "Grid_Size", "Grid_X") if k in row), "?")
-        dur = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
-        e = by_grid.setdefault(str(g), [0, 0.0])
-        e[0] += 1
-        e[1] += dur
-summary["k_rays_by_grid_size"] = {g: {"Calls": n, "AverageNs": t / n} for g, (n, t) in by_grid.items()}
-json.dump(summary, open(os.path.join(PROF, f"{tag}_kernel_stats.json"), "w"), indent=1)
+d = None if NO_TRACE else run("trace", ["--kernel-trace", "--stats"])
+stats = None if NO_TRACE else find(d, "kernel_stats.csv")
+if not NO_TRACE:
+    shutil.copy(stats, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+    summary = {}
+    with open(stats) as f:
+        for row in csv.DictReader(f):
+            summary[row["Name"][:80]] = {k: row[k] for k in ("Calls", "TotalDurationNs", "AverageNs", "Percentage")
+                                         if k in row}
+    # the default bench launches k_rays at two grid sizes: the timed region's
+    # sub-shards (E/S cars each, concurrent streams) and the isolated full-shard
+    # roofline pass (E cars, one stream).  Split the averages by grid size so the
+    # roofline's kernel_ms can be matched against the E-car launches.
+    trace = find(d, "kernel_trace.csv")
+    by_grid = {}
+    with open(trace) as f:
+        for row in csv.DictReader(f):
+            if "k_rays" not in row.get("Kernel_Name", ""):
+                continue
+            g = next((row[k] for k in ("Grid_Size_X", "Grid_Size", "Grid_X") if k in row), "?")
+            dur = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+            e = by_grid.setdefault(str(g), [0, 0.0])
+            e[0] += 1
+            e[1] += dur
+    summary["k_rays_by_grid_size"] = {g: {"Calls": n, "AverageNs": t / n} for g, (n, t) in by_grid.items()}
+    json.dump(summary, open(os.path.join(PROF, f"{tag}_kernel_stats.json"), "w"), indent=1)
 
-res = {"kernel": "k_rays", "envs": ENVS, "agents": 1}
+res = {"kernel": "k_rays", "envs": ENVS, "agents": 1, "refill": REFILL}
 for grp in (["FETCH_SIZE"], ["WRITE_SIZE"], ["TCC_HIT_sum", "TCC_MISS_sum"]):
     name = "pmc_" + "_".join(g.lower() for g in grp)
     try:
         dd = run(name, ["--pmc"] + grp, target=RAYPMC)  # the isolated E-car launch
-        res.update(counters(dd, os.path.join(PROF, f"{tag}_{name}.csv")))
+        res.update(counters(dd, os.path.join(PROF, f"{tag}_{name}_E{ENVS}{SUFFIX}.csv")))
     except Exception as exc:  # record, do not hide
         res[name + "_error"] = repr(exc)
 if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
@@ -113,18 +121,18 @@ if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
                    "counted by these TCC_EA counters")
 if "TCC_HIT_sum" in res:
     res["l2_hit_rate"] = res["TCC_HIT_sum"] / max(1.0, res["TCC_HIT_sum"] + res["TCC_MISS_sum"])
-json.dump(res, open(os.path.join(PROF, f"pmc_traffic_E{ENVS}_A1.json"), "w"), indent=1)
+json.dump(res, open(os.path.join(PROF, f"pmc_traffic_E{ENVS}_A1{SUFFIX}.json"), "w"), indent=1)
 print(json.dumps(res))
 
 # 3. issue / occupancy pass: VALU busy and resident waves per SIMD of the isolated E-car launch.
 #    SQ_* cycle counters are quad-cycles summed over waves; GRBM_GUI_ACTIVE is summed over the 8 XCDs
 #    (MI355X_MICROARCH.md), so kernel cycles = GRBM_GUI_ACTIVE / 8 and SIMDs = CUs x 4.
-busy = {"kernel": "k_rays", "envs": ENVS, "agents": 1}
+busy = {"kernel": "k_rays", "envs": ENVS, "agents": 1, "refill": REFILL}
 grp = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
        "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"]
 try:
     dd = run("pmc_busy", ["--pmc"] + grp, target=RAYPMC)
-    busy.update(counters(dd, os.path.join(PROF, f"{tag}_pmc_busy.csv")))
+    busy.update(counters(dd, os.path.join(PROF, f"{tag}_pmc_busy_E{ENVS}{SUFFIX}.csv")))
     simds = 256 * 4
     cyc = busy["GRBM_GUI_ACTIVE"] / 8.0
     busy["valu_busy"] = busy["SQ_ACTIVE_INST_VALU"] * 4.0 / (simds * cyc)
@@ -140,7 +148,7 @@ grp = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_
        "SQ_INST_CYCLES_SALU", "SQ_ACTIVE_INST_SCA", "GRBM_GUI_ACTIVE"]
 try:
     dd = run("pmc_issue", ["--pmc"] + grp, target=RAYPMC)
-    iss = counters(dd, os.path.join(PROF, f"{tag}_pmc_issue.csv"))
+    iss = counters(dd, os.path.join(PROF, f"{tag}_pmc_issue_E{ENVS}{SUFFIX}.csv"))
     busy.update(iss)
     cyc = iss["GRBM_GUI_ACTIVE"] / 8.0
     # SALU instructions issued per CU per kernel cycle (one scalar ALU per CU: 1.0 = every cycle);
@@ -155,9 +163,9 @@ except Exception as exc:
 #    busy cycles (TA_BUSY_avr: per TA instance, one per CU), the bound of the gather loop
 grp = ["SQ_INSTS_VMEM_RD", "SQ_WAVES", "TA_BUSY_avr", "TA_FLAT_READ_WAVEFRONTS_sum", "GRBM_GUI_ACTIVE"]
 try:
-    counts_path = os.path.join(OUT, "ray_counts_pmc_ta.json")
+    counts_path = os.path.join(OUT, f"ray_counts_pmc_ta_E{ENVS}{SUFFIX}.json")
     dd = run("pmc_ta", ["--pmc"] + grp, target=RAYPMC, env_extra={"RAY_PMC_COUNTS": counts_path})
-    ta = counters(dd, os.path.join(PROF, f"{tag}_pmc_ta.csv"))
+    ta = counters(dd, os.path.join(PROF, f"{tag}_pmc_ta_E{ENVS}{SUFFIX}.csv"))
     if os.path.exists(counts_path):  # the kernel's own count of its wave-level loads, same launches
         kc = json.load(open(counts_path))
         busy["kernel_counted_loads_per_launch"] = kc["vmem_loads_per_launch"]
@@ -172,5 +180,5 @@ try:
     busy["ta_cycles_per_vmem_rd"] = ta["TA_BUSY_avr"] * 256 / max(1.0, ta["SQ_INSTS_VMEM_RD"])
 except Exception as exc:
     busy["ta_error"] = repr(exc)
-json.dump(busy, open(os.path.join(PROF, f"pmc_busy_E{ENVS}_A1.json"), "w"), indent=1)
+json.dump(busy, open(os.path.join(PROF, f"pmc_busy_E{ENVS}_A1{SUFFIX}.json"), "w"), indent=1)
 print(json.dumps(busy))

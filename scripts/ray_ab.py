@@ -5,7 +5,7 @@ scans, states, collisions after the same steps, noise + autoreset on, a masked
 reset in the middle).  Prints one JSON line.
 
 A variant is `name:KEY=V,KEY=V`; keys: F110_RAY_KERNEL / F110_FX_PAD (env at
-create), LANES (f110_set_ray_lanes), REFILL (f110_set_ray_refill), HEAVY=0
+create; F110_FXS_SG: k_rays_fxs's scalar gathers), LANES (f110_set_ray_lanes), REFILL (f110_set_ray_refill), HEAVY=0
 (f110_disable_heavy_first), NOISE.
 
     AB_ENVS=8192,65536 AB_VARIANTS='fxn:REFILL=0,LANES=2;fxs:REFILL=1,LANES=2' python scripts/ray_ab.py
@@ -22,7 +22,7 @@ from f110_gymnasium_ros2_jazzy_amd import _lib  # noqa: E402
 from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns, load_map  # noqa: E402
 from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim  # noqa: E402
 
-ENV_KNOBS = ("F110_RAY_KERNEL", "F110_FX_PAD")
+ENV_KNOBS = ("F110_RAY_KERNEL", "F110_FX_PAD", "F110_FXS_SG")
 
 
 def parse_variants(spec):
@@ -132,8 +132,10 @@ def main():
                 lk, rays = sm.read_counters()
                 slots = sm.read_counter(2)
                 cars = E * A * steps
-                diag[n] = {"simt": (lk - rays) / max(slots, 1), "slot_gathers_per_car": slots / 64 / cars,
-                           "other_loads_per_car": sm.read_counter(3) / cars}
+                sg = sm.read_counter(4)  # lookups gathered by scalar loads (k_rays_fxs, SG > 0)
+                diag[n] = {"simt": (lk - rays - sg) / max(slots, 1), "slot_gathers_per_car": slots / 64 / cars,
+                           "other_loads_per_car": sm.read_counter(3) / cars, "scalar_gathers_per_car": sg / cars,
+                           "closed_slot_trips_per_car": sm.read_counter(5) / cars}
                 sm.set_simt(False)
         line = {"kernels": kernels, "identical": ident, "mean_lookups": look, "diag": diag}
         for n, ts in times.items():

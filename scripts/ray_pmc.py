@@ -14,6 +14,9 @@ sim = BatchSim(load_map("Spielberg_map"), n_envs=E, n_agents=A, autoreset=True, 
 if os.environ.get("MB_HEAVY", "0") != "1":
     from f110_gymnasium_ros2_jazzy_amd import _lib
     _lib.check(sim.L.f110_disable_heavy_first(sim.ctx), "f110_disable_heavy_first")
+if os.environ.get("MB_REFILL"):  # k_rays_fxs (waves per car) instead of the size's default ray kernel
+    sim.set_ray_lanes(2)
+    sim.set_ray_refill(int(os.environ["MB_REFILL"]))
 rng = np.random.default_rng(0)
 sim.reset(sp[rng.integers(0, sp.shape[0], E)])
 g = torch.Generator(device="cuda"); g.manual_seed(0)
@@ -34,7 +37,10 @@ if counts:
     _, slots = sim.read_simt()
     other = sim.read_counter(3)
     with open(counts, "w") as f:
-        json.dump({"envs": E, "agents": A, "launches": 100, "slot_gathers_per_launch": slots / 64.0 / 100,
+        json.dump({"envs": E, "agents": A, "launches": 100, "ray_kernel": sim.ray_kernel, "lanes": sim.ray_lanes,
+               "refill": sim.ray_refill, "scalar_gathers_per_launch": sim.read_counter(4) / 100.0,
+               "closed_slot_trips_per_launch": sim.read_counter(5) / 100.0,
+               "slot_gathers_per_launch": slots / 64.0 / 100,
                    "other_loads_per_launch": other / 100.0, "vmem_loads_per_launch": (slots / 64.0 + other) / 100},
                   f)
 print("done")

@@ -360,20 +360,32 @@ def test_actor_explore_head(gpu):
     for _ in range(3):
         sg = max(sg * 0.9, 0.02)
     assert ln.sigma == sg
+    # a single observation (1-D) keeps the reference's [act_dim] shape, also into a 1-D out
+    a_1d = ln.choose_action(S[7], training=False)
+    assert a_1d.shape == (2,)
+    torch.testing.assert_close(a_1d, base[7], rtol=0, atol=0)
+    o1 = torch.empty(2, device="cuda")
+    assert ln.choose_action(S[7], training=False, out=o1) is o1 and torch.equal(o1, base[7])
+    assert ln.choose_action(S[7], training=True).shape == (2,)
 
 
 def test_trainer_step_graphs_match_eager(gpu, monkeypatch):
     """VectorTrainer's whole-step graphs (two captured vector steps, even / odd,
     replayed after the learner's eager warm-up updates) against the same loop
     run eagerly (F110_STEP_GRAPH=0): after 14 steps the actor / critic weights,
-    the replay ring, the noise state and the last losses are bit-identical."""
+    the replay ring, the noise state and the last losses are bit-identical, and
+    so are the losses after 13 steps (an even-parity replay: each parity's
+    graph keeps its own loss outputs)."""
     from f110_gymnasium_ros2_jazzy_amd.train import VectorTrainer
     runs = []
+    l13 = []
     for flag in ("1", "0"):
         monkeypatch.setenv("F110_STEP_GRAPH", flag)
         tr = VectorTrainer(256, batch_size=256, memory_size=4096, warmup_steps=3, seed=11)
-        for _ in range(14):
+        for _ in range(13):
             tr.step()
+        l13.append((float(tr.last["critic_loss"]), float(tr.last["actor_loss"])))
+        tr.step()
         torch.cuda.synchronize()
         assert (tr._sg[0] is not None and tr._sg[1] is not None) == (flag == "1")
         ag = tr.agent
@@ -390,3 +402,4 @@ def test_trainer_step_graphs_match_eager(gpu, monkeypatch):
         assert torch.equal(ra[k], rb_[k]), k
     assert (ca, aa, sa, na, la, ga) == (cb, ab, sb, nb, lb, gb)
     assert torch.equal(oa, ob)
+    assert l13[0] == l13[1]
