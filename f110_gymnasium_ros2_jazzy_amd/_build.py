@@ -37,6 +37,7 @@ def _stale() -> bool:
         return True
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(REPO, "include", "f110.h"),
+                                                                  os.path.join(REPO, "include", "f110_debug.h"),
                                                                   __file__]
     return any(os.path.getmtime(d) > t for d in deps)
 

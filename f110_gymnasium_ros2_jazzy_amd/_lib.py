@@ -59,6 +59,7 @@ class F110WgradOp(ctypes.Structure):  # f110_wgrad_op
 
 REWARD_STATE_BYTES = 8 * 12 + 4 * 4   # f110_reward_state
 
+ABI_VERSION = 3  # include/f110.h F110_ABI_VERSION
 F32 = 0
 F64 = 1
 INTEGRATOR_RK4 = 1
@@ -67,13 +68,13 @@ INTEGRATOR_EULER = 2
 EXPORTS = [
     "f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config", "f110_edt_k",
     "f110_create", "f110_destroy", "f110_reset", "f110_step", "f110_get_state", "f110_set_state",
-    "f110_scan_batch", "f110_dynamics_batch", "f110_read_counters", "f110_reset_counters", "f110_read_simt", "f110_set_simt",
+    "f110_scan_batch", "f110_dynamics_batch", "f110_read_counters", "f110_reset_counters", "f110_debug_read_simt", "f110_debug_set_simt",
     "f110_profile_begin", "f110_profile_end", "f110_host_tables", "f110_host_beam_indices",
     "f110_set_scan_noise", "f110_set_params", "f110_host_cell_index", "f110_gap_follow",
     "f110_host_window_ranges", "f110_track_create", "f110_track_destroy", "f110_track_arrays",
     "f110_default_reward_params", "f110_reward", "f110_replay_create", "f110_replay_destroy", "f110_replay_add", "f110_replay_add_env",
     "f110_replay_sample", "f110_replay_update_priorities", "f110_replay_length", "f110_replay_arrays",
-    "f110_debug_wave_trace", "f110_set_ray_gate", "f110_disable_heavy_first", "f110_ray_kernel", "f110_ray_lanes", "f110_ray_refill", "f110_set_ray_refill", "f110_read_counter", "f110_step_n", "f110_set_ray_lanes", "f110_set_reset_dtype", "f110_host_np_sincosf", "f110_host_sincos", "f110_host_map_table", "f110_get_lap_state",
+    "f110_debug_wave_trace", "f110_debug_set_ray_gate", "f110_debug_disable_heavy_first", "f110_debug_ray_kernel", "f110_debug_ray_lanes", "f110_debug_ray_refill", "f110_debug_set_ray_refill", "f110_debug_read_counter", "f110_step_n", "f110_debug_set_ray_lanes", "f110_set_reset_dtype", "f110_set_device_share", "f110_host_np_sincosf", "f110_host_sincos", "f110_host_map_table", "f110_get_lap_state",
     "f110_dynamics_ks_batch", "f110_collision_batch", "f110_collision_multiple", "f110_adam_step", "f110_ddpg_scratch_floats", "f110_ddpg_actor_head", "f110_ddpg_actor_explore",
     "f110_ddpg_actor_head_bwd", "f110_ddpg_td_target", "f110_ddpg_critic_loss", "f110_ddpg_critic_loss_bwd",
     "f110_ddpg_q_mean", "f110_ddpg_q_mean_bwd", "f110_ddpg_relu_bwd_scratch_floats", "f110_ddpg_relu_bwd",
@@ -111,6 +112,12 @@ def load(build_if_missing: bool = True):
     except Exception:
         pass
     L = ctypes.CDLL(path)
+    alternate = path != _build.LIB
+    if alternate:  # an older build for A/B (ABI 2): its diagnostics under their pre-f110_debug_ names
+        for name in EXPORTS:
+            old = name.replace("f110_debug_", "f110_")
+            if name.startswith("f110_debug_") and not hasattr(L, name) and hasattr(L, old):
+                setattr(L, name, getattr(L, old))
     i32, i64, u64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
     L.f110_abi_version.restype = ctypes.c_int
     L.f110_last_error.restype = ctypes.c_char_p
@@ -131,8 +138,8 @@ def load(build_if_missing: bool = True):
     L.f110_collision_multiple.argtypes = [_P, i64, ctypes.c_int32, _P, _P, _P]
     L.f110_read_counters.argtypes = [_P, ctypes.POINTER(u64), ctypes.POINTER(u64), _P]
     L.f110_reset_counters.argtypes = [_P, _P]
-    L.f110_read_simt.argtypes = [_P, ctypes.POINTER(u64), ctypes.POINTER(u64), _P]
-    L.f110_set_simt.argtypes = [_P, ctypes.c_int32]
+    L.f110_debug_read_simt.argtypes = [_P, ctypes.POINTER(u64), ctypes.POINTER(u64), _P]
+    L.f110_debug_set_simt.argtypes = [_P, ctypes.c_int32]
     L.f110_set_scan_noise.argtypes = [_P, _P]
     L.f110_host_window_ranges.argtypes = [ctypes.c_double, ctypes.c_double, i32, ctypes.c_double, ctypes.c_double,
                                           _P]
@@ -162,15 +169,17 @@ def load(build_if_missing: bool = True):
     L.f110_replay_length.argtypes = [_P, ctypes.POINTER(i64), ctypes.POINTER(i64), _P]
     L.f110_replay_arrays.argtypes = [_P] + [ctypes.POINTER(_P)] * 6
     L.f110_debug_wave_trace.argtypes = [_P, i32, _P, i64, ctypes.POINTER(i64), _P]
-    L.f110_set_ray_gate.argtypes = [_P, _P, _P]
-    L.f110_disable_heavy_first.argtypes = [_P]
-    L.f110_ray_kernel.argtypes = [_P]
-    L.f110_ray_lanes.argtypes = [_P]
-    L.f110_ray_refill.argtypes = [_P]
-    L.f110_set_ray_refill.argtypes = [_P, ctypes.c_int32]
+    L.f110_debug_set_ray_gate.argtypes = [_P, _P, _P]
+    L.f110_debug_disable_heavy_first.argtypes = [_P]
+    L.f110_debug_ray_kernel.argtypes = [_P]
+    L.f110_debug_ray_lanes.argtypes = [_P]
+    L.f110_debug_ray_refill.argtypes = [_P]
+    L.f110_debug_set_ray_refill.argtypes = [_P, ctypes.c_int32]
     L.f110_step_n.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, _P, _P]
-    L.f110_read_counter.argtypes = [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), _P]
-    L.f110_set_ray_lanes.argtypes = [_P, ctypes.c_int32]
+    L.f110_debug_read_counter.argtypes = [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), _P]
+    L.f110_debug_set_ray_lanes.argtypes = [_P, ctypes.c_int32]
+    if hasattr(L, "f110_set_device_share") or not alternate:
+        L.f110_set_device_share.argtypes = [_P, i64, i32]
     L.f110_set_reset_dtype.argtypes = [_P, ctypes.c_int32]
     L.f110_get_lap_state.argtypes = [_P, _P, _P, _P]
     L.f110_host_np_sincosf.argtypes = [_P, i64, ctypes.c_int32, _P]
@@ -203,6 +212,8 @@ def load(build_if_missing: bool = True):
     L.f110_ddpg_row_blocks.argtypes = [i32]
     L.f110_ddpg_row_blocks.restype = i32
     for name in EXPORTS:
+        if alternate and not hasattr(L, name):
+            continue
         if name not in ("f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config",
                         "f110_host_np_sincosf", "f110_host_sincos",
                         "f110_host_tables", "f110_host_window_ranges", "f110_track_arrays",
@@ -212,8 +223,8 @@ def load(build_if_missing: bool = True):
     L.f110_ddpg_scratch_floats.restype = i64
     L.f110_ddpg_relu_bwd_scratch_floats.restype = i64
     L.f110_learner_wgrad_scratch_floats.restype = i64
-    if L.f110_abi_version() != 2:
-        raise F110Error("libf110.so ABI version mismatch")
+    if L.f110_abi_version() != ABI_VERSION and not (alternate and L.f110_abi_version() == 2):
+        raise F110Error(f"libf110.so ABI version mismatch ({L.f110_abi_version()} != {ABI_VERSION})")
     _lib = L
     return L
 

@@ -78,9 +78,9 @@ struct f110_ctx {
     int prof_max = 0, prof_n = 0;
     const double *noise_ext = nullptr;  // f110_set_scan_noise (caller-owned)
     uint64_t *wtrace = nullptr;         // f110_debug_wave_trace buffer (diagnostics)
-    bool heavy_off = false;             // f110_disable_heavy_first
+    bool heavy_off = false;             // f110_debug_disable_heavy_first
     bool reset_f32 = false;             // f110_set_reset_dtype
-    hipEvent_t gate_wait = nullptr;     // f110_set_ray_gate (caller-owned events)
+    hipEvent_t gate_wait = nullptr;     // f110_debug_set_ray_gate (caller-owned events)
     hipEvent_t gate_record = nullptr;
     // heavy-first ray dispatch (chunked kernel)
     uint8_t *wcost = nullptr;
@@ -98,10 +98,9 @@ struct f110_ctx {
     int32_t rmp_w = 0, rmp_P = 0, rmp_h = 0;
     uint32_t rmp_zero = 0;
     bool fx_pad = false;    // the padded table is wanted (from 32768 cars or with refill; F110_FX_PAD=0: never)
-    int32_t fx_refill = 0;   // waves per car of k_rays_fxs (0 = k_rays_fxn; f110_set_ray_refill)
-    int32_t fxs_sg = 1;      // k_rays_fxs's scalar gathers for slots with <= fxs_sg rays left (F110_FXS_SG, A/B)
-    bool count_slots = false;  // f110_set_simt: lane-slot counter of the fixed-point loops (f110_read_simt)
-    int fx_ilp = 1;         // rays per lane (f110_set_ray_lanes; default by car count)
+    int32_t fx_refill = 0;   // waves per car of k_rays_fxs (0 = k_rays_fxn; f110_debug_set_ray_refill)
+    bool count_slots = false;  // f110_debug_set_simt: lane-slot counter of the fixed-point loops (f110_debug_read_simt)
+    int fx_ilp = 1;         // rays per lane (f110_debug_set_ray_lanes; default by car count)
 
     hipEvent_t *next_prof_events() {
         if (prof_n >= prof_max) return nullptr;
@@ -762,7 +761,6 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     // 65536 envs as 2 x 32768 67.1 vs 63.0 M env-steps/s; at 16384 cars its long waves
     // leave a tail (0.324 vs 0.289 ms); it runs only without heavy-first and masks
     c->fx_refill = (EA >= 32768 || multi_refill) ? 1 : 0;
-    if (const char *v = std::getenv("F110_FXS_SG")) c->fxs_sg = std::min(2, std::max(0, std::atoi(v)));
     const double pad_q = std::ceil(C.max_range / resolution) + 8.0;
     const int32_t fx_pad_cells = pad_q > 0.0 && pad_q < 65536.0 ? (int32_t)pad_q : 0;  // else no padded table
     if (e == hipSuccess)
@@ -881,7 +879,6 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.fxs_ok = fxs_ok(c) ? 1 : 0;
     a.count_slots = c->count_slots ? 1 : 0;
     a.fx_refill = c->fx_refill;
-    a.fxs_sg = c->fxs_sg;
     a.fx_ilp = c->fx_ilp;
     a.gate_wait = c->gate_wait;
     a.gate_record = c->gate_record;
@@ -958,19 +955,19 @@ extern "C" void f110_host_np_sincosf(const float *x, int64_t n, int32_t cos_op, 
     for (int64_t i = 0; i < n; ++i) out[i] = np_sincosf(x[i], cos_op != 0);
 }
 
-extern "C" int f110_ray_kernel(const f110_ctx *ctx) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_ray_kernel: null context");
+extern "C" int f110_debug_ray_kernel(const f110_ctx *ctx) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_debug_ray_kernel: null context");
     return ctx->ray_kernel;
 }
 
-extern "C" int f110_ray_lanes(const f110_ctx *ctx) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_ray_lanes: null context");
+extern "C" int f110_debug_ray_lanes(const f110_ctx *ctx) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_debug_ray_lanes: null context");
     return ctx->ray_kernel == 3 ? ctx->fx_ilp : 1;
 }
 
 // k_rays_fxs's waves per car for unmasked steps, as launch_env_step decides it
-extern "C" int f110_ray_refill(const f110_ctx *ctx) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_ray_refill: null context");
+extern "C" int f110_debug_ray_refill(const f110_ctx *ctx) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_debug_ray_refill: null context");
     const bool fx = ctx->ray_kernel == 3 && ctx->fx_ilp == 2 && fxs_ok(ctx);
     const int waves = std::min<int>(ctx->fx_refill, (ctx->cfg.n_beams + 63) / 64);  // as the launch clamps it
     return fx && waves > 0 && (ctx->heavy_off || !ctx->wcost) ? waves : 0;
@@ -1000,11 +997,11 @@ static int ensure_padded_table(f110_ctx *ctx) {
 }
 
 // waves > 0 also turns heavy-first off: k_rays_fxs takes no heavy-first list
-extern "C" int f110_set_ray_refill(f110_ctx *ctx, int32_t waves) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_refill: null context");
-    if (waves < 0 || waves > 16) return fail(F110_E_INVALID, "f110_set_ray_refill: waves must be in 0..16");
+extern "C" int f110_debug_set_ray_refill(f110_ctx *ctx, int32_t waves) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_debug_set_ray_refill: null context");
+    if (waves < 0 || waves > 16) return fail(F110_E_INVALID, "f110_debug_set_ray_refill: waves must be in 0..16");
     const bool fx = ctx->ray_kernel == 3;
-    if (!fx && waves != 0) return fail(F110_E_INVALID, "f110_set_ray_refill: this context's ray kernel has no refill");
+    if (!fx && waves != 0) return fail(F110_E_INVALID, "f110_debug_set_ray_refill: this context's ray kernel has no refill");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     ctx->fx_refill = waves;
     if (waves > 0) {
@@ -1014,25 +1011,50 @@ extern "C" int f110_set_ray_refill(f110_ctx *ctx, int32_t waves) {
     return F110_OK;
 }
 
-extern "C" int f110_disable_heavy_first(f110_ctx *ctx) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_disable_heavy_first: null context");
+extern "C" int f110_debug_disable_heavy_first(f110_ctx *ctx) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_debug_disable_heavy_first: null context");
     ctx->heavy_off = true;
     return F110_OK;
 }
 
-extern "C" int f110_set_ray_lanes(f110_ctx *ctx, int32_t n) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_lanes: null context");
-    if (n < 1 || n > 2) return fail(F110_E_INVALID, "f110_set_ray_lanes: n must be 1 or 2");
+extern "C" int f110_debug_set_ray_lanes(f110_ctx *ctx, int32_t n) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_debug_set_ray_lanes: null context");
+    if (n < 1 || n > 2) return fail(F110_E_INVALID, "f110_debug_set_ray_lanes: n must be 1 or 2");
     if (ctx->launch_n != 0)
-        return fail(F110_E_INVALID, "f110_set_ray_lanes: call before the first reset/step (heavy-first state is per group)");
+        return fail(F110_E_INVALID, "f110_debug_set_ray_lanes: call before the first reset/step (heavy-first state is per group)");
     const bool fx = ctx->ray_kernel == 3;
-    if (!fx && n != 1) return fail(F110_E_INVALID, "f110_set_ray_lanes: this context's ray kernel traces one ray per lane");
+    if (!fx && n != 1) return fail(F110_E_INVALID, "f110_debug_set_ray_lanes: this context's ray kernel traces one ray per lane");
     if (fx) ctx->fx_ilp = n;
     return F110_OK;
 }
 
-extern "C" int f110_set_ray_gate(f110_ctx *ctx, void *wait_event, void *record_event) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_set_ray_gate: null context");
+// The product-side form of the three knobs above for a caller that splits one GPU's cars over
+// several concurrent contexts (streams.StreamShards): f110_create's size rules applied to the cars
+// the device traces at once.
+extern "C" int f110_set_device_share(f110_ctx *ctx, int64_t device_cars, int32_t contexts) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_set_device_share: null context");
+    const int64_t own = (int64_t)ctx->cfg.n_envs * ctx->cfg.n_agents;
+    if (contexts < 1 || device_cars < own)
+        return fail(F110_E_INVALID, "f110_set_device_share: contexts >= 1 and device_cars >= this context's cars");
+    if (ctx->launch_n != 0) return fail(F110_E_INVALID, "f110_set_device_share: call before the first reset/step");
+    if (ctx->ray_kernel != 3) {  // one ray per lane, no refill: only the heavy-first rule applies
+        if (contexts > 1) ctx->heavy_off = true;
+        return F110_OK;
+    }
+    // 2 rays per lane from 12288 cars on the device: 16384 envs as 2 x 8192 59.9 vs 56.0 M env-steps/s,
+    // 8192 as 4 x 2048 53.1 vs 47.6 M (profiles/r02_share_map/)
+    const int lanes = device_cars >= 12288 ? 2 : 1;
+    // k_rays_fxs from 32768 cars, or from 16384 with 4+ contexts: 32768 envs as 2 x 16384 69.2 vs 62.6 M,
+    // 16384 as 4 x 4096 65.3 vs 63.1 M; 16384 as 2 x 8192 lost (58.3 vs 61.3 M, profiles/r02_refill_*)
+    const int refill = (lanes == 2 && (device_cars >= 32768 || (device_cars >= 16384 && contexts >= 4))) ? 1 : 0;
+    int rc = f110_debug_set_ray_lanes(ctx, lanes);
+    if (rc == F110_OK) rc = f110_debug_set_ray_refill(ctx, refill);
+    if (rc == F110_OK && contexts > 1) ctx->heavy_off = true;  // the other contexts fill this one's tail
+    return rc;
+}
+
+extern "C" int f110_debug_set_ray_gate(f110_ctx *ctx, void *wait_event, void *record_event) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_debug_set_ray_gate: null context");
     ctx->gate_wait = static_cast<hipEvent_t>(wait_event);
     ctx->gate_record = static_cast<hipEvent_t>(record_event);
     return F110_OK;
@@ -1142,8 +1164,8 @@ extern "C" int f110_read_counters(f110_ctx *ctx, uint64_t *lookups, uint64_t *ra
     return F110_OK;
 }
 
-extern "C" int f110_read_counter(f110_ctx *ctx, int32_t idx, uint64_t *value, void *stream) {
-    if (!ctx || !value || idx < 0 || idx >= kCtrStride) return fail(F110_E_INVALID, "f110_read_counter: bad argument");
+extern "C" int f110_debug_read_counter(f110_ctx *ctx, int32_t idx, uint64_t *value, void *stream) {
+    if (!ctx || !value || idx < 0 || idx >= kCtrStride) return fail(F110_E_INVALID, "f110_debug_read_counter: bad argument");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     std::vector<unsigned long long> h((size_t)kCtrSlots * kCtrStride);
     HIP_TRY(hipMemcpyAsync(h.data(), ctx->ctr, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
@@ -1155,14 +1177,14 @@ extern "C" int f110_read_counter(f110_ctx *ctx, int32_t idx, uint64_t *value, vo
     return F110_OK;
 }
 
-extern "C" int f110_set_simt(f110_ctx *ctx, int32_t on) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_set_simt: null context");
+extern "C" int f110_debug_set_simt(f110_ctx *ctx, int32_t on) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_debug_set_simt: null context");
     ctx->count_slots = on != 0;
     return F110_OK;
 }
 
-extern "C" int f110_read_simt(f110_ctx *ctx, uint64_t *loop_lookups, uint64_t *lane_slots, void *stream) {
-    if (!ctx) return fail(F110_E_INVALID, "f110_read_simt: null context");
+extern "C" int f110_debug_read_simt(f110_ctx *ctx, uint64_t *loop_lookups, uint64_t *lane_slots, void *stream) {
+    if (!ctx) return fail(F110_E_INVALID, "f110_debug_read_simt: null context");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     std::vector<unsigned long long> h((size_t)kCtrSlots * kCtrStride);
     HIP_TRY(hipMemcpyAsync(h.data(), ctx->ctr, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,

@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include "../../include/f110.h"
+#include "../../include/f110_debug.h"
 
 #define F110_HD __host__ __device__ __forceinline__
 #define F110_D __device__ __forceinline__

@@ -34,8 +34,8 @@ struct StepArgs {
                               // (k_rays_fx / k_rays_fxn / k_rays_fxs: fixed-point cell index, scalar per-car set-up)
     uint8_t chunk_order[kMaxChunks];  // beam-chunk dispatch order of the chunked ray kernel
     uint64_t *wtrace;         // diagnostic wave trace of the next ray launch (f110_debug_wave_trace) or null
-    hipEvent_t gate_wait;     // f110_set_ray_gate: waited on before the ray launch, or null
-    hipEvent_t gate_record;   // f110_set_ray_gate: recorded after the ray launch, or null
+    hipEvent_t gate_wait;     // f110_debug_set_ray_gate: waited on before the ray launch, or null
+    hipEvent_t gate_record;   // f110_debug_set_ray_gate: recorded after the ray launch, or null
     // heavy-first ray dispatch (chunked kernel): per (car, chunk) wave cost of
     // the previous ray launch, this step's list of predicted-heavy waves
     uint8_t *wcost;           // [EA][nch] min(255, longest ray of the wave) or null
@@ -59,8 +59,7 @@ struct StepArgs {
     int32_t fx_pad;     // the padded table is built (k_rays_fxn on it unless F110_FX_PAD=0; k_rays_fxs)
     int32_t fxs_ok;     // the padded table's rows and columns are below 2^20 (kFxsBase's offsets)
     int32_t fx_refill;  // waves per car of k_rays_fxs (two chunk slots with refill; 0 = off)
-    int32_t fxs_sg;     // k_rays_fxs: a slot with <= fxs_sg rays left gathers them with scalar loads (0, 1, 2)
-    int32_t count_slots;  // f110_set_simt: lane-slot counter of the fixed-point loops
+    int32_t count_slots;  // f110_debug_set_simt: lane-slot counter of the fixed-point loops
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2: k_rays_fxn / k_rays_fxs)
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
     double side_max;  // max of the RaceCar side table (the TTC pre-test of k_rays_fxs)
@@ -161,7 +160,7 @@ struct RayArgs {
     double fxp_lo, fxp_hx, fxp_hy;
     int32_t fxp_P;
     double fxs_cx, fxs_cy;  // k_rays_fxs: 2^20 + P + 2^-26 - origin / res (see kFxsBase)
-    int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_read_simt)
+    int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_debug_read_simt)
     const double *cs2, *bs2;  // k_rays_fxs: interleaved (cos, sin) / (side, beam_cos) tables
 };
 

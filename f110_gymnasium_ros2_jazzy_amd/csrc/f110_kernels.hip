@@ -1127,7 +1127,7 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
 // gather every trip, a closed slot on the zero cell).  Per slot and trip: the
 // total (:141), the activity test (:133), the refill when the slot's chunk has
 // ended, the step (:135-136) and its gather.
-template <bool HANDOFF, int SG>
+template <bool HANDOFF>
 __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
     constexpr int NS = 2;
     wave_stamp_start(a.wtrace);
@@ -1182,7 +1182,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
         int ti = (int)beam_theta(K.runs + (size_t)g * kMaxSeg, ld_const(K.nruns + g), lo, k * 64, bc);  // :124
         if (ti >= K.theta_dis) ti = 0;
         const double2 t2 = ld_off(reinterpret_cast<const double2 *>(K.cs2), (uint32_t)ti * 16u);
-        ++loads;
+        loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
         c[r] = t2.x;
         sn[r] = t2.y;
         x[r] = x00;
@@ -1206,7 +1206,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
         double nz = 0.0;
         if (K.noise_ext) {
             nz = K.noise_ext[(size_t)e * B + bc];
-            ++loads;
+            loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
         } else if (K.noise_std > 0.0) {
             const int pp = kk[r] >> 1, ci = kpar[r];
             float nv;
@@ -1234,7 +1234,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
                 const bool may = ttc_may_fire_lane(range, K.side_max, v, K.ttc_thresh);
                 if (__builtin_amdgcn_ballot_w64(may)) {
                     const double2 t2 = ld_off(reinterpret_cast<const double2 *>(K.bs2), boff * 2u);  // (side, beam_cos)
-                    ++loads;
+                    loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
                     if (may && ttc_fires(range, t2.x, v * t2.y, K.ttc_thresh)) K.ttc_hit[g] = 1;
                 }
             }
@@ -1252,29 +1252,16 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
     };
 
     uint32_t lane_iters = 0, slot_gathers = 0;
-    uint32_t scalar_gathers = 0, closed_trips = 0;
+    uint32_t closed_trips = 0;
     const double ux = fma(ld_const(a.ray0 + g), L.ir, L.cxk) - kFxpBase;
     const double uy = fma(ld_const(a.ray0 + a.EA + g), L.ir, L.cyk) - kFxpBase;
     // q + P of the scan origin inside [fxp_lo, fxp_h*): its rays stay in the padded table (false for NaN)
     const bool fast_car = (ux >= a.fxp_lo) & (ux < a.fxp_hx) & (uy >= a.fxp_lo) & (uy < a.fxp_hy);
     if (fast_car) {
-        // SG > 0: a slot with at most SG rays still tracing gathers their cells with scalar loads
-        // (readlane of the lane's offset, s_load_dwordx2 through the scalar cache) instead of a
-        // 64-lane vector gather: the texture-address unit, the kernel's bound, costs the same ~23
-        // cycles per vector load whatever its active lanes, and 9.5 % of fxs's slot
-        // gathers carry one ray (scripts/slot_merge_model.py's schedule).  The scalar result
-        // lands in the slot's d at its next step.  A closed slot (no chunk left) neither steps
-        // nor gathers (it used to gather the zero cell every trip: 7.9 % of the slot gathers).
-        bool sm[NS];
-        int sl0[NS], sl1[NS];
-        double sv0[NS], sv1[NS];
 #pragma unroll
         for (int r = 0; r < NS; ++r) {
             kk[r] = -1;
             d[r] = tot[r] = x[r] = y[r] = c[r] = sn[r] = 0.0;
-            sm[r] = false;
-            sl0[r] = sl1[r] = 64;
-            sv0[r] = sv1[r] = 0.0;
         }
 #pragma unroll
         for (int r = 0; r < NS; ++r)
@@ -1284,11 +1271,6 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
         // chunk has ended (a slot with no chunk left to arm closes: kk = -1, m = 0), the step
         // and its gather
         auto slot_step = [&](int r) {
-            if (SG && sm[r]) {  // the scalar gather of the slot's last ray(s) lands
-                double dv = lane == sl0[r] ? sv0[r] : 0.0;
-                if (SG > 1 && lane == sl1[r]) dv = sv1[r];
-                d[r] = dv;
-            }
             tot[r] += d[r];  // :141 (d00 for a freshly armed slot: tot = d00, :130)
             bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
             uint64_t m = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
@@ -1309,43 +1291,21 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
             bool near;
             const uint32_t off = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act,
                                                zero_v, near);
-            const uint32_t na = (uint32_t)__popcll(m);
-            if (SG && na - 1u < (uint32_t)SG) {  // wave-uniform: one (two) ray(s) left in the slot
-                uint32_t o = off;
-                const uint64_t nb = __builtin_amdgcn_ballot_w64(near) & m;
-                if (nb) {  // rare: the IEEE cell of a lane within the guard band
-                    const RayArgs &K = kernarg_here();
-                    if (lane_in(nb)) o = exact_offset_pad(K.m, x[r], y[r], (uint32_t)K.fxp_P);
-                    ++loads;
-                }
-                const int l0 = (int)__builtin_ctzll(m);
-                const uint32_t o0 = (uint32_t)__builtin_amdgcn_readlane((int)o, l0);
-                sv0[r] = ld_const(reinterpret_cast<const double *>(reinterpret_cast<const char *>(dt) + o0));
-                sl0[r] = l0;
-                if (SG > 1) {
-                    const int l1 = na > 1u ? 63 - (int)__builtin_clzll(m) : 64;
-                    if (na > 1u) {
-                        const uint32_t o1 = (uint32_t)__builtin_amdgcn_readlane((int)o, l1);
-                        sv1[r] = ld_const(reinterpret_cast<const double *>(reinterpret_cast<const char *>(dt) + o1));
-                    }
-                    sl1[r] = l1;
-                }
-                sm[r] = true;
-                scalar_gathers += na;
-            } else {
-                if (SG) sm[r] = false;
-                d[r] = ld_off(dt, off);
-                ++slot_gathers;
-                const uint64_t nb = __builtin_amdgcn_ballot_w64(near) & m;
-                if (nb) {  // rare: lanes within the guard band re-gather from the IEEE cell
-                    const RayArgs &K = kernarg_here();
-                    if (lane_in(nb)) d[r] = ld_off(dt, exact_offset_pad(K.m, x[r], y[r], (uint32_t)K.fxp_P));
-                    ++loads;
-                }
+            d[r] = ld_off(dt, off);
+            ++slot_gathers;
+            const uint64_t nb = __builtin_amdgcn_ballot_w64(near) & m;
+            if (nb) {  // rare: lanes within the guard band re-gather from the IEEE cell
+                const RayArgs &K = kernarg_here();
+                if (lane_in(nb)) d[r] = ld_off(dt, exact_offset_pad(K.m, x[r], y[r], (uint32_t)K.fxp_P));
+                loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
             }
         };
-        // both slots open: two gathers in flight per trip until a slot closes (its chunk ended
-        // with none left to arm; in that trip it gathers the zero cell once more)
+        // Both slots open: two gathers in flight per trip until a slot closes (its chunk has
+        // ended with none of the car's chunks left to arm; in that trip it gathers the zero cell
+        // once more).  Then the open slot runs alone: a closed slot used to gather the zero cell
+        // every trip until the other one ended (7.9 % of the slot gathers, 16 slot-trips per car;
+        // each such load costs the texture-address unit what a full one does):
+        // 0.706 -> 0.682 ms at 65536 cars, 0.156 -> 0.136 ms at 8192 (profiles/r05_ab/).
         if (kk[1] >= 0) {
             for (;;) {
 #pragma unroll
@@ -1362,17 +1322,9 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
                 sn[0] = sn[1];
                 kk[0] = kk[1];
                 kpar[0] = kpar[1];
-                if (SG) {
-                    sm[0] = sm[1];
-                    sl0[0] = sl0[1];
-                    sl1[0] = sl1[1];
-                    sv0[0] = sv0[1];
-                    sv1[0] = sv1[1];
-                }
             }
         }
-        // one slot left: the closed one no longer gathers
-        while (kk[0] >= 0) {
+        while (kk[0] >= 0) {  // one slot left
             slot_step(0);
             ++trips;
             ++closed_trips;
@@ -1402,13 +1354,12 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
         unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
         atomicAdd(cs, (unsigned long long)(lanes + lane_iters));  // the first lookup came from k_agents
         atomicAdd(cs + 1, (unsigned long long)lanes);
-        // lane slots of the vector gathers the loop issued: 64 per wave-level gather, the ended
-        // lanes' zero-cell reads included (SIMT = vector-gathered lookups / lane slots); counter 4:
-        // the lookups gathered by scalar loads; counter 5: slot-trips of a closed slot (no gather)
+        // lane slots of the gathers the loop issued: 64 per wave-level gather, the ended lanes'
+        // zero-cell reads included (SIMT = loop lookups / lane slots); counter 5: trips a slot
+        // spent closed (no gather issued for it)
         if (K.count_slots) {
             atomicAdd(cs + 2, (unsigned long long)slot_gathers * 64ull);
             atomicAdd(cs + 3, (unsigned long long)loads);
-            atomicAdd(cs + 4, (unsigned long long)scalar_gathers);
             atomicAdd(cs + 5, (unsigned long long)closed_trips);
         }
     }
@@ -1869,13 +1820,8 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                 ra.fxs_cy = std::fma(-a.tmap.oy, a.tmap.inv_res, kFxsBase + P + kFxsShift);
                 if (a.fx_refill > 0 && a.fxs_ok && !mask && ra.HB == 0 && !ra.wcost) {
                     // one wave per car, two chunk slots with refill (k_rays_fxs; no heavy-first)
-                    const void *fn_s[2][3] = {{reinterpret_cast<const void *>(&k_rays_fxs<false, 0>),
-                                               reinterpret_cast<const void *>(&k_rays_fxs<false, 1>),
-                                               reinterpret_cast<const void *>(&k_rays_fxs<false, 2>)},
-                                              {reinterpret_cast<const void *>(&k_rays_fxs<true, 0>),
-                                               reinterpret_cast<const void *>(&k_rays_fxs<true, 1>),
-                                               reinterpret_cast<const void *>(&k_rays_fxs<true, 2>)}};
-                    f = fn_s[single ? 0 : 1][std::min(2, std::max(0, a.fxs_sg))];
+                    f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false>)
+                               : reinterpret_cast<const void *>(&k_rays_fxs<true>);
                     ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
                     g2 = dim3((unsigned)(ra.EA * ra.G4));
                 }

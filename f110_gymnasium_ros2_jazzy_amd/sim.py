@@ -276,22 +276,22 @@ class BatchSim:
         return lk.value, rays.value
 
     def set_simt(self, on: bool = True):
-        """Count the fixed-point ray loops' lane slots (f110_set_simt; off by default)."""
-        _lib.check(self.L.f110_set_simt(self.ctx, int(bool(on))), "f110_set_simt")
+        """Count the fixed-point ray loops' lane slots (f110_debug_set_simt; off by default)."""
+        _lib.check(self.L.f110_debug_set_simt(self.ctx, int(bool(on))), "f110_debug_set_simt")
 
     def read_simt(self):
         """(loop lookups, lane slots) of the fixed-point ray loops since the
-        last counter reset (f110_read_simt); their ratio is the loop's SIMT
+        last counter reset (f110_debug_read_simt); their ratio is the loop's SIMT
         efficiency, None when the ray kernel keeps no lane-slot count."""
         lk, sl = ctypes.c_uint64(), ctypes.c_uint64()
-        _lib.check(self.L.f110_read_simt(self.ctx, ctypes.byref(lk), ctypes.byref(sl), self._stream()),
-                   "f110_read_simt")
+        _lib.check(self.L.f110_debug_read_simt(self.ctx, ctypes.byref(lk), ctypes.byref(sl), self._stream()),
+                   "f110_debug_read_simt")
         return lk.value, sl.value
 
     def read_counter(self, idx: int) -> int:
-        """Diagnostic counter idx summed over its lines (f110_read_counter)."""
+        """Diagnostic counter idx summed over its lines (f110_debug_read_counter)."""
         v = ctypes.c_uint64()
-        _lib.check(self.L.f110_read_counter(self.ctx, int(idx), ctypes.byref(v), self._stream()), "f110_read_counter")
+        _lib.check(self.L.f110_debug_read_counter(self.ctx, int(idx), ctypes.byref(v), self._stream()), "f110_debug_read_counter")
         return v.value
 
     def reset_counters(self):
@@ -318,32 +318,32 @@ class BatchSim:
 
     @property
     def ray_kernel(self) -> int:
-        """The ray kernel this context launches (f110_ray_kernel: 3 = the fixed-point kernels)."""
-        return _lib.check(self.L.f110_ray_kernel(self.ctx), "f110_ray_kernel")
+        """The ray kernel this context launches (f110_debug_ray_kernel: 3 = the fixed-point kernels)."""
+        return _lib.check(self.L.f110_debug_ray_kernel(self.ctx), "f110_debug_ray_kernel")
 
     @property
     def ray_lanes(self) -> int:
-        """Rays per lane of the fixed-point ray kernel (f110_ray_lanes: 1 = k_rays_fx, 2 = k_rays_fxn / fxs)."""
-        return _lib.check(self.L.f110_ray_lanes(self.ctx), "f110_ray_lanes")
+        """Rays per lane of the fixed-point ray kernel (f110_debug_ray_lanes: 1 = k_rays_fx, 2 = k_rays_fxn / fxs)."""
+        return _lib.check(self.L.f110_debug_ray_lanes(self.ctx), "f110_debug_ray_lanes")
 
     def set_ray_lanes(self, n: int):
-        """Rays per lane, 1 or 2 (f110_set_ray_lanes; before the first reset / step)."""
-        _lib.check(self.L.f110_set_ray_lanes(self.ctx, int(n)), "f110_set_ray_lanes")
+        """Rays per lane, 1 or 2 (f110_debug_set_ray_lanes; before the first reset / step)."""
+        _lib.check(self.L.f110_debug_set_ray_lanes(self.ctx, int(n)), "f110_debug_set_ray_lanes")
 
     def set_ray_refill(self, waves: int):
         """k_rays_fxs's waves per car (0: k_rays_fxn), with the padded EDT and heavy-first off
-        (f110_set_ray_refill)."""
-        _lib.check(self.L.f110_set_ray_refill(self.ctx, int(waves)), "f110_set_ray_refill")
+        (f110_debug_set_ray_refill)."""
+        _lib.check(self.L.f110_debug_set_ray_refill(self.ctx, int(waves)), "f110_debug_set_ray_refill")
 
     @property
     def ray_refill(self) -> int:
-        """k_rays_fxs's waves per car for unmasked steps (f110_ray_refill), 0 when k_rays_fxn /
+        """k_rays_fxs's waves per car for unmasked steps (f110_debug_ray_refill), 0 when k_rays_fxn /
         k_rays_fx trace this context's rays."""
-        return _lib.check(self.L.f110_ray_refill(self.ctx), "f110_ray_refill")
+        return _lib.check(self.L.f110_debug_ray_refill(self.ctx), "f110_debug_ray_refill")
 
     def disable_heavy_first(self):
-        """Heavy-first ray dispatch off for good (f110_disable_heavy_first; results unchanged)."""
-        _lib.check(self.L.f110_disable_heavy_first(self.ctx), "f110_disable_heavy_first")
+        """Heavy-first ray dispatch off for good (f110_debug_disable_heavy_first; results unchanged)."""
+        _lib.check(self.L.f110_debug_disable_heavy_first(self.ctx), "f110_debug_disable_heavy_first")
 
     def close(self):
         if getattr(self, "ctx", None):

@@ -84,32 +84,29 @@ class StreamShards:
         self.device = dev
         self.n_agents = int(kw.get("n_agents", 2))
         self.streams = [dedicated_stream(self.device) for _ in range(self.S)]
-        if ray_lanes is None:
-            # f110_create's rule (2 rays per lane from 12288 cars up) applied to the cars the GPU
-            # traces at once, not to one sub-shard's: 16384 envs as 2 x 8192 59.9 vs 56.0 M
-            # env-steps/s, 8192 as 4 x 2048 53.1 vs 47.6 M (profiles/r02_share_map/)
-            ray_lanes = 2 if n_envs * self.n_agents >= 12288 else 1
-        self.ray_lanes = ray_lanes
-        if refill is None:
-            # k_rays_fxs (one wave per car, refilled chunk slots, padded EDT) from 32768 cars on the
-            # GPU, as f110_create's rule for one context: 32768 envs as 2 x 16384 69.2 vs 62.6 M
-            # env-steps/s, 16384 as 2 x 8192 58.7 vs 61.5 M (profiles/r02_refill_sizes/)
-            # (with 4 sub-shards from 16384 cars: 65.3 vs 63.1 M; with 2 it lost there, 58.3 vs 61.3 M)
-            cars = n_envs * self.n_agents
-            refill = 1 if ((cars >= 32768 or (cars >= 16384 and n_streams >= 4)) and ray_lanes == 2
-                           and not heavy_first) else 0
-        self.refill = refill
+        # the ray kernel for the cars the GPU traces at once (f110_set_device_share applies
+        # f110_create's size rules to the device's cars: 8192 envs as 4 x 2048 53.1 vs 47.6 M env-steps/s
+        # with 1 vs 2 rays per lane, 32768 as 2 x 16384 69.2 vs 62.6 M with k_rays_fxs);
+        # explicit ray_lanes / refill (A/B runs) go through the f110_debug_* knobs instead
+        explicit = ray_lanes is not None or refill is not None or heavy_first
+        cars = n_envs * self.n_agents
         for s in range(self.S):
             with torch.cuda.stream(self.streams[s]):
                 sm = BatchSim(track, n_envs=self.Es, env_offset=env_offset + s * self.Es, device=self.device, **kw)
-                if not heavy_first and (n_streams > 1 or refill):
-                    # the other sub-shard's ray pass fills this one's tail; heavy-first's list
-                    # upkeep then costs more than it saves (42.5 vs 41.8 M env-steps/s)
-                    _lib.check(sm.L.f110_disable_heavy_first(sm.ctx), "f110_disable_heavy_first")
-                if sm.ray_kernel == 3:  # the fixed-point kernel (the others trace one ray per lane)
-                    _lib.check(sm.L.f110_set_ray_lanes(sm.ctx, int(ray_lanes)), "f110_set_ray_lanes")
-                    _lib.check(sm.L.f110_set_ray_refill(sm.ctx, int(refill)), "f110_set_ray_refill")
+                if not explicit:
+                    _lib.check(sm.L.f110_set_device_share(sm.ctx, cars, self.S), "f110_set_device_share")
+                else:
+                    lanes = ray_lanes if ray_lanes is not None else (2 if cars >= 12288 else 1)
+                    rf = refill if refill is not None else (
+                        1 if ((cars >= 32768 or (cars >= 16384 and n_streams >= 4)) and lanes == 2
+                              and not heavy_first) else 0)
+                    if not heavy_first and (n_streams > 1 or rf):
+                        _lib.check(sm.L.f110_debug_disable_heavy_first(sm.ctx), "f110_debug_disable_heavy_first")
+                    if sm.ray_kernel == 3:  # the fixed-point kernel (the others trace one ray per lane)
+                        _lib.check(sm.L.f110_debug_set_ray_lanes(sm.ctx, int(lanes)), "f110_debug_set_ray_lanes")
+                        _lib.check(sm.L.f110_debug_set_ray_refill(sm.ctx, int(rf)), "f110_debug_set_ray_refill")
                 self.sims.append(sm)
+        self.ray_lanes = self.sims[0].ray_lanes
         # what the contexts actually run (an unsupported map can override the request)
         self.refill = self.sims[0].ray_refill
         self._sl = [slice(s * self.Es, (s + 1) * self.Es) for s in range(self.S)]

@@ -75,7 +75,7 @@ def lib():
         L.f110_scan_batch.argtypes = [_P, _P, _i64, _P, _P, _P, _P]
         L.f110_set_params.argtypes = [_P, ctypes.POINTER(f110_params), _i32, _P]
         L.f110_set_scan_noise.argtypes = [_P, _P]
-        if L.f110_abi_version() != 2:
+        if L.f110_abi_version() != 3:  # include/f110.h F110_ABI_VERSION
             raise RuntimeError("libf110.so ABI version mismatch")
         _lib = L
     return _lib

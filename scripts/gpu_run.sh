@@ -20,6 +20,7 @@
 #   pmc        scripts/profile_round.py TAG (kernel trace + PMC passes of the headline ray kernel)
 #   ab         scripts/ray_ab.py with the caller's AB_* environment -> ab.json
 #   abhead     the same A/B with ab_libs/head.so (F110_LIB: the previous commit's build) -> abhead.json
+#   rules      scripts/shard_rules.py with the caller's SR_* environment -> rules.jsonl
 #   pmcsmall   PMC passes (no kernel trace) at 8192 and 4096 cars, the default ray kernel and k_rays_fxs
 #   trace      scripts/wave_trace.py (WT_ENVS), one context and bench's sub-shards -> trace_*.json
 #   agents     scripts/agents_probe.py (k_agents per launch: car counts, RK4 / Euler) -> agents.json
@@ -84,6 +85,7 @@ for step in "$@"; do
         ab) run ab 900 python -u scripts/ray_ab.py && cp "$OUT/ab.out" "$OUT/ab.json" ;;
         abhead) F110_LIB=$R/ab_libs/head.so run abhead 900 python -u scripts/ray_ab.py &&
                 cp "$OUT/abhead.out" "$OUT/abhead.json" ;;
+        rules) run rules 900 python -u scripts/shard_rules.py && cp "$OUT/rules.out" "$OUT/rules.jsonl" ;;
         pmcsmall) for e in 8192 4096; do
                       PROFILE_NO_TRACE=1 PROFILE_ENVS=$e run "pmc_$e" 600 python -u scripts/profile_round.py "$TAG" &&
                       PROFILE_NO_TRACE=1 PROFILE_ENVS=$e PROFILE_REFILL=1 run "pmc_${e}_fxs" 600 \

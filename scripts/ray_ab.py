@@ -5,8 +5,8 @@ scans, states, collisions after the same steps, noise + autoreset on, a masked
 reset in the middle).  Prints one JSON line.
 
 A variant is `name:KEY=V,KEY=V`; keys: F110_RAY_KERNEL / F110_FX_PAD (env at
-create; F110_FXS_SG: k_rays_fxs's scalar gathers), LANES (f110_set_ray_lanes), REFILL (f110_set_ray_refill), HEAVY=0
-(f110_disable_heavy_first), NOISE.
+create; F110_FXS_SG: k_rays_fxs's scalar gathers), LANES (f110_debug_set_ray_lanes), REFILL (f110_debug_set_ray_refill), HEAVY=0
+(f110_debug_disable_heavy_first), NOISE.
 
     AB_ENVS=8192,65536 AB_VARIANTS='fxn:REFILL=0,LANES=2;fxs:REFILL=1,LANES=2' python scripts/ray_ab.py
 """
@@ -22,7 +22,7 @@ from f110_gymnasium_ros2_jazzy_amd import _lib  # noqa: E402
 from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns, load_map  # noqa: E402
 from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim  # noqa: E402
 
-ENV_KNOBS = ("F110_RAY_KERNEL", "F110_FX_PAD", "F110_FXS_SG")
+ENV_KNOBS = ("F110_RAY_KERNEL", "F110_FX_PAD", "F110_FXS_SG", "F110_FX_SG")
 
 
 def parse_variants(spec):

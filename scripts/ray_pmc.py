@@ -13,7 +13,7 @@ sp = centerline_spawns("Spielberg", A)
 sim = BatchSim(load_map("Spielberg_map"), n_envs=E, n_agents=A, autoreset=True, spawn_poses=sp)
 if os.environ.get("MB_HEAVY", "0") != "1":
     from f110_gymnasium_ros2_jazzy_amd import _lib
-    _lib.check(sim.L.f110_disable_heavy_first(sim.ctx), "f110_disable_heavy_first")
+    _lib.check(sim.L.f110_debug_disable_heavy_first(sim.ctx), "f110_debug_disable_heavy_first")
 if os.environ.get("MB_REFILL"):  # k_rays_fxs (waves per car) instead of the size's default ray kernel
     sim.set_ray_lanes(2)
     sim.set_ray_refill(int(os.environ["MB_REFILL"]))

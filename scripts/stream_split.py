@@ -51,7 +51,7 @@ def run(E, S, K, W, seed, track, spawn, dev, join=False, fast=False, gate=False,
             streams.append(torch.cuda.Stream(dev) if S > 1 else torch.cuda.current_stream(dev))
     sl = [slice(s * Es, (s + 1) * Es) for s in range(S)]
     evs = []
-    if gate:   # ring of events: sub-shard s's ray pass waits for s-1's (f110_set_ray_gate)
+    if gate:   # ring of events: sub-shard s's ray pass waits for s-1's (f110_debug_set_ray_gate)
         import ctypes
         hip = ctypes.CDLL("libamdhip64.so")
         for s in range(S):
@@ -59,7 +59,7 @@ def run(E, S, K, W, seed, track, spawn, dev, join=False, fast=False, gate=False,
             assert hip.hipEventCreateWithFlags(ctypes.byref(e), 0x2) == 0   # hipEventDisableTiming
             evs.append(e)
         for s in range(S):
-            assert sims[s].L.f110_set_ray_gate(sims[s].ctx, evs[(s - 1) % S], evs[s]) == 0
+            assert sims[s].L.f110_debug_set_ray_gate(sims[s].ctx, evs[(s - 1) % S], evs[s]) == 0
     torch.cuda.synchronize(dev)
     for s in range(S):
         with torch.cuda.stream(streams[s]):
@@ -108,7 +108,7 @@ def run(E, S, K, W, seed, track, spawn, dev, join=False, fast=False, gate=False,
     run.host_ms = t_sub / K * 1e3
     for s in range(S):
         if gate:
-            sims[s].L.f110_set_ray_gate(sims[s].ctx, None, None)
+            sims[s].L.f110_debug_set_ray_gate(sims[s].ctx, None, None)
     obs = torch.cat([sims[s].out.obs for s in range(S)], 0).cpu()
     return E * K / dt, dt / K * 1e3, obs
 

@@ -173,8 +173,8 @@ def test_stream_shards_match_single_context(tracks, gpu, lanes, refill):
     4 dedicated-queue streams, never joined between steps, end bit-identical
     to one context stepping all envs (noise and autoreset on; the actions are
     resident before the loop, as in the bench), with the sub-shards' map
-    tables shared and 1 or 2 rays per lane (f110_set_ray_lanes), and with
-    k_rays_fxs switched on per sub-shard (f110_set_ray_refill)."""
+    tables shared and 1 or 2 rays per lane (f110_debug_set_ray_lanes), and with
+    k_rays_fxs switched on per sub-shard (f110_debug_set_ray_refill)."""
     from f110_gymnasium_ros2_jazzy_amd import _lib
     from f110_gymnasium_ros2_jazzy_amd.streams import StreamShards
     E, A, T = 256, 1, 60
@@ -187,11 +187,11 @@ def test_stream_shards_match_single_context(tracks, gpu, lanes, refill):
     sh = StreamShards(tracks("Spielberg_map"), n_envs=E, n_streams=4, ray_lanes=lanes, refill=refill,
                       n_agents=A, device=gpu, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=9)
     assert all(sm.ray_lanes == lanes for sm in sh.sims)
-    assert all(sm.ray_refill == refill for sm in sh.sims)  # f110_set_ray_refill (k_rays_fxs + padded EDT)
+    assert all(sm.ray_refill == refill for sm in sh.sims)  # f110_debug_set_ray_refill (k_rays_fxs + padded EDT)
     full.reset(poses)
     sh.reset(poses)
     with pytest.raises(RuntimeError, match="before the first"):
-        _lib.check(sh.sims[0].L.f110_set_ray_lanes(sh.sims[0].ctx, 1), "f110_set_ray_lanes")
+        _lib.check(sh.sims[0].L.f110_debug_set_ray_lanes(sh.sims[0].ctx, 1), "f110_debug_set_ray_lanes")
     for t in range(T):
         full.step(acts[t], minimal_outputs=True)
         sh.step(acts[t], minimal_outputs=True)
@@ -288,7 +288,7 @@ def test_rays_per_lane_identical_across_beam_counts(tracks, gpu, beams, A):
 
 @pytest.mark.parametrize("lanes,refill", [(1, 0), (2, 0), (2, 1)])
 def test_simt_counters(tracks, gpu, lanes, refill):
-    """f110_set_simt / f110_read_simt: the fixed-point loops count the lane
+    """f110_debug_set_simt / f110_debug_read_simt: the fixed-point loops count the lane
     slots of the gathers they issue (64 per wave-level gather: trip count x
     rays per lane, or k_rays_fxs's trips x 2 slots, closed slots included);
     loop lookups = all lookups less the first lookup of each ray (k_agents'),
@@ -323,7 +323,7 @@ def test_simt_counters(tracks, gpu, lanes, refill):
 
 @pytest.mark.parametrize("A,beams", [(1, 1080), (2, 1080), (1, 333), (1, 64)])
 def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
-    """k_rays_fxs (f110_set_ray_refill: one wave per car, two chunk slots, a
+    """k_rays_fxs (f110_debug_set_ray_refill: one wave per car, two chunk slots, a
     slot refilled with the car's next chunk as soon as its chunk ends; 1 and
     3 waves per car) against k_rays_fxn's adjacent pairs on the clamped and
     the padded table: scans, obs, collisions and states bit-identical over 25

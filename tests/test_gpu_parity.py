@@ -323,7 +323,7 @@ def test_fixed_point_cell_index_adversarial_vs_oracle(gpu, tracks, oracle_scanne
     table or, F110_FX_PAD=1, the padded one: 2^24 binade, u24 offsets, no
     clamp; origins 1-20 cells outside the map edges straddle its per-car
     test, the fast loop up to 6 cells out, the IEEE loop beyond) and
-    k_rays_fxs (f110_set_ray_refill: 1 or 3 waves per car, kFxsBase
+    k_rays_fxs (f110_debug_set_ray_refill: 1 or 3 waves per car, kFxsBase
     offsets on the padded table)."""
     from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
     monkeypatch.setenv("F110_RAY_KERNEL", kernel)

@@ -38,7 +38,7 @@ def test_exports_every_declared_symbol(L):
 
 def test_abi_and_defaults(L):
     from f110_gymnasium_ros2_jazzy_amd import _lib
-    assert L.f110_abi_version() == 2
+    assert L.f110_abi_version() == 3
     p = _lib.default_params().as_dict()
     # F110Env default params (f110_env.py:132-156)
     assert p["v_min"] == 1e-8 and p["a_max"] == 9.51 and p["sv_max"] == 3.2 and p["lidar_max"] == 30.0
