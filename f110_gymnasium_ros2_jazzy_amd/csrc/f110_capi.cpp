@@ -586,6 +586,16 @@ static void adopt_padded_table(f110_ctx *c) {
 // table's rows and columns below 2^20 (else the refill runs k_rays_fxn instead)
 static bool fxs_ok(const f110_ctx *c) { return c->rmp && c->rmp_w < (1 << 20) && c->rmp_h < (1 << 20); }
 
+// k_rays_fxs's waves per car for `cars` traced at once on the device (one context's cars, or the
+// device's under f110_set_device_share).  Round 5 (profiles/r05_ab/shard_rules_*.jsonl, env-steps/s,
+// 1 / 2 / 3 waves per car; k_rays_fx in brackets): one context 65536 90.5 / 87.6 / 82.9 M, 32768
+// 77.4 / 77.2 / 73.9, 16384 60.9 / 63.1 / 62.0, 8192 46.7 / 49.0 / 49.6 (40.2), 4096 31.8 / 34.9 /
+// 35.9 (29.6); 4 sub-shards 16384 73.7 / 74.4 / 74.0, 8192 57.1 / 60.5 / 63.0 (52.0), 4096 36.9 /
+// 41.1 / 42.2 (36.1); two-agent envs alike (8192 x 2: 25.4 / 26.3 / 25.8).  A car split over more
+// waves shortens the longest car's chain, the launch's tail where the grid is one round deep; where
+// it is many rounds deep the extra waves re-fetch the car's neighbourhood on other CUs.
+static int32_t refill_waves(int64_t cars) { return cars >= 32768 ? 1 : cars >= 16384 ? 2 : 3; }
+
 extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cfg, const f110_params *params,
                            const uint32_t *edt_k, int32_t H, int32_t W, double resolution, const double origin[3],
                            const double *spawn_poses, int32_t n_spawn) {
@@ -690,24 +700,19 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
         const uint64_t rm_bytes = ((uint64_t)W + 16) / 16 * 16 * ((uint64_t)H + 1) * 8 + 128;
         if (rm_bytes >= (1ull << 32)) c->ray_kernel = 2;
     }
-    // two or more agents per env from 8192 cars: k_rays_fxs (refill) with 2 rays per lane, one context
-    // (round 4, profiles/r04_ab/refill_sweep_a2.json: 4096 x 2 0.173 -> 0.165 ms, 8192 x 2 0.298 -> 0.261;
-    // one agent at 16384 cars keeps k_rays_fxn, 0.289 vs 0.324 ms)
-    const bool multi_refill = C.n_agents >= 2 && EA >= 8192;
+    // k_rays_fxs (one or a few waves per car, two chunk slots with refill, padded EDT) at every size
+    // since round 5, when closed slots stopped gathering; it takes no heavy-first list
+    // and needs 2 rays per lane (k_rays_fxn<2> runs the masked resets)
     if (c->ray_kernel == 3) {
-        // rays per lane: 2 keeps 2 gathers in flight per lane where the grid is deep enough
-        // (measured; k_rays ms, 1 vs 2 rays per lane: 4096 cars 0.107 / 0.124,
-        // 8192 0.165 / 0.175, 16384 0.304 / 0.284, 32768 0.637 / 0.547, 65536 1.190 / 1.054;
-        // profiles/r02_ray_ab/)
-        c->fx_ilp = (EA >= 12288 || multi_refill) ? 2 : 1;
+        c->fx_ilp = 2;
+        c->heavy_T = 0;
+    } else if (EA >= 32768 || EA <= 8192) {
+        // heavy-first (the tiled kernels) pays where one ray grid is a few rounds of waves deep (16384
+        // cars: 0.281 vs 0.287 ms), costs where it is deep (65536: 1.288 vs 1.251 ms) or one round or
+        // less (8192 cars 0.172 vs 0.167, 4096 cars 0.124 vs 0.109 ms; profiles/r02_ray_ab/ab_heavy.json,
+        // profiles/r03_ab/small_shards.json)
+        c->heavy_T = 0;
     }
-    // heavy-first pays where one ray grid is a few rounds of waves deep (16384 cars: 0.281 vs 0.287 ms)
-    // and costs where it is deep (65536 cars: 1.288 vs 1.251 ms without; profiles/r02_ray_ab/ab_heavy.json)
-    // or one round or less (round 3, every wave starts at once: 8192 cars 0.172 vs 0.167, 4096 cars
-    // 0.124 vs 0.109 ms without; profiles/r03_ab/small_shards.json); off from 32768 cars, where the
-    // refill kernel (which takes no heavy-first list) runs: at exactly 32768 it used to stay on and
-    // turn the refill off (one context 57.0 M env-steps/s, profiles/r03_ab/e32768_*.json)
-    if (EA >= 32768 || EA <= 8192 || multi_refill) c->heavy_T = 0;
     if (c->ray_kernel >= 2 && c->heavy_T > 0) {
         // up to 1/6 of the waves (measured: ~7% of the waves have a ray longer
         // than 40 lookups and carry ~46% of the wave-iterations)
@@ -749,18 +754,13 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     if (e == hipSuccess && c->spawn)
         e = hipMemcpy(c->spawn, spawn_poses, (size_t)n_spawn * C.n_agents * 3 * sizeof(double),
                       hipMemcpyHostToDevice);
-    // PAD: the clamp-free loop on a table padded by the max range (+ 8 cells of margin) where
-    // k_rays_fxs runs (from 32768 cars): there the loop is issue-bound (VALU busy 88 %) and the
-    // clamp-free offsets (46 -> 36 VALU per two-ray iteration) measured 0.999 -> 0.956 ms at 65536;
-    // k_rays_fxn, latency-bound, did not gain from them (1.029 vs 1.026 ms), DESIGN §3.3.
-    // F110_FX_PAD (A/B): 1 builds the table at any size (k_rays_fxn then runs on it), 0 never.
+    // PAD: the clamp-free loop on a table padded by the max range (+ 8 cells of margin), which
+    // k_rays_fxs needs (its offsets, kFxsBase); F110_FX_PAD=0 (A/B) never builds it: the context then
+    // steps with k_rays_fxn / k_rays_fx.
     const bool fx_ok = c->ray_kernel == 3;
-    c->fx_pad = fx_ok && (EA >= 32768 || multi_refill);
+    c->fx_pad = fx_ok;
     if (const char *v = std::getenv("F110_FX_PAD")) c->fx_pad = fx_ok && std::atoi(v) != 0;
-    // k_rays_fxs (one wave per car, two chunk slots with refill) where the grid is deep:
-    // 65536 envs as 2 x 32768 67.1 vs 63.0 M env-steps/s; at 16384 cars its long waves
-    // leave a tail (0.324 vs 0.289 ms); it runs only without heavy-first and masks
-    c->fx_refill = (EA >= 32768 || multi_refill) ? 1 : 0;
+    c->fx_refill = fx_ok && c->fx_pad ? refill_waves(EA) : 0;
     const double pad_q = std::ceil(C.max_range / resolution) + 8.0;
     const int32_t fx_pad_cells = pad_q > 0.0 && pad_q < 65536.0 ? (int32_t)pad_q : 0;  // else no padded table
     if (e == hipSuccess)
@@ -1041,12 +1041,10 @@ extern "C" int f110_set_device_share(f110_ctx *ctx, int64_t device_cars, int32_t
         if (contexts > 1) ctx->heavy_off = true;
         return F110_OK;
     }
-    // 2 rays per lane from 12288 cars on the device: 16384 envs as 2 x 8192 59.9 vs 56.0 M env-steps/s,
-    // 8192 as 4 x 2048 53.1 vs 47.6 M (profiles/r02_share_map/)
-    const int lanes = device_cars >= 12288 ? 2 : 1;
-    // k_rays_fxs from 32768 cars, or from 16384 with 4+ contexts: 32768 envs as 2 x 16384 69.2 vs 62.6 M,
-    // 16384 as 4 x 4096 65.3 vs 63.1 M; 16384 as 2 x 8192 lost (58.3 vs 61.3 M, profiles/r02_refill_*)
-    const int refill = (lanes == 2 && (device_cars >= 32768 || (device_cars >= 16384 && contexts >= 4))) ? 1 : 0;
+    // k_rays_fxs at every size, its waves per car by the device's cars (refill_waves); without the
+    // padded table (F110_FX_PAD=0) the old size rule: 2 rays per lane from 12288 cars
+    const int lanes = (ctx->fx_pad || device_cars >= 12288) ? 2 : 1;
+    const int refill = (lanes == 2 && ctx->fx_pad) ? refill_waves(device_cars) : 0;
     int rc = f110_debug_set_ray_lanes(ctx, lanes);
     if (rc == F110_OK) rc = f110_debug_set_ray_refill(ctx, refill);
     if (rc == F110_OK && contexts > 1) ctx->heavy_off = true;  // the other contexts fill this one's tail

@@ -86,9 +86,9 @@ for step in "$@"; do
         abhead) F110_LIB=$R/ab_libs/head.so run abhead 900 python -u scripts/ray_ab.py &&
                 cp "$OUT/abhead.out" "$OUT/abhead.json" ;;
         rules) run rules 900 python -u scripts/shard_rules.py && cp "$OUT/rules.out" "$OUT/rules.jsonl" ;;
-        pmcsmall) for e in 8192 4096; do
+        pmcsmall) for e in 8192 4096; do  # the default dispatch (k_rays_fxs, 3 waves per car) and round 4's k_rays_fx
                       PROFILE_NO_TRACE=1 PROFILE_ENVS=$e run "pmc_$e" 600 python -u scripts/profile_round.py "$TAG" &&
-                      PROFILE_NO_TRACE=1 PROFILE_ENVS=$e PROFILE_REFILL=1 run "pmc_${e}_fxs" 600 \
+                      PROFILE_NO_TRACE=1 PROFILE_ENVS=$e PROFILE_REFILL=0 run "pmc_${e}_fx" 600 \
                           python -u scripts/profile_round.py "$TAG" || exit $?
                   done ;;
         trace) WT_MODE=one run trace 600 python -u scripts/wave_trace.py && cp "$OUT/trace.out" "$OUT/trace_one.json" &&

@@ -24,7 +24,7 @@ ENVS = int(os.environ.get("PROFILE_ENVS", "65536"))  # the headline configuratio
 # PROFILE_REFILL=<waves per car>: the PMC passes run k_rays_fxs (2 rays per lane) instead of the size's
 # default ray kernel (files suffixed _fxs); PROFILE_NO_TRACE=1 skips the bench kernel trace (step 1)
 REFILL = os.environ.get("PROFILE_REFILL")
-SUFFIX = "_fxs" if REFILL else ""
+SUFFIX = "" if not REFILL else ("_fx" if REFILL == "0" else f"_fxs{REFILL}")
 NO_TRACE = os.environ.get("PROFILE_NO_TRACE") == "1"
 BENCH = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "300", "--warmup", "50", "--no-cpu-baseline",
          "--no-secondary", "--no-full-outputs", "--global-envs", str(ENVS)]
@@ -37,6 +37,7 @@ RAYPMC = [sys.executable, os.path.join(REPO, "scripts", "ray_pmc.py")]
 env["MB_ENVS"] = str(ENVS)
 if REFILL:
     env["MB_REFILL"] = REFILL
+    env["MB_LANES"] = "1" if REFILL == "0" else "2"  # 0: k_rays_fx, one ray per lane (the round-4 small-shard default)
 
 
 def run(name, extra, timeout=400, bench_extra=(), target=None, env_extra=None):

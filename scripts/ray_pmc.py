@@ -14,8 +14,8 @@ sim = BatchSim(load_map("Spielberg_map"), n_envs=E, n_agents=A, autoreset=True, 
 if os.environ.get("MB_HEAVY", "0") != "1":
     from f110_gymnasium_ros2_jazzy_amd import _lib
     _lib.check(sim.L.f110_debug_disable_heavy_first(sim.ctx), "f110_debug_disable_heavy_first")
-if os.environ.get("MB_REFILL"):  # k_rays_fxs (waves per car) instead of the size's default ray kernel
-    sim.set_ray_lanes(2)
+if os.environ.get("MB_REFILL"):  # a forced ray kernel: k_rays_fxs (waves per car) or, with 0, k_rays_fx(n)
+    sim.set_ray_lanes(int(os.environ.get("MB_LANES", 2)))
     sim.set_ray_refill(int(os.environ["MB_REFILL"]))
 rng = np.random.default_rng(0)
 sim.reset(sp[rng.integers(0, sp.shape[0], E)])

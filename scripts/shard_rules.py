@@ -29,22 +29,23 @@ def main():
     K = int(os.environ.get("SR_STEPS", 300))
     W = int(os.environ.get("SR_WARMUP", 30))
     rounds = int(os.environ.get("SR_ROUNDS", 3))
+    A = int(os.environ.get("SR_AGENTS", 1))
     dev = torch.device("cuda:0")
     track = load_map("Spielberg_map")
     track.ensure_edt()
-    spawn = centerline_spawns("Spielberg", 1)
+    spawn = centerline_spawns("Spielberg", A)
     for E in envs:
         rng = np.random.default_rng(12345)
         p0 = spawn[rng.integers(0, spawn.shape[0], E)]
         g = torch.Generator(device=dev)
         g.manual_seed(12345)
-        acts = torch.rand(W + K, E, 1, 2, device=dev, generator=g)
+        acts = torch.rand(W + K, E, A, 2, device=dev, generator=g)
         acts[..., 0] = acts[..., 0] * (2 * 0.4189) - 0.4189
         acts[..., 1] *= 20.0
         for S in streams:
             if E % S:
                 continue
-            kw = dict(n_agents=1, device=dev, seed=12345, noise_std=0.01, autoreset=True, spawn_poses=spawn)
+            kw = dict(n_agents=A, device=dev, seed=12345, noise_std=0.01, autoreset=True, spawn_poses=spawn)
             runs = {}
             for lanes, refill in choices:
                 name = f"lanes{lanes}_refill{refill}"
@@ -78,7 +79,7 @@ def main():
                     times[n].append(time.perf_counter() - t0)
                     last[n] = (r.obs if hasattr(r, "sims") else r.out.obs).clone()
             ref = next(iter(last.values()))
-            line = {"envs": E, "streams": S, "steps": K, "rounds": rounds}
+            line = {"envs": E, "agents": A, "streams": S, "steps": K, "rounds": rounds}
             for n in runs:
                 t = float(np.median(times[n]))
                 line[n] = {"value": E * K / t, "ms_per_step": t / K * 1e3,
