@@ -66,6 +66,7 @@ struct f110_ctx {
     double *st = nullptr, *sb = nullptr, *start = nullptr, *sim_time = nullptr, *ray0 = nullptr, *scan = nullptr;
     BeamRun *runs = nullptr;
     int32_t *nruns = nullptr;
+    PairGeom *geo = nullptr;  // [E][A][A-1] ray_cast pair geometry (A >= 2)
     uint64_t *noise_step = nullptr;
     int32_t *scnt = nullptr, *toggles = nullptr;
     uint8_t *near_start = nullptr, *pending = nullptr, *reset_flag = nullptr, *ttc_hit = nullptr;
@@ -677,6 +678,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     ALLOC(c->ray0, 3 * EA);
     ALLOC(c->runs, (size_t)kMaxSeg * EA);
     ALLOC(c->nruns, EA);
+    if (C.n_agents >= 2) ALLOC(c->geo, (size_t)EA * (C.n_agents - 1));
     ALLOC(c->scan, EA * (size_t)C.n_beams);
     ALLOC(c->reset_flag, (size_t)C.n_envs);
     ALLOC(c->ttc_hit, EA);
@@ -845,6 +847,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.ray0 = c->ray0;
     a.runs = c->runs;
     a.nruns = c->nruns;
+    a.geo = c->geo;
     a.scan = c->scan;
     a.reset_flag = c->reset_flag;
     a.ttc_hit = c->ttc_hit;

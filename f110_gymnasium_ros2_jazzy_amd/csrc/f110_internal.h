@@ -19,6 +19,8 @@ constexpr int kMaxMultiBodies = 64;  // f110_collision_multiple: bodies per set
 constexpr int kMaxChunks = 32;  // 64-beam chunks per scan (n_beams <= 2048) for the chunked ray dispatch
 
 // Everything one env step (k_agents, a ray kernel, a post kernel) needs, passed by value.
+struct PairGeom;  // below
+
 struct StepArgs {
     MapView map;
     TiledMapView tmap;
@@ -59,6 +61,8 @@ struct StepArgs {
     int32_t fx_pad;     // the padded table is built (k_rays_fxn on it unless F110_FX_PAD=0; k_rays_fxs)
     int32_t fxs_ok;     // the padded table's rows and columns are below 2^20 (kFxsBase's offsets)
     int32_t fx_refill;  // waves per car of k_rays_fxs (two chunk slots with refill; 0 = off)
+    PairGeom *geo;      // [E][A][A-1] pair geometry (A >= 2), see RayArgs::geo
+    int32_t geo_ready;  // set by launch_env_step: this step's ray kernel computed geo
     int32_t count_slots;  // f110_debug_set_simt: lane-slot counter of the fixed-point loops
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2: k_rays_fxn / k_rays_fxs)
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
@@ -109,6 +113,20 @@ inline float obs_reciprocal(float lmax) {
 
 // k_rays_tiled's own argument block: only what the ray loop and its epilogue
 // read (the full StepArgs kept 90 SGPRs live: 7 instead of 8 blocks per CU).
+// One (car, opponent) pair's agent ray_cast geometry (RaceCar.ray_cast_agents,
+// base_classes.py:206-227; laser_models.py:282-346): the opponent's box as the
+// car sees it (get_vertices with the car's params), the box's beam window at
+// the scan origin and the beam-index ranges of the blocked view the window can
+// hold.  Computed by the ray kernel's leading geometry blocks (k_rays_fxs with
+// other cars in the env) from the post-update, pre-TTC poses; k_post_multi
+// recomputes the pairs whose car's TTC fired (its yaw is zeroed).
+struct PairGeom {
+    double rv[8];
+    double phi[4];  // vertex bearings (box_beam_window's input)
+    double wc, wh;
+    int32_t rng[4];
+};
+
 struct RayArgs {
     TiledMapView m;
     const double *sines, *cosines;
@@ -162,6 +180,12 @@ struct RayArgs {
     double fxs_cx, fxs_cy;  // k_rays_fxs: 2^20 + P + 2^-26 - origin / res (see kFxsBase)
     int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_debug_read_simt)
     const double *cs2, *bs2;  // k_rays_fxs: interleaved (cos, sin) / (side, beam_cos) tables
+    // k_rays_fxs<HANDOFF>: geo_blocks leading one-wave blocks compute every pair's PairGeom
+    PairGeom *geo;
+    int32_t geo_blocks;
+    const double *st;          // state [7][EA] after k_agents
+    const f110_params *pa;     // [A] per-agent params (RaceCar.params)
+    double fov, beam_incr;
 };
 
 // k_rays_fx's magic offset: 1.5 * 2^22.  t = M + q for q in [0, 2^21) lies in

@@ -1094,6 +1094,66 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
     return act ? fast : zero_v;
 }
 
+// One (car i, opponent j) pair's ray_cast geometry, serially on one lane: the
+// same functions and operands as k_post_multi's lane-parallel phases, so the
+// same bits.  (xi, yi, yawi): car i's state pose (after the TTC response);
+// (xj, yj, thj): opponent j's agent pose (before it, base_classes.py:587).
+__device__ __forceinline__ void pair_geometry(double xi, double yi, double yawi, double xj, double yj, double thj,
+                                              double length_i, double width_i, int B, double fov, double incr,
+                                              double *rv, double *phi, double &wc, double &wh, int32_t *rng) {
+    // rv / phi point into the result's own memory (global or LDS): box_beam_window indexes them
+    // with loop variables, which local arrays would turn into scratch
+    get_vertices(xj, yj, thj, length_i, width_i, rv);  // RaceCar i's params
+    double ys, yc;
+    cr_sincos(yawi, ys, yc);
+    const double ego = atan2(ys, yc);
+    int lo = 0, hi = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int k = blocked_vertex_beam(xi, yi, ego, rv[2 * q], rv[2 * q + 1], B, fov, incr, phi[q]);
+        lo = (q == 0 || k < lo) ? k : lo;
+        hi = (q == 0 || k > hi) ? k : hi;
+    }
+    double c, h;
+    box_beam_window(xi, yi, rv, phi, c, h);
+    int r0a, r0b, r1a, r1b;
+    window_beam_ranges(yawi, fov, incr, B, c, h, r0a, r0b, r1a, r1b);
+    wc = c;
+    wh = h;
+    rng[0] = r0a > lo ? r0a : lo;
+    rng[1] = r0b < hi ? r0b : hi;
+    rng[2] = r1a > lo ? r1a : lo;
+    rng[3] = r1b < hi ? r1b : hi;
+}
+
+// pair_geometry out of line (k_post_multi's rare recompute after a TTC response):
+// inlined, its transcendentals' constants were hoisted out of the block's loops
+// and spilled
+__device__ __noinline__ void pair_geometry_ool(double xi, double yi, double yawi, double xj, double yj, double thj,
+                                               double length_i, double width_i, int B, double fov, double incr,
+                                               double *rv, double *phi, double *wc, double *wh, int32_t *rng) {
+    pair_geometry(xi, yi, yawi, xj, yj, thj, length_i, width_i, B, fov, incr, rv, phi, *wc, *wh, rng);
+}
+
+// The leading geometry blocks of k_rays_fxs<HANDOFF>: one lane per (car,
+// opponent) pair, from the state k_agents wrote (pre-TTC), beside the ray waves
+// instead of on 2-8 lanes of k_post_multi's serial chain.
+__device__ __noinline__ void ray_pair_geometry(const RayArgs &a, int blk) {
+    const int A = a.A, EA = a.EA;
+    const int NP = A - 1;
+    const int pr = blk * 64 + (int)threadIdx.x;  // pair index over the context: car g's pairs g * NP + jj
+    if (pr >= EA * NP) return;
+    const int g = pr / NP, jj = pr - g * NP;
+    const int e = g / A, i = g - e * A;
+    const int j = jj < i ? jj : jj + 1;
+    const int gj = e * A + j;
+    const f110_params &pi = a.pa[i];
+    PairGeom &o = a.geo[pr];
+    pair_geometry(a.st[g], a.st[EA + g], a.st[(size_t)4 * EA + g], a.st[gj], a.st[EA + gj],
+                  a.st[(size_t)4 * EA + gj], pi.length, pi.width, a.B, a.fov, a.beam_incr, o.rv, o.phi, o.wc, o.wh,
+                  o.rng);
+}
+
 // ------------------------------------------------------------------------
 // k_rays_fxs: one wave per car (a.G4 waves per car: wave j takes the car's
 // chunks at positions j, j+G4, ... of its chunk order; car-minor block order
@@ -1130,9 +1190,14 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
 template <bool HANDOFF>
 __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
     constexpr int NS = 2;
+    if (HANDOFF && (int)blockIdx.x < a.geo_blocks) {  // wave-uniform: a geometry block
+        ray_pair_geometry(kernarg_here(), (int)blockIdx.x);
+        return;
+    }
     wave_stamp_start(a.wtrace);
-    const int wj = (int)blockIdx.x / a.EA;
-    const int g = (int)blockIdx.x - wj * a.EA;
+    const int bid = HANDOFF ? (int)blockIdx.x - a.geo_blocks : (int)blockIdx.x;
+    const int wj = bid / a.EA;
+    const int g = bid - wj * a.EA;
     const int lane = (int)threadIdx.x;
     const int B = a.B;
     const int e = HANDOFF ? g / a.A : g;
@@ -1518,6 +1583,7 @@ struct MultiShared {
     int32_t blo[kMaxAgents * (kMaxAgents - 1)], bhi[kMaxAgents * (kMaxAgents - 1)];
     int32_t rng[kMaxAgents * (kMaxAgents - 1)][4]; // window_beam_ranges, clipped to [blo, bhi]
     int32_t col[kMaxAgents];
+    int32_t ttc[kMaxAgents];  // the car's TTC fired (its state[3:] was zeroed)
     EpiCar epi[kMaxAgents];  // env_epilogue inputs, prefetched at kernel start
     EpiEnv epe;
     int32_t do_reset;
@@ -1551,6 +1617,7 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
         get_vertices(sh.stl[tid][0], sh.stl[tid][1], sh.stl[tid][4], a.p.length, a.p.width, sh.verts[tid]);
         const int hit = a.ttc_hit[g];
         sh.col[tid] = hit;  // Simulator.step :601-602
+        sh.ttc[tid] = hit;
         if (hit) {          // RaceCar.check_ttc (base_classes.py:246-249): state[3:] = 0
 #pragma unroll
             for (int k = 3; k < 7; ++k) {
@@ -1572,7 +1639,30 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
                     sh.col[j] = 1;
                 }
     }
-    if (tid >= 64) {
+    if (tid >= 64 && a.geo_ready) {
+        // the ray launch's geometry blocks computed every pair from the pre-TTC poses; a car whose
+        // TTC fired sees its opponents from a zeroed yaw: its pairs are recomputed here
+        const int lane = tid & 63;
+        const int NP = A * (A - 1);
+        for (int pr = lane; pr < NP; pr += 64) {
+            const int i = pr / (A - 1);
+            const int jj = pr - i * (A - 1);
+            const int j = jj < i ? jj : jj + 1;
+            if (sh.ttc[i]) {
+                pair_geometry_ool(sh.stl[i][0], sh.stl[i][1], sh.stl[i][4], sh.pose0[j][0], sh.pose0[j][1],
+                                  sh.pose0[j][2], a.pa[i].length, a.pa[i].width, B, a.fov, a.beam_incr, sh.rv[pr],
+                                  sh.phi[pr], &sh.wcen[pr], &sh.whalf[pr], sh.rng[pr]);
+            } else {
+                const PairGeom &o = a.geo[(size_t)e * NP + pr];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) sh.rv[pr][k] = o.rv[k];
+                sh.wcen[pr] = o.wc;
+                sh.whalf[pr] = o.wh;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) sh.rng[pr][k] = o.rng[k];
+            }
+        }
+    } else if (tid >= 64) {
         // per-pair geometry (on wave 1 when there are two), spread over lanes:
         // boxes and ego headings, then one (pair, vertex) per lane, then
         // per-pair reductions
@@ -1770,6 +1860,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
          reinterpret_cast<const void *>(&k_rays_tiled<true, true, true, true>)}};
     const void *f = tiled_fn[ch ? 1 : 0][vt];
     unsigned bdim = ch ? 64u * (unsigned)ra.wpb : (unsigned)kBlock;
+    bool geo_ready = false;  // the ray launch computes the pairs' ray_cast geometry (k_post_multi reads it)
     // the fixed-point kernels (f110_create checked their preconditions: axis-aligned map,
     // one-wave blocks, W, H < 2^21, |origin / res| < 2^20, EDT entries 0 or > eps)
     const bool fx = a.ray_kernel == 3 && !rot && ra.wpb == 1 && a.rm;
@@ -1823,7 +1914,16 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                     f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false>)
                                : reinterpret_cast<const void *>(&k_rays_fxs<true>);
                     ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
-                    g2 = dim3((unsigned)(ra.EA * ra.G4));
+                    if (!single && a.geo) {  // leading geometry blocks (a multiple of 8: XCD mapping kept)
+                        ra.geo = a.geo;
+                        ra.geo_blocks = ((ra.EA * (a.A - 1) + 63) / 64 + 7) / 8 * 8;
+                        ra.st = a.st;
+                        ra.pa = a.pa;
+                        ra.fov = a.fov;
+                        ra.beam_incr = a.beam_incr;
+                        geo_ready = true;
+                    }
+                    g2 = dim3((unsigned)(ra.geo_blocks + ra.EA * ra.G4));
                 }
             }
         }
@@ -1839,8 +1939,11 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     if (a.gate_record && (e = hipEventRecord(a.gate_record, s)) != hipSuccess) return e;
     if (single)
         hipExtLaunchKernelGGL(k_post_single, dim3((a.E + 63) / 64), dim3(64), 0, s, evk(4), evk(5), 0, a);
-    else
-        hipExtLaunchKernelGGL(k_post_multi, dim3(a.E), dim3(kMultiBlock), 0, s, evk(4), evk(5), 0, a);
+    else {
+        StepArgs pa_ = a;
+        pa_.geo_ready = geo_ready ? 1 : 0;
+        hipExtLaunchKernelGGL(k_post_multi, dim3(a.E), dim3(kMultiBlock), 0, s, evk(4), evk(5), 0, pa_);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return hipSuccess;
 }

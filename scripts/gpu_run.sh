@@ -27,6 +27,8 @@
 #   post       scripts/post_probe.py (k_post_multi per launch at 4096 / 8192 two-agent envs) -> post.json
 #   c4one      bench.py --agents 2 --global-envs 8192 --runner one (one context) -> c4one.json
 #   x2         the headline bench as 2 ranks on the one GPU over gloo (the multi-rank path of the driver's scaling runs)
+#   weak       C3's weak-scaling shape: 2 ranks x 8192 envs per GPU on the one GPU (gloo) and 1 rank x 16384
+#              envs, same K / W / seed: their trajectory_digest must agree
 #   c5x2       the DDPG bench as 2 ranks on the one GPU over gloo (the data-parallel path, no step graphs)
 #   c4 / c5    bench.py --agents 2 --global-envs 8192 / --workload ddpg -> c4.json / c5.json
 set -o pipefail
@@ -103,6 +105,11 @@ for step in "$@"; do
         x2) F110_SAME_DEVICE=1 F110_DIST_BACKEND=gloo run x2 600 python -m torch.distributed.run --nnodes=1 \
                 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 20 \
                 --warmup 5 && cp "$OUT/x2.out" "$OUT/x2.json" ;;
+        weak) F110_SAME_DEVICE=1 F110_DIST_BACKEND=gloo run weak2 600 python -m torch.distributed.run --nnodes=1 \
+                  --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --envs-per-gpu 8192 \
+                  --steps 20 --warmup 5 && cp "$OUT/weak2.out" "$OUT/weak2.json" &&
+              run weak1 600 python -u bench.py --global-envs 16384 --steps 20 --warmup 5 --no-cpu-baseline \
+                  --no-secondary && cp "$OUT/weak1.out" "$OUT/weak1.json" ;;
         c5x2) F110_SAME_DEVICE=1 F110_DIST_BACKEND=gloo run c5x2 600 python -m torch.distributed.run --nnodes=1 \
                   --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --workload ddpg --steps 50 \
                   --warmup 20 && cp "$OUT/c5x2.out" "$OUT/c5x2.json" ;;
