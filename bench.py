@@ -141,6 +141,19 @@ def bench_ddpg(args):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     KP = min(K, 100)
     ph = {"env_step_reward_ms": 0.0, "replay_add_ms": 0.0, "learner_update_ms": 0.0}
+    # the gradient-bucket all-reduces inside the update (several ranks): events around each
+    # GradBucket.reduce on the current stream (RCCL enqueues there; gloo blocks the host meanwhile)
+    ar_pairs = []
+    if world > 1:
+        ph["learner_allreduce_ms"] = 0.0
+        for bucket in (tr.agent.critic_grads, tr.agent.actor_grads):
+            def timed_reduce(f=bucket.reduce):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                f()
+                e1.record(stream)
+                ar_pairs.append((e0, e1))
+            bucket.reduce = timed_reduce
     for _ in range(KP):
         act = tr.agent.choose_action(tr.obs, training=True, out=tr.env.agent_actions())  # as VectorTrainer.step
         ev[0].record(stream)
@@ -155,6 +168,9 @@ def bench_ddpg(args):
         ph["env_step_reward_ms"] += ev[0].elapsed_time(ev[1]) / KP
         ph["replay_add_ms"] += ev[1].elapsed_time(ev[2]) / KP
         ph["learner_update_ms"] += ev[2].elapsed_time(ev[3]) / KP
+        if ar_pairs:
+            ph["learner_allreduce_ms"] += sum(e0.elapsed_time(e1) for e0, e1 in ar_pairs) / KP
+            ar_pairs.clear()
     # data-parallel consistency: every rank must hold the same weights
     wsum = float(sum(float(p.detach().double().sum()) for p in tr.agent.actor.parameters()))
     in_sync = D.max_over_ranks(wsum) == -D.max_over_ranks(-wsum)
