@@ -16,7 +16,7 @@ LIB = os.path.join(PKG, "libf110.so")
 SOURCES = ["f110_kernels.hip", "f110_opponent.hip", "f110_reward.hip", "f110_replay.hip", "f110_adam.hip", "f110_ddpg.hip", "f110_gemm.hip",
            "f110_capi.cpp",
            "f110_replay_capi.cpp"]
-HEADERS = ["f110_device.h", "f110_internal.h"]
+HEADERS = ["f110_device.h", "f110_internal.h", "f110_sincos_table.h"]
 ARCH = os.environ.get("F110_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: the reference (Python/Numba) never fuses a*b+c; hipcc

@@ -74,7 +74,7 @@ EXPORTS = [
     "f110_host_window_ranges", "f110_track_create", "f110_track_destroy", "f110_track_arrays",
     "f110_default_reward_params", "f110_reward", "f110_replay_create", "f110_replay_destroy", "f110_replay_add", "f110_replay_add_env",
     "f110_replay_sample", "f110_replay_update_priorities", "f110_replay_length", "f110_replay_arrays",
-    "f110_debug_wave_trace", "f110_debug_set_ray_gate", "f110_debug_disable_heavy_first", "f110_debug_ray_kernel", "f110_debug_ray_lanes", "f110_debug_ray_refill", "f110_debug_set_ray_refill", "f110_debug_read_counter", "f110_step_n", "f110_debug_set_ray_lanes", "f110_set_reset_dtype", "f110_set_device_share", "f110_host_np_sincosf", "f110_host_sincos", "f110_host_map_table", "f110_get_lap_state",
+    "f110_debug_wave_trace", "f110_debug_set_ray_gate", "f110_debug_disable_heavy_first", "f110_debug_ray_kernel", "f110_debug_ray_lanes", "f110_debug_ray_refill", "f110_debug_set_ray_refill", "f110_debug_read_counter", "f110_step_n", "f110_debug_set_ray_lanes", "f110_set_reset_dtype", "f110_set_device_share", "f110_host_np_sincosf", "f110_host_sincos", "f110_host_sincos_series", "f110_host_map_table", "f110_get_lap_state",
     "f110_dynamics_ks_batch", "f110_collision_batch", "f110_collision_multiple", "f110_adam_step", "f110_ddpg_scratch_floats", "f110_ddpg_actor_head", "f110_ddpg_actor_explore",
     "f110_ddpg_actor_head_bwd", "f110_ddpg_td_target", "f110_ddpg_critic_loss", "f110_ddpg_critic_loss_bwd",
     "f110_ddpg_q_mean", "f110_ddpg_q_mean_bwd", "f110_ddpg_relu_bwd_scratch_floats", "f110_ddpg_relu_bwd",
@@ -186,6 +186,8 @@ def load(build_if_missing: bool = True):
     L.f110_host_np_sincosf.restype = None
     L.f110_host_sincos.argtypes = [_P, i64, _P, _P]
     L.f110_host_sincos.restype = None
+    L.f110_host_sincos_series.argtypes = [_P, i64, _P, _P]
+    L.f110_host_sincos_series.restype = None
     L.f110_host_map_table.argtypes = [_P, i32, i32, ctypes.c_double, i32, i32, _P, i64, _P]
     L.f110_host_map_table.restype = ctypes.c_int64
     L.f110_adam_step.argtypes = [_P, _P, _P, _P, i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
@@ -215,7 +217,7 @@ def load(build_if_missing: bool = True):
         if alternate and not hasattr(L, name):
             continue
         if name not in ("f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config",
-                        "f110_host_np_sincosf", "f110_host_sincos",
+                        "f110_host_np_sincosf", "f110_host_sincos", "f110_host_sincos_series",
                         "f110_host_tables", "f110_host_window_ranges", "f110_track_arrays",
                         "f110_default_reward_params", "f110_ddpg_scratch_floats",
                         "f110_ddpg_relu_bwd_scratch_floats", "f110_learner_wgrad_scratch_floats"):

@@ -954,6 +954,10 @@ extern "C" void f110_host_sincos(const double *x, int64_t n, double *sn, double 
     for (int64_t i = 0; i < n; ++i) cr_sincos(x[i], sn[i], cs[i]);
 }
 
+extern "C" void f110_host_sincos_series(const double *x, int64_t n, double *sn, double *cs) {
+    for (int64_t i = 0; i < n; ++i) cr_sincos_series(x[i], sn[i], cs[i]);
+}
+
 extern "C" void f110_host_np_sincosf(const float *x, int64_t n, int32_t cos_op, float *out) {
     for (int64_t i = 0; i < n; ++i) out[i] = np_sincosf(x[i], cos_op != 0);
 }

@@ -13,6 +13,7 @@
 
 #include "../../include/f110.h"
 #include "../../include/f110_debug.h"
+#include "f110_sincos_table.h"
 
 #define F110_HD __host__ __device__ __forceinline__
 #define F110_D __device__ __forceinline__
@@ -95,24 +96,20 @@ F110_HD DD dd_add(DD a, DD b) {
 // acc = c + z * acc in double-double
 F110_HD DD dd_horner(DD c, DD z, DD acc) { return dd_add(c, dd_mul(z, acc)); }
 
-F110_HD void cr_sincos(double x, double &sn, double &cs) {
-    if (!(fabs(x) < 1048576.0)) {  // NaN, inf, or beyond the exact reduction
-        sn = sin(x);
-        cs = cos(x);
-        return;
-    }
-    if (x == 0.0) {  // +-0 (keeps the sign of sin(-0.0))
-        sn = x;
-        cs = 1.0;
-        return;
-    }
+// x - k pi/2 as a double-double, k the nearest quadrant (|x| < 2^20, x != 0).
+F110_HD DD sincos_reduce(double x, double &k) {
     const double P1 = 0x1.921fb54442d18p+0, P2 = 0x1.1a62633145c07p-54, P3 = -0x1.f1976b7ed8fbcp-110;
-    const double k = rint(x * 0x1.45f306dc9c883p-1);  // x * 2/pi, nearest quadrant
-    const double r1 = fma(-k, P1, x);                 // exact: |x| >= pi/4 has ulp >= 2^-53
+    k = rint(x * 0x1.45f306dc9c883p-1);  // x * 2/pi, nearest quadrant
+    const double r1 = fma(-k, P1, x);    // exact: |x| >= pi/4 has ulp >= 2^-53
     const double q2 = k * P2;
     const double q2l = fma(k, P2, -q2);
     const DD s1 = dd_two_sum(r1, -q2);
-    const DD r = dd_fast(s1.h, s1.l - q2l - k * P3);  // x - k pi/2, double-double
+    return dd_fast(s1.h, s1.l - q2l - k * P3);
+}
+
+// sin / cos of the reduced r by the double-double series (the slow, always
+// certain path).
+F110_HD void sincos_series(DD r, double &s, double &c) {
     const DD z = dd_mul(r, r);
     const double zh = z.h;
     // sin(r) = r (1 - z/3! + z^2/5! - z^3/7! + z^4 ps(z)),  ps = 1/9! - z/11! + ... - z^5/19!
@@ -138,7 +135,91 @@ F110_HD void cr_sincos(double x, double &sn, double &cs) {
     ac = dd_horner({0x1.5555555555555p-5, 0x1.5555555555555p-59}, z, ac);    // 1/4!
     ac = dd_horner({-0.5, 0.0}, z, ac);
     ac = dd_horner({1.0, 0.0}, z, ac);
-    const double s = sr.h + sr.l, c = ac.h + ac.l;
+    s = sr.h + sr.l;
+    c = ac.h + ac.l;
+}
+
+// sin(i/64), cos(i/64) as double-doubles, i = 0..52 (scripts/gen_sincos_table.py).
+constexpr double kSinCosTab[F110_SINCOS_TAB_N][4] = {F110_SINCOS_TAB_DATA};
+
+// sin / cos of the reduced r by the table: a = |r| = i/64 + t, |t| <= 1/128,
+// sin a = S cos t + C sin t, cos a = C cos t - S sin t with (S, C) the table's
+// double-doubles and sin t / cos t short series in double with their leading
+// products exact.  The sum before the last rounding is within ~2^-68 relative
+// of sin a / cos a (the largest term is the rounding of t^3/6 against a result
+// >= 1/128 for i >= 1; i = 0 is relative to t itself); a rounding that a 2^-64
+// relative error could flip is not certain, and the caller then takes the
+// series path (about 0.1 % of the values).  Where it returns true the result
+// is the one sincos_series gives (both round the same certain value), which
+// tests/test_host_lib.py checks over a few million arguments.
+F110_HD bool sincos_table(DD r, double &s, double &c) {
+    const bool neg = r.h < 0.0;
+    const double ah = fabs(r.h), al = neg ? -r.l : r.l;
+    const int i = (int)rint(ah * 64.0);
+    const double *T = kSinCosTab[i];
+    const double th = ah - (double)i * 0.015625;  // exact (Sterbenz)
+    const double tl = al;
+    const double zh = th * th;
+    const double zl = fma(th, th, -zh);
+    // sin t = th + slo:  t - t^3/6 + t^5/120 - ...  with the t^2 tl / 2 cross term of t^3 / 6
+    const double P = -0x1.5555555555555p-3 +
+                     zh * (0x1.1111111111111p-7 + zh * (-0x1.a01a01a01a01ap-13 + zh * 0x1.71de3a556c734p-19));
+    const double slo = tl + (th * (zh * P) - (0.5 * zh) * tl);
+    // cos t = ch + cl:  1 - t^2/2 + t^4/24 - t^6/720 + t^8/40320
+    const double Q = 0x1.5555555555555p-5 + zh * (-0x1.6c16c16c16c17p-10 + zh * 0x1.a01a01a01a01ap-16);
+    const double hz = 0.5 * zh;
+    const double ch = 1.0 - hz;
+    const double cl = ((1.0 - ch) - hz) - ((0.5 * zl + th * tl) - (zh * zh) * Q);
+    const double Sh = T[0], Sl = T[1], Ch = T[2], Cl = T[3];
+    // sin a = Sh ch + Ch th + (Sh cl + Sl ch + Ch slo + Cl th)
+    const double p1 = Sh * ch, e1 = fma(Sh, ch, -p1);
+    const double p2 = Ch * th, e2 = fma(Ch, th, -p2);
+    const DD sa = dd_two_sum(p1, p2);
+    const double sl = sa.l + (e1 + e2) + (((Sh * cl + Sl * ch) + Cl * th) + Ch * slo);
+    // cos a = Ch ch - Sh th + (Ch cl + Cl ch - Sh slo - Sl th)
+    const double q1 = Ch * ch, f1 = fma(Ch, ch, -q1);
+    const double q2 = -(Sh * th), f2 = fma(-Sh, th, -q2);
+    const DD ca = dd_two_sum(q1, q2);
+    const double cl2 = ca.l + (f1 + f2) + (((Ch * cl + Cl * ch) - Sl * th) - Sh * slo);
+    const double es = fabs(sa.h) * 0x1p-64, ec = 0x1p-64;  // |cos a| > 0.7
+    const double s_up = sa.h + (sl + es), s_dn = sa.h + (sl - es);
+    const double c_up = ca.h + (cl2 + ec), c_dn = ca.h + (cl2 - ec);
+    if (s_up != s_dn || c_up != c_dn) return false;
+    s = neg ? -s_up : s_up;
+    c = c_up;
+    return true;
+}
+
+F110_HD void cr_sincos(double x, double &sn, double &cs) {
+    if (!(fabs(x) < 1048576.0)) {  // NaN, inf, or beyond the exact reduction
+        sn = sin(x);
+        cs = cos(x);
+        return;
+    }
+    if (x == 0.0) {  // +-0 (keeps the sign of sin(-0.0))
+        sn = x;
+        cs = 1.0;
+        return;
+    }
+    double k, s, c;
+    const DD r = sincos_reduce(x, k);
+    if (!sincos_table(r, s, c)) sincos_series(r, s, c);
+    switch ((int)((int64_t)k & 3)) {
+        case 0: sn = s; cs = c; break;
+        case 1: sn = c; cs = -s; break;
+        case 2: sn = -s; cs = -c; break;
+        default: sn = -c; cs = s; break;
+    }
+}
+
+// The series path alone (tests: the table path must give the same bits).
+F110_HD void cr_sincos_series(double x, double &sn, double &cs) {
+    if (!(fabs(x) < 1048576.0) || x == 0.0) {
+        cr_sincos(x, sn, cs);
+        return;
+    }
+    double k, s, c;
+    sincos_series(sincos_reduce(x, k), s, c);
     switch ((int)((int64_t)k & 3)) {
         case 0: sn = s; cs = c; break;
         case 1: sn = c; cs = -s; break;

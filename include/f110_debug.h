@@ -157,6 +157,9 @@ F110_API int64_t f110_host_map_table(const uint32_t *edt_k, int32_t H, int32_t W
  * the non-exact budgets (tests/golden/nonexact_beams.json) pin.  Test hook,
  * no reference counterpart. */
 F110_API void f110_host_sincos(const double *x, int64_t n, double *sn, double *cs);
+/* The same with the table path off (every value by the double-double
+ * series): f110_host_sincos must give the same bits (test hook). */
+F110_API void f110_host_sincos_series(const double *x, int64_t n, double *sn, double *cs);
 /* NumPy's float32 np.cos (cos_op != 0) / np.sin over n values, as the
  * device evaluates F110Env.reset's float32 start_rot (test hook). */
 F110_API void f110_host_np_sincosf(const float *x, int64_t n, int32_t cos_op, float *out);

@@ -314,7 +314,31 @@ def test_cr_sincos_matches_numpy():
     assert np.isnan(sn).all() and np.isnan(cn).all()
 
 
-@pytest.mark.parametrize("H,W,pad", [(7, 5, 3), (40, 33, 12), (1, 1, 1), (16, 15, 0)])
+def test_cr_sincos_table_equals_series():
+    """cr_sincos's table path (sin / cos of i/64 plus short series, taken
+    where its rounding is certain) gives the same bits as the double-double
+    series alone (f110_host_sincos_series) on uniform, scan-grid, tiny,
+    large, table-cell-edge and near-quadrant arguments."""
+    import ctypes
+    from f110_gymnasium_ros2_jazzy_amd import _lib
+    L = _lib.load()
+    rng = np.random.default_rng(29)
+    x = np.concatenate([
+        rng.uniform(-2 * np.pi, 2 * np.pi, 1_500_000), rng.uniform(-1e5, 1e5, 300_000),
+        np.exp(rng.uniform(np.log(1e-300), 0.0, 300_000)) * rng.choice([-1.0, 1.0], 300_000),
+        ((-2.35 + np.arange(1080) * (4.7 / 1079))[None, :] + rng.uniform(-np.pi, np.pi, (300, 1))).ravel(),
+        ((np.arange(-60, 60)[:, None] + 0.5) / 64 + np.arange(-100, 101)[None, :] * 2.0 ** -52).ravel(),
+        ((np.arange(-40000, 40000) * (np.pi / 2))[:, None] * (1 + np.arange(-3, 4)[None, :] * 2.0 ** -52)).ravel(),
+    ])
+    out = [np.empty_like(x) for _ in range(4)]
+    p = [a.ctypes.data_as(ctypes.c_void_p) for a in [x] + out]
+    L.f110_host_sincos(p[0], x.size, p[1], p[2])
+    L.f110_host_sincos_series(p[0], x.size, p[3], p[4])
+    assert np.array_equal(out[0].view(np.int64), out[2].view(np.int64))
+    assert np.array_equal(out[1].view(np.int64), out[3].view(np.int64))
+
+
+@pytest.mark.parametrize("H,W,pad",[(7, 5, 3), (40, 33, 12), (1, 1, 1), (16, 15, 0)])
 def test_host_map_tables(L, H, W, pad):
     """The fixed-point kernels' EDT tables as f110_create builds them
     (f110_host_map_table, the same host code): the row-major table (rows of
