@@ -327,10 +327,13 @@ struct ReplayBatch {     // one sample(): the gathered batch (device, contiguous
     int32_t vec4;
 };
 
-hipError_t launch_replay_add(const ReplayView &v, const ReplayRows &in, const uint8_t *mask, int mask_skip,
-                             int64_t n, hipStream_t s);
-hipError_t launch_replay_sample(const ReplayView &v, int32_t batch, double beta, int64_t *idx, float *w,
-                                const ReplayBatch &out, bool known_full, hipStream_t s);
+hipError_t launch_replay_add_index(const ReplayView &v, const uint8_t *mask, int mask_skip, const float *priority,
+                                   int64_t n, hipStream_t s);  // ring slots, priorities, header
+hipError_t launch_replay_add_copy(const ReplayView &v, const ReplayRows &in, int64_t n, hipStream_t s);  // the rows
+hipError_t launch_replay_select(const ReplayView &v, int32_t batch, double beta, int64_t *idx, float *w,
+                                bool known_full, hipStream_t s);  // idx / weights (reads no row data)
+hipError_t launch_replay_gather(const ReplayView &v, int32_t batch, const int64_t *idx, const ReplayBatch &out,
+                                hipStream_t s);
 hipError_t launch_replay_update(const ReplayView &v, const int64_t *idx, const float *val, int64_t n, float add_eps,
                                 int32_t from_td, int32_t serial, hipStream_t s);
 hipError_t prepare_replay(int32_t max_batch);

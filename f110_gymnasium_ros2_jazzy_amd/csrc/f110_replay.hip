@@ -43,6 +43,8 @@ namespace {
 
 constexpr int kRB = 256;         // threads per block of the streaming kernels
 constexpr int kOneBlock = 1024;  // single-workgroup kernels
+constexpr int kKB = 1024;        // threads per block of k_keys (4 streaming blocks in one: a quarter of the
+                                 // same-address atomics merging the blocks' top-digit histograms)
 
 __device__ __forceinline__ uint32_t f32_bits(float v) { return __float_as_uint(v); }
 
@@ -51,6 +53,13 @@ __device__ __forceinline__ uint32_t f32_bits(float v) { return __float_as_uint(v
 __device__ __forceinline__ double prio_weight(float p, float eps, double alpha) {
     const float s = p + eps;
     return pow((double)s, alpha);
+}
+
+// One row's IS weight before the normalisation (replay_buffer.py:103-108):
+// probs[i] = w_i / den, (len * probs[i]) ** -beta.
+__device__ __forceinline__ double is_weight(const ReplayView &v, int64_t i, int64_t len, double den, double beta) {
+    const double p = v.wt[i] / den;
+    return pow((double)len * p, -beta);
 }
 
 // p0 of add() (replay_buffer.py:52-63) from the max priority.
@@ -78,6 +87,20 @@ __device__ __forceinline__ double block_sum_f64(double v, double *sh) {
     if (threadIdx.x == 0)
         for (int w = 0; w < nw; ++w) t += sh[w];
     return t;  // valid in thread 0
+}
+
+// hist[bin] += 1 for every active lane, one LDS atomic per distinct bin of
+// the wave: the top digit of the keys falls into a few bins (the exponent's
+// high bits), and same-address LDS atomics of a wave serialise lane by lane.
+__device__ __forceinline__ void hist_add_wave(uint32_t *hist, uint32_t bin) {
+    uint64_t pending = __builtin_amdgcn_read_exec();
+    while (pending) {  // wave-uniform: one trip per distinct bin
+        const int leader = __builtin_ctzll(pending);
+        const uint32_t lb = __builtin_amdgcn_readlane(bin, leader);
+        const uint64_t same = __builtin_amdgcn_ballot_w64(bin == lb) & pending;
+        if ((int)(threadIdx.x & 63) == leader) atomicAdd(&hist[lb], (uint32_t)__builtin_popcountll(same));
+        pending &= ~same;
+    }
 }
 
 }  // namespace
@@ -210,29 +233,45 @@ __global__ void __launch_bounds__(kRB) k_add_copy(ReplayView v, ReplayRows in, i
 // ------------------------------------------------------------- sample ------
 // Pass 0: sampling weights w_i, per-block partial sums of w (den, :88-89),
 // exponential-race keys and the top-digit histogram.
-__global__ void __launch_bounds__(kRB) k_keys(ReplayView v, int32_t batch) {
+// Launched as keys_grid(vgrid) blocks of kKB threads: block b runs the
+// kKB / kRB virtual blocks 4b .. 4b+3 of the streaming grid (vgrid blocks of
+// kRB threads: the same rows per thread and the same den partials, summed
+// per virtual block in wave order, as one kRB block each), with one LDS
+// histogram and one set of global atomics per real block.
+__global__ void __launch_bounds__(kKB) k_keys(ReplayView v, int32_t batch, int vgrid) {
+    constexpr int Q = kKB / kRB;
     __shared__ uint32_t hist[256];
-    __shared__ double sh[kRB / 64];
+    __shared__ double sh[kKB / 64];
     const int64_t len = v.hdr->length;
     if (len < batch) return;  // block-uniform
     const uint64_t draw = v.hdr->draws;
-    hist[threadIdx.x] = 0;
+    const int q = (int)threadIdx.x / kRB, t = (int)threadIdx.x - q * kRB;
+    const int vb = (int)blockIdx.x * Q + q;
+    if (threadIdx.x < 256) hist[threadIdx.x] = 0;
     __syncthreads();
     double acc = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kRB + threadIdx.x; i < len; i += (int64_t)gridDim.x * kRB) {
-        const double w = v.wt[i];  // prio_weight(prio[i]), cached at add / update
-        acc += w;
-        U4 c = {(uint32_t)i, (uint32_t)((uint64_t)i >> 32), (uint32_t)draw, (uint32_t)(draw >> 32)};
-        U4 r = philox(c, (uint32_t)v.seed, (uint32_t)(v.seed >> 32) ^ 0x9E3779B9u);
-        const double e = -log(u01_open(r.x, r.y));  // Exp(1)
-        const uint32_t key = f32_bits((float)(e / w));
-        v.keys[i] = key;
-        atomicAdd(&hist[key >> 24], 1u);
-    }
-    const double bsum = block_sum_f64(acc, sh);
-    if (threadIdx.x == 0) v.den_part[blockIdx.x] = bsum;
+    if (vb < vgrid)
+        for (int64_t i = (int64_t)vb * kRB + t; i < len; i += (int64_t)vgrid * kRB) {
+            const double w = v.wt[i];  // prio_weight(prio[i]), cached at add / update
+            acc += w;
+            U4 c = {(uint32_t)i, (uint32_t)((uint64_t)i >> 32), (uint32_t)draw, (uint32_t)(draw >> 32)};
+            U4 r = philox(c, (uint32_t)v.seed, (uint32_t)(v.seed >> 32) ^ 0x9E3779B9u);
+            const double e = -log(u01_open(r.x, r.y));  // Exp(1)
+            const uint32_t key = f32_bits((float)(e / w));
+            v.keys[i] = key;
+            hist_add_wave(hist, key >> 24);
+        }
+    // per virtual block: a shuffle tree per wave, its waves added in order (block_sum_f64)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (hist[threadIdx.x]) atomicAdd(&v.hist[threadIdx.x], hist[threadIdx.x]);
+    if ((int)threadIdx.x < Q && (int)blockIdx.x * Q + (int)threadIdx.x < vgrid) {
+        double tsum = 0.0;
+        for (int w = 0; w < kRB / 64; ++w) tsum += sh[threadIdx.x * (kRB / 64) + w];
+        v.den_part[blockIdx.x * Q + threadIdx.x] = tsum;
+    }
+    if (threadIdx.x < 256 && hist[threadIdx.x]) atomicAdd(&v.hist[threadIdx.x], hist[threadIdx.x]);
 }
 
 // The digits of the batch-th smallest key from the histograms of passes
@@ -371,17 +410,14 @@ __global__ void __launch_bounds__(kRB) k_place(ReplayView v, int32_t batch) {
     if (blockIdx.x == gridDim.x - 1 && t == 0) v.hdr->n_lt = off;  // total below T
 }
 
-// IS weights (replay_buffer.py:103-113) of the selected rows.
-__device__ void write_weights(const ReplayView &v, const int64_t *idx, int32_t batch, int64_t len, double den,
-                              double beta, double *wsh, int64_t *idx_out, float *w_out) {
+// IS weights (replay_buffer.py:103-113) of the selected rows: wsh[j] holds
+// row idx[j]'s weight before the normalisation (is_weight); divided by their
+// max (:109-112) into w_out.
+__device__ void normalize_weights(const int64_t *idx, int32_t batch, const double *wsh, int64_t *idx_out,
+                                  float *w_out) {
     __shared__ double wm[kOneBlock / 64];
     double m = -INFINITY;
-    for (int j = threadIdx.x; j < batch; j += blockDim.x) {
-        const double p = v.wt[idx[j]] / den;
-        const double w = pow((double)len * p, -beta);
-        wsh[j] = w;
-        m = fmax(m, w);
-    }
+    for (int j = threadIdx.x; j < batch; j += blockDim.x) m = fmax(m, wsh[j]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
     if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
@@ -439,7 +475,8 @@ __global__ void __launch_bounds__(kOneBlock) k_finish(ReplayView v, int32_t batc
         idx[lo + c] = (int64_t)ti;
     }
     __syncthreads();
-    write_weights(v, idx, batch, len, v.hdr->den, beta, wsh, idx_out, w_out);
+    for (int j = threadIdx.x; j < batch; j += blockDim.x) wsh[j] = is_weight(v, idx[j], len, v.hdr->den, beta);
+    normalize_weights(idx, batch, wsh, idx_out, w_out);
     if (threadIdx.x == 0) {
         v.hdr->draws += 1;
         v.hdr->replace = 0;
@@ -483,7 +520,8 @@ __global__ void __launch_bounds__(kOneBlock) k_sample_replace(ReplayView v, int3
         idx[j] = lo;
     }
     __syncthreads();
-    write_weights(v, idx, batch, len, den, beta, wsh, idx_out, w_out);
+    for (int j = threadIdx.x; j < batch; j += blockDim.x) wsh[j] = is_weight(v, idx[j], len, den, beta);
+    normalize_weights(idx, batch, wsh, idx_out, w_out);
     if (threadIdx.x == 0) {
         v.hdr->draws += 1;
         v.hdr->replace = 1;
@@ -575,26 +613,34 @@ int replay_grid(int64_t capacity) {
     return (int)(g < 1 ? 1 : (g > kReplayMaxGrid ? kReplayMaxGrid : g));
 }
 
+// k_keys's blocks for a streaming grid of `grid` blocks
+int keys_grid(int grid) { return (grid + kKB / kRB - 1) / (kKB / kRB); }
+
 size_t replay_finish_lds(int32_t batch) { return (size_t)batch * 16; }
 
 size_t replay_replace_lds(int32_t batch) { return (size_t)batch * 24; }
 
-hipError_t launch_replay_add(const ReplayView &v, const ReplayRows &in, const uint8_t *mask, int mask_skip,
-                             int64_t n, hipStream_t s) {
+hipError_t launch_replay_add_index(const ReplayView &v, const uint8_t *mask, int mask_skip, const float *priority,
+                                   int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int grid = replay_grid(v.capacity);
     hipLaunchKernelGGL(k_prio_max, dim3(grid), dim3(kRB), 0, s, v);
-    hipLaunchKernelGGL(k_add_scan, dim3(1), dim3(kOneBlock), 0, s, v, mask, in.priority, n, grid, mask_skip);
+    hipLaunchKernelGGL(k_add_scan, dim3(1), dim3(kOneBlock), 0, s, v, mask, priority, n, grid, mask_skip);
+    return hipGetLastError();
+}
+
+hipError_t launch_replay_add_copy(const ReplayView &v, const ReplayRows &in, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_add_copy, dim3((unsigned)n), dim3(kRB), 0, s, v, in, n);
     return hipGetLastError();
 }
 
-hipError_t launch_replay_sample(const ReplayView &v, int32_t batch, double beta, int64_t *idx, float *w,
-                                const ReplayBatch &out, bool known_full, hipStream_t s) {
+hipError_t launch_replay_select(const ReplayView &v, int32_t batch, double beta, int64_t *idx, float *w,
+                                bool known_full, hipStream_t s) {
     const int grid = replay_grid(v.capacity);
     // histograms and tie count are cleared by k_place / k_finish of the previous sample
     // (and at create), so a sample is kernels only
-    hipLaunchKernelGGL(k_keys, dim3(grid), dim3(kRB), 0, s, v, batch);
+    hipLaunchKernelGGL(k_keys, dim3(keys_grid(grid)), dim3(kKB), 0, s, v, batch, grid);
     for (int pass = 1; pass < 4; ++pass)  // each block selects the digits so far from the histograms itself
         hipLaunchKernelGGL(k_hist, dim3(grid), dim3(kRB), 0, s, v, batch, pass);
     hipLaunchKernelGGL(k_count, dim3(grid), dim3(kRB), 0, s, v, batch, grid);
@@ -603,6 +649,11 @@ hipError_t launch_replay_sample(const ReplayView &v, int32_t batch, double beta,
     if (!known_full)  // (f110_replay_length has seen length >= batch: the with-replacement path cannot run)
         hipLaunchKernelGGL(k_sample_replace, dim3(1), dim3(kOneBlock), replay_replace_lds(batch), s, v, batch, beta,
                            idx, w);
+    return hipGetLastError();
+}
+
+hipError_t launch_replay_gather(const ReplayView &v, int32_t batch, const int64_t *idx, const ReplayBatch &out,
+                                hipStream_t s) {
     if (out.obs) hipLaunchKernelGGL(k_gather, dim3((unsigned)batch), dim3(kRB), 0, s, v, batch, idx, out);
     return hipGetLastError();
 }

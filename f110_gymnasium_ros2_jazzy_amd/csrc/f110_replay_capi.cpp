@@ -127,7 +127,9 @@ int replay_add(f110_replay *rb, const char *fn, const float *obs, int64_t obs_st
     in.act_stride = act_stride;
     in.vec4 = (v.obs_dim % 4 == 0 && obs_stride % 4 == 0 && next_stride % 4 == 0 && aligned16(obs) &&
                aligned16(next_obs)) ? 1 : 0;
-    hipError_t e = launch_replay_add(v, in, mask, mask_skip, n, (hipStream_t)stream);
+    const hipStream_t s = (hipStream_t)stream;
+    hipError_t e = launch_replay_add_index(v, mask, mask_skip, priority, n, s);
+    if (e == hipSuccess) e = launch_replay_add_copy(v, in, n, s);
     if (e != hipSuccess) return fail(F110_E_HIP, std::string(fn) + ": " + hipGetErrorString(e));
     return F110_OK;
 }
@@ -165,8 +167,9 @@ extern "C" int f110_replay_sample(f110_replay *rb, int32_t batch, double beta, i
     out.reward = reward;
     out.done = done;
     out.vec4 = (rb->v.obs_dim % 4 == 0 && obs && aligned16(obs) && aligned16(next_obs)) ? 1 : 0;
-    hipError_t e = launch_replay_sample(rb->v, batch, beta, idx, weights, out, rb->known_len >= batch,
-                                        (hipStream_t)stream);
+    const hipStream_t s = (hipStream_t)stream;
+    hipError_t e = launch_replay_select(rb->v, batch, beta, idx, weights, rb->known_len >= batch, s);
+    if (e == hipSuccess) e = launch_replay_gather(rb->v, batch, idx, out, s);
     if (e != hipSuccess) return fail(F110_E_HIP, std::string("f110_replay_sample: ") + hipGetErrorString(e));
     return F110_OK;
 }
