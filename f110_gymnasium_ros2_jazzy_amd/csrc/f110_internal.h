@@ -180,7 +180,7 @@ struct RayArgs {
     double fxs_cx, fxs_cy;  // k_rays_fxs: 2^20 + P + 2^-26 - origin / res (see kFxsBase)
     int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_debug_read_simt)
     const double *cs2, *bs2;  // k_rays_fxs: interleaved (cos, sin) / (side, beam_cos) tables
-    // k_rays_fxs<HANDOFF>: geo_blocks leading one-wave blocks compute every pair's PairGeom
+    // k_rays_fxs<HANDOFF>: geo_blocks leading work items (one wave each) compute every pair's PairGeom
     PairGeom *geo;
     int32_t geo_blocks;
     const double *st;          // state [7][EA] after k_agents
@@ -221,6 +221,8 @@ constexpr uint32_t kFxpBand = 4u;
 constexpr double kFxsBase = 1048576.0;
 constexpr double kFxsShift = 0x1p-26;
 constexpr uint32_t kFxsBand = 64u;  // 2^-26 in units of 2^-32
+constexpr int kFxsWaves = 8;         // k_rays_fxs: work items (one wave each) per block, sharing one LDS theta table
+constexpr int kFxsLdsTheta = 2048;   // theta table entries the block's LDS copy holds (32 KB; theta_dis 2000)
 
 struct ScanArgs {
     MapView map;

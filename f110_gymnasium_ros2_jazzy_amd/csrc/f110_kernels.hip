@@ -637,6 +637,21 @@ __device__ __forceinline__ void wave_stamp_end(uint64_t *wt, uint32_t item, uint
         o[3] = ((uint64_t)item << 32) | g;
     }
 }
+// the same per wave of a multi-wave block (k_rays_fxs): record w = the wave's work item
+__device__ __forceinline__ void wave_stamp_start_w(uint64_t *wt, int w) {
+    if (wt && (threadIdx.x & 63) == 0) wt[4 * (size_t)w] = __builtin_amdgcn_s_memrealtime();
+}
+__device__ __forceinline__ void wave_stamp_end_w(uint64_t *wt, int w, uint32_t item, uint32_t g) {
+    if (wt && (threadIdx.x & 63) == 0) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        uint64_t *o = wt + 4 * (size_t)w;
+        o[1] = __builtin_amdgcn_s_memrealtime();
+        o[2] = ((uint64_t)xcc << 32) | hw;
+        o[3] = ((uint64_t)item << 32) | g;
+    }
+}
 
 // Every lane runs one ray; lanes whose ray has ended leave the loop (exec
 // mask), each lane counts its own lookups (summed once per wave), and cars
@@ -1141,7 +1156,7 @@ __device__ __noinline__ void pair_geometry_ool(double xi, double yi, double yawi
 __device__ __noinline__ void ray_pair_geometry(const RayArgs &a, int blk) {
     const int A = a.A, EA = a.EA;
     const int NP = A - 1;
-    const int pr = blk * 64 + (int)threadIdx.x;  // pair index over the context: car g's pairs g * NP + jj
+    const int pr = blk * 64 + (int)(threadIdx.x & 63);  // pair index over the context: car g's pairs g * NP + jj
     if (pr >= EA * NP) return;
     const int g = pr / NP, jj = pr - g * NP;
     const int e = g / A, i = g - e * A;
@@ -1187,18 +1202,34 @@ __device__ __noinline__ void ray_pair_geometry(const RayArgs &a, int blk) {
 // gather every trip, a closed slot on the zero cell).  Per slot and trip: the
 // total (:141), the activity test (:133), the refill when the slot's chunk has
 // ended, the step (:135-136) and its gather.
+// Single-agent contexts (HANDOFF false) run kFxsWaves work items per block with the theta
+// table's (cos, sin) pairs in one LDS copy per block: the arms read them there instead of a
+// 16-byte gather each (a wave-level load for the texture-address unit, ~24 cycles like a slot
+// gather: 17 per car).  Multi-agent contexts keep one-wave blocks and the
+// gathers: the 8-wave blocks were slower there (C4 one context 27.7 -> 25.2 M).
 template <bool HANDOFF>
-__global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
+__global__ void __launch_bounds__(HANDOFF ? 64 : 64 * kFxsWaves, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
     constexpr int NS = 2;
-    if (HANDOFF && (int)blockIdx.x < a.geo_blocks) {  // wave-uniform: a geometry block
-        ray_pair_geometry(kernarg_here(), (int)blockIdx.x);
+    constexpr bool LDS = !HANDOFF;
+    constexpr int W = LDS ? kFxsWaves : 1;  // work items (waves) per block
+    __shared__ double2 cs_lds[LDS ? kFxsLdsTheta : 1];
+    const int wave = LDS ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+    if (LDS) {
+        const double2 *src = reinterpret_cast<const double2 *>(a.cs2);
+        for (int k = (int)threadIdx.x; k < a.theta_dis; k += 64 * W) cs_lds[k] = src[k];
+        __syncthreads();
+    }
+    const int item = (int)blockIdx.x * W + wave;  // the wave's work item
+    if (item >= (HANDOFF ? a.geo_blocks : 0) + a.EA * a.G4) return;  // the last block's spare waves
+    if (HANDOFF && item < a.geo_blocks) {  // wave-uniform: a geometry item
+        ray_pair_geometry(kernarg_here(), item);
         return;
     }
-    wave_stamp_start(a.wtrace);
-    const int bid = HANDOFF ? (int)blockIdx.x - a.geo_blocks : (int)blockIdx.x;
+    wave_stamp_start_w(a.wtrace, item);
+    const int bid = HANDOFF ? item - a.geo_blocks : item;
     const int wj = bid / a.EA;
     const int g = bid - wj * a.EA;
-    const int lane = (int)threadIdx.x;
+    const int lane = (int)(threadIdx.x & 63);
     const int B = a.B;
     const int e = HANDOFF ? g / a.A : g;
     const int nch = (B + 63) >> 6;
@@ -1232,8 +1263,9 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
         kinfo = lo;
     }
     // wave-level vector loads other than the slot gathers (SIMT / TA accounting, counter 3):
-    // the arms' and finishes' table loads, the guard-band re-gathers (wave-uniform, scalar)
-    uint32_t loads = 0;
+    // the wave's share of the block's table copy (LDS) or the arms' table loads, the finishes'
+    // TTC table loads, the guard-band re-gathers (wave-uniform, scalar)
+    uint32_t loads = LDS ? (uint32_t)((a.theta_dis - 64 * wave + 64 * W - 1) / (64 * W)) : 0u;
     uint32_t trips = 0;
     // in_loop: the slot's next `tot += d` completes tot = d (:130)
     auto arm = [&](int r, bool in_loop) {
@@ -1246,8 +1278,13 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
         const int lo = __builtin_amdgcn_readlane(kinfo, k);
         int ti = (int)beam_theta(K.runs + (size_t)g * kMaxSeg, ld_const(K.nruns + g), lo, k * 64, bc);  // :124
         if (ti >= K.theta_dis) ti = 0;
-        const double2 t2 = ld_off(reinterpret_cast<const double2 *>(K.cs2), (uint32_t)ti * 16u);
-        loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
+        double2 t2;
+        if (LDS) {
+            t2 = cs_lds[ti];
+        } else {
+            t2 = ld_off(reinterpret_cast<const double2 *>(K.cs2), (uint32_t)ti * 16u);
+            loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
+        }
         c[r] = t2.x;
         sn[r] = t2.y;
         x[r] = x00;
@@ -1416,7 +1453,7 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
     }
     if (lane == 0) {
         const RayArgs &K = kernarg_here();
-        unsigned long long *cs = K.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride;
+        unsigned long long *cs = K.ctr + (size_t)(item % kCtrSlots) * kCtrStride;
         atomicAdd(cs, (unsigned long long)(lanes + lane_iters));  // the first lookup came from k_agents
         atomicAdd(cs + 1, (unsigned long long)lanes);
         // lane slots of the gathers the loop issued: 64 per wave-level gather, the ended lanes'
@@ -1430,10 +1467,10 @@ __global__ void __launch_bounds__(64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per
     }
     if (a.count_slots) {  // the run search's wave-level loads (counter 3)
         const uint32_t ws = wave_max(srch);
-        if (lane == 0) atomicAdd(a.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride + 3, (unsigned long long)ws);
+        if (lane == 0) atomicAdd(a.ctr + (size_t)(item % kCtrSlots) * kCtrStride + 3, (unsigned long long)ws);
     }
-    wave_stamp_end(kernarg_here().wtrace, (uint32_t)(trips < 0xffffu ? trips : 0xffffu) << 8 | (uint32_t)wj,
-                   (uint32_t)g);
+    wave_stamp_end_w(kernarg_here().wtrace, item, (uint32_t)(trips < 0xffffu ? trips : 0xffffu) << 8 | (uint32_t)wj,
+                     (uint32_t)g);
 }
 
 // F110Env.step's time + _check_done (f110_env.py:404-406, :310-352) and the
@@ -1909,12 +1946,12 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                 ra.fxp_hy = (double)a.tmap.H + 2.0 * P - Rn;
                 ra.fxs_cx = std::fma(-a.tmap.ox, a.tmap.inv_res, kFxsBase + P + kFxsShift);
                 ra.fxs_cy = std::fma(-a.tmap.oy, a.tmap.inv_res, kFxsBase + P + kFxsShift);
-                if (a.fx_refill > 0 && a.fxs_ok && !mask && ra.HB == 0 && !ra.wcost) {
+                if (a.fx_refill > 0 && a.fxs_ok && !mask && ra.HB == 0 && !ra.wcost && a.theta_dis <= kFxsLdsTheta) {
                     // one wave per car, two chunk slots with refill (k_rays_fxs; no heavy-first)
                     f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false>)
                                : reinterpret_cast<const void *>(&k_rays_fxs<true>);
                     ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
-                    if (!single && a.geo) {  // leading geometry blocks (a multiple of 8: XCD mapping kept)
+                    if (!single && a.geo) {  // leading geometry items (a multiple of 8: XCD mapping kept)
                         ra.geo = a.geo;
                         ra.geo_blocks = ((ra.EA * (a.A - 1) + 63) / 64 + 7) / 8 * 8;
                         ra.st = a.st;
@@ -1923,11 +1960,14 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                         ra.beam_incr = a.beam_incr;
                         geo_ready = true;
                     }
-                    g2 = dim3((unsigned)(ra.geo_blocks + ra.EA * ra.G4));
+                    const int wpb = single ? kFxsWaves : 1;  // k_rays_fxs's work items per block
+                    g2 = dim3((unsigned)((ra.geo_blocks + ra.EA * ra.G4 + wpb - 1) / wpb));
+                    bdim = 64u * (unsigned)wpb;
                 }
             }
         }
-        bdim = 64u;
+        if (f != reinterpret_cast<const void *>(&k_rays_fxs<false>) && f != reinterpret_cast<const void *>(&k_rays_fxs<true>))
+            bdim = 64u;
     }
     if (a.wtrace && ch && !rot && !mask && !fx)  // diagnostic wave trace (f110_debug_wave_trace)
         f = single ? reinterpret_cast<const void *>(&k_rays_tiled<false, false, false, true, true>)

@@ -60,6 +60,24 @@ __global__ void __launch_bounds__(64) k_gather(const T *tab, uint32_t lines, int
     if (acc == (T)-1) sink[blockIdx.x] = acc;  // never true: keeps the loads
 }
 
+// the ray kernel's arm load: lane l reads the 16-byte (cos, sin) entry at base + l * 1.3865 (consecutive
+// beams' theta indices), 64 lanes over ~90 entries
+__global__ void __launch_bounds__(64) k_arm16(const double2 *tab, uint32_t n, int iters, double *sink) {
+    const uint32_t lane = threadIdx.x;
+    double acc = 0;
+    for (int it = 0; it < iters; ++it) {
+        double2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t base = hash32((blockIdx.x * 131071u) ^ (uint32_t)(it * U + u) * 2654435761u) % (n - 100);
+            v[u] = tab[base + (lane * 13865u) / 10000u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += v[u].x + v[u].y;
+    }
+    if (acc == -1.0) sink[blockIdx.x] = acc;
+}
+
 template <class T>
 static void run(const char *name, size_t bytes, int K, int blocks, int iters) {
     T *tab, *sink;
@@ -93,7 +111,39 @@ static void run(const char *name, size_t bytes, int K, int blocks, int iters) {
     CHECK(hipFree(sink));
 }
 
+static void run_arm(int blocks, int iters) {
+    const uint32_t n = 2000;
+    double2 *tab;
+    double *sink;
+    CHECK(hipMalloc(&tab, n * sizeof(double2)));
+    CHECK(hipMemset(tab, 0, n * sizeof(double2)));
+    CHECK(hipMalloc(&sink, (size_t)blocks * sizeof(double)));
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    for (int w = 0; w < 3; ++w) k_arm16<<<blocks, 64>>>(tab, n, iters, sink);
+    CHECK(hipDeviceSynchronize());
+    float best = 1e30f;
+    for (int r = 0; r < 5; ++r) {
+        CHECK(hipEventRecord(a));
+        k_arm16<<<blocks, 64>>>(tab, n, iters, sink);
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        best = ms < best ? ms : best;
+    }
+    const double loads = (double)blocks * iters * U;
+    printf("{\"cell\": \"arm16_consecutive\", \"table_kb\": 32, \"ms\": %.4f, \"wave_loads\": %.0f, "
+           "\"cyc_per_load_per_cu_2p4ghz\": %.2f}\n", best, loads, best * 1e6 * 2.4 / (loads / 256.0));
+    fflush(stdout);
+    CHECK(hipFree(tab));
+    CHECK(hipFree(sink));
+}
+
 int main() {
+    run_arm(256 * 16, 256);
+    if (getenv("GMB_ARM_ONLY")) return 0;
     const int blocks = 256 * 16, iters = 256;
     const size_t sizes[2] = {(size_t)2 << 20, (size_t)48 << 20};
     const int Ks[8] = {1, 2, 4, 8, 12, 16, 32, 64};

@@ -293,7 +293,9 @@ def test_simt_counters(tracks, gpu, lanes, refill):
     rays per lane, or k_rays_fxs's trips x 2 slots, closed slots included);
     loop lookups = all lookups less the first lookup of each ray (k_agents'),
     and never exceed the slots.  k_rays_fxs also counts its other vector loads
-    (counter 3: tables, guard-band re-gathers): at least one arm per chunk."""
+    (counter 3: each wave's share of its block's LDS copy of the theta table,
+    TTC tables, guard-band re-gathers): at least the table shares, and fewer
+    than one load per arm plus the shares (the arms read the LDS copy)."""
     E, A = 512, 1
     sp = _spawns(A)
     rng = np.random.default_rng(3)
@@ -314,7 +316,9 @@ def test_simt_counters(tracks, gpu, lanes, refill):
     assert 0.2 < loop / slots <= 1.0
     other = sim.read_counter(3)
     if refill:
-        assert other >= 5 * E * ((sim.B + 63) // 64)  # one (cos, sin) load per arm
+        waves = E * A * refill  # refill = waves per car here (set_ray_refill)
+        share = -(-2000 // 512)  # theta_dis entries over a block's 512 threads
+        assert 5 * waves * share <= other < 5 * waves * share + 5 * E * A * ((sim.B + 63) // 64)
     sim.set_simt(False)
     sim.step(np.zeros((E, A, 2), np.float32))
     assert sim.read_simt()[1] == slots  # off: no lane slots added
