@@ -78,6 +78,68 @@ __global__ void __launch_bounds__(64) k_arm16(const double2 *tab, uint32_t n, in
     if (acc == -1.0) sink[blockIdx.x] = acc;
 }
 
+// ended rays (k_rays_fxs): every active lane reads one common line (the quad rule's floor: one
+// cycle per 4-lane group), a fixed random set of lanes "ended"; ZERO = 1: ended lanes load one
+// fixed other line (the kernel's zero cell), 0: their load is masked off (exec).  Addresses are
+// a uniform offset plus a per-lane constant (no per-load VALU hashing).
+template <int ZERO>
+__global__ void __launch_bounds__(64) k_ended(const double *tab, uint32_t lines, int iters, int keep_pct,
+                                              double *sink) {
+    const uint32_t lane = threadIdx.x;
+    const bool act = hash32(lane * 0x9E3779B9u + 7u) % 100u < (uint32_t)keep_pct;
+    const uint32_t word = lane & 15u;
+    double acc = 0;
+    for (int it = 0; it < iters; ++it) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t line = 1u + (uint32_t)(it * U + u) % (lines - 1u);  // uniform (line 0: the zero cell)
+            const uint32_t idx = line * 16u + word;
+            if (ZERO) {
+                v[u] = tab[act ? idx : 0u];
+            } else {
+                v[u] = 0.0;
+                if (act) v[u] = tab[idx];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += v[u];
+    }
+    if (acc == -1.0) sink[blockIdx.x] = acc;
+}
+
+template <int ZERO>
+static void run_ended(int keep_pct, int blocks, int iters) {
+    const size_t bytes = (size_t)64 << 10;  // L1 / L2 resident: the address path is the limit
+    double *tab, *sink;
+    CHECK(hipMalloc(&tab, bytes));
+    CHECK(hipMemset(tab, 0, bytes));
+    CHECK(hipMalloc(&sink, (size_t)blocks * sizeof(double)));
+    const uint32_t lines = (uint32_t)(bytes / 128);
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    for (int w = 0; w < 3; ++w) k_ended<ZERO><<<blocks, 64>>>(tab, lines, iters, keep_pct, sink);
+    CHECK(hipDeviceSynchronize());
+    float best = 1e30f;
+    for (int r = 0; r < 5; ++r) {
+        CHECK(hipEventRecord(a));
+        k_ended<ZERO><<<blocks, 64>>>(tab, lines, iters, keep_pct, sink);
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        best = ms < best ? ms : best;
+    }
+    const double loads = (double)blocks * iters * U;
+    printf("{\"cell\": \"ended_%s\", \"active_pct\": %d, \"ms\": %.4f, \"wave_loads\": %.0f, "
+           "\"cyc_per_load_per_cu_2p4ghz\": %.2f}\n", ZERO ? "zero_line" : "masked", keep_pct, best, loads,
+           best * 1e6 * 2.4 / (loads / 256.0));
+    fflush(stdout);
+    CHECK(hipFree(tab));
+    CHECK(hipFree(sink));
+}
+
 template <class T>
 static void run(const char *name, size_t bytes, int K, int blocks, int iters) {
     T *tab, *sink;
@@ -142,6 +204,14 @@ static void run_arm(int blocks, int iters) {
 }
 
 int main() {
+    if (getenv("GMB_ENDED_ONLY")) {
+        const int pcts[5] = {100, 75, 50, 25, 10};
+        for (int p : pcts) {
+            run_ended<1>(p, 256 * 16, 256);
+            run_ended<0>(p, 256 * 16, 256);
+        }
+        return 0;
+    }
     run_arm(256 * 16, 256);
     if (getenv("GMB_ARM_ONLY")) return 0;
     const int blocks = 256 * 16, iters = 256;
