@@ -545,14 +545,16 @@ int fail(const char *fn, const char *what) { return f110_set_error(F110_E_INVALI
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 bool aligned8(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
 
-// blocks per slice count S for a grouped weight-gradient launch: ~320 blocks,
-// at least two 8-row chunks per wave; a function of the shapes only
+// blocks per slice count S for a grouped weight-gradient launch: at most 256
+// blocks, one per CU (at ~320, a third of the CUs ran two blocks and the
+// launch took their time: 28.1 -> 23.4 us for the 128 x 1088 gradient, DESIGN
+// §8), at least two 8-row chunks per wave; a function of the shapes only
 int wgrad_slices(const f110_wgrad_op *ops, int nops, int M) {
     int64_t tiles = 0;
     for (int q = 0; q < nops; ++q)
         tiles += (int64_t)((ops[q].N + kWN - 1) / kWN) * ((ops[q].KX + kWK - 1) / kWK);
     const int64_t mch = (M + 7) / 8;
-    int64_t S = (320 + tiles - 1) / tiles;
+    int64_t S = std::max<int64_t>(1, 256 / tiles);
     S = std::min<int64_t>(S, std::max<int64_t>(1, mch / 8));
     return (int)std::max<int64_t>(1, S);
 }
