@@ -291,9 +291,9 @@ __device__ __forceinline__ int32_t wave_count_le(const uint32_t (&v)[NQ], uint32
 
 // k-th smallest (0-based) of the values held across the wave (non-negative
 // floats by bit pattern, NQ slots per lane), by bisection on the bit pattern
-// between the smallest and the largest held value.  (A 4-pass 8-bit radix
-// select over an LDS histogram measured slower: the few exponent values put
-// most of a wave's atomics on the same bins.)
+// in [lo, hi].  (A 4-pass 8-bit radix select over an LDS histogram measured
+// slower: the few exponent values put most of a wave's atomics on the same
+// bins.)
 template <int NQ>
 __device__ __forceinline__ uint32_t kth_bits(const uint32_t (&v)[NQ], uint32_t lo, uint32_t hi, int32_t k) {
     while (lo < hi) {
@@ -304,11 +304,80 @@ __device__ __forceinline__ uint32_t kth_bits(const uint32_t (&v)[NQ], uint32_t l
     return lo;
 }
 
+template <bool MAX>
+__device__ __forceinline__ uint32_t wave_ext(uint32_t m) {  // wave min / max
+#pragma unroll
+    for (int s2 = 32; s2 > 0; s2 >>= 1) {
+        const uint32_t om = __shfl_xor(m, s2, 64);
+        m = MAX ? (om > m ? om : m) : (om < m ? om : m);
+    }
+    return m;
+}
+
+// The order statistics k and k + 1 (0-based, k + 1 < B) of the wave's values
+// (B real values in [vmin, vmax], kNoValue fillers).  Bisection with every
+// slot narrows [lo, hi] while it holds both statistics, until at most 64
+// values lie in it; those are packed one per lane through `pack` (64 words of
+// LDS) and the bisection goes on over one slot (a compare and a popcount per
+// step instead of NQ of each: the counting's scalar popcounts bound the
+// NQ-slot steps).  A split that separates the two statistics ends it at once:
+// k is the largest value <= mid, k + 1 the smallest above.
+template <int NQ>
+__device__ __forceinline__ void kth_pair(const uint32_t (&v)[NQ], uint32_t vmin, uint32_t vmax, int32_t B, int32_t k,
+                                         int lane, uint32_t *pack, uint32_t &a, uint32_t &b) {
+    uint32_t lo = vmin, hi = vmax;
+    int32_t clt = 0, cle = B;  // values < lo, values <= hi: clt <= k, cle >= k + 2
+    while (cle - clt > 64 && lo < hi) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        const int32_t c = wave_count_le<NQ>(v, mid);
+        if (c >= k + 2) {
+            hi = mid;
+            cle = c;
+        } else if (c <= k) {
+            lo = mid + 1;
+            clt = c;
+        } else {  // c == k + 1
+            uint32_t mx = 0u, mn = kNoValue;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                if (v[q] <= mid && v[q] > mx) mx = v[q];
+                if (v[q] > mid && v[q] < mn) mn = v[q];
+            }
+            a = wave_ext<true>(mx);
+            b = wave_ext<false>(mn);
+            return;
+        }
+    }
+    if (lo == hi) {  // both statistics are this value (more than 64 values hold it)
+        a = b = lo;
+        return;
+    }
+    int32_t n = 0;  // the cle - clt values in [lo, hi], one per lane
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const bool in = v[q] >= lo && v[q] <= hi;
+        const uint64_t m = __ballot(in);
+        if (in) pack[n + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = v[q];
+        n += (int32_t)__popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t w[1] = {lane < n ? pack[lane] : kNoValue};
+    const int32_t kk = k - clt;
+    a = kth_bits<1>(w, lo, hi, kk);
+    if (wave_count_le<1>(w, a) >= kk + 2) {
+        b = a;
+    } else {
+        b = wave_ext<false>(w[0] > a ? w[0] : kNoValue);
+    }
+}
+
 // The wall term's np.quantile(clip(where(x <= 0 | ~finite, lmax, x), 0, lmax), q)
 // in float32 (rewards.py:312-320): q cast to float32, virtual index (n-1)*q,
 // numpy's _lerp in float32.  NQ slots of 64 beams per lane (B <= 64 * NQ).
 template <int NQ>
-__device__ float wall_quantile(const float *o, int B, float lmax, float qf, int lane) {
+__device__ float wall_quantile(const float *o, int B, float lmax, float qf, int lane, uint32_t *pack) {
     uint32_t v[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -336,26 +405,12 @@ __device__ float wall_quantile(const float *o, int B, float lmax, float qf, int 
         vmax = b > vmax ? b : vmax;
     }
     const float vi = (float)(B - 1) * qf;
-    if (vi >= (float)(B - 1)) return __uint_as_float(kth_bits<NQ>(v, vmin, vmax, B - 1));
+    if (vi >= (float)(B - 1)) return __uint_as_float(vmax);  // the largest value
     const float pv = floorf(vi < 0.0f ? 0.0f : vi);
-    const int32_t k = (int32_t)pv;
+    const int32_t k = (int32_t)pv;  // <= B - 2
     const float g = vi - pv;
-    const uint32_t ab = kth_bits<NQ>(v, vmin, vmax, k);
-    uint32_t bb;
-    if (wave_count_le<NQ>(v, ab) >= k + 2) {
-        bb = ab;
-    } else {  // the smallest value above a
-        uint32_t m = kNoValue;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q)
-            if (v[q] > ab && v[q] < m) m = v[q];
-#pragma unroll
-        for (int s2 = 32; s2 > 0; s2 >>= 1) {
-            const uint32_t om = __shfl_xor(m, s2, 64);
-            m = om < m ? om : m;
-        }
-        bb = m;
-    }
+    uint32_t ab, bb;
+    kth_pair<NQ>(v, vmin, vmax, B, k, lane, pack, ab, bb);
     const float fa = __uint_as_float(ab), fb = __uint_as_float(bb);
     const float diff = fb - fa;
     return g >= 0.5f ? fb - diff * (1.0f - g) : fa + diff * g;
@@ -506,8 +561,9 @@ __global__ void __launch_bounds__(64 * kRwWaves) k_reward(RewardArgs a) {
         if (B > 0 && st.steps >= P.grace_steps_wall) {  // wall term (:312-320)
             const float lmax = (float)P.lidar_max;
             const float qf = (float)P.wall_quantile;
-            const float dmin_f = B <= 64 * 17 ? wall_quantile<17>(o, B, lmax, qf, lane)
-                                              : wall_quantile<kRwPerLane>(o, B, lmax, qf, lane);
+            __shared__ uint32_t pack[64];  // kth_pair's packed values (one wave per block)
+            const float dmin_f = B <= 64 * 17 ? wall_quantile<17>(o, B, lmax, qf, lane, pack)
+                                              : wall_quantile<kRwPerLane>(o, B, lmax, qf, lane, pack);
             const double dmin = (double)dmin_f;
             if (dmin < P.near_wall_dist) {
                 const double x = (P.near_wall_dist - dmin) / pymax(1e-6, P.near_wall_dist);

@@ -119,3 +119,48 @@ def test_vector_env_reward_fn(track):
                     assert rew[e].item() == pytest.approx(refs[e](o[e]), rel=1e-9, abs=1e-12)
     finally:
         venv.close()
+
+
+def _tie_scans(rng, E, B):
+    """Scans whose order statistics tie: a few distinct values, runs of one
+    value, lmax-clipped and invalid beams, and plain uniform ones."""
+    s = np.empty((E, B), np.float32)
+    for e in range(E):
+        kind = e % 6
+        if kind == 0:
+            s[e] = rng.choice(np.float32([0.1, 0.2, 0.3]), B)
+        elif kind == 1:
+            s[e] = np.float32(0.25)
+        elif kind == 2:
+            s[e] = rng.choice(np.float32([0.0, np.nan, 2.0, 0.5]), B)
+        elif kind == 3:
+            s[e] = rng.uniform(0.0, 1.0, B)
+        elif kind == 4:
+            s[e] = rng.uniform(0.0, 0.02, B)
+            s[e][rng.random(B) < 0.5] = np.float32(0.0123)
+        else:
+            s[e] = np.float32(0.4) + np.float32(1e-7) * rng.integers(0, 3, B)
+    return s
+
+
+@pytest.mark.parametrize("B", [1, 2, 63, 64, 65, 130, 1080, 2000])
+def test_reward_wall_quantile_ties(gpu, B):
+    """The wall term's float32 np.quantile on scans with tied order
+    statistics, every quantile edge (q = 0, 1 and between) and beam counts
+    around the 64-value packing of the device selection; near_wall_dist above
+    lidar_max keeps the term live, so the reward carries the quantile."""
+    import reward_oracle as R
+    from f110_gymnasium_ros2_jazzy_amd.reward import BatchedCenterlineReward
+    E = 60
+    rng = np.random.default_rng(B)
+    for q in (0.0, 0.05, 0.1, 0.5, 0.999, 1.0):
+        kw = dict(_kwargs("all_terms"))
+        kw.update(near_wall_dist=2.0, grace_steps_wall=0, wall_quantile=q)
+        f = BatchedCenterlineReward(E, dt=0.01, progress=None, num_beams=B, **kw)
+        o = np.zeros((E, B + 8), np.float32)
+        o[:, :B] = _tie_scans(rng, E, B)
+        o[:, B:B + 2] = rng.uniform(-5, 5, (E, 2))
+        o[:, B + 4:B + 6] = o[:, B:B + 2] + 3.0
+        got = f(torch.as_tensor(o, device="cuda")).cpu().numpy()
+        exp = np.array([R.RewardOracle(None, **kw)(o[e]) for e in range(E)])
+        np.testing.assert_allclose(got, exp, rtol=1e-12, atol=1e-15, err_msg=f"q {q}")
