@@ -1642,6 +1642,16 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
     const int A = a.A, B = a.B;
     const int EA = a.E * A;
     if (a.mode == 1 && a.reset_mask && !a.reset_mask[e]) return;  // uniform per block
+#ifdef F110_POST_PHASES  // timing build (scripts/post_phases.py): counters 8-11 = wall_clock64 ticks per phase, 12 = blocks
+    uint64_t tph = wall_clock64();
+    auto phase = [&](int k) {
+        const uint64_t t = wall_clock64();
+        if (tid == 0) atomicAdd(a.ctr + (size_t)(e % kCtrSlots) * kCtrStride + 8 + k, (unsigned long long)(t - tph));
+        tph = t;
+    };
+#else
+    auto phase = [](int) {};
+#endif
     double *scan = a.scan + (size_t)e * A * B;
     if (tid < A) {
         const int g = e * A + tid;
@@ -1668,6 +1678,7 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
         epilogue_load_env(a, e, sh.epe);
     }
     __syncthreads();
+    phase(0);
     if (tid == 0) {  // collision_multiple (collision_models.py:184-212)
         for (int i = 0; i < A - 1; ++i)
             for (int j = i + 1; j < A; ++j)
@@ -1749,6 +1760,7 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
         }
     }
     __syncthreads();
+    phase(1);
     // agent ray_cast (base_classes.py:206-227; laser_models.py:318-346), one
     // opponent at a time per car (each pass min-updates the same beams), all
     // cars' passes of one round in one sweep over the block; only the beams
@@ -1790,6 +1802,7 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
         }
         __syncthreads();
     }
+    phase(2);
 
     // ---- outputs --------------------------------------------------------
     // the scan entries were written by the ray pass (and patched above)
@@ -1802,6 +1815,10 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
     }
     if (a.out.collisions && tid < A) a.out.collisions[(size_t)e * A + tid] = (uint8_t)sh.col[tid];
     if (tid == 0) env_epilogue(a, e, &sh.stl[0][0], 7, sh.col, sh.do_reset, sh.epe, sh.epi);
+#ifdef F110_POST_PHASES
+    phase(3);
+    if (tid == 0) atomicAdd(a.ctr + (size_t)(e % kCtrSlots) * kCtrStride + 12, 1ull);
+#endif
 }
 
 // One f110_step / f110_reset: k_agents, the ray kernel, the post stage.

@@ -1,4 +1,5 @@
-"""k_post_multi's per-block phase times (GPU box, a timing build via F110_LIB:
+"""k_post_multi's per-block phase times (GPU box, a timing build via F110_LIB
+(hipcc ... -DF110_POST_PHASES, the _build.py flags and sources):
 counters 8-12 = summed wall_clock64 ticks (100 MHz) of prologue, GJK + pair
 geometry, agent ray_cast, outputs + epilogue, and the block count), two-agent
 envs at the C4 / C5 shapes, post_probe.py's inputs.  One JSON line (us per
