@@ -100,6 +100,7 @@ struct f110_ctx {
     uint32_t rmp_zero = 0;
     bool fx_pad = false;    // the padded table is wanted (from 32768 cars or with refill; F110_FX_PAD=0: never)
     int32_t fx_refill = 0;   // waves per car of k_rays_fxs (0 = k_rays_fxn; f110_debug_set_ray_refill)
+    bool fxs_lds = false;    // single-agent k_rays_fxs with the LDS theta table (f110_set_device_share, > 1 context)
     bool count_slots = false;  // f110_debug_set_simt: lane-slot counter of the fixed-point loops (f110_debug_read_simt)
     int fx_ilp = 1;         // rays per lane (f110_debug_set_ray_lanes; default by car count)
 
@@ -882,6 +883,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.fxs_ok = fxs_ok(c) ? 1 : 0;
     a.count_slots = c->count_slots ? 1 : 0;
     a.fx_refill = c->fx_refill;
+    a.fxs_lds = c->fxs_lds ? 1 : 0;
     a.fx_ilp = c->fx_ilp;
     a.gate_wait = c->gate_wait;
     a.gate_record = c->gate_record;
@@ -1054,7 +1056,13 @@ extern "C" int f110_set_device_share(f110_ctx *ctx, int64_t device_cars, int32_t
     const int refill = (lanes == 2 && ctx->fx_pad) ? refill_waves(device_cars) : 0;
     int rc = f110_debug_set_ray_lanes(ctx, lanes);
     if (rc == F110_OK) rc = f110_debug_set_ray_refill(ctx, refill);
-    if (rc == F110_OK && contexts > 1) ctx->heavy_off = true;  // the other contexts fill this one's tail
+    if (rc == F110_OK && contexts > 1) {
+        ctx->heavy_off = true;  // the other contexts fill this one's tail
+        // and its 8-wave blocks' idle slots: the LDS theta table pays off beside other contexts
+        // (65536 cars in 2 sub-shards 89.5 -> 95.9 M) but not alone (one context 88.3 -> 87.2 M,
+        // DESIGN §3.14)
+        ctx->fxs_lds = true;
+    }
     return rc;
 }
 

@@ -61,6 +61,7 @@ struct StepArgs {
     int32_t fx_pad;     // the padded table is built (k_rays_fxn on it unless F110_FX_PAD=0; k_rays_fxs)
     int32_t fxs_ok;     // the padded table's rows and columns are below 2^20 (kFxsBase's offsets)
     int32_t fx_refill;  // waves per car of k_rays_fxs (two chunk slots with refill; 0 = off)
+    int32_t fxs_lds;    // single-agent k_rays_fxs in 8-wave blocks with the theta table in LDS (shared device)
     PairGeom *geo;      // [E][A][A-1] pair geometry (A >= 2), see RayArgs::geo
     int32_t geo_ready;  // set by launch_env_step: this step's ray kernel computed geo
     int32_t count_slots;  // f110_debug_set_simt: lane-slot counter of the fixed-point loops

@@ -1202,15 +1202,17 @@ __device__ __noinline__ void ray_pair_geometry(const RayArgs &a, int blk) {
 // gather every trip, a closed slot on the zero cell).  Per slot and trip: the
 // total (:141), the activity test (:133), the refill when the slot's chunk has
 // ended, the step (:135-136) and its gather.
-// Single-agent contexts (HANDOFF false) run kFxsWaves work items per block with the theta
-// table's (cos, sin) pairs in one LDS copy per block: the arms read them there instead of a
-// 16-byte gather each (a wave-level load for the texture-address unit, ~24 cycles like a slot
-// gather: 17 per car).  Multi-agent contexts keep one-wave blocks and the
-// gathers: the 8-wave blocks were slower there (C4 one context 27.7 -> 25.2 M).
-template <bool HANDOFF>
-__global__ void __launch_bounds__(HANDOFF ? 64 : 64 * kFxsWaves, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
+// LDS: kFxsWaves work items per block with the theta table's (cos, sin) pairs in one LDS copy
+// per block: the arms read them there instead of a 16-byte gather each (a wave-level load for the
+// texture-address unit, ~24 cycles like a slot gather: 17 per car).  Single-agent
+// contexts that share the device with others (f110_set_device_share, the stream sub-shards) take
+// it; a lone context keeps one-wave blocks and the gathers, whose launch is shorter (0.685 vs
+// 0.697 ms at 65536 cars: the 8-wave blocks hold their LDS until their slowest car ends), as do
+// multi-agent contexts (the 8-wave blocks were slower there: C4 one context 27.7 -> 25.2 M).
+template <bool HANDOFF, bool LDS>
+__global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
+    static_assert(!(HANDOFF && LDS), "the LDS table is the single-agent kernel's");
     constexpr int NS = 2;
-    constexpr bool LDS = !HANDOFF;
     constexpr int W = LDS ? kFxsWaves : 1;  // work items (waves) per block
     __shared__ double2 cs_lds[LDS ? kFxsLdsTheta : 1];
     const int wave = LDS ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
@@ -1915,6 +1917,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     const void *f = tiled_fn[ch ? 1 : 0][vt];
     unsigned bdim = ch ? 64u * (unsigned)ra.wpb : (unsigned)kBlock;
     bool geo_ready = false;  // the ray launch computes the pairs' ray_cast geometry (k_post_multi reads it)
+    bool fxs = false, lds = false;  // k_rays_fxs; with the LDS theta table
     // the fixed-point kernels (f110_create checked their preconditions: axis-aligned map,
     // one-wave blocks, W, H < 2^21, |origin / res| < 2^20, EDT entries 0 or > eps)
     const bool fx = a.ray_kernel == 3 && !rot && ra.wpb == 1 && a.rm;
@@ -1963,10 +1966,13 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                 ra.fxp_hy = (double)a.tmap.H + 2.0 * P - Rn;
                 ra.fxs_cx = std::fma(-a.tmap.ox, a.tmap.inv_res, kFxsBase + P + kFxsShift);
                 ra.fxs_cy = std::fma(-a.tmap.oy, a.tmap.inv_res, kFxsBase + P + kFxsShift);
-                if (a.fx_refill > 0 && a.fxs_ok && !mask && ra.HB == 0 && !ra.wcost && a.theta_dis <= kFxsLdsTheta) {
+                if (a.fx_refill > 0 && a.fxs_ok && !mask && ra.HB == 0 && !ra.wcost) {
                     // one wave per car, two chunk slots with refill (k_rays_fxs; no heavy-first)
-                    f = single ? reinterpret_cast<const void *>(&k_rays_fxs<false>)
-                               : reinterpret_cast<const void *>(&k_rays_fxs<true>);
+                    lds = single && a.fxs_lds && a.theta_dis <= kFxsLdsTheta;
+                    f = lds ? reinterpret_cast<const void *>(&k_rays_fxs<false, true>)
+                            : single ? reinterpret_cast<const void *>(&k_rays_fxs<false, false>)
+                                     : reinterpret_cast<const void *>(&k_rays_fxs<true, false>);
+                    fxs = true;
                     ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
                     if (!single && a.geo) {  // leading geometry items (a multiple of 8: XCD mapping kept)
                         ra.geo = a.geo;
@@ -1977,14 +1983,13 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                         ra.beam_incr = a.beam_incr;
                         geo_ready = true;
                     }
-                    const int wpb = single ? kFxsWaves : 1;  // k_rays_fxs's work items per block
+                    const int wpb = lds ? kFxsWaves : 1;  // k_rays_fxs's work items per block
                     g2 = dim3((unsigned)((ra.geo_blocks + ra.EA * ra.G4 + wpb - 1) / wpb));
                     bdim = 64u * (unsigned)wpb;
                 }
             }
         }
-        if (f != reinterpret_cast<const void *>(&k_rays_fxs<false>) && f != reinterpret_cast<const void *>(&k_rays_fxs<true>))
-            bdim = 64u;
+        if (!fxs) bdim = 64u;
     }
     if (a.wtrace && ch && !rot && !mask && !fx)  // diagnostic wave trace (f110_debug_wave_trace)
         f = single ? reinterpret_cast<const void *>(&k_rays_tiled<false, false, false, true, true>)

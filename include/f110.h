@@ -243,10 +243,11 @@ F110_API int f110_set_reset_dtype(f110_ctx *ctx, int32_t dtype);
  * device (e.g. sub-shards of one GPU's envs on separate streams): this context
  * is one of `contexts` whose ray passes run together, tracing `device_cars`
  * cars (envs x agents) in all.  The library then picks the ray kernel for the
- * device's load instead of this context's alone (2
- * rays per lane from 12288 cars; k_rays_fxs's refilled chunk slots from 32768
- * cars, or from 16384 with 4 or more contexts; no heavy-first dispatch when
- * other contexts' ray passes fill this one's tail).  Call before the first
+ * device's load instead of this context's alone (DESIGN.md §3.3-3.4, §3.14,
+ * §5.1: k_rays_fxs with 1 / 2 / 3 waves per car by the device's cars; with
+ * other contexts, no heavy-first dispatch and, for single-agent contexts,
+ * the 8-wave blocks that keep the theta table in LDS, since the other
+ * contexts' ray passes fill this one's tail and idle slots).  Call before the first
  * reset / step.  Scheduling only: results are bit-identical with or without
  * it.  No reference counterpart (the reference steps one env per process). */
 F110_API int f110_set_device_share(f110_ctx *ctx, int64_t device_cars, int32_t contexts);

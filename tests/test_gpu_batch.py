@@ -286,20 +286,25 @@ def test_rays_per_lane_identical_across_beam_counts(tracks, gpu, beams, A):
                 assert torch.equal(x, y), f"step {t}"
 
 
-@pytest.mark.parametrize("lanes,refill", [(1, 0), (2, 0), (2, 1)])
-def test_simt_counters(tracks, gpu, lanes, refill):
+@pytest.mark.parametrize("lanes,refill,shared", [(1, 0, False), (2, 0, False), (2, 1, False), (2, 1, True)])
+def test_simt_counters(tracks, gpu, lanes, refill, shared):
     """f110_debug_set_simt / f110_debug_read_simt: the fixed-point loops count the lane
     slots of the gathers they issue (64 per wave-level gather: trip count x
     rays per lane, or k_rays_fxs's trips x 2 slots, closed slots included);
     loop lookups = all lookups less the first lookup of each ray (k_agents'),
     and never exceed the slots.  k_rays_fxs also counts its other vector loads
-    (counter 3: each wave's share of its block's LDS copy of the theta table,
-    TTC tables, guard-band re-gathers): at least the table shares, and fewer
-    than one load per arm plus the shares (the arms read the LDS copy)."""
+    (counter 3: the arms' theta-table loads, TTC tables, guard-band re-gathers,
+    run searches).  A context sharing the device (f110_set_device_share with
+    two contexts) runs the kernel with the theta table in LDS: each wave counts
+    its share of its block's LDS copy, and fewer than one load per arm plus the
+    shares; alone, at least one load per arm."""
+    from f110_gymnasium_ros2_jazzy_amd import _lib
     E, A = 512, 1
     sp = _spawns(A)
     rng = np.random.default_rng(3)
     sim = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=2)
+    if shared:
+        _lib.check(sim.L.f110_set_device_share(sim.ctx, 2 * E * A, 2), "f110_set_device_share")
     sim.set_ray_lanes(lanes)
     sim.set_ray_refill(refill)
     assert sim.ray_kernel == 3 and sim.ray_lanes == lanes and sim.ray_refill == refill
@@ -315,10 +320,13 @@ def test_simt_counters(tracks, gpu, lanes, refill):
     assert 0 < loop <= slots
     assert 0.2 < loop / slots <= 1.0
     other = sim.read_counter(3)
-    if refill:
+    nch = (sim.B + 63) // 64
+    if refill and shared:
         waves = E * A * refill  # refill = waves per car here (set_ray_refill)
         share = -(-2000 // 512)  # theta_dis entries over a block's 512 threads
-        assert 5 * waves * share <= other < 5 * waves * share + 5 * E * A * ((sim.B + 63) // 64)
+        assert 5 * waves * share <= other < 5 * waves * share + 5 * E * A * nch
+    elif refill:  # one load per arm, at most one TTC table load per chunk, the run searches
+        assert 5 * E * A * nch <= other < 5 * E * A * (2 * nch + 8)
     sim.set_simt(False)
     sim.step(np.zeros((E, A, 2), np.float32))
     assert sim.read_simt()[1] == slots  # off: no lane slots added
