@@ -1,0 +1,22 @@
+# Round 5 (kag): vehicle_dynamics_st skipping a model no car of the wave needs (k_agents) against
+# HEAD: GPU suite, scripts/agents_probe.py per build, the bench per build (interleaved, twice).
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-/root/repo}
+OUT=$R/gpurun_out/r05kag
+mkdir -p "$OUT"
+cd "$R"
+step() {  # name seconds cmd...
+    local name=$1 secs=$2
+    shift 2
+    echo "[$(date +%T)] $name" >&2
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err" || { echo "step $name failed rc=$?" >&2; tail -30 "$OUT/$name.err" >&2; exit 1; }
+}
+step suite 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider
+step agents_cur 300 python -u scripts/agents_probe.py
+F110_LIB=$R/ab_libs/head.so step agents_head 300 python -u scripts/agents_probe.py
+for k in 1 2; do
+    F110_LIB=$R/ab_libs/head.so step bench_head_$k 600 python -u bench.py --no-cpu-baseline
+    step bench_cur_$k 600 python -u bench.py --no-cpu-baseline
+done
+echo "[$(date +%T)] done" >&2
