@@ -67,6 +67,7 @@ struct f110_ctx {
     BeamRun *runs = nullptr;
     int32_t *nruns = nullptr;
     PairGeom *geo = nullptr;  // [E][A][A-1] ray_cast pair geometry (A >= 2)
+    uint32_t *hmask = nullptr;  // [E*A] hand-off chunk masks of k_rays_fxs<HANDOFF> (A >= 2 dividing 64)
     uint64_t *noise_step = nullptr;
     int32_t *scnt = nullptr, *toggles = nullptr;
     uint8_t *near_start = nullptr, *pending = nullptr, *reset_flag = nullptr, *ttc_hit = nullptr;
@@ -680,6 +681,7 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     ALLOC(c->runs, (size_t)kMaxSeg * EA);
     ALLOC(c->nruns, EA);
     if (C.n_agents >= 2) ALLOC(c->geo, (size_t)EA * (C.n_agents - 1));
+    if (C.n_agents >= 2 && 64 % C.n_agents == 0) ALLOC(c->hmask, (size_t)EA);  // k_agents' hand-off chunk masks
     ALLOC(c->scan, EA * (size_t)C.n_beams);
     ALLOC(c->reset_flag, (size_t)C.n_envs);
     ALLOC(c->ttc_hit, EA);
@@ -849,6 +851,7 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.runs = c->runs;
     a.nruns = c->nruns;
     a.geo = c->geo;
+    a.hmask = c->hmask;
     a.scan = c->scan;
     a.reset_flag = c->reset_flag;
     a.ttc_hit = c->ttc_hit;

@@ -62,6 +62,7 @@ struct StepArgs {
     int32_t fxs_ok;     // the padded table's rows and columns are below 2^20 (kFxsBase's offsets)
     int32_t fx_refill;  // waves per car of k_rays_fxs (two chunk slots with refill; 0 = off)
     int32_t fxs_lds;    // single-agent k_rays_fxs in 8-wave blocks with the theta table in LDS (shared device)
+    uint32_t *hmask;    // [E*A] k_agents' hand-off chunk masks (A >= 2 dividing 64), or null
     PairGeom *geo;      // [E][A][A-1] pair geometry (A >= 2), see RayArgs::geo
     int32_t geo_ready;  // set by launch_env_step: this step's ray kernel computed geo
     int32_t count_slots;  // f110_debug_set_simt: lane-slot counter of the fixed-point loops
@@ -182,6 +183,7 @@ struct RayArgs {
     int32_t count_slots;  // the fixed-point loops add their lane slots to ctr[.][2] (f110_debug_read_simt)
     const double *cs2, *bs2;  // k_rays_fxs: interleaved (cos, sin) / (side, beam_cos) tables
     // k_rays_fxs<HANDOFF>: geo_blocks leading work items (one wave each) compute every pair's PairGeom
+    const uint32_t *hmask;     // [EA] the chunks whose hand-off k_post_multi may read (k_agents), or null: all
     PairGeom *geo;
     int32_t geo_blocks;
     const double *st;          // state [7][EA] after k_agents

@@ -135,6 +135,77 @@ __device__ __forceinline__ void reset_next_heavy(const StepArgs &a) {
     if (a.heavy_count && blockIdx.x == 0 && threadIdx.x == 0) a.heavy_count[a.parity ^ 1] = 0;
 }
 
+// The 64-beam chunks of car g whose f64 scans k_post_multi may read (bit k: chunk k), for the ray
+// kernel's hand-off: its agent ray_cast visits only beams of each (car, opponent) pair's blocked
+// view [lo, hi] -- the nearest beams of the opponent box's vertex bearings
+// (get_blocked_view_indices, laser_models.py:282-315) -- seen from the car's yaw or, after a TTC
+// response, from yaw 0 (base_classes.py:246-249).  Here in f32 (the box from fast sin / cos, the
+// bearings from a polynomial atan2 good to ~2e-4 rad: errors far below a beam's 4.4e-3 rad), the
+// range widened by 3 beams; a bearing within 1e-2 rad of the +-pi wrap, or a NaN, marks every chunk.  The other chunks skip the
+// hand-off store (its stores cost the two-agent ray launch ~6 %).  The poses of an env's cars meet
+// in LDS: A divides 64 (the context allocates no mask otherwise).
+__device__ __forceinline__ float bearing_f32(float y, float x) {  // atan2(y, x) within ~2e-4 rad (finite x, y)
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float a = __fdividef(fminf(ax, ay), fmaxf(ax, ay));
+    const float s = a * a;
+    float r = ((-0.0464964749f * s + 0.15931422f) * s - 0.327622764f) * s * a + a;
+    if (ay > ax) r = 1.57079637f - r;
+    if (x < 0.0f) r = 3.14159274f - r;
+    if (y < 0.0f) r = -r;
+    return (ax == 0.0f && ay == 0.0f) ? 0.0f : r;
+}
+
+// sx / sy / sth: the block's cars' poses (LDS, k_agents writes them before a barrier).
+__device__ void handoff_chunks(const StepArgs &a, int g, const float *sx, const float *sy, const float *sth,
+                               float len, float wid) {
+    const int t = (int)threadIdx.x;
+    const int A = a.A, B = a.B;
+    const int ag = g % A, t0 = t - ag;  // the env's first car in the block
+    const int nch = (B + 63) >> 6;
+    const uint32_t all = nch >= 32 ? 0xFFFFFFFFu : ((1u << nch) - 1u);
+    const float fov = (float)a.fov, incr = (float)a.beam_incr;
+    const float xi = sx[t], yi = sy[t];
+    uint32_t m = nch > 32 ? all : 0u;
+    for (int j = 0; j < A && m != all; ++j) {
+        if (j == ag) continue;
+        float sj, cj;
+        __sincosf(sth[t0 + j], &sj, &cj);
+        const float px[4] = {-len / 2, -len / 2, len / 2, len / 2};
+        const float py[4] = {wid / 2, -wid / 2, -wid / 2, wid / 2};
+        float bear[4];
+        bool unsure = !(sth[t] == sth[t]);
+        for (int q = 0; q < 4; ++q) {
+            const float vx = cj * px[q] - sj * py[q] + sx[t0 + j], vy = sj * px[q] + cj * py[q] + sy[t0 + j];
+            const float dx = vx - xi, dy = vy - yi;
+            unsure |= !(dx == dx) || !(dy == dy) || fabsf(dx) > 1e30f || fabsf(dy) > 1e30f;  // NaN / inf
+            bear[q] = bearing_f32(dy, dx);
+        }
+        for (int w = 0; w < 2 && !unsure; ++w) {
+            const float ego = w == 0 ? sth[t] : 0.0f;
+            int lo = B, hi = -1;
+            for (int q = 0; q < 4; ++q) {
+                float ang = ego - bear[q];
+                unsure |= !(fabsf(fabsf(ang) - 3.14159265f) > 1e-2f);
+                if (ang > 3.14159265f) ang -= 6.28318531f;
+                else if (ang < -3.14159265f) ang += 6.28318531f;
+                const float gk = (-ang + fov * 0.5f) / incr;
+                const int k = gk < 0.0f ? 0 : (gk > (float)(B - 1) ? B - 1 : (int)(gk + 0.5f));
+                lo = k < lo ? k : lo;
+                hi = k > hi ? k : hi;
+            }
+            lo = lo - 3 < 0 ? 0 : lo - 3;
+            hi = hi + 3 > B - 1 ? B - 1 : hi + 3;
+            for (int c = lo >> 6; c <= hi >> 6; ++c) m |= 1u << c;
+        }
+        if (unsure) m = all;
+    }
+    a.hmask[g] = m;
+}
+
+// HMASK: the context keeps hand-off chunk masks (A >= 2 dividing 64): the block's new poses meet in
+// LDS after the update and each car's mask is written at the end; without it the update's stores
+// follow it directly (the single-agent form, one dependent chain less to schedule around a barrier).
+template <bool HMASK>
 __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
     const int g = blockIdx.x * 64 + threadIdx.x;
     const int EA = a.E * a.A;
@@ -144,7 +215,7 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
     const int ag = g - e * A;
     // Every input of the car is loaded first, before the heavy-list atomic
     // and before anything waits: one memory round trip for the whole prologue.
-    double s[7];
+    double s[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     double b0 = 0.0, b1 = 0.0, raw_steer = 0.0, vel = 0.0;
     int cnt = 0, gate = 0;
     uint32_t episode = 0;
@@ -170,10 +241,42 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
             }
         }
     }
+    // RaceCar ag's box (its opponents' vertices for the hand-off mask), loaded with the prologue
+    const float box_len = HMASK ? (float)a.pa[ag].length : 0.0f, box_wid = HMASK ? (float)a.pa[ag].width : 0.0f;
     if (a.heavy_build) build_heavy_list(a, g, valid);  // block-uniform branch, before any return
+    // the car's update (its returns leave the lambda: the hand-off poses below need every thread)
+    int do_reset = 0;
+    bool act = false;
+    // the update's stores, the scan pose, the first lookup and the beam runs
+    auto tail = [&]() {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) a.st[(size_t)k * EA + g] = s[k];
+    a.sb[g] = b0;
+    a.sb[EA + g] = b1;
+    a.scnt[g] = cnt;
+    // scan pose (base_classes.py:420-422) and everything every ray of this car shares
+    // base_classes.py:420-422; with lidar_dist == 0 the offset is +-0 for any
+    // finite yaw, so the transcendentals are skipped (a non-finite yaw keeps
+    // the reference's NaN)
+    const bool no_offset = a.lidar_dist == 0.0 && isfinite(s[4]);
+    double sy4 = 0.0, cy4 = 1.0;
+    if (!no_offset) cr_sincos(s[4], sy4, cy4);
+    const double sx = no_offset ? s[0] + 0.0 : s[0] + a.lidar_dist * cy4;
+    const double sy = no_offset ? s[1] + 0.0 : s[1] + a.lidar_dist * sy4;
+    a.ray0[g] = sx;
+    a.ray0[EA + g] = sy;
+    a.ray0[2 * EA + g] = a.map.dt[cell_index(a.map, sx, sy)];  // first lookup (laser_models.py:129)
+    double t0 = first_theta_index(s[4], a.fov, a.theta_dis);
+    a.nruns[g] = build_beam_runs(t0, a.inc, a.theta_dis, a.B, a.runs + (size_t)g * kMaxSeg, kMaxSeg);
+    a.ttc_hit[g] = 0;
+    if (ag == 0) {
+        a.reset_flag[e] = (uint8_t)do_reset;
+        a.noise_step[e] = do_reset ? 0ull : nstep;
+    }
+    };
+    auto car = [&]() {
     if (!valid) return;
     const uint64_t genv = (uint64_t)(a.env_offset + e);
-    int do_reset;
     if (a.mode == 1) {
         if (!gate) return;
         do_reset = 1;
@@ -227,29 +330,20 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
         a.lap_counts[g] = 0.0f;
     }
     update_pose(s, b0, b1, cnt, raw_steer, vel, a.pa[ag], a.dt, a.integrator);  // RaceCar.params (per agent)
-#pragma unroll
-    for (int k = 0; k < 7; ++k) a.st[(size_t)k * EA + g] = s[k];
-    a.sb[g] = b0;
-    a.sb[EA + g] = b1;
-    a.scnt[g] = cnt;
-    // scan pose (base_classes.py:420-422) and everything every ray of this car shares
-    // base_classes.py:420-422; with lidar_dist == 0 the offset is +-0 for any
-    // finite yaw, so the transcendentals are skipped (a non-finite yaw keeps
-    // the reference's NaN)
-    const bool no_offset = a.lidar_dist == 0.0 && isfinite(s[4]);
-    double sy4 = 0.0, cy4 = 1.0;
-    if (!no_offset) cr_sincos(s[4], sy4, cy4);
-    const double sx = no_offset ? s[0] + 0.0 : s[0] + a.lidar_dist * cy4;
-    const double sy = no_offset ? s[1] + 0.0 : s[1] + a.lidar_dist * sy4;
-    a.ray0[g] = sx;
-    a.ray0[EA + g] = sy;
-    a.ray0[2 * EA + g] = a.map.dt[cell_index(a.map, sx, sy)];  // first lookup (laser_models.py:129)
-    double t0 = first_theta_index(s[4], a.fov, a.theta_dis);
-    a.nruns[g] = build_beam_runs(t0, a.inc, a.theta_dis, a.B, a.runs + (size_t)g * kMaxSeg, kMaxSeg);
-    a.ttc_hit[g] = 0;
-    if (ag == 0) {
-        a.reset_flag[e] = (uint8_t)do_reset;
-        a.noise_step[e] = do_reset ? 0ull : nstep;
+    act = true;
+    if (!HMASK) tail();
+    };
+    car();
+    if (HMASK) {
+        // the hand-off mask's poses (every car of the block, the new or the unchanged ones), shared
+        // before the state stores so that the barrier waits on no memory operation
+        __shared__ float hx[64], hy[64], hth[64];
+        hx[threadIdx.x] = (float)s[0];
+        hy[threadIdx.x] = (float)s[1];
+        hth[threadIdx.x] = (float)s[4];
+        __syncthreads();
+        if (act) tail();
+        if (valid) handoff_chunks(a, g, hx, hy, hth, box_len, box_wid);  // (A divides 64: an env's cars share the block)
     }
 }
 
@@ -1236,6 +1330,8 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
     const int e = HANDOFF ? g / a.A : g;
     const int nch = (B + 63) >> 6;
     const int wstride = a.G4;
+    // the chunks whose scans k_post_multi may read (k_agents' handoff_chunks; without it every chunk)
+    const uint32_t hmask = HANDOFF ? (a.hmask ? ld_const(a.hmask + g) : 0xFFFFFFFFu) : 0u;
     const double *dt = a.m.dt;
     const FxLoop L = fx_loop(a);
     // the scan origin and first lookup in VGPRs (re-arm copies them into a slot)
@@ -1350,7 +1446,8 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
             const size_t row = (size_t)g * B;
             if (K.scans_f32) *reinterpret_cast<float *>(reinterpret_cast<char *>(K.scans_f32 + row) + (uint32_t)b * 4u) = (float)range;
             if (K.scans_f64) *reinterpret_cast<double *>(reinterpret_cast<char *>(K.scans_f64 + row) + (uint32_t)b * 8u) = range;
-            if (HANDOFF) *reinterpret_cast<double *>(reinterpret_cast<char *>(K.scan + row) + (uint32_t)b * 8u) = range;
+            if (HANDOFF && ((hmask >> kk[r]) & 1u))
+                *reinterpret_cast<double *>(reinterpret_cast<char *>(K.scan + row) + (uint32_t)b * 8u) = range;
         }
         lanes += (uint32_t)min(64, B - kk[r] * 64);  // the chunk's beams (scalar)
     };
@@ -1835,7 +1932,10 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     hipError_t e;
     auto evk = [&](int i) -> hipEvent_t { return ev ? ev[i] : nullptr; };  // (start, stop) per kernel
     // 64-thread blocks: a few thousand cars must still spread over all CUs
-    hipExtLaunchKernelGGL(k_agents, dim3((EA + 63) / 64), dim3(64), 0, s, evk(0), evk(1), 0, a);
+    if (a.hmask)
+        hipExtLaunchKernelGGL(k_agents<true>, dim3((EA + 63) / 64), dim3(64), 0, s, evk(0), evk(1), 0, a);
+    else
+        hipExtLaunchKernelGGL(k_agents<false>, dim3((EA + 63) / 64), dim3(64), 0, s, evk(0), evk(1), 0, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (a.gate_wait && (e = hipStreamWaitEvent(s, a.gate_wait, 0)) != hipSuccess) return e;
     const bool single = a.A == 1;
@@ -1976,6 +2076,7 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                     ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
                     if (!single && a.geo) {  // leading geometry items (a multiple of 8: XCD mapping kept)
                         ra.geo = a.geo;
+                        ra.hmask = a.hmask;
                         ra.geo_blocks = ((ra.EA * (a.A - 1) + 63) / 64 + 7) / 8 * 8;
                         ra.st = a.st;
                         ra.pa = a.pa;
