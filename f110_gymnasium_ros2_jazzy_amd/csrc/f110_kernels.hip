@@ -342,8 +342,8 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
         hy[threadIdx.x] = (float)s[1];
         hth[threadIdx.x] = (float)s[4];
         __syncthreads();
-        if (act) tail();
         if (valid) handoff_chunks(a, g, hx, hy, hth, box_len, box_wid);  // (A divides 64: an env's cars share the block)
+        if (act) tail();
     }
 }
 
