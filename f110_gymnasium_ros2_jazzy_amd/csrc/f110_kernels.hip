@@ -163,7 +163,7 @@ __device__ void handoff_chunks(const StepArgs &a, int g, const float *sx, const 
     const int ag = g % A, t0 = t - ag;  // the env's first car in the block
     const int nch = (B + 63) >> 6;
     const uint32_t all = nch >= 32 ? 0xFFFFFFFFu : ((1u << nch) - 1u);
-    const float fov = (float)a.fov, incr = (float)a.beam_incr;
+    const float half_fov = (float)(a.fov * 0.5), inv_incr = (float)(1.0 / a.beam_incr);
     const float xi = sx[t], yi = sy[t];
     uint32_t m = nch > 32 ? all : 0u;
     for (int j = 0; j < A && m != all; ++j) {
@@ -188,14 +188,14 @@ __device__ void handoff_chunks(const StepArgs &a, int g, const float *sx, const 
                 unsure |= !(fabsf(fabsf(ang) - 3.14159265f) > 1e-2f);
                 if (ang > 3.14159265f) ang -= 6.28318531f;
                 else if (ang < -3.14159265f) ang += 6.28318531f;
-                const float gk = (-ang + fov * 0.5f) / incr;
+                const float gk = (half_fov - ang) * inv_incr;
                 const int k = gk < 0.0f ? 0 : (gk > (float)(B - 1) ? B - 1 : (int)(gk + 0.5f));
                 lo = k < lo ? k : lo;
                 hi = k > hi ? k : hi;
             }
             lo = lo - 3 < 0 ? 0 : lo - 3;
             hi = hi + 3 > B - 1 ? B - 1 : hi + 3;
-            for (int c = lo >> 6; c <= hi >> 6; ++c) m |= 1u << c;
+            m |= (2u << (hi >> 6)) - (1u << (lo >> 6));  // chunks lo / 64 .. hi / 64 (hi / 64 <= 31)
         }
         if (unsure) m = all;
     }
