@@ -141,7 +141,8 @@ __device__ __forceinline__ void reset_next_heavy(const StepArgs &a) {
 // (get_blocked_view_indices, laser_models.py:282-315) -- seen from the car's yaw or, after a TTC
 // response, from yaw 0 (base_classes.py:246-249).  Here in f32 (the box from fast sin / cos, the
 // bearings from a polynomial atan2 good to ~2e-4 rad: errors far below a beam's 4.4e-3 rad), the
-// range widened by 3 beams; a bearing within 1e-2 rad of the +-pi wrap, or a NaN, marks every chunk.  The other chunks skip the
+// range widened by 3 beams; a bearing within 1e-2 rad of the +-pi wrap, a vertex within 1 cm of the
+// car, or a NaN, marks every chunk.  The other chunks skip the
 // hand-off store (its stores cost the two-agent ray launch ~6 %).  The poses of an env's cars meet
 // in LDS: A divides 64 (the context allocates no mask otherwise).
 __device__ __forceinline__ float bearing_f32(float y, float x) {  // atan2(y, x) within ~2e-4 rad (finite x, y)
@@ -177,7 +178,10 @@ __device__ void handoff_chunks(const StepArgs &a, int g, const float *sx, const 
         for (int q = 0; q < 4; ++q) {
             const float vx = cj * px[q] - sj * py[q] + sx[t0 + j], vy = sj * px[q] + cj * py[q] + sy[t0 + j];
             const float dx = vx - xi, dy = vy - yi;
-            unsure |= !(dx == dx) || !(dy == dy) || fabsf(dx) > 1e30f || fabsf(dy) > 1e30f;  // NaN / inf
+            // NaN / inf, or a vertex within 1 cm of the car (its f32 bearing is not reliable there; the
+            // reference's is NaN at distance 0: beam 0)
+            unsure |= !(dx == dx) || !(dy == dy) || fabsf(dx) > 1e30f || fabsf(dy) > 1e30f ||
+                      fabsf(dx) + fabsf(dy) < 0.01f;
             bear[q] = bearing_f32(dy, dx);
         }
         for (int w = 0; w < 2 && !unsure; ++w) {
