@@ -135,16 +135,6 @@ __device__ __forceinline__ void reset_next_heavy(const StepArgs &a) {
     if (a.heavy_count && blockIdx.x == 0 && threadIdx.x == 0) a.heavy_count[a.parity ^ 1] = 0;
 }
 
-// The 64-beam chunks of car g whose f64 scans k_post_multi may read (bit k: chunk k), for the ray
-// kernel's hand-off: its agent ray_cast visits only beams of each (car, opponent) pair's blocked
-// view [lo, hi] -- the nearest beams of the opponent box's vertex bearings
-// (get_blocked_view_indices, laser_models.py:282-315) -- seen from the car's yaw or, after a TTC
-// response, from yaw 0 (base_classes.py:246-249).  Here in f32 (the box from fast sin / cos, the
-// bearings from a polynomial atan2 good to ~2e-4 rad: errors far below a beam's 4.4e-3 rad), the
-// range widened by 3 beams; a bearing within 1e-2 rad of the +-pi wrap, a vertex within 1 cm of the
-// car, or a NaN, marks every chunk.  The other chunks skip the
-// hand-off store (its stores cost the two-agent ray launch ~6 %).  The poses of an env's cars meet
-// in LDS: A divides 64 (the context allocates no mask otherwise).
 __device__ __forceinline__ float bearing_f32(float y, float x) {  // atan2(y, x) within ~2e-4 rad (finite x, y)
     const float ax = fabsf(x), ay = fabsf(y);
     const float a = __fdividef(fminf(ax, ay), fmaxf(ax, ay));
@@ -156,6 +146,16 @@ __device__ __forceinline__ float bearing_f32(float y, float x) {  // atan2(y, x)
     return (ax == 0.0f && ay == 0.0f) ? 0.0f : r;
 }
 
+// The 64-beam chunks of car g whose f64 scans k_post_multi may read (bit k: chunk k), for the ray
+// kernel's hand-off: its agent ray_cast visits only beams of each (car, opponent) pair's blocked
+// view [lo, hi] -- the nearest beams of the opponent box's vertex bearings
+// (get_blocked_view_indices, laser_models.py:282-315) -- seen from the car's yaw or, after a TTC
+// response, from yaw 0 (base_classes.py:246-249).  Here in f32 (the box from fast sin / cos, the
+// bearings from a polynomial atan2 good to ~2e-4 rad: errors far below a beam's 4.4e-3 rad), the
+// range widened by 3 beams; a bearing within 1e-2 rad of the +-pi wrap, a vertex within 1 cm of the
+// car, or a NaN, marks every chunk.  The other chunks skip the hand-off store (its stores cost the
+// two-agent ray launch ~6 %).  The poses of an env's cars meet in LDS: A divides 64 (the context
+// allocates no mask otherwise).
 // sx / sy / sth: the block's cars' poses (LDS, k_agents writes them before a barrier).
 __device__ void handoff_chunks(const StepArgs &a, int g, const float *sx, const float *sy, const float *sth,
                                float len, float wid) {
