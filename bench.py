@@ -15,6 +15,12 @@ baseline.
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+`--gpus N > 1` without a launcher (no WORLD_SIZE in the environment) starts
+its own N ranks: the parent decides from argv / env alone, before anything
+touches the GPU (no torch import), runs torch.distributed.run over 127.0.0.1
+with the same arguments and exits with its return code.  Under a launcher,
+WORLD_SIZE must equal --gpus (else exit 2).
+
 Prints ONE JSON line on rank 0.  See DESIGN.md §Measurement for the
 roofline accounting; the cpu_baseline leg (rank 0, N=1) times the C oracle
 (oracle/) on the host cores for a bounded sample of the same workload.
@@ -92,6 +98,43 @@ def parse():
     return ap.parse_args()
 
 
+def free_port() -> int:
+    """A free TCP port on 127.0.0.1 for the self-launched ranks' rendezvous."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def launcher_cmd(argv: list, n: int, port: int) -> list:
+    """The command the parent runs for --gpus n without an outer launcher:
+    torch.distributed.run, one node, n ranks, rendezvous on 127.0.0.1, this
+    file with the caller's own arguments (--gpus n among them)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def self_launch(args, argv: list) -> int:
+    """--gpus N > 1 with no WORLD_SIZE: run the N ranks as children and return
+    their launcher's exit code (non-zero when any rank failed).  Called before
+    any torch import, so this process never initialises HIP."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL's IPC on this host (dmabuf only)
+    env.setdefault("OMP_NUM_THREADS", "1")  # torch.distributed.run would warn and set it anyway
+    return subprocess.call(launcher_cmd(argv, args.gpus, free_port()), env=env)
+
+
+def check_world(args) -> None:
+    """Under a launcher, its WORLD_SIZE must be --gpus: a mismatch exits 2
+    instead of printing an N-GPU line for a different rank count."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to report a mismatched run",
+              file=sys.stderr)
+        sys.exit(2)
+
+
 def learner_roofline(M: int, obs: int, update_ms: float) -> dict:
     """The learner update against the fp32 MFMA peak (its GEMMs run on
     v_mfma_f32_32x32x2_f32, csrc/f110_gemm.hip): GEMM FLOPs per update / the
@@ -111,17 +154,39 @@ def bench_ddpg(args):
     critic gradients all-reduced over the ranks by RCCL)."""
     import torch
     from f110_gymnasium_ros2_jazzy_amd import distributed as D
-    from f110_gymnasium_ros2_jazzy_amd.train import VectorTrainer
     rank, world, local = D.init()
     dev_index = D.local_device_index(local)
     torch.cuda.set_device(dev_index)
-    per_gpu = args.envs_per_gpu or 4096  # C5: 32768 envs over 8 GPUs
+    result = run_ddpg(args, args.envs_per_gpu or 4096, args.steps, args.warmup)  # C5: 32768 envs over 8 GPUs
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    D.shutdown()
+
+
+def run_ddpg(args, per_gpu: int, K: int, W: int) -> dict:
+    """The C5 loop on this rank's share of per_gpu x world envs: W untimed
+    vector steps, K timed ones (barrier + synchronize, max over ranks), then a
+    phase split and the data-parallel consistency check.  Returns the line."""
+    import torch
+    from f110_gymnasium_ros2_jazzy_amd import distributed as D
+    from f110_gymnasium_ros2_jazzy_amd.train import VectorTrainer
+    rank, world, _ = D.env_rank_world()
     shard = D.shard_range(per_gpu * world, world, rank)
-    K, W = args.steps, args.warmup
     # learner updates start once the memory holds a batch: ceil(batch / envs) steps
     fill = -(-args.ddpg_batch // max(shard.count, 1)) + 1
     tr = VectorTrainer(shard.count, batch_size=args.ddpg_batch, memory_size=args.ddpg_memory,
                        warmup_steps=min(fill, W), seed=args.seed, env_offset=shard.offset, rank_seed=rank)
+    # untimed steps for >= ramp_s seconds first (the idle GPU clocks down; DVFS ramp), in blocks of 25
+    # whose end every rank agrees on (the learner's all-reduces need the same step count on each rank)
+    t_end = time.perf_counter() + args.ramp_s
+    ramp = 0
+    while args.ramp_s > 0:
+        for _ in range(25):
+            tr.step()
+        ramp += 25
+        torch.cuda.synchronize()
+        if D.max_over_ranks(float(time.perf_counter() >= t_end)) > 0:
+            break
     for _ in range(W):
         tr.step()
     assert tr.last is not None, "warm-up too short: no learner update ran"
@@ -183,16 +248,17 @@ def bench_ddpg(args):
                                f"PER replay, 1 learner update of {args.ddpg_batch} rows per vector step",
                    "envs_per_gpu": per_gpu, "global_envs": per_gpu * world,
                    "batch_per_rank": args.ddpg_batch, "memory_per_rank": args.ddpg_memory,
-                   "parallelism": f"env-shard x{world}, DDPG data-parallel (RCCL all-reduce of grads)"},
+                   "ramp": {"seconds": args.ramp_s, "steps": ramp},
+                   "parallelism": (f"env-shard x{world}, DDPG data-parallel ({D.describe()['backend']} all-reduce of grads; nccl = RCCL)"
+                                   if world > 1 else "one GPU, one learner (no all-reduce)"),
+                   "dist": D.describe()},
         "phases_ms": ph,
         "learner_roofline": learner_roofline(args.ddpg_batch, tr.agent.obs_dim, ph["learner_update_ms"]),
         "learner": {"critic_loss": float(tr.last["critic_loss"]), "actor_loss": float(tr.last["actor_loss"]),
                     "updates": tr.agent.global_step, "ranks_in_sync": in_sync},
     }
-    if rank == 0:
-        print(json.dumps(result), flush=True)
     tr.close()
-    D.shutdown()
+    return result
 
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (exact f32), dense
@@ -348,18 +414,21 @@ def scan_check(O, scanner, runner, act, threads):
     poses = np.concatenate(poses)
     ref = scanner.scan(poses, threads=threads)
     diff = g - ref
-    return {"kernel": f"{ray_kernel_name(sims[0])} (the timed runner, one extra step)", "cars": int(poses.shape[0]),
+    return {"kernel": f"{ray_kernel_name(sims[0], shared=len(sims) > 1)} (the timed runner, one extra step)", "cars": int(poses.shape[0]),
             "cars_skipped_ttc": skipped, "rays": int(diff.size),
             "l2": float(np.sqrt(np.sum(diff * diff))), "max_abs": float(np.max(np.abs(diff))),
             "bit_exact_fraction": float(np.mean(diff == 0.0))}
 
 
-def ray_kernel_name(sm):
-    """The ray kernel launch_env_step picks for this context's unmasked steps."""
+def ray_kernel_name(sm, shared=False):
+    """The ray kernel launch_env_step picks for this context's unmasked steps (shared: a stream
+    sub-shard, f110_set_device_share with several contexts: single-agent k_rays_fxs then takes the
+    theta table in LDS, 8 waves per block)."""
     names = {1: "k_rays_tiled (flat)", 2: "k_rays_tiled (chunked)", 3: "k_rays_fx"}
     if sm.ray_kernel == 3 and sm.ray_refill > 0:
+        lds = ", theta table in LDS" if shared and sm.A == 1 else ""
         return (f"k_rays_fxs ({sm.ray_refill} wave(s) per car, 2 software-pipelined chunk slots with refill, "
-                f"padded EDT)")
+                f"padded EDT{lds})")
     if sm.ray_kernel == 3 and sm.ray_lanes > 1:
         return f"k_rays_fxn ({sm.ray_lanes} rays per lane)"
     return names.get(sm.ray_kernel, str(sm.ray_kernel))
@@ -406,6 +475,18 @@ def scan_check_multi(O, scanner, runner, act, threads, S=256):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args, sys.argv[1:]))
+    check_world(args)
+    if os.environ.get("F110_BENCH_ECHO_RANKS") == "1":  # launcher test hook (tests/test_bench_launch.py): no GPU
+        print(json.dumps({"rank": int(os.environ.get("RANK", 0)), "world": int(os.environ.get("WORLD_SIZE", 1)),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", 0)),
+                          "master_addr": os.environ.get("MASTER_ADDR"), "gpus": args.gpus,
+                          "argv": sys.argv[1:]}), flush=True)
+        return
     if args.workload == "ddpg":
         return bench_ddpg(args)
     import numpy as np
@@ -416,8 +497,6 @@ def main():
     from f110_gymnasium_ros2_jazzy_amd.streams import StreamShards
 
     rank, world, local = D.init()
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     dev_index = D.local_device_index(local)
     torch.cuda.set_device(dev_index)
     dev = torch.device(f"cuda:{dev_index}")
@@ -437,13 +516,13 @@ def main():
     gidx = rng.integers(0, spawn.shape[0], size=G)[shard.offset:shard.offset + E]
     poses0 = spawn[gidx]
 
-    def actions(n_steps, n_envs, offset, n_global):
+    def actions(n_steps, n_envs, offset, n_global, A_=A):
         """Uniform random actions keyed by GLOBAL env id: the job's [T, n_global]
         draw (one seed, one shape on every rank), then this rank's columns, so
         an env steps the same actions whatever the GPU count."""
         gen = torch.Generator(device=dev)
         gen.manual_seed(args.seed)
-        a = torch.rand(n_steps, n_global, A, 2, device=dev, generator=gen, dtype=torch.float32)
+        a = torch.rand(n_steps, n_global, A_, 2, device=dev, generator=gen, dtype=torch.float32)
         a = a[:, offset:offset + n_envs].contiguous()
         a[..., 0] = a[..., 0] * (2 * 0.4189) - 0.4189   # steer in [-0.4189, 0.4189]
         a[..., 1] = a[..., 1] * 20.0                   # speed in [0, 20] (ddpg_config.yaml:19-20)
@@ -457,11 +536,11 @@ def main():
         kind = "streams"
     policy_kind = "one"  # what a policy loop steps: one call per step, one context
 
-    def make(n_envs, offset, kind_):
-        kw = dict(n_agents=A, device=dev, seed=args.seed, noise_std=noise, autoreset=True, spawn_poses=spawn,
+    def make(n_envs, offset, kind_, A_=A, spawn_=spawn):
+        kw = dict(n_agents=A_, device=dev, seed=args.seed, noise_std=noise, autoreset=True, spawn_poses=spawn_,
                   keep_f64_scans=True)
         if kind_ == "streams":
-            s = args.streams if args.streams > 0 else auto_streams(n_envs, A)
+            s = args.streams if args.streams > 0 else auto_streams(n_envs, A_)
             if s > 1 and n_envs % s == 0:
                 r = StreamShards(track, n_envs=n_envs, n_streams=s, env_offset=offset, **kw)
                 r.kind = "streams"
@@ -504,7 +583,25 @@ def main():
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         D.barrier()
-        return D.max_over_ranks(t1 - t0), r.read_counters()
+        return D.max_over_ranks(t1 - t0)
+
+    def count_replay(r, p0, a):
+        """(lookups, rays) of the timed steps: the default ray kernel counts only in its counting build
+        (f110_debug_set_simt), so the timed region runs uncounted and this replays it counted -- reset,
+        the W warm-up steps, then the same K steps: trajectories are deterministic after a reset (the
+        digest's premise), so the counts are the timed steps' own."""
+        r.reset(p0)
+        steps(r, a, 0, W, True)
+        torch.cuda.synchronize(dev)
+        r.set_simt(True)
+        r.reset_counters()
+        steps(r, a, W, K, True)
+        if hasattr(r, "join"):
+            r.join()
+        torch.cuda.synchronize(dev)
+        out = r.read_counters()
+        r.set_simt(False)
+        return out
 
     def digest(r):
         """trajectory_digest: sha256 over the obs rows (f32 bytes) of global envs
@@ -523,9 +620,30 @@ def main():
         h = D.sum_tensor_over_ranks(h)
         return {"sha256": hashlib.sha256(h.numpy().tobytes()).hexdigest()[:32], "envs": len(ids), "stride": stride}
 
+    def secondary_c4(n):
+        """BASELINE config 4 on this GPU: n two-agent envs (ego + opponent, inter-car GJK and agent
+        ray_cast), the same runners and K / W as the headline, the scan check in lock-step with the
+        oracle (its non-bit-exact ray_cast beams counted)."""
+        sp2 = centerline_spawns(args.map.replace("_map", ""), 2)
+        p2 = sp2[np.random.default_rng(args.seed + 4).integers(0, sp2.shape[0], size=n)]
+        a2 = actions(W + K + 1, n, 0, n, A_=2)
+        r2 = make(n, 0, kind, A_=2, spawn_=sp2)
+        el2 = timed(r2, p2, a2)
+        line = {"envs": n, "agents": 2, "value": n * K / el2, "ms_per_step": el2 / K * 1e3, "runner_kind": r2.kind,
+                "streams": r2.S if not isinstance(r2, BatchSim) else 1}
+        line["scan_check"] = scan_check_multi(O, scanner, r2, a2[W + K], cpu_threads())
+        r2.close()
+        if kind != policy_kind:
+            r1 = make(n, 0, policy_kind, A_=2, spawn_=sp2)
+            el1 = timed(r1, p2, a2)
+            line["single_stream"] = {"value": n * K / el1, "ms_per_step": el1 / K * 1e3, "runner_kind": r1.kind}
+            r1.close()
+        return line
+
     runner = make(E, shard.offset, kind)
-    elapsed, (lookups, rays) = timed(runner, poses0, acts)
+    elapsed = timed(runner, poses0, acts)
     traj = digest(runner)
+    lookups, rays = count_replay(runner, poses0, acts)
     mean_look = lookups / max(rays, 1)
     total_env_steps = D.sum_over_ranks(E * K)
     RUNNER_TEXT = {
@@ -589,6 +707,49 @@ def main():
             prof_n += n
     per_kernel = {key: acc[key] / max(launches, 1) for key in acc}
     per_kernel["steps"] = launches
+
+    def runner_ray_time(r, n_steps):
+        """The timed runner's own ray time (StreamShards: its sub-shards' ray launches run concurrently on
+        their streams): every launch's begin / end (HIP events on the kernels' own dispatches, against one
+        reference event), the union of those intervals over chunks of PC steps, per step; and each
+        launch's mean duration (what rocprofv3 averages per kernel).  Not part of `value`."""
+        union = 0.0
+        durs = []
+        done = 0
+        wall = 0.0
+        while done < n_steps:
+            n = min(PC, n_steps - done, K)
+            k0 = chunk_rows(n)
+            ref = torch.cuda.Event(enable_timing=True)
+            ref.record(torch.cuda.current_stream(dev))
+            for sm in r.sims:
+                sm.profile_begin(n)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            steps(r, acts, k0, n, True)
+            r.join()
+            torch.cuda.synchronize(dev)
+            wall += time.perf_counter() - t0
+            iv = []
+            for sm in r.sims:
+                st = sm.profile_stamps(ref, n)
+                sm.profile_end()
+                iv += [(float(a), float(b)) for a, b in st[:, 2:4]]
+                durs += list(st[:, 3] - st[:, 2])
+            iv.sort()
+            cur_a, cur_b = iv[0]
+            for a_, b_ in iv[1:]:
+                if a_ > cur_b:
+                    union += cur_b - cur_a
+                    cur_a, cur_b = a_, b_
+                else:
+                    cur_b = max(cur_b, b_)
+            union += cur_b - cur_a
+            done += n
+        return {"ray_union_ms_per_step": union / n_steps, "launch_ms_mean": float(sum(durs) / len(durs)),
+                "launches_per_step": len(r.sims), "steps": n_steps, "pass_wall_ms_per_step": wall / n_steps * 1e3}
+
+    timed_rays = runner_ray_time(runner, KP) if not isinstance(runner, BatchSim) else None
     prof_step_ms = prof_s / max(prof_n, 1) * 1e3  # wall time per profiled step (events included)
     plain_step_ms = plain_s / max(plain_n, 1) * 1e3
     single = None
@@ -610,7 +771,7 @@ def main():
     prof.set_simt(False)
     full_outputs = None
     if not args.no_full_outputs:
-        el_full, _ = timed(sim, poses0, acts, minimal=False)
+        el_full = timed(sim, poses0, acts, minimal=False)
         full_outputs = {"value": total_env_steps / el_full, "ms_per_step": el_full / K * 1e3,
                         "runner": RUNNER_TEXT[policy_kind] + ", every output (f32 + f64 scans, laps, sim_time, "
                                                              "was_reset)"}
@@ -627,25 +788,40 @@ def main():
     # cell) + 4 B of f32 range out; the 120 B/agent of state I/O
     # go with the step (k_agents).
     kernel_bytes = E * A * B * (4.0 * mean_look + 4.0)
-    k_ms = per_kernel["k_rays_ms"]  # per step
+    one_ms = per_kernel["k_rays_ms"]  # the one-context runner's ray launch, per step
+    # the roofline of the timed runner's own ray launches: with stream sub-shards, the union of their
+    # (concurrent) launch intervals per step; with one context, its launch
+    k_ms = timed_rays["ray_union_ms_per_step"] if timed_rays else one_ms
     achieved = kernel_bytes / (k_ms * 1e-3) / 1e9
     pmc = load_profile("pmc_traffic", E, A)
     busy = load_profile("pmc_busy", E, A)
     traffic = pmc.get("bytes_per_launch") if pmc else None
     roof = {
         "kernel": "k_rays",
+        "timed_runner": (
+            {"ray_kernel": ray_kernel_name(runner.sims[0], shared=runner.S > 1) +
+                           f", {runner.S} concurrent sub-shard launches per step",
+             "kernel_ms_is": "the union of the sub-shards' ray-launch intervals per step (HIP events on the "
+                             "kernels' own dispatches)", **timed_rays}
+            if timed_rays else {"ray_kernel": ray_kernel_name(runner), "kernel_ms_is": "the one launch per step"}),
+        "one_context": {"ray_kernel": ray_kernel_name(prof), "kernel_ms": one_ms,
+                        "achieved": kernel_bytes / (one_ms * 1e-3) / 1e9,
+                        "frac": kernel_bytes / (one_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "profiled_launches": per_kernel["steps"]},
         "profiled_steps": KP,
         "profiled_launches": per_kernel["steps"],
         "bound": ("the texture-address path, per wave-level vector load (gather_roofline.ta_cycles_per_load TA cycles "
                   "each whatever its lanes do; HBM is not the limit: see hbm_traffic_frac; DESIGN.md 3.9)" if prof.ray_kernel == 3 and prof.ray_refill > 0
                   else "latency of the dependent EDT gather chain (HBM is not the limit: see hbm_traffic_frac; capping "
                   "occupancy at 6/4/2 waves per SIMD costs 1.31x/1.62x/2.9x, DESIGN.md 3.2)"),
-        "ray_kernel": ray_kernel_name(prof),
+        "ray_kernel": (ray_kernel_name(runner.sims[0], shared=runner.S > 1) if timed_rays else ray_kernel_name(runner)),
         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
         "traffic": traffic, "kernel_ms": k_ms, "algorithmic_bytes_per_launch": kernel_bytes,
-        "kernel_ms_note": "per step (a profiled launch's time / its steps)",
+        "kernel_ms_note": "per step: the timed runner's ray time (timed_runner.kernel_ms_is); bytes: all of the "
+                          "step's cars (every sub-shard launch), lookups from a counting replay of the timed steps",
         "mean_lookups_per_ray": mean_look,
-        "step_kernels_ms": {"k_agents": per_kernel["k_agents_ms"], "k_rays": k_ms, "k_post": per_kernel["k_post_ms"]},
+        "step_kernels_ms_one_context": {"k_agents": per_kernel["k_agents_ms"], "k_rays": one_ms,
+                                        "k_post": per_kernel["k_post_ms"]},
         "step_algorithmic_bytes_per_env": algorithmic_bytes_per_env_step(B, A, mean_look),
         # vector-gathered lookups of the loop / (64 x the wave-level vector gathers it issued, the ended
         # lanes' zero-cell reads included), from the kernel's own counters; lookups a k_rays_fxs slot
@@ -672,13 +848,19 @@ def main():
         gathers = lane_slots / 64.0 / max(1, simt_steps)  # per launch
         loads = gathers + other_loads / max(1, simt_steps)
         min_ms = loads * ta_cyc / N_CU / (CLOCK_GHZ * 1e9) * 1e3
+        # the counts and the TA cycles per load are the one-context kernel's (its SIMT pass, its PMC file)
         roof["gather_roofline"].update({"slot_gathers_per_launch": gathers, "vmem_loads_per_launch": loads,
-                                        "ta_min_ms": min_ms, "ta_frac": min_ms / k_ms})
-    # consistency: the kernel runs inside the step it is timed in (the one-context runner's own wall time
-    # per step, measured in the chunks interleaved with the profiled ones)
-    roof["kernel_le_step"] = {"ok": bool(k_ms <= plain_step_ms), "kernel_ms": k_ms, "runner_step_ms": plain_step_ms,
-                              "profiled_pass_step_ms": prof_step_ms,
-                              "kernels_sum_ms": sum(per_kernel[k] for k in ("k_agents_ms", "k_rays_ms", "k_post_ms"))}
+                                        "ta_min_ms": min_ms, "ta_frac_one_context": min_ms / one_ms})
+    # consistency: each kernel runs inside the step it is timed in (the timed runner's ray time against its
+    # ms_per_step; the one-context launch against that runner's own wall time per step, measured in the
+    # chunks interleaved with the profiled ones)
+    pass_ms = timed_rays["pass_wall_ms_per_step"] if timed_rays else plain_step_ms
+    roof["kernel_le_step"] = {"ok": bool(k_ms <= pass_ms and one_ms <= plain_step_ms), "kernel_ms": k_ms,
+                              "kernel_pass_ms_per_step": pass_ms, "timed_ms_per_step": elapsed / K * 1e3,
+                              "one_context_kernel_ms": one_ms,
+                              "one_context_step_ms": plain_step_ms, "profiled_pass_step_ms": prof_step_ms,
+                              "one_context_kernels_sum_ms": sum(per_kernel[k] for k in ("k_agents_ms", "k_rays_ms",
+                                                                                          "k_post_ms"))}
     if pmc and traffic:
         roof["hbm_traffic_gbs"] = traffic / (k_ms * 1e-3) / 1e9
         roof["hbm_traffic_frac"] = roof["hbm_traffic_gbs"] / HBM_PEAK_GBS
@@ -711,6 +893,7 @@ def main():
             "global_envs": G, "envs_per_gpu": E, "agents": A, "beams": B, "map": args.map,
             "integrator": "RK4", "scan_noise": not args.no_noise, "autoreset": True,
             "parallelism": f"env-shard x{world} (no collectives)",
+            "dist": D.describe(),
             "streams_per_gpu": runner.S if not isinstance(runner, BatchSim) else 1,
             "ramp": ramp,
             "runner": RUNNER_TEXT[runner.kind] + "; minimal outputs (obs, collisions, terminated): no f32 "
@@ -732,16 +915,18 @@ def main():
             p2 = spawn[rng.integers(0, spawn.shape[0], size=n)]
             a2 = actions(W + K, n, 0, n)
             r2 = make(n, 0, kind)
-            el2, _ = timed(r2, p2, a2)
+            el2 = timed(r2, p2, a2)
             line = {"envs": n, "value": n * K / el2, "ms_per_step": el2 / K * 1e3, "runner_kind": r2.kind,
                     "streams": r2.S if not isinstance(r2, BatchSim) else 1}
             r2.close()
             if kind != policy_kind:
                 r1 = make(n, 0, policy_kind)
-                el1, _ = timed(r1, p2, a2)
+                el1 = timed(r1, p2, a2)
                 line["single_stream"] = {"value": n * K / el1, "ms_per_step": el1 / K * 1e3, "runner_kind": r1.kind}
                 r1.close()
             sec[label] = line
+        if A == 1:
+            sec["C4_8192x2"] = secondary_c4(8192)
         result["secondary"] = sec
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -751,11 +936,17 @@ def main():
             result["cpu_baseline"] = cpu_baseline(O, scanner, poses0[:n], a_cpu[:T, :n].cpu().numpy(), args)
         except Exception as exc:  # report, never hide
             result["cpu_baseline"] = {"error": repr(exc)}
-    if rank == 0:
-        print(json.dumps(result), flush=True)
     if sim is not runner:
         sim.close()
     runner.close()
+    if rank == 0 and world == 1 and not args.no_secondary and A == 1:
+        # BASELINE config 5's per-GPU share (4096 two-agent envs, the batched train_ddpg loop)
+        c5 = run_ddpg(args, 4096, K, max(W, 2))
+        result["secondary"]["C5_ddpg_4096"] = {k: c5[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup",
+                                                                 "phases_ms", "learner_roofline", "learner")}
+        result["secondary"]["C5_ddpg_4096"]["workload"] = c5["config"]["workload"]
+    if rank == 0:
+        print(json.dumps(result), flush=True)
     D.shutdown()
 
 

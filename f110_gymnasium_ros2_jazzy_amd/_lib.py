@@ -68,7 +68,7 @@ INTEGRATOR_EULER = 2
 EXPORTS = [
     "f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config", "f110_edt_k",
     "f110_create", "f110_destroy", "f110_reset", "f110_step", "f110_get_state", "f110_set_state",
-    "f110_scan_batch", "f110_dynamics_batch", "f110_read_counters", "f110_reset_counters", "f110_debug_read_simt", "f110_debug_set_simt",
+    "f110_scan_batch", "f110_dynamics_batch", "f110_read_counters", "f110_reset_counters", "f110_debug_read_simt", "f110_debug_set_simt", "f110_debug_set_handoff_check", "f110_debug_profile_stamps",
     "f110_profile_begin", "f110_profile_end", "f110_host_tables", "f110_host_beam_indices",
     "f110_set_scan_noise", "f110_set_params", "f110_host_cell_index", "f110_gap_follow",
     "f110_host_window_ranges", "f110_track_create", "f110_track_destroy", "f110_track_arrays",
@@ -87,6 +87,16 @@ _lib = None
 
 class F110Error(RuntimeError):
     pass
+
+
+class _Missing:
+    """An entry point an older A/B build (F110_LIB) does not export."""
+
+    def __init__(self, name):
+        self.name, self.argtypes, self.restype = name, None, None
+
+    def __call__(self, *a):
+        raise F110Error(f"{self.name}: not exported by this (alternate) build")
 
 
 def lib_path() -> str:
@@ -118,6 +128,8 @@ def load(build_if_missing: bool = True):
             old = name.replace("f110_debug_", "f110_")
             if name.startswith("f110_debug_") and not hasattr(L, name) and hasattr(L, old):
                 setattr(L, name, getattr(L, old))
+            elif not hasattr(L, name):  # newer than that build: fails when called
+                setattr(L, name, _Missing(name))
     i32, i64, u64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
     L.f110_abi_version.restype = ctypes.c_int
     L.f110_last_error.restype = ctypes.c_char_p
@@ -140,6 +152,8 @@ def load(build_if_missing: bool = True):
     L.f110_reset_counters.argtypes = [_P, _P]
     L.f110_debug_read_simt.argtypes = [_P, ctypes.POINTER(u64), ctypes.POINTER(u64), _P]
     L.f110_debug_set_simt.argtypes = [_P, ctypes.c_int32]
+    L.f110_debug_set_handoff_check.argtypes = [_P, ctypes.c_int32]
+    L.f110_debug_profile_stamps.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]
     L.f110_set_scan_noise.argtypes = [_P, _P]
     L.f110_host_window_ranges.argtypes = [ctypes.c_double, ctypes.c_double, i32, ctypes.c_double, ctypes.c_double,
                                           _P]

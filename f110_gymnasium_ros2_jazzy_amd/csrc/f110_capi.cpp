@@ -103,6 +103,8 @@ struct f110_ctx {
     int32_t fx_refill = 0;   // waves per car of k_rays_fxs (0 = k_rays_fxn; f110_debug_set_ray_refill)
     bool fxs_lds = false;    // single-agent k_rays_fxs with the LDS theta table (f110_set_device_share, > 1 context)
     bool count_slots = false;  // f110_debug_set_simt: lane-slot counter of the fixed-point loops (f110_debug_read_simt)
+    int32_t hcheck = 0;        // f110_debug_set_handoff_check: bit 0 poison + count misses, bit 1 mask off,
+                               // bit 2 an empty mask (the check's own test)
     int fx_ilp = 1;         // rays per lane (f110_debug_set_ray_lanes; default by car count)
 
     hipEvent_t *next_prof_events() {
@@ -681,7 +683,13 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
     ALLOC(c->runs, (size_t)kMaxSeg * EA);
     ALLOC(c->nruns, EA);
     if (C.n_agents >= 2) ALLOC(c->geo, (size_t)EA * (C.n_agents - 1));
-    if (C.n_agents >= 2 && 64 % C.n_agents == 0) ALLOC(c->hmask, (size_t)EA);  // k_agents' hand-off chunk masks
+    {
+        // k_agents' hand-off chunk masks: their f32 bearings hold to a beam for coordinates below 1 km
+        // (handoff_chunks); a larger map stores every chunk instead
+        const double extent = std::max(std::fabs(origin[0]), std::fabs(origin[1])) +
+                              1.5 * resolution * (double)std::max(H, W);
+        if (C.n_agents >= 2 && 64 % C.n_agents == 0 && extent < 1000.0) ALLOC(c->hmask, (size_t)EA);
+    }
     ALLOC(c->scan, EA * (size_t)C.n_beams);
     ALLOC(c->reset_flag, (size_t)C.n_envs);
     ALLOC(c->ttc_hit, EA);
@@ -851,7 +859,8 @@ static StepArgs make_step_args(f110_ctx *c, const f110_outputs *out) {
     a.runs = c->runs;
     a.nruns = c->nruns;
     a.geo = c->geo;
-    a.hmask = c->hmask;
+    a.hmask = (c->hcheck & 2) ? nullptr : c->hmask;  // f110_debug_set_handoff_check bit 1: every chunk stored
+    a.hcheck = c->hcheck & 5;
     a.scan = c->scan;
     a.reset_flag = c->reset_flag;
     a.ttc_hit = c->ttc_hit;
@@ -1199,6 +1208,12 @@ extern "C" int f110_debug_set_simt(f110_ctx *ctx, int32_t on) {
     return F110_OK;
 }
 
+extern "C" int f110_debug_set_handoff_check(f110_ctx *ctx, int32_t mode) {
+    if (!ctx || mode < 0 || mode > 7) return fail(F110_E_INVALID, "f110_debug_set_handoff_check: bad argument");
+    ctx->hcheck = mode;
+    return F110_OK;
+}
+
 extern "C" int f110_debug_read_simt(f110_ctx *ctx, uint64_t *loop_lookups, uint64_t *lane_slots, void *stream) {
     if (!ctx) return fail(F110_E_INVALID, "f110_debug_read_simt: null context");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
@@ -1266,6 +1281,25 @@ extern "C" int f110_profile_begin(f110_ctx *ctx, int32_t max_steps) {
     return F110_OK;
 }
 
+extern "C" int f110_debug_profile_stamps(f110_ctx *ctx, void *ref_event, double *out, int32_t max_steps,
+                                         int32_t *steps_out) {
+    if (!ctx || !ref_event || !out || max_steps < 0)
+        return fail(F110_E_INVALID, "f110_debug_profile_stamps: bad arguments");
+    if (use_device(ctx) != F110_OK) return F110_E_HIP;
+    const int n = ctx->prof_n < max_steps ? ctx->prof_n : max_steps;
+    for (int i = 0; i < n; ++i) {
+        hipEvent_t *ev = &ctx->prof_ev[(size_t)6 * i];
+        HIP_TRY(hipEventSynchronize(ev[5]));
+        for (int k = 0; k < 6; ++k) {
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, static_cast<hipEvent_t>(ref_event), ev[k]));
+            out[(size_t)6 * i + k] = ms;
+        }
+    }
+    if (steps_out) *steps_out = n;
+    return F110_OK;
+}
+
 extern "C" int f110_profile_end(f110_ctx *ctx, double ms_out[3], int32_t *steps_out) {
     if (!ctx) return fail(F110_E_INVALID, "f110_profile_end: null context");
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
@@ -1292,8 +1326,10 @@ extern "C" int f110_debug_wave_trace(f110_ctx *ctx, int32_t arm, uint64_t *host_
     if (use_device(ctx) != F110_OK) return F110_E_HIP;
     const int64_t EA = (int64_t)ctx->cfg.n_envs * ctx->cfg.n_agents;
     // an upper bound of any ray launch's waves (one-wave blocks: the chunked grids' EA x nch
-    // plus the heavy-first prefix; k_rays_fxs: EA x waves per car <= EA x nch)
-    const int64_t waves = EA * ((ctx->cfg.n_beams + 63) / 64) + ctx->heavy_cap + 64;
+    // plus the heavy-first prefix; k_rays_fxs: EA x waves per car <= EA x nch, after the multi-agent
+    // launch's leading geometry items, ceil(EA (A - 1) / 64) rounded up to 8)
+    const int64_t geo_items = ctx->cfg.n_agents > 1 ? ((EA * (ctx->cfg.n_agents - 1) + 63) / 64 + 7) / 8 * 8 : 0;
+    const int64_t waves = EA * ((ctx->cfg.n_beams + 63) / 64) + ctx->heavy_cap + 64 + geo_items;
     if (!ctx->wtrace) {
         void *q = nullptr;
         HIP_TRY(hipMalloc(&q, (size_t)waves * 4 * sizeof(uint64_t)));

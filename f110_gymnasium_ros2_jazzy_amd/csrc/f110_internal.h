@@ -66,6 +66,9 @@ struct StepArgs {
     PairGeom *geo;      // [E][A][A-1] pair geometry (A >= 2), see RayArgs::geo
     int32_t geo_ready;  // set by launch_env_step: this step's ray kernel computed geo
     int32_t count_slots;  // f110_debug_set_simt: lane-slot counter of the fixed-point loops
+    int32_t hcheck;       // f110_debug_set_handoff_check bit 0: the hand-off buffer is NaN-poisoned before the
+                          // ray launch and k_post_multi counts its reads outside hmask (ctr[.][6]); bit 2:
+                          // k_agents stores empty masks (a forced miss, the check's own test)
     int32_t fx_ilp;     // rays per lane of the fixed-point ray kernel (1: k_rays_fx, 2: k_rays_fxn / k_rays_fxs)
     double fov, eps, max_range, dt, lidar_dist, ttc_thresh, noise_std, inc, beam_incr;
     double side_max;  // max of the RaceCar side table (the TTC pre-test of k_rays_fxs)

@@ -151,7 +151,9 @@ __device__ __forceinline__ float bearing_f32(float y, float x) {  // atan2(y, x)
 // view [lo, hi] -- the nearest beams of the opponent box's vertex bearings
 // (get_blocked_view_indices, laser_models.py:282-315) -- seen from the car's yaw or, after a TTC
 // response, from yaw 0 (base_classes.py:246-249).  Here in f32 (the box from fast sin / cos, the
-// bearings from a polynomial atan2 good to ~2e-4 rad: errors far below a beam's 4.4e-3 rad), the
+// bearings from a polynomial atan2 good to ~2e-4 rad: errors far below a beam's 4.4e-3 rad for
+// vertices beyond the 1 cm cutoff while |x|, |y| < 1 km (f32 position rounding ulp(coord) / 1 cm
+// stays under a beam there; f110_create keeps no mask for a map that reaches beyond), the
 // range widened by 3 beams; a bearing within 1e-2 rad of the +-pi wrap, a vertex within 1 cm of the
 // car, or a NaN, marks every chunk.  The other chunks skip the hand-off store (its stores cost the
 // two-agent ray launch ~6 %).  The poses of an env's cars meet in LDS: A divides 64 (the context
@@ -203,7 +205,7 @@ __device__ void handoff_chunks(const StepArgs &a, int g, const float *sx, const 
         }
         if (unsure) m = all;
     }
-    a.hmask[g] = m;
+    a.hmask[g] = (a.hcheck & 4) ? 0u : m;  // f110_debug_set_handoff_check bit 2: a forced miss
 }
 
 // HMASK: the context keeps hand-off chunk masks (A >= 2 dividing 64): the block's new poses meet in
@@ -216,7 +218,7 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
     const bool valid = g < EA;
     const int A = a.A;
     const int e = valid ? g / A : 0;
-    const int ag = g - e * A;
+    const int ag = valid ? g - e * A : 0;  // padding threads: agent 0 (a.pa holds A entries)
     // Every input of the car is loaded first, before the heavy-list atomic
     // and before anything waits: one memory round trip for the whole prologue.
     double s[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -1192,9 +1194,9 @@ __device__ __forceinline__ T ld_off(const T *base, uint32_t byte_off) {  // glob
 // edge (the caller takes the IEEE path for those lanes, both slots at once)
 // (kFxsBase: the high dwords of t feed the u24 multiplies directly, the low
 // dwords hold the shifted fractions; cx / cy are RayArgs::fxs_cx / fxs_cy)
-__device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, double cy, double &x, double &y,
-                                                  double d, double c, double s, bool act, uint32_t zero_v,
-                                                  bool &near) {
+__device__ __forceinline__ uint32_t fxs_offset_m(const FxLoop &L, double cx, double cy, double &x, double &y,
+                                                 double d, double c, double s, uint64_t m, uint32_t zero_v,
+                                                 bool &near) {
     x += d * c;  // :135
     y += d * s;  // :136
     double tx, ty;
@@ -1202,9 +1204,16 @@ __device__ __forceinline__ uint32_t fxs_offset_nb(const FxLoop &L, double cx, do
     asm("v_fma_f64 %0, %1, %2, %3" : "=v"(ty) : "v"(y), "v"(L.ir), "s"(cy));
     near = min(dlo(tx), dlo(ty)) < 2u * kFxsBand;
     const uint32_t prow = __umul24(dhi(ty), L.k1);
-    uint32_t fast;
+    uint32_t fast, off;
     asm volatile("v_mad_u32_u24 %0, %1, 8, %2" : "=v"(fast) : "v"(dhi(tx)), "v"(prow));
-    return act ? fast : zero_v;
+    // lanes of the activity mask m take the cell, the others the zero cell: the mask (the slot's
+    // ballot, an SGPR pair) is the select's condition as it is, no per-lane copy of it (readfirstlane:
+    // the mask is wave-uniform; where the compiler cannot prove it, it must still land in SGPRs)
+    // (readfirstlane returns int: each half goes through uint32_t, or the low half would sign-extend)
+    const uint64_t ms = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)m);
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(off) : "v"(zero_v), "v"(fast), "s"(ms));
+    return off;
 }
 
 // One (car i, opponent j) pair's ray_cast geometry, serially on one lane: the
@@ -1307,7 +1316,7 @@ __device__ __noinline__ void ray_pair_geometry(const RayArgs &a, int blk) {
 // it; a lone context keeps one-wave blocks and the gathers, whose launch is shorter (0.685 vs
 // 0.697 ms at 65536 cars: the 8-wave blocks hold their LDS until their slowest car ends), as do
 // multi-agent contexts (the 8-wave blocks were slower there: C4 one context 27.7 -> 25.2 M).
-template <bool HANDOFF, bool LDS>
+template <bool HANDOFF, bool LDS, bool COUNT>
 __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayArgs a) {  // 8 waves per SIMD: <= 64 VGPRs
     static_assert(!(HANDOFF && LDS), "the LDS table is the single-agent kernel's");
     constexpr int NS = 2;
@@ -1325,8 +1334,8 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
         ray_pair_geometry(kernarg_here(), item);
         return;
     }
-    wave_stamp_start_w(a.wtrace, item);
-    const int bid = HANDOFF ? item - a.geo_blocks : item;
+    wave_stamp_start_w(a.wtrace, item);  // (the buffer holds the geometry items too: f110_debug_wave_trace)
+    const int bid = HANDOFF ? item - a.geo_blocks : item;  // the ray item (geometry items come first)
     const int wj = bid / a.EA;
     const int g = bid - wj * a.EA;
     const int lane = (int)(threadIdx.x & 63);
@@ -1360,7 +1369,7 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
             const int mid = (lo + hi + 1) >> 1;
             if (R[mid].start <= lane * 64) lo = mid;
             else hi = mid - 1;
-            ++srch;
+            if (COUNT) ++srch;
         }
         kinfo = lo;
     }
@@ -1385,7 +1394,7 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
             t2 = cs_lds[ti];
         } else {
             t2 = ld_off(reinterpret_cast<const double2 *>(K.cs2), (uint32_t)ti * 16u);
-            loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
+            if (COUNT) loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
         }
         c[r] = t2.x;
         sn[r] = t2.y;
@@ -1410,7 +1419,7 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
         double nz = 0.0;
         if (K.noise_ext) {
             nz = K.noise_ext[(size_t)e * B + bc];
-            loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
+            if (COUNT) loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
         } else if (K.noise_std > 0.0) {
             const int pp = kk[r] >> 1, ci = kpar[r];
             float nv;
@@ -1438,7 +1447,7 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
                 const bool may = ttc_may_fire_lane(range, K.side_max, v, K.ttc_thresh);
                 if (__builtin_amdgcn_ballot_w64(may)) {
                     const double2 t2 = ld_off(reinterpret_cast<const double2 *>(K.bs2), boff * 2u);  // (side, beam_cos)
-                    loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
+                    if (COUNT) loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
                     if (may && ttc_fires(range, t2.x, v * t2.y, K.ttc_thresh)) K.ttc_hit[g] = 1;
                 }
             }
@@ -1453,10 +1462,10 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
             if (HANDOFF && ((hmask >> kk[r]) & 1u))
                 *reinterpret_cast<double *>(reinterpret_cast<char *>(K.scan + row) + (uint32_t)b * 8u) = range;
         }
-        lanes += (uint32_t)min(64, B - kk[r] * 64);  // the chunk's beams (scalar)
+        if (COUNT) lanes += (uint32_t)min(64, B - kk[r] * 64);  // the chunk's beams (scalar)
     };
 
-    uint32_t lane_iters = 0, slot_gathers = 0;
+    uint32_t lane_iters = 0, slot_gathers = 0;  // COUNT only
     uint32_t closed_trips = 0;
     const double ux = fma(ld_const(a.ray0 + g), L.ir, L.cxk) - kFxpBase;
     const double uy = fma(ld_const(a.ray0 + a.EA + g), L.ir, L.cyk) - kFxpBase;
@@ -1472,18 +1481,19 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
         for (int r = 0; r < NS; ++r)
             if (pnext < nch) arm(r, true);  // tot = 0: the first trip's total completes tot = d00
         __builtin_amdgcn_s_waitcnt(0);
-        // one step of slot r (:133-141): the total, the activity test, the refill when the slot's
-        // chunk has ended (a slot with no chunk left to arm closes: kk = -1, m = 0), the step
-        // and its gather
+        // one step of slot r (:133-141): the total, the activity mask, the refill when the slot's
+        // chunk has ended (a slot with no chunk left to arm closes: kk = -1, m = 0), the step and its
+        // gather.  The mask (two ballots of the bare compares: their AND is one SALU op) selects the
+        // gather's offset itself; an ended lane reads the zero cell.  The lookup / lane-slot
+        // counters exist in the COUNT build only.
+        uint64_t nb[NS];
         auto slot_step = [&](int r) {
             tot[r] += d[r];  // :141 (d00 for a freshly armed slot: tot = d00, :130)
-            bool act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
             uint64_t m = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
             if (!m && kk[r] >= 0) {  // wave-uniform, rare: the slot's chunk has ended; refill it
                 finish(r);
                 if (pnext < nch) {
                     arm(r, false);  // tot = d = d00
-                    act = (dhi(d[r]) != 0u) & (tot[r] <= L.mr);
                     m = __builtin_amdgcn_ballot_w64(dhi(d[r]) != 0u) & __builtin_amdgcn_ballot_w64(tot[r] <= L.mr);
                 } else {
                     kk[r] = -1;
@@ -1492,30 +1502,42 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
                 // before the step stays vmcnt(1) (the other slot's gather may be in flight)
                 __builtin_amdgcn_s_waitcnt(0);
             }
-            lane_iters += (uint32_t)__popcll(m);
-            bool near;
-            const uint32_t off = fxs_offset_nb(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], act,
-                                               zero_v, near);
-            d[r] = ld_off(dt, off);
-            ++slot_gathers;
-            const uint64_t nb = __builtin_amdgcn_ballot_w64(near) & m;
-            if (nb) {  // rare: lanes within the guard band re-gather from the IEEE cell
-                const RayArgs &K = kernarg_here();
-                if (lane_in(nb)) d[r] = ld_off(dt, exact_offset_pad(K.m, x[r], y[r], (uint32_t)K.fxp_P));
-                loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
+            if (COUNT) {
+                lane_iters += (uint32_t)__popcll(m);
+                ++slot_gathers;
             }
+            bool near;
+            const uint32_t off = fxs_offset_m(L, a.fxs_cx, a.fxs_cy, x[r], y[r], d[r], c[r], sn[r], m, zero_v, near);
+            d[r] = ld_off(dt, off);
+            nb[r] = __builtin_amdgcn_ballot_w64(near) & m;
+            // nothing of the next slot's step moves above this gather: its total waits for the
+            // next slot's own gather (vmcnt(1)), which would otherwise become vmcnt(0) here
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        // the lanes of nb[r] (within the guard band of a cell edge) re-gather slot r's cell from the
+        // IEEE cell index (exec-masked, rare); the load lands before the slot's next step (loads
+        // return in order)
+        auto regather = [&](int r) {
+            const RayArgs &K = kernarg_here();
+            if (lane_in(nb[r])) d[r] = ld_off(dt, exact_offset_pad(K.m, x[r], y[r], (uint32_t)K.fxp_P));
+            if (COUNT) loads = __builtin_amdgcn_readfirstlane(loads + 1u);  // uniform: kept in an SGPR
         };
         // Both slots open: two gathers in flight per trip until a slot closes (its chunk has
         // ended with none of the car's chunks left to arm; in that trip it gathers the zero cell
-        // once more).  Then the open slot runs alone: a closed slot used to gather the zero cell
-        // every trip until the other one ended (7.9 % of the slot gathers, 16 slot-trips per car;
-        // each such load costs the texture-address unit what a full one does):
-        // 0.706 -> 0.682 ms at 65536 cars, 0.156 -> 0.136 ms at 8192 (profiles/r05_ab/).
+        // once more).  Then the open slot runs alone.  One guard-band test per trip
+        // covers both slots' gathers.
         if (kk[1] >= 0) {
             for (;;) {
 #pragma unroll
                 for (int r = 0; r < NS; ++r) slot_step(r);
-                ++trips;
+                if (nb[0] | nb[1]) {
+                    if (nb[0]) regather(0);
+                    if (nb[1]) regather(1);
+                    // slot 0's re-gather was issued after slot 1's gather: wait for both here, so
+                    // that the common path's wait before slot 0's next step stays vmcnt(1)
+                    __builtin_amdgcn_s_waitcnt(0);
+                }
+                if (COUNT) ++trips;
                 if ((kk[0] < 0) | (kk[1] < 0)) break;
             }
             if (kk[0] < 0) {  // the open slot moves into slot 0 (wave-uniform copies)
@@ -1531,8 +1553,11 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
         }
         while (kk[0] >= 0) {  // one slot left
             slot_step(0);
-            ++trips;
-            ++closed_trips;
+            if (nb[0]) regather(0);
+            if (COUNT) {
+                ++trips;
+                ++closed_trips;
+            }
         }
     } else {  // an origin off the map: the IEEE cell of every lookup, chunk after chunk
         uint32_t cnt = 0;
@@ -1548,32 +1573,31 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
                 ++cc;
             }
             cnt += cc;
-            trips += wave_max(cc);  // the chunk's wave-level gathers (its trip count for ORD)
+            if (COUNT) trips += wave_max(cc);  // the chunk's wave-level gathers
             finish(0);
         }
-        lane_iters = wave_sum(cnt);
-        slot_gathers = trips;
+        if (COUNT) {
+            lane_iters = wave_sum(cnt);
+            slot_gathers = trips;
+        }
     }
-    if (lane == 0) {
-        const RayArgs &K = kernarg_here();
-        unsigned long long *cs = K.ctr + (size_t)(item % kCtrSlots) * kCtrStride;
-        atomicAdd(cs, (unsigned long long)(lanes + lane_iters));  // the first lookup came from k_agents
-        atomicAdd(cs + 1, (unsigned long long)lanes);
-        // lane slots of the gathers the loop issued: 64 per wave-level gather, the ended lanes'
-        // zero-cell reads included (SIMT = loop lookups / lane slots); counter 5: trips a slot
-        // spent closed (no gather issued for it)
-        if (K.count_slots) {
+    if (COUNT) {
+        if (lane == 0) {
+            const RayArgs &K = kernarg_here();
+            unsigned long long *cs = K.ctr + (size_t)(item % kCtrSlots) * kCtrStride;
+            atomicAdd(cs, (unsigned long long)(lanes + lane_iters));  // the first lookup came from k_agents
+            atomicAdd(cs + 1, (unsigned long long)lanes);
+            // lane slots of the gathers the loop issued: 64 per wave-level gather, the ended lanes'
+            // zero-cell reads included (SIMT = loop lookups / lane slots); counter 5: trips a slot
+            // spent alone (the other one closed)
             atomicAdd(cs + 2, (unsigned long long)slot_gathers * 64ull);
             atomicAdd(cs + 3, (unsigned long long)loads);
             atomicAdd(cs + 5, (unsigned long long)closed_trips);
         }
-    }
-    if (a.count_slots) {  // the run search's wave-level loads (counter 3)
-        const uint32_t ws = wave_max(srch);
+        const uint32_t ws = wave_max(srch);  // the run search's wave-level loads (counter 3)
         if (lane == 0) atomicAdd(a.ctr + (size_t)(item % kCtrSlots) * kCtrStride + 3, (unsigned long long)ws);
     }
-    wave_stamp_end_w(kernarg_here().wtrace, item, (uint32_t)(trips < 0xffffu ? trips : 0xffffu) << 8 | (uint32_t)wj,
-                     (uint32_t)g);
+    wave_stamp_end_w(a.wtrace, item, (uint32_t)(trips < 0xffffu ? trips : 0xffffu) << 8 | (uint32_t)wj, (uint32_t)g);
 }
 
 // F110Env.step's time + _check_done (f110_env.py:404-406, :310-352) and the
@@ -1884,6 +1908,8 @@ __global__ void __launch_bounds__(kMultiBlock, 6) k_post_multi(StepArgs a) {
             const double *v = sh.rv[pr];
             const double ang = beam_angle(b, a.fov, a.beam_incr);
             if (!(fabs(wrap_pm_pi(oth + ang - sh.wcen[pr])) <= sh.whalf[pr])) continue;  // box_beam_window
+            if ((a.hcheck & 1) && a.hmask && !((a.hmask[(size_t)e * A + i] >> (b >> 6)) & 1u))  // debug: a hand-off miss
+                atomicAdd(a.ctr + (size_t)(e % kCtrSlots) * kCtrStride + 6, 1ull);
             const double bt = oth + ang + kPi / 2.;
             double v31, v30;
             cr_sincos(bt, v31, v30);
@@ -1943,6 +1969,10 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (a.gate_wait && (e = hipStreamWaitEvent(s, a.gate_wait, 0)) != hipSuccess) return e;
     const bool single = a.A == 1;
+    // f110_debug_set_handoff_check: every hand-off entry NaN (all-ones) before the ray launch, so a
+    // k_post_multi read of an entry the ray kernel skipped cannot pass for a fresh one
+    if ((a.hcheck & 1) && !single && (e = hipMemsetAsync(a.scan, 0xFF, (size_t)EA * a.B * sizeof(double), s)) != hipSuccess)
+        return e;
     RayArgs ra{};
     ra.m = a.tmap;
     ra.sines = a.sines;
@@ -2073,9 +2103,15 @@ hipError_t launch_env_step(const StepArgs &a, hipStream_t s, hipEvent_t *ev) {
                 if (a.fx_refill > 0 && a.fxs_ok && !mask && ra.HB == 0 && !ra.wcost) {
                     // one wave per car, two chunk slots with refill (k_rays_fxs; no heavy-first)
                     lds = single && a.fxs_lds && a.theta_dis <= kFxsLdsTheta;
-                    f = lds ? reinterpret_cast<const void *>(&k_rays_fxs<false, true>)
-                            : single ? reinterpret_cast<const void *>(&k_rays_fxs<false, false>)
-                                     : reinterpret_cast<const void *>(&k_rays_fxs<true, false>);
+                    // COUNT (f110_debug_set_simt): the variant that counts lookups, rays, lane slots
+                    const void *fxs_fn[2][3] = {
+                        {reinterpret_cast<const void *>(&k_rays_fxs<false, false, false>),
+                         reinterpret_cast<const void *>(&k_rays_fxs<false, true, false>),
+                         reinterpret_cast<const void *>(&k_rays_fxs<true, false, false>)},
+                        {reinterpret_cast<const void *>(&k_rays_fxs<false, false, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxs<false, true, true>),
+                         reinterpret_cast<const void *>(&k_rays_fxs<true, false, true>)}};
+                    f = fxs_fn[a.count_slots ? 1 : 0][lds ? 1 : single ? 0 : 2];
                     fxs = true;
                     ra.G4 = std::min(a.fx_refill, (a.B + 63) / 64);  // waves per car
                     if (!single && a.geo) {  // leading geometry items (a multiple of 8: XCD mapping kept)

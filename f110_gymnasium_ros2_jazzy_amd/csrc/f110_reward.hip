@@ -26,6 +26,7 @@ namespace f110 {
 namespace {
 
 constexpr int kRwWaves = 1;  // envs per block: one-wave blocks free their slot as the env finishes
+static_assert(kRwWaves == 1, "k_reward's kth_pair LDS buffer (pack[64]) is one wave's: size it [kRwWaves][64] first");
 constexpr int kTop = 5;      // kd.query(p, k=5)
 
 struct Cand {

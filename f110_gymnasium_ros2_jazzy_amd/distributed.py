@@ -41,7 +41,13 @@ def env_rank_world():
 def local_device_index(local_rank: int) -> int:
     """GPU of this rank: LOCAL_RANK (one process per GPU).  F110_SAME_DEVICE=1
     maps every rank to GPU 0 (rehearsing the multi-rank path on a 1-GPU box)."""
-    return 0 if os.environ.get("F110_SAME_DEVICE") == "1" else local_rank
+    if os.environ.get("F110_SAME_DEVICE") == "1":
+        return 0
+    n = torch.cuda.device_count()  # counts devices without initialising HIP
+    if local_rank >= n:
+        raise RuntimeError(f"LOCAL_RANK {local_rank} but {n} visible GPU(s): one rank per GPU "
+                           "(F110_SAME_DEVICE=1 rehearses several ranks on GPU 0)")
+    return local_rank
 
 
 def init(backend: str | None = None) -> tuple[int, int, int]:
@@ -58,6 +64,15 @@ def init(backend: str | None = None) -> tuple[int, int, int]:
             kw["device_id"] = torch.device(f"cuda:{local_device_index(local)}")
         dist.init_process_group(backend=backend, **kw)
     return rank, world, local
+
+
+def describe() -> dict:
+    """What the ranks run on: torch.distributed's backend (None for one
+    process) and world size, for the bench line's config."""
+    if dist.is_available() and dist.is_initialized():
+        return {"backend": str(dist.get_backend()), "world_size": dist.get_world_size(),
+                "same_device": os.environ.get("F110_SAME_DEVICE") == "1"}
+    return {"backend": None, "world_size": 1, "same_device": False}
 
 
 def barrier():

@@ -276,8 +276,15 @@ class BatchSim:
         return lk.value, rays.value
 
     def set_simt(self, on: bool = True):
-        """Count the fixed-point ray loops' lane slots (f110_debug_set_simt; off by default)."""
+        """Counting on / off (f110_debug_set_simt; off by default): the fixed-point ray loops count their
+        lane slots, and k_rays_fxs (the default ray kernel) counts lookups and rays only while it is on."""
         _lib.check(self.L.f110_debug_set_simt(self.ctx, int(bool(on))), "f110_debug_set_simt")
+
+    def set_handoff_check(self, mode: int):
+        """Hand-off mask check (f110_debug_set_handoff_check): bit 0 NaN-poisons the hand-off buffer
+        before each ray launch and counts k_post_multi's reads outside the mask (read_counter(6));
+        bit 1 turns the mask off (every chunk stored).  Debug only."""
+        _lib.check(self.L.f110_debug_set_handoff_check(self.ctx, int(mode)), "f110_debug_set_handoff_check")
 
     def read_simt(self):
         """(loop lookups, lane slots) of the fixed-point ray loops since the
@@ -300,6 +307,17 @@ class BatchSim:
     def profile_begin(self, max_steps: int):
         """Time each kernel of the next max_steps step/reset calls (HIP events)."""
         _lib.check(self.L.f110_profile_begin(self.ctx, int(max_steps)), "f110_profile_begin")
+
+    def profile_stamps(self, ref_event, max_steps: int = 4096) -> np.ndarray:
+        """Before profile_end: [steps, 6] ms after ref_event (a torch.cuda.Event with timing, recorded
+        before the profiled steps) of each step's k_agents / ray kernel / k_post begin and end
+        (f110_debug_profile_stamps)."""
+        n = int(max_steps)
+        buf = np.zeros((n, 6), np.float64)
+        got = ctypes.c_int32()
+        _lib.check(self.L.f110_debug_profile_stamps(self.ctx, ctypes.c_void_p(ref_event.cuda_event), buf.ctypes.data,
+                                                    n, ctypes.byref(got)), "f110_debug_profile_stamps")
+        return buf[:got.value]
 
     def profile_end(self) -> dict:
         ms = (ctypes.c_double * 3)()

@@ -221,6 +221,12 @@ class StreamShards:
             rays += b
         return lk, rays
 
+    def set_simt(self, on: bool = True):
+        """Counting on / off for every sub-shard (f110_debug_set_simt: k_rays_fxs counts lookups, rays
+        and lane slots only while it is on)."""
+        for sm in self.sims:
+            sm.set_simt(on)
+
     def reset_counters(self):
         self._fork()
         for s in range(self.S):

@@ -21,7 +21,10 @@ extern "C" {
 /* ---- counters -------------------------------------------------------------
  * EDT lookups and rays traced by f110_step/f110_reset/f110_scan_batch since
  * the last reset of the counters (device-side accumulation; reading syncs
- * `stream`).  Used for the measured mean lookups per ray (roofline). */
+ * `stream`).  Used for the measured mean lookups per ray (roofline).
+ * k_rays_fxs, the default ray kernel of f110_step, counts only while counting
+ * is on (f110_debug_set_simt): its uncounted build keeps the per-trip
+ * bookkeeping out of the timed loop; the other ray kernels always count. */
 F110_API int f110_read_counters(f110_ctx *ctx, uint64_t *lookups, uint64_t *rays, void *stream);
 F110_API int f110_reset_counters(f110_ctx *ctx, void *stream);
 /* Diagnostic: the sum over the counter lines of counter idx (0..15): 0
@@ -37,9 +40,21 @@ F110_API int f110_debug_read_counter(f110_ctx *ctx, int32_t idx, uint64_t *value
  * kernels, and launches made while the count is off, leave lane_slots as
  * they are.  f110_debug_set_simt(ctx, 1) turns the count on (off by default: its
  * extra atomic per wave costs ~2 % of k_rays).  Diagnostics (no reference
- * counterpart). */
+ * counterpart).  While it is on, f110_step runs k_rays_fxs's counting build
+ * (lookups, rays, lane slots, other loads: counters 0-3 and 5). */
 F110_API int f110_debug_set_simt(f110_ctx *ctx, int32_t on);
 F110_API int f110_debug_read_simt(f110_ctx *ctx, uint64_t *loop_lookups, uint64_t *lane_slots, void *stream);
+
+/* Hand-off mask check (multi-agent contexts).  k_agents marks, per car, the
+ * 64-beam chunks whose f64 scan k_post_multi's agent ray_cast may read, and
+ * the ray kernel stores only those chunks into the hand-off buffer.  mode bit
+ * 0: before each ray launch the hand-off buffer is filled with NaN and
+ * k_post_multi counts every read of a beam whose chunk bit is clear into
+ * counter 6 (f110_debug_read_counter); bit 1: no mask (every chunk stored, the
+ * reference for bit-identity); bit 2: every mask empty (a forced miss: the
+ * check's own test).  0 restores the default.  Debug only: with the
+ * mask correct, outputs are the same bits in every mode. */
+F110_API int f110_debug_set_handoff_check(f110_ctx *ctx, int32_t mode);
 
 /* ---- per-kernel timing ----------------------------------------------------
  * Attaches a (start, stop) HIP event pair to the dispatch of each of the
@@ -51,6 +66,14 @@ F110_API int f110_debug_read_simt(f110_ctx *ctx, uint64_t *loop_lookups, uint64_
  * roofline of the dominant kernel (k_rays). */
 F110_API int f110_profile_begin(f110_ctx *ctx, int32_t max_steps);
 F110_API int f110_profile_end(f110_ctx *ctx, double ms_out[3], int32_t *steps_out);
+/* Before f110_profile_end: the recorded steps' six timestamps (begin / end of
+ * k_agents, the ray kernel, k_post) in ms after ref_event (a caller-owned
+ * hipEvent_t with timing, recorded before those steps on any stream of the
+ * device): out[step][6], up to max_steps steps; steps_out gets the count.
+ * bench.py takes the union of the ray kernels' intervals over concurrent
+ * stream sub-shards from it (the timed runner's own ray time). */
+F110_API int f110_debug_profile_stamps(f110_ctx *ctx, void *ref_event, double *out, int32_t max_steps,
+                                       int32_t *steps_out);
 
 /* ---- diagnostics -------------------------------------------------------------
  * Wave trace of the ray kernel (one-wave blocks: k_rays_fx / k_rays_fxn /

@@ -20,13 +20,17 @@
 #   pmc        scripts/profile_round.py TAG (kernel trace + PMC passes of the headline ray kernel)
 #   ab         scripts/ray_ab.py with the caller's AB_* environment -> ab.json
 #   abhead     the same A/B with ab_libs/head.so (F110_LIB: the previous commit's build) -> abhead.json
+#   libab      scripts/lib_ab.py: this build against ab_libs/head.so in one process (65536 / 8192 cars) -> libab.json
+#   libab2     the same for 8192 two-agent envs -> libab2.json
+#   c4s / c5s  bench.py C4 / C5 at the driver's --steps 20 --warmup 5 -> c4s.json / c5s.json
 #   rules      scripts/shard_rules.py with the caller's SR_* environment -> rules.jsonl
 #   pmcsmall   PMC passes (no kernel trace) at 8192 and 4096 cars, the default ray kernel and k_rays_fxs
 #   trace      scripts/wave_trace.py (WT_ENVS), one context and bench's sub-shards -> trace_*.json
 #   agents     scripts/agents_probe.py (k_agents per launch: car counts, RK4 / Euler) -> agents.json
 #   post       scripts/post_probe.py (k_post_multi per launch at 4096 / 8192 two-agent envs) -> post.json
 #   c4one      bench.py --agents 2 --global-envs 8192 --runner one (one context) -> c4one.json
-#   x2         the headline bench as 2 ranks on the one GPU over gloo (the multi-rank path of the driver's scaling runs)
+#   x2         the headline bench as 2 ranks on the one GPU over gloo, self-launched by bench.py --gpus 2
+#   handoff    tests/test_gpu_handoff.py (the two-agent hand-off mask's hard cases)
 #   weak       C3's weak-scaling shape: 2 ranks x 8192 envs per GPU on the one GPU (gloo) and 1 rank x 16384
 #              envs, same K / W / seed: their trajectory_digest must agree
 #   c5x2       the DDPG bench as 2 ranks on the one GPU over gloo (the data-parallel path, no step graphs)
@@ -85,6 +89,11 @@ for step in "$@"; do
               find "$OUT/prof" -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} "$OUT/kernel_stats.csv" ;;
         pmc) run pmc 900 python -u scripts/profile_round.py "$TAG" ;;
         ab) run ab 900 python -u scripts/ray_ab.py && cp "$OUT/ab.out" "$OUT/ab.json" ;;
+        libab) run libab 900 python -u scripts/lib_ab.py && cp "$OUT/libab.out" "$OUT/libab.json" ;;
+        libab2) AB_AGENTS=2 AB_ENVS=8192 run libab2 900 python -u scripts/lib_ab.py && cp "$OUT/libab2.out" "$OUT/libab2.json" ;;
+        c4s) run c4s 600 python -u bench.py --agents 2 --global-envs 8192 --no-cpu-baseline --no-secondary --steps 20 \
+                 --warmup 5 && cp "$OUT/c4s.out" "$OUT/c4s.json" ;;
+        c5s) run c5s 600 python -u bench.py --workload ddpg --steps 20 --warmup 5 && cp "$OUT/c5s.out" "$OUT/c5s.json" ;;
         abhead) F110_LIB=$R/ab_libs/head.so run abhead 900 python -u scripts/ray_ab.py &&
                 cp "$OUT/abhead.out" "$OUT/abhead.json" ;;
         rules) run rules 900 python -u scripts/shard_rules.py && cp "$OUT/rules.out" "$OUT/rules.jsonl" ;;
@@ -102,9 +111,10 @@ for step in "$@"; do
         post) run post 300 python -u scripts/post_probe.py && cp "$OUT/post.out" "$OUT/post.json" ;;
         c4one) run c4one 600 python -u bench.py --agents 2 --global-envs 8192 --no-cpu-baseline --no-secondary \
                    --runner one && cp "$OUT/c4one.out" "$OUT/c4one.json" ;;
-        x2) F110_SAME_DEVICE=1 F110_DIST_BACKEND=gloo run x2 600 python -m torch.distributed.run --nnodes=1 \
-                --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 20 \
+        x2) F110_SAME_DEVICE=1 F110_DIST_BACKEND=gloo run x2 600 python -u bench.py --gpus 2 --steps 20 \
                 --warmup 5 && cp "$OUT/x2.out" "$OUT/x2.json" ;;
+        handoff) run handoff 600 python -u -m pytest tests/test_gpu_handoff.py -m gpu -x -v --timeout 300 \
+                     --timeout-method thread -p no:cacheprovider ;;
         weak) F110_SAME_DEVICE=1 F110_DIST_BACKEND=gloo run weak2 600 python -m torch.distributed.run --nnodes=1 \
                   --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --envs-per-gpu 8192 \
                   --steps 20 --warmup 5 && cp "$OUT/weak2.out" "$OUT/weak2.json" &&

@@ -103,6 +103,7 @@ def test_full_size_properties(tracks, gpu):
                    spawn_poses=sp, keep_f64_scans=True)
     rng = np.random.default_rng(1)
     sim.reset(sp[rng.integers(0, sp.shape[0], E)])
+    sim.set_simt(True)  # k_rays_fxs counts lookups / rays while counting is on
     sim.reset_counters()
     g = torch.Generator(device=gpu)
     g.manual_seed(3)
@@ -188,6 +189,8 @@ def test_stream_shards_match_single_context(tracks, gpu, lanes, refill):
                       n_agents=A, device=gpu, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=9)
     assert all(sm.ray_lanes == lanes for sm in sh.sims)
     assert all(sm.ray_refill == refill for sm in sh.sims)  # f110_debug_set_ray_refill (k_rays_fxs + padded EDT)
+    full.set_simt(True)  # k_rays_fxs counts lookups / rays while counting is on
+    sh.set_simt(True)
     full.reset(poses)
     sh.reset(poses)
     with pytest.raises(RuntimeError, match="before the first"):
@@ -354,6 +357,7 @@ def test_refill_kernel_identical(tracks, gpu, monkeypatch, A, beams):
                    spawn_poses=sp, seed=6, keep_f64_scans=True)
         sim.set_ray_lanes(2)
         sim.set_ray_refill(refill)
+        sim.set_simt(True)  # k_rays_fxs counts lookups / rays while counting is on
         assert sim.ray_refill == min(refill, (beams + 63) // 64)
         sim.reset(poses)
         sim.reset_counters()
@@ -387,6 +391,7 @@ def test_step_n_matches_single_steps(tracks, gpu):
         for n_call in (False, True):
             sim = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=9,
                        keep_f64_scans=True)
+            sim.set_simt(True)  # k_rays_fxs counts lookups / rays while counting is on
             sim.reset(poses)
             sim.reset_counters()
             if n_call:
@@ -400,3 +405,39 @@ def test_step_n_matches_single_steps(tracks, gpu):
         for x, y in zip(runs[0][:3], runs[1][:3]):
             assert torch.equal(x, y)
         assert runs[0][3] == runs[1][3]
+
+
+@pytest.mark.parametrize("A", [1, 2])
+def test_counting_build_identical(tracks, gpu, A):
+    """k_rays_fxs's counting build (f110_debug_set_simt on: lookups, rays, lane
+    slots) and its uncounted build (the default: no per-trip bookkeeping) step
+    the same bits (obs, f64 scans, states, collisions over 20 noisy steps with
+    autoreset); the uncounted build adds nothing to the counters."""
+    E, T = 384, 20
+    sp = _spawns(A)
+    rng = np.random.default_rng(77 + A)
+    poses = sp[rng.integers(0, sp.shape[0], E)]
+    acts = np.stack([rng.uniform(-0.4189, 0.4189, (T, E, A)), rng.uniform(0, 20, (T, E, A))], -1).astype(np.float32)
+    runs = []
+    for counting in (False, True):
+        sim = _sim(tracks, gpu, n_envs=E, n_agents=A, noise_std=0.01, autoreset=True, spawn_poses=sp, seed=5,
+                   keep_f64_scans=True)
+        assert sim.ray_kernel == 3 and sim.ray_refill > 0  # k_rays_fxs
+        sim.set_simt(counting)
+        sim.reset(poses)
+        sim.reset_counters()
+        rec = []
+        for t in range(T):
+            o = sim.step(acts[t])
+            rec.append((o.obs.clone(), o.scans_f64.clone(), o.collisions.clone(), sim.agent_states().clone()))
+        torch.cuda.synchronize()
+        lk, rays = sim.read_counters()
+        if counting:
+            assert rays == T * E * A * sim.B and lk > 4 * rays
+        else:
+            assert (lk, rays) == (0, 0)
+        runs.append(rec)
+        sim.close()
+    for t, (a, b) in enumerate(zip(*runs)):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y), f"step {t}"

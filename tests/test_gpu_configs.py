@@ -33,6 +33,7 @@ def test_c3_65536_single_agent(tracks, gpu, oracle_scanners):
                    spawn_poses=sp, keep_f64_scans=True)
     assert sim.ray_kernel == 3
     rng = np.random.default_rng(65536)
+    sim.set_simt(True)  # k_rays_fxs counts lookups / rays while counting is on
     sim.reset(sp[rng.integers(0, sp.shape[0], E)])
     sim.reset_counters()
     g = torch.Generator(device=gpu)
@@ -77,6 +78,8 @@ def test_c2_4096_single_agent(tracks, gpu, oracle_scanners):
     one = BatchSim(tracks("Spielberg_map"), n_envs=E, **kw)
     rng = np.random.default_rng(4096)
     p0 = sp[rng.integers(0, sp.shape[0], E)]
+    shards.set_simt(True)  # k_rays_fxs counts lookups / rays while counting is on
+    one.set_simt(True)
     shards.reset(p0)
     one.reset(p0)
     shards.reset_counters()
@@ -127,6 +130,8 @@ def test_c4_8192x2_lockstep_sample(tracks, gpu, oracle_scanners, nonexact_budget
     gap = np.where(np.arange(E) % 2 == 0, rng.integers(1, 4, E), rng.integers(10, 31, E))
     poses = np.stack([cl[i0], cl[(i0 + gap) % n]], 1)
     sim = BatchSim(tracks("Spielberg_map"), n_envs=E, n_agents=A, device=gpu, noise_std=0.0, keep_f64_scans=True)
+    sim.set_handoff_check(1)  # hand-off buffer NaN-poisoned per step, reads outside the mask counted
+    sim.reset_counters()
     ref = O.OracleSim(oracle_scanners("Spielberg_map"), S, A)
     # residue attribution: the oracle with the device's correctly rounded sin / cos
     refd = O.OracleSim(oracle_scanners("Spielberg_map"), S, A)
@@ -170,6 +175,7 @@ def test_c4_8192x2_lockstep_sample(tracks, gpu, oracle_scanners, nonexact_budget
         full = out.scans_f64
         assert bool(((full >= 0) & (full <= 30)).all()) and bool(torch.isfinite(out.obs).all())
     assert gjk > 0 and occluded > 0, (gjk, occluded)
+    assert sim.read_counter(6) == 0, "k_post_multi read hand-off beams outside the mask"
     nonexact_budget("c4_8192x2_sample256_20steps", nonexact)
     nonexact_budget("c4_8192x2_sample256_20steps/device_trig_oracle", nonexact_d)
     clean.close()

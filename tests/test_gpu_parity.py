@@ -279,6 +279,8 @@ def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A, nonexact
     rng = np.random.default_rng(100 + A)
     poses = _adversarial_poses(rng, E, A, centerline_spawns("Spielberg", 1))
     sim = sims("Spielberg_map", E, A)
+    sim.set_handoff_check(1)  # hand-off buffer NaN-poisoned per step, reads outside the mask counted
+    sim.reset_counters()
     ref = O.OracleSim(oracle_scanners("Spielberg_map"), E, A)
     # residue attribution: the same oracle with the device's correctly rounded
     # sin / cos in place of glibc's at the sites the device computes them
@@ -303,6 +305,8 @@ def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A, nonexact
         rs, rc = ref.step(act)
         with O.device_trig():
             rd, _ = refd.step(act)
+    assert sim.read_counter(6) == 0, "k_post_multi read hand-off beams outside the mask"
+    sim.set_handoff_check(0)
     nonexact_budget(f"ray_cast_adversarial_A{A}", nonexact)
     nonexact_budget(f"ray_cast_adversarial_A{A}/device_trig_oracle", nonexact_d)
 
