@@ -7,10 +7,12 @@ same 1088-float flat observation, the same ``info`` keys, ``timestep``
 attribute and ``close()``, so rl_training/train_ddpg.py runs unchanged.
 
 The physics + lidar + collision step runs on the GPU (one env of a
-BatchSim).  The reference's lap bookkeeping (_check_done, f110_env.py:310-352)
-is evaluated here on the host with NumPy exactly as the reference writes it
-(including its dtype behaviour when ``options`` are float32), because it is
-a handful of scalar operations on two cars.
+BatchSim), and so does the reference's lap bookkeeping (_check_done,
+f110_env.py:310-352): the device epilogue (k_post_*'s env_epilogue) keeps the
+start poses, start_rot, toggles, lap times / counts and terminated, with the
+reference's dtype behaviour for float32 ``options`` (f110_set_reset_dtype:
+float32 poses and NumPy's float32 start_rot).  The facade reads them back;
+there is no second (host) implementation of the lap logic.
 
 Scan noise is the reference's own stream: every RaceCar re-creates
 ``np.random.default_rng(seed)`` at reset and ScanSimulator2D.scan adds
@@ -160,31 +162,16 @@ class F110Env(_EnvBase):
         self.render_obs = None
 
     # ------------------------------------------------------------------
-    def _check_done(self):
-        """Lap toggles + ego collision (f110_env.py:310-352), NumPy on the host."""
-        left_t, right_t = 2, 2
-        dx = np.array(self.poses_x) - self.start_xs
-        dy = np.array(self.poses_y) - self.start_ys
-        delta_pt = np.dot(self.start_rot, np.stack((dx, dy), axis=0))
-        temp_y = delta_pt[1, :]
-        beyond_left = temp_y > left_t
-        beyond_right = temp_y < -right_t
-        temp_y[beyond_left] -= left_t
-        temp_y[beyond_right] = -right_t - temp_y[beyond_right]
-        temp_y[np.invert(np.logical_or(beyond_left, beyond_right))] = 0
-        closes = (delta_pt[0, :] ** 2 + temp_y ** 2) <= 0.1
-        for i in range(self.num_agents):
-            if closes[i] and not self.near_starts[i]:
-                self.near_starts[i] = True
-                self.toggle_list[i] += 1
-            elif not closes[i] and self.near_starts[i]:
-                self.near_starts[i] = False
-                self.toggle_list[i] += 1
-            self.lap_counts[i] = self.toggle_list[i] // 2
-            if self.toggle_list[i] < 4:
-                self.lap_times[i] = self.current_time
-        done = (self.collisions[self.ego_idx]) or np.all(self.toggle_list >= 4)
-        return bool(done), self.toggle_list >= 4
+    def _check_done(self, out):
+        """Lap toggles + ego collision (f110_env.py:310-352) as the device's step epilogue computed
+        them: terminated, lap times / counts (f110_outputs) and the toggles (f110_get_lap_state).
+        The reference's attributes mirror them (toggle_list and lap_counts as float64, lap_times
+        as the float32 values the reference reports in its info)."""
+        _, tog = self.sim.lap_state()
+        self.toggle_list = tog[0].cpu().numpy().astype(np.float64)
+        self.lap_counts = out.lap_counts[0].cpu().numpy().astype(np.float64)
+        self.lap_times = out.lap_times[0].cpu().numpy().astype(np.float64)
+        return bool(out.terminated[0].item()), self.toggle_list >= 4
 
     def _obs_dict(self, out):
         """Simulator.step's observation dict (base_classes.py:607-625) from device outputs."""
@@ -205,6 +192,7 @@ class F110Env(_EnvBase):
 
     def _finish_step(self, out):
         obs_dict, flat = self._obs_dict(out)
+        terminated, toggle_list = self._check_done(out)
         obs_dict['lap_times'] = self.lap_times.astype(np.float32)
         obs_dict['lap_counts'] = self.lap_counts.astype(np.float32)
         F110Env.current_obs = obs_dict
@@ -216,7 +204,6 @@ class F110Env(_EnvBase):
         self.poses_y = obs_dict['poses_y']
         self.poses_theta = obs_dict['poses_theta']
         self.collisions = obs_dict['collisions']
-        terminated, toggle_list = self._check_done()
         info = self._build_info(obs_dict)
         info["checkpoint_done"] = toggle_list
         return flat, reward, terminated, False, info
@@ -276,6 +263,11 @@ class F110Env(_EnvBase):
         self.start_thetas = poses[:, 2]
         th = self.start_thetas[self.ego_idx]
         self.start_rot = np.array([[np.cos(-th), -np.sin(-th)], [np.sin(-th), np.cos(-th)]])
+        # the device's lap bookkeeping takes the options' dtype (float32 poses: float32 start poses and
+        # start_rot, as NumPy computes them in the reference, f110_env.py:444-451)
+        dt = np.float32 if poses.dtype == np.float32 else np.float64
+        if self.sim.reset_dtype != dt:
+            self.sim.set_reset_dtype(dt)
         # device: RaceCar.reset for every car + the reference's zero-action step (f110_env.py:457)
         self._scan_rng = np.random.default_rng(seed=self.seed)  # RaceCar.reset, base_classes.py:204
         self._draw_noise()

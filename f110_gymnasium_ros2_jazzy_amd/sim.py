@@ -330,7 +330,10 @@ class BatchSim:
         """F110Env.reset semantics for the following resets and autoresets
         (f110_set_reset_dtype): float32 options round the poses to float32
         and give start_rot NumPy's float32 cos / sin (f110_env.py:448-451)."""
-        f32 = np.dtype(str(dtype).replace("torch.", "")) == np.float32
+        try:  # a NumPy dtype / type, or a dtype name
+            f32 = np.dtype(dtype) == np.float32
+        except TypeError:  # a torch dtype
+            f32 = np.dtype(str(dtype).replace("torch.", "")) == np.float32
         _lib.check(self.L.f110_set_reset_dtype(self.ctx, _lib.F32 if f32 else _lib.F64), "f110_set_reset_dtype")
         self.reset_dtype = np.float32 if f32 else np.float64
 

@@ -306,6 +306,53 @@ def gap_follow_action(scan, angle_min=-np.pi / 2, angle_increment=np.pi / 1080):
     return act, gap
 
 
+class LapOracle:
+    """F110Env's lap bookkeeping (_check_done, f110_env.py:310-352, with the
+    start state of reset, :444-451), restated in NumPy for the checker: start
+    zone 2 m either side of the ego start line, toggles on entering / leaving
+    it (squared distance <= 0.1), lap_counts = toggles // 2, lap_times frozen
+    at the fourth toggle, done on the ego's collision or every car's fourth
+    toggle.  float32 reset poses keep the reference's dtype behaviour (float32
+    start poses and start_rot, float64 arithmetic after the upcast)."""
+
+    def __init__(self, poses, ego_idx=0):
+        poses = np.asarray(poses)
+        n = poses.shape[0]
+        self.ego_idx = ego_idx
+        self.start_xs, self.start_ys = poses[:, 0], poses[:, 1]
+        th = poses[ego_idx, 2]
+        self.start_rot = np.array([[np.cos(-th), -np.sin(-th)], [np.sin(-th), np.cos(-th)]])
+        self.near_starts = np.array([True] * n)
+        self.toggle_list = np.zeros((n,))
+        self.lap_counts = np.zeros((n,))
+        self.lap_times = np.zeros((n,))
+
+    def check_done(self, poses_x, poses_y, collisions, current_time):
+        left_t = right_t = 2
+        dx = np.array(poses_x) - self.start_xs
+        dy = np.array(poses_y) - self.start_ys
+        delta_pt = np.dot(self.start_rot, np.stack((dx, dy), axis=0))
+        temp_y = delta_pt[1, :]
+        beyond_left = temp_y > left_t
+        beyond_right = temp_y < -right_t
+        temp_y[beyond_left] -= left_t
+        temp_y[beyond_right] = -right_t - temp_y[beyond_right]
+        temp_y[np.invert(np.logical_or(beyond_left, beyond_right))] = 0
+        closes = (delta_pt[0, :] ** 2 + temp_y ** 2) <= 0.1
+        for i in range(len(closes)):
+            if closes[i] and not self.near_starts[i]:
+                self.near_starts[i] = True
+                self.toggle_list[i] += 1
+            elif not closes[i] and self.near_starts[i]:
+                self.near_starts[i] = False
+                self.toggle_list[i] += 1
+            self.lap_counts[i] = self.toggle_list[i] // 2
+            if self.toggle_list[i] < 4:
+                self.lap_times[i] = current_time
+        done = collisions[self.ego_idx] or np.all(self.toggle_list >= 4)
+        return bool(done), self.toggle_list >= 4
+
+
 def load_map(yaml_path, map_ext=".png"):
     """ScanSimulator2D.set_map (laser_models.py:383-427) restated:
     PIL load -> FLIP_TOP_BOTTOM -> (<=128 -> occupied) ; returns

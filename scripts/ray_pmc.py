@@ -17,8 +17,7 @@ if os.environ.get("MB_HEAVY", "0") != "1":
 if os.environ.get("MB_REFILL"):  # a forced ray kernel: k_rays_fxs (waves per car) or, with 0, k_rays_fx(n)
     sim.set_ray_lanes(int(os.environ.get("MB_LANES", 2)))
     sim.set_ray_refill(int(os.environ["MB_REFILL"]))
-rng = np.random.default_rng(0)
-sim.reset(sp[rng.integers(0, sp.shape[0], E)])
+sim.reset(sp[np.random.default_rng(0).integers(0, sp.shape[0], E)])
 g = torch.Generator(device="cuda"); g.manual_seed(0)
 acts = torch.rand(100, E, A, 2, device="cuda", generator=g)
 acts[..., 0] = acts[..., 0] * 0.8378 - 0.4189; acts[..., 1] *= 20
@@ -26,13 +25,18 @@ acts[..., 0] = acts[..., 0] * 0.8378 - 0.4189; acts[..., 1] *= 20
 # the loop's gathers, counter 3 = its other wave-level loads; returnless lane-0 atomics, no reads),
 # written to <path> beside the PMC pass that counts SQ_INSTS_VMEM_RD on them
 counts = os.environ.get("RAY_PMC_COUNTS")
-if counts:
-    sim.set_simt(True)
-    sim.reset_counters()
+p0 = sp[np.random.default_rng(0).integers(0, sp.shape[0], E)]
 for k in range(100):
     sim.step(acts[k], minimal_outputs=True)
 torch.cuda.synchronize()
-if counts:
+if counts:  # k_rays_fxs counts in its COUNT build (another kernel name, left out of the PMC averages):
+    # the same 100 steps again from the same reset, counted
+    sim.reset(p0)
+    sim.set_simt(True)
+    sim.reset_counters()
+    for k in range(100):
+        sim.step(acts[k], minimal_outputs=True)
+    torch.cuda.synchronize()
     import json
     _, slots = sim.read_simt()
     other = sim.read_counter(3)

@@ -182,3 +182,30 @@ def test_vector_env_float32_lap_boundary(gpu, options_dtype):
         assert bool(term[0]) and d["lap_counts"][-1].min() >= 2
     finally:
         env.close()
+
+
+def test_f110env_float32_lap_boundary(gpu):
+    """The facade's _check_done reads the device epilogue (terminated, lap
+    times / counts, toggles): with float32 reset options (train_ddpg's dtype)
+    it follows the reference F110Env episode of tests/golden/env_lap_f32.npz
+    through both cars' start-zone crossings to the lap termination, step by
+    step (terminated, lap_counts, lap_times, checkpoint_done, collisions)."""
+    from f110_gym.envs import F110Env
+    d = golden("env_lap_f32.npz")
+    env = F110Env(map_dir=MAPS + os.sep, map="Spielberg_map", map_ext=".png", num_agents=2, noise_std=0.0)
+    try:
+        poses = d["reset_poses"]
+        assert poses.dtype == np.float32
+        obs, info = env.reset(options=poses)
+        for t in range(d["terminated"].shape[0]):
+            if t:
+                obs, r, term, trunc, info = env.step(d["actions"])
+                assert term == bool(d["terminated"][t]), t
+            assert np.array_equal(info["lap_counts"], d["lap_counts"][t].astype(np.float32)), t
+            assert np.array_equal(info["lap_times"], d["lap_times"][t].astype(np.float32)), t
+            assert np.array_equal(info["checkpoint_done"], d["toggles"][t] >= 4), t
+            assert np.array_equal(info["collisions"], d["collisions"][t].astype(np.int8)), t
+            assert np.array_equal(env.toggle_list, d["toggles"][t].astype(np.float64)), t
+        assert term and d["lap_counts"][-1].min() >= 2
+    finally:
+        env.close()

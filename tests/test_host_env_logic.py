@@ -1,5 +1,6 @@
-"""Host-side (CPU) logic of the facade: lap bookkeeping (_check_done,
-f110_env.py:310-352) replayed against the reference trace, env-shard
+"""Host-side (CPU) checks: the oracle's lap bookkeeping (_check_done,
+f110_env.py:310-352; the device epilogue is checked against the same traces
+in tests/test_gpu_env.py) replayed against the reference traces, env-shard
 arithmetic, the f110_gym drop-in package, and a gloo world_size-2 run of the
 sharding + timing reduction bench.py uses."""
 import os
@@ -12,34 +13,24 @@ from conftest import golden
 
 
 def test_check_done_replay():
-    """Feed the reference's per-step poses/collisions through our _check_done
-    and compare terminated / lap counters / checkpoint flags."""
-    from f110_gymnasium_ros2_jazzy_amd.f110_env import F110Env
+    """Feed the reference's per-step poses/collisions through the oracle's
+    _check_done and compare terminated / lap counters / checkpoint flags."""
+    import oracle as O
     d = golden("env_2agent.npz")
-    env = F110Env.__new__(F110Env)           # host logic only: no device
-    env.num_agents, env.ego_idx = 2, 0
-    poses = d["reset_poses"]
-    env.start_xs, env.start_ys, env.start_thetas = poses[:, 0], poses[:, 1], poses[:, 2]
-    th = env.start_thetas[0]
-    env.start_rot = np.array([[np.cos(-th), -np.sin(-th)], [np.sin(-th), np.cos(-th)]])
-    env.near_starts = np.array([True, True])
-    env.toggle_list = np.zeros(2)
-    env.lap_counts = np.zeros(2)
-    env.lap_times = np.zeros(2)
-    env.current_time = 0.0
+    lap = O.LapOracle(d["reset_poses"], ego_idx=0)
+    current_time = 0.0
     T = d["info_poses_x"].shape[0]
     for t in range(T):
-        env.current_time = env.current_time + 0.01
+        current_time = current_time + 0.01
         # the reference keeps float64 poses; the f32 info copies differ from
         # them by < 1e-6 m, far from the 0.1 m^2 zone boundary here
-        env.poses_x = list(d["info_poses_x"][t].astype(np.float64))
-        env.poses_y = list(d["info_poses_y"][t].astype(np.float64))
-        env.collisions = d["info_collisions"][t].astype(np.float64)
-        term, cp = env._check_done()
+        term, cp = lap.check_done(list(d["info_poses_x"][t].astype(np.float64)),
+                                  list(d["info_poses_y"][t].astype(np.float64)),
+                                  d["info_collisions"][t].astype(np.float64), current_time)
         if t:
             assert term == bool(d["terminated"][t - 1])
         assert np.array_equal(cp, d["info_checkpoint_done"][t])
-        assert np.array_equal(env.lap_counts.astype(np.float32), d["info_lap_counts"][t])
+        assert np.array_equal(lap.lap_counts.astype(np.float32), d["info_lap_counts"][t])
 
 
 def test_shard_range():
