@@ -63,7 +63,22 @@ def init(backend: str | None = None) -> tuple[int, int, int]:
             torch.cuda.set_device(local_device_index(local))
             kw["device_id"] = torch.device(f"cuda:{local_device_index(local)}")
         dist.init_process_group(backend=backend, **kw)
+        self_check()
     return rank, world, local
+
+
+def self_check() -> None:
+    """One all-reduce of (rank + 1) on the backend's own device: every rank must
+    see 1 + 2 + ... + world.  A broken collective path (RCCL over xGMI, or a
+    rank on the wrong device) fails here, loudly, before any timed work."""
+    world = dist.get_world_size()
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([float(dist.get_rank() + 1)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    want = world * (world + 1) / 2.0
+    if float(t.item()) != want:
+        raise RuntimeError(f"torch.distributed self-check failed: all-reduce gave {float(t.item())}, want {want} "
+                           f"(backend {dist.get_backend()}, rank {dist.get_rank()} of {world})")
 
 
 def describe() -> dict:

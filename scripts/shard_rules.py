@@ -3,8 +3,10 @@ stream sub-shards (streams.StreamShards) for each ray-kernel choice, in one
 process, interleaved rounds (the bench's timing: clock ramp, W warm-up, K
 timed steps between synchronizes).  The choices are (rays per lane, waves per
 car of k_rays_fxs): (1, 0) k_rays_fx, (2, 0) k_rays_fxn<2>, (2, w) k_rays_fxs
-with w waves per car.  Bit-identity of the obs rows against the first choice
-is checked after the timed steps.  Prints one JSON line per (E, S).
+with w waves per car; (0, w): the bench's own sub-shards (f110_set_device_share:
+single-agent k_rays_fxs with the LDS theta table) with their waves per car set
+to w afterwards (0: the size rule's).  Bit-identity of the obs rows against the
+first choice is checked after the timed steps.  Prints one JSON line per (E, S).
 
     SR_ENVS=8192,4096 SR_STREAMS=1,2,4 SR_CHOICES=1:0,2:1 python scripts/shard_rules.py
 """
@@ -48,8 +50,14 @@ def main():
             kw = dict(n_agents=A, device=dev, seed=12345, noise_std=0.01, autoreset=True, spawn_poses=spawn)
             runs = {}
             for lanes, refill in choices:
-                name = f"lanes{lanes}_refill{refill}"
-                if S == 1:
+                name = f"lanes{lanes}_refill{refill}" if lanes else f"shared_refill{refill}"
+                if lanes == 0:  # the bench's runner (device share), then its waves per car
+                    r = (StreamShards(track, n_envs=E, n_streams=S, **kw) if S > 1
+                         else BatchSim(track, n_envs=E, **kw))
+                    if refill:
+                        for sm in getattr(r, "sims", [r]):
+                            sm.set_ray_refill(refill)
+                elif S == 1:
                     r = BatchSim(track, n_envs=E, **kw)
                     r.set_ray_lanes(lanes)
                     r.set_ray_refill(refill)
