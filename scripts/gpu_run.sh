@@ -120,9 +120,8 @@ for step in "$@"; do
                   --steps 20 --warmup 5 && cp "$OUT/weak2.out" "$OUT/weak2.json" &&
               run weak1 600 python -u bench.py --global-envs 16384 --steps 20 --warmup 5 --no-cpu-baseline \
                   --no-secondary && cp "$OUT/weak1.out" "$OUT/weak1.json" ;;
-        c5x2) F110_SAME_DEVICE=1 F110_DIST_BACKEND=gloo run c5x2 600 python -m torch.distributed.run --nnodes=1 \
-                  --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --workload ddpg --steps 50 \
-                  --warmup 20 && cp "$OUT/c5x2.out" "$OUT/c5x2.json" ;;
+        c5x2) F110_SAME_DEVICE=1 F110_DIST_BACKEND=gloo run c5x2 600 python -u bench.py --gpus 2 --workload ddpg \
+                  --steps 50 --warmup 20 && cp "$OUT/c5x2.out" "$OUT/c5x2.json" ;;
         c5) run c5 600 python -u bench.py --workload ddpg --steps 200 --warmup 20 && cp "$OUT/c5.out" "$OUT/c5.json" ;;
         *) echo "unknown step $step" >&2; exit 2 ;;
     esac
