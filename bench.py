@@ -201,10 +201,12 @@ def run_ddpg(args, per_gpu: int, K: int, W: int) -> dict:
     D.barrier()
     elapsed = D.max_over_ranks(t1 - t0)
     total = D.sum_over_ranks(shard.count * K)
-    # phase split (separate pass, events on the current stream; not part of `value`)
+    # phase split (separate pass of 100 steps, events on the current stream; not part of `value`):
+    # the steps are submitted back to back as in the timed loop (no synchronize between them, which
+    # would start every phase on an idle GPU) and the events read once at the end
     stream = torch.cuda.current_stream()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    KP = min(K, 100)
+    KP = 100
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(KP)]
     ph = {"env_step_reward_ms": 0.0, "replay_add_ms": 0.0, "learner_update_ms": 0.0}
     # the gradient-bucket all-reduces inside the update (several ranks): events around each
     # GradBucket.reduce on the current stream (RCCL enqueues there; gloo blocks the host meanwhile)
@@ -219,7 +221,7 @@ def run_ddpg(args, per_gpu: int, K: int, W: int) -> dict:
                 e1.record(stream)
                 ar_pairs.append((e0, e1))
             bucket.reduce = timed_reduce
-    for _ in range(KP):
+    for ev in evs:
         act = tr.agent.choose_action(tr.obs, training=True, out=tr.env.agent_actions())  # as VectorTrainer.step
         ev[0].record(stream)
         nxt, rew, term, was_reset = tr.env.step_transition(act)
@@ -229,13 +231,13 @@ def run_ddpg(args, per_gpu: int, K: int, W: int) -> dict:
         tr.last = tr.agent.replay()
         ev[3].record(stream)
         tr.obs = nxt
-        torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    for ev in evs:
         ph["env_step_reward_ms"] += ev[0].elapsed_time(ev[1]) / KP
         ph["replay_add_ms"] += ev[1].elapsed_time(ev[2]) / KP
         ph["learner_update_ms"] += ev[2].elapsed_time(ev[3]) / KP
-        if ar_pairs:
-            ph["learner_allreduce_ms"] += sum(e0.elapsed_time(e1) for e0, e1 in ar_pairs) / KP
-            ar_pairs.clear()
+    if ar_pairs:
+        ph["learner_allreduce_ms"] = sum(e0.elapsed_time(e1) for e0, e1 in ar_pairs) / KP
     # data-parallel consistency: every rank must hold the same weights
     wsum = float(sum(float(p.detach().double().sum()) for p in tr.agent.actor.parameters()))
     in_sync = D.max_over_ranks(wsum) == -D.max_over_ranks(-wsum)
@@ -482,10 +484,12 @@ def main():
         sys.exit(self_launch(args, sys.argv[1:]))
     check_world(args)
     if os.environ.get("F110_BENCH_ECHO_RANKS") == "1":  # launcher test hook (tests/test_bench_launch.py): no GPU
-        print(json.dumps({"rank": int(os.environ.get("RANK", 0)), "world": int(os.environ.get("WORLD_SIZE", 1)),
-                          "local_rank": int(os.environ.get("LOCAL_RANK", 0)),
-                          "master_addr": os.environ.get("MASTER_ADDR"), "gpus": args.gpus,
-                          "argv": sys.argv[1:]}), flush=True)
+        line = json.dumps({"rank": int(os.environ.get("RANK", 0)), "world": int(os.environ.get("WORLD_SIZE", 1)),
+                           "local_rank": int(os.environ.get("LOCAL_RANK", 0)),
+                           "master_addr": os.environ.get("MASTER_ADDR"), "gpus": args.gpus,
+                           "argv": sys.argv[1:]}) + "\n"
+        sys.stdout.flush()
+        os.write(1, line.encode())  # one write: the ranks share the launcher's stdout pipe
         return
     if args.workload == "ddpg":
         return bench_ddpg(args)
