@@ -1158,6 +1158,51 @@ __device__ __forceinline__ double beam_theta(const BeamRun *R, int n, int lo, in
 }
 
 
+// k_rays_fxs: the car's first kRunsLds beam runs sit in a wave-private LDS copy (3-13 runs for
+// the default scan), so the per-car run search and every chunk arm read LDS instead of making
+// dependent trips to L2 (the runs were written by k_agents just before); runs past kRunsLds (other
+// scan configurations) are read from memory as before.
+constexpr int kRunsLds = 16;
+
+__device__ __forceinline__ double rfl64(double v) {  // a wave-uniform VGPR double into SGPRs
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// run j's (start, t0, delta) from the LDS copy RL or, past kRunsLds, from RG (j wave-uniform)
+__device__ __forceinline__ void run_at(const BeamRun *RL, const BeamRun *RG, int j, int &st, double &t0, double &dl) {
+    if (j < kRunsLds) {
+        st = __builtin_amdgcn_readfirstlane(RL[j].start);
+        t0 = rfl64(RL[j].t0);
+        dl = rfl64(RL[j].delta);
+    } else {
+        st = ld_const(&RG[j].start);
+        t0 = ld_const(&RG[j].t0);
+        dl = ld_const(&RG[j].delta);
+    }
+}
+
+// beam_theta over the LDS copy (k_rays_fxs)
+__device__ __forceinline__ double beam_theta_l(const BeamRun *RL, const BeamRun *RG, int n, int lo, int b0, int bc) {
+    int rs;
+    double t0, dl;
+    run_at(RL, RG, lo, rs, t0, dl);
+    for (int j = lo + 1; j < n; ++j) {
+        int s2;
+        double u0, u1;
+        run_at(RL, RG, j, s2, u0, u1);
+        if (s2 > b0 + 63) break;
+        if (bc >= s2) {
+            rs = s2;
+            t0 = u0;
+            dl = u1;
+        }
+    }
+    return t0 + (double)(bc - rs) * dl;  // get_scan's theta_index (laser_models.py:167-184)
+}
+
 __device__ __forceinline__ bool lane_in(uint64_t mask) {
     return (uint32_t)(mask >> (threadIdx.x & 63)) & 1u;
 }
@@ -1322,10 +1367,21 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
     constexpr int NS = 2;
     constexpr int W = LDS ? kFxsWaves : 1;  // work items (waves) per block
     __shared__ double2 cs_lds[LDS ? kFxsLdsTheta : 1];
+    __shared__ BeamRun runs_l[W][kRunsLds];  // each wave's car's first beam runs (kRunsLds)
     const int wave = LDS ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
-    if (LDS) {
+    if (LDS) {  // every load of the block's table copy in flight at once, then the LDS writes
+        constexpr int kIt = (kFxsLdsTheta + 64 * W - 1) / (64 * W);
+        static_assert(!LDS || kIt * 64 * W == kFxsLdsTheta, "the copy's slots cover the LDS table exactly");
         const double2 *src = reinterpret_cast<const double2 *>(a.cs2);
-        for (int k = (int)threadIdx.x; k < a.theta_dis; k += 64 * W) cs_lds[k] = src[k];
+        double2 v[kIt];
+#pragma unroll
+        for (int i = 0; i < kIt; ++i) {  // (clamped: every load in bounds and unconditional)
+            const int k = (int)threadIdx.x + i * 64 * W;
+            v[i] = src[k < a.theta_dis ? k : a.theta_dis - 1];
+        }
+#pragma unroll
+        for (int i = 0; i < kIt; ++i)  // k < kIt * 64 W = kFxsLdsTheta: in bounds (entries >= theta_dis never read)
+            cs_lds[(int)threadIdx.x + i * 64 * W] = v[i];
         __syncthreads();
     }
     const int item = (int)blockIdx.x * W + wave;  // the wave's work item
@@ -1347,11 +1403,20 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
     const uint32_t hmask = HANDOFF ? (a.hmask ? ld_const(a.hmask + g) : 0xFFFFFFFFu) : 0u;
     const double *dt = a.m.dt;
     const FxLoop L = fx_loop(a);
+    // Every per-car input is requested before anything waits: the scan origin and first lookup
+    // (scalar), the run count, and the LDS copy of the first kRunsLds beam runs (lanes < kRunsLds
+    // load whatever the car's run slots hold; only runs < nr are ever read) -- one round trip.
+    const double rx = ld_const(a.ray0 + g), ry = ld_const(a.ray0 + a.EA + g), rd = ld_const(a.ray0 + 2 * a.EA + g);
+    const int nr = ld_const(a.nruns + g);
+    const BeamRun *RG = a.runs + (size_t)g * kMaxSeg;
+    BeamRun *RL = runs_l[wave];
+    if (lane < kRunsLds) RL[lane] = RG[lane];  // wave-private LDS
     // the scan origin and first lookup in VGPRs (re-arm copies them into a slot)
     double x00, y00, d00;
-    asm volatile("v_mov_b64 %0, %1" : "=v"(x00) : "s"(ld_const(a.ray0 + g)));
-    asm volatile("v_mov_b64 %0, %1" : "=v"(y00) : "s"(ld_const(a.ray0 + a.EA + g)));
-    asm volatile("v_mov_b64 %0, %1" : "=v"(d00) : "s"(ld_const(a.ray0 + 2 * a.EA + g)));  // :129
+    asm volatile("v_mov_b64 %0, %1" : "=v"(x00) : "s"(rx));
+    asm volatile("v_mov_b64 %0, %1" : "=v"(y00) : "s"(ry));
+    asm volatile("v_mov_b64 %0, %1" : "=v"(d00) : "s"(rd));  // :129
+    asm volatile("" ::"s"(nr));  // (keeps the run count's load with the others, not sunk into the search)
     uint32_t zero_v;  // the zero cell's offset in a VGPR (the select's other operand is its SGPR mask)
     asm volatile("v_mov_b32 %0, %1" : "=v"(zero_v) : "s"(a.fx_zero));
 
@@ -1361,22 +1426,29 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
     int kpar[NS];         // the noise cache entry of the slot's chunk pair
     int pnext = wj;       // position of this wave's next chunk in the car's chunk order
     int kinfo = 0;        // lane k < nch: the run holding beam 64 k (one divergent search per car)
-    uint32_t srch = 0;    // the search's vector loads (lane-divergent: their wave-level count is the max)
+    uint32_t srch = 0;    // the search's vector loads past the LDS copy (their wave-level count is the max)
     if (lane < nch) {
-        const BeamRun *R = a.runs + (size_t)g * kMaxSeg;
-        int lo = 0, hi = ld_const(a.nruns + g) - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (R[mid].start <= lane * 64) lo = mid;
-            else hi = mid - 1;
-            if (COUNT) ++srch;
+        int lo = 0, hi = nr - 1;
+        if (nr <= kRunsLds) {  // wave-uniform: the LDS copy holds every run
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (RL[mid].start <= lane * 64) lo = mid;
+                else hi = mid - 1;
+            }
+        } else {
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (RG[mid].start <= lane * 64) lo = mid;
+                else hi = mid - 1;
+                if (COUNT) ++srch;
+            }
         }
         kinfo = lo;
     }
     // wave-level vector loads other than the slot gathers (SIMT / TA accounting, counter 3):
     // the wave's share of the block's table copy (LDS) or the arms' table loads, the finishes'
     // TTC table loads, the guard-band re-gathers (wave-uniform, scalar)
-    uint32_t loads = LDS ? (uint32_t)((a.theta_dis - 64 * wave + 64 * W - 1) / (64 * W)) : 0u;
+    uint32_t loads = (LDS ? (uint32_t)((a.theta_dis - 64 * wave + 64 * W - 1) / (64 * W)) : 0u) + 2u;  // + the run copy
     uint32_t trips = 0;
     // in_loop: the slot's next `tot += d` completes tot = d (:130)
     auto arm = [&](int r, bool in_loop) {
@@ -1387,7 +1459,8 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
         kk[r] = k;
         const int b = k * 64 + lane, bc = b < B ? b : B - 1;
         const int lo = __builtin_amdgcn_readlane(kinfo, k);
-        int ti = (int)beam_theta(K.runs + (size_t)g * kMaxSeg, ld_const(K.nruns + g), lo, k * 64, bc);  // :124
+        int ti = (int)beam_theta_l(runs_l[wave], K.runs + (size_t)g * kMaxSeg, ld_const(K.nruns + g), lo, k * 64,
+                                   bc);  // :124 (nruns: a scalar-cache hit since the wave's start)
         if (ti >= K.theta_dis) ti = 0;
         double2 t2;
         if (LDS) {
