@@ -187,6 +187,22 @@ extern "C" int f110_host_beam_indices(double yaw, double fov, int32_t theta_dis,
     return n;
 }
 
+// The two run builders against each other at yaw (k_agents uses build_beam_runs_fast): 1 when
+// they give the same runs, 0 when not, < 0 on error.
+extern "C" int f110_host_beam_runs_agree(double yaw, double fov, int32_t theta_dis, int32_t n_beams) {
+    const double inc = (double)theta_dis * (fov / (double)(n_beams - 1)) / (2. * kPi);
+    BeamRun r0[kMaxSeg], r1[kMaxSeg];
+    const double t0 = first_theta_index(yaw, fov, theta_dis);
+    const int n0 = build_beam_runs(t0, inc, theta_dis, n_beams, r0, kMaxSeg);
+    const int n1 = build_beam_runs_fast(t0, inc, theta_dis, n_beams, r1, kMaxSeg);
+    if (n0 != n1) return 0;
+    for (int i = 0; i < n0; ++i)
+        if (r0[i].start != r1[i].start || r0[i].count != r1[i].count ||
+            std::memcmp(&r0[i].t0, &r1[i].t0, 8) != 0 || std::memcmp(&r0[i].delta, &r1[i].delta, 8) != 0)
+            return 0;
+    return 1;
+}
+
 // ---------------------------------------------------------------- EDT ----
 // 1-D lower envelope of parabolas y = (x - q)^2 + f[q] over the finite sites,
 // compared as exact rationals (Felzenszwalb & Huttenlocher 2012).

@@ -152,11 +152,11 @@ constexpr double kSinCosTab[F110_SINCOS_TAB_N][4] = {F110_SINCOS_TAB_DATA};
 // series path (about 0.1 % of the values).  Where it returns true the result
 // is the one sincos_series gives (both round the same certain value), which
 // tests/test_host_lib.py checks over a few million arguments.
-F110_HD bool sincos_table(DD r, double &s, double &c) {
+F110_HD bool sincos_table(DD r, double &s, double &c, const double (*tab)[4] = kSinCosTab) {
     const bool neg = r.h < 0.0;
     const double ah = fabs(r.h), al = neg ? -r.l : r.l;
     const int i = (int)rint(ah * 64.0);
-    const double *T = kSinCosTab[i];
+    const double *T = tab[i];
     const double th = ah - (double)i * 0.015625;  // exact (Sterbenz)
     const double tl = al;
     const double zh = th * th;
@@ -190,7 +190,8 @@ F110_HD bool sincos_table(DD r, double &s, double &c) {
     return true;
 }
 
-F110_HD void cr_sincos(double x, double &sn, double &cs) {
+// tab: kSinCosTab or a copy of it (k_agents reads an LDS copy: one short dependent load per call)
+F110_HD void cr_sincos(double x, double &sn, double &cs, const double (*tab)[4] = kSinCosTab) {
     if (!(fabs(x) < 1048576.0)) {  // NaN, inf, or beyond the exact reduction
         sn = sin(x);
         cs = cos(x);
@@ -203,7 +204,7 @@ F110_HD void cr_sincos(double x, double &sn, double &cs) {
     }
     double k, s, c;
     const DD r = sincos_reduce(x, k);
-    if (!sincos_table(r, s, c)) sincos_series(r, s, c);
+    if (!sincos_table(r, s, c, tab)) sincos_series(r, s, c);
     switch ((int)((int64_t)k & 3)) {
         case 0: sn = s; cs = c; break;
         case 1: sn = c; cs = -s; break;
@@ -234,9 +235,9 @@ F110_HD double cr_sin(double x) {
     return s;
 }
 
-F110_HD double cr_cos(double x) {
+F110_HD double cr_cos(double x, const double (*tab)[4] = kSinCosTab) {
     double s, c;
-    cr_sincos(x, s, c);
+    cr_sincos(x, s, c, tab);
     return c;
 }
 
@@ -285,7 +286,7 @@ F110_HD void vehicle_dynamics_ks(const double x[5], double u0_in, double u1_in, 
 // vehicle_dynamics_st, dynamic_models.py:123-176 (KS branch :152-160 via
 // vehicle_dynamics_ks :90-121).  Python's left-to-right order kept.
 F110_HD void vehicle_dynamics_st(const double x[7], double u0_in, double u1_in, const f110_params &p,
-                                 double f[7]) {
+                                 double f[7], const double (*tab)[4] = kSinCosTab) {
     const double mu = p.mu, C_Sf = p.C_Sf, C_Sr = p.C_Sr, lf = p.lf, lr = p.lr, h = p.h, m = p.m, I = p.I;
     double u0 = steering_constraint(x[2], u0_in, p.s_min, p.s_max, p.sv_min, p.sv_max);
     double u1 = accl_constraints(x[3], u1_in, p.v_switch, p.a_max, p.v_min, p.v_max);
@@ -297,13 +298,13 @@ F110_HD void vehicle_dynamics_st(const double x[7], double u0_in, double u1_in, 
     // one sincos of the car's own angle (the yaw, or yaw + slip).
     const bool kinematic = fabs(x[3]) < 0.5;
     double sy, cy;
-    cr_sincos(kinematic ? x[4] : x[6] + x[4], sy, cy);
+    cr_sincos(kinematic ? x[4] : x[6] + x[4], sy, cy, tab);
     // kinematic (vehicle_dynamics_ks re-applies the (idempotent) constraints to u)
     const double lwb = lf + lr;
     const double k0 = steering_constraint(x[2], u0, p.s_min, p.s_max, p.sv_min, p.sv_max);
     const double k1 = accl_constraints(x[3], u1, p.v_switch, p.a_max, p.v_min, p.v_max);
     const double tn = tan(x[2]);
-    const double c2 = cr_cos(x[2]);
+    const double c2 = cr_cos(x[2], tab);
     const double kf4 = x[3] / lwb * tn;
     const double kf5 = u1 / lwb * tn + x[3] / (lwb * (c2 * c2)) * u0;
     // single track
@@ -347,7 +348,7 @@ F110_HD void pid(double speed, double steer, double cur_speed, double cur_steer,
 // is in registers at a time).  Same operations in the same order either way.
 template <class V>
 F110_HD void update_pose_impl(V s, V acc, double &b0, double &b1, int &cnt, double raw_steer, double vel,
-                              const f110_params &p, double dt, int integrator) {
+                              const f110_params &p, double dt, int integrator, const double (*tab)[4] = kSinCosTab) {
     double steer;
     if (cnt < 2) {  // :272-274
         steer = 0.0;
@@ -370,30 +371,30 @@ F110_HD void update_pose_impl(V s, V acc, double &b0, double &b1, int &cnt, doub
         // k1 + 2*k2 + 2*k3 + k4 is summed left to right as the stages come
         // (((k1 + 2k2) + 2k3) + k4: the reference's rounding order), so only
         // one stage's k is live at a time
-        vehicle_dynamics_st(xs, sv, accl, p, k);
+        vehicle_dynamics_st(xs, sv, accl, p, k, tab);
 #pragma unroll
         for (int i = 0; i < 7; ++i) {
             acc[i] = k[i];
             xs[i] = s[i] + dt * (k[i] / 2);
         }
-        vehicle_dynamics_st(xs, sv, accl, p, k);
+        vehicle_dynamics_st(xs, sv, accl, p, k, tab);
 #pragma unroll
         for (int i = 0; i < 7; ++i) {
             acc[i] = acc[i] + 2 * k[i];
             xs[i] = s[i] + dt * (k[i] / 2);
         }
-        vehicle_dynamics_st(xs, sv, accl, p, k);
+        vehicle_dynamics_st(xs, sv, accl, p, k, tab);
 #pragma unroll
         for (int i = 0; i < 7; ++i) {
             acc[i] = acc[i] + 2 * k[i];
             xs[i] = s[i] + dt * k[i];
         }
-        vehicle_dynamics_st(xs, sv, accl, p, k);
+        vehicle_dynamics_st(xs, sv, accl, p, k, tab);
         const double w = dt * (1.0 / 6.0);
 #pragma unroll
         for (int i = 0; i < 7; ++i) s[i] = s[i] + w * (acc[i] + k[i]);
     } else {                                  // :376-396
-        vehicle_dynamics_st(xs, sv, accl, p, k);
+        vehicle_dynamics_st(xs, sv, accl, p, k, tab);
 #pragma unroll
         for (int i = 0; i < 7; ++i) s[i] = s[i] + dt * k[i];
     }
@@ -410,9 +411,9 @@ F110_HD void update_pose_impl(V s, V acc, double &b0, double &b1, int &cnt, doub
 }
 
 F110_HD void update_pose(double s[7], double &b0, double &b1, int &cnt, double raw_steer, double vel,
-                         const f110_params &p, double dt, int integrator) {
+                         const f110_params &p, double dt, int integrator, const double (*tab)[4] = kSinCosTab) {
     double acc[7];
-    update_pose_impl<double *>(s, acc, b0, b1, cnt, raw_steer, vel, p, dt, integrator);
+    update_pose_impl<double *>(s, acc, b0, b1, cnt, raw_steer, vel, p, dt, integrator, tab);
 }
 
 // -------------------------------------------------------------- the map --
@@ -634,6 +635,63 @@ F110_HD int build_beam_runs(double t, double inc, int theta_dis, int B, BeamRun 
                     else if ((kmax + 1) * d_u <= span_u - 1) ++kmax;
                     int64_t left = (int64_t)(B - i - 1);
                     run = 1 + (int)(kmax < left ? kmax : left);
+                }
+            }
+        }
+        runs[n].start = i;
+        runs[n].count = run;
+        runs[n].t0 = t;
+        runs[n].delta = delta;
+        ++n;
+        double last = t + (double)(run - 1) * delta;
+        i += run;
+        t = last + inc;               // :180
+        while (t >= td) t -= td;      // :183-184
+    }
+    return n;
+}
+
+// build_beam_runs with the same runs (start, count, t0, delta) and a shorter
+// dependent chain per run, for k_agents (one thread per car, latency-bound):
+// the exponent and the tie test from the bits of t, and the run length
+// kmax = max{k : t + k delta < lim} from an approximate quotient fixed up by
+// exact sign tests (fma(k, delta, -span) rounds once, so its sign is the exact
+// one), instead of 64-bit integer conversions and an IEEE division.  The
+// multiples t + k delta (k <= kmax) all lie in t's binade on its ulp grid, as
+// in build_beam_runs.  tests/test_host_lib.py checks the two against each
+// other over yaws and scan configurations.
+F110_HD int build_beam_runs_fast(double t, double inc, int theta_dis, int B, BeamRun *runs, int max_runs) {
+    const double td = (double)theta_dis;
+    int i = 0, n = 0;
+    while (i < B) {
+        if (n >= max_runs) return -1;
+        int run = 1;
+        double delta = 0.0;
+        if (t >= 1.0 && t < td) {
+            int e;
+            frexp(t, &e);  // t in [2^(e-1), 2^e)
+            double lim = ldexp(1.0, e);
+            if (lim > td) lim = td;
+            const double v = t + inc;
+            if (v < lim) {
+                delta = v - t;                // exact (same binade)
+                const double rem = inc - delta;
+                const bool tie = fabs(rem) == ldexp(1.0, e - 54);
+                const uint64_t tb = __builtin_bit_cast(uint64_t, t);
+                if (!tie || (tb & 1u) == 0) {  // t's last mantissa bit (t normal): even
+                    const double span = lim - t;  // exact
+#if defined(__HIP_DEVICE_COMPILE__)
+                    const double qa = span * __builtin_amdgcn_rcp(delta);
+#else
+                    const double qa = span / delta;
+#endif
+                    // (int)qa is kmax - 1, kmax or kmax + 1 (qa within 2^-20 relative of q < 2^31):
+                    // one exact test each way, branch-free
+                    int k = (int)qa;
+                    k -= fma((double)k, delta, -span) >= 0.0 ? 1 : 0;
+                    k += fma((double)(k + 1), delta, -span) < 0.0 ? 1 : 0;
+                    const int left = B - i - 1;
+                    run = 1 + (k < left ? k : left);
                 }
             }
         }

@@ -250,6 +250,38 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
     // RaceCar ag's box (its opponents' vertices for the hand-off mask), loaded with the prologue
     const float box_len = HMASK ? (float)a.pa[ag].length : 0.0f, box_wid = HMASK ? (float)a.pa[ag].width : 0.0f;
     if (a.heavy_build) build_heavy_list(a, g, valid);  // block-uniform branch, before any return
+    // an LDS copy of cr_sincos's table (sin / cos of i/64): every sincos of the car's update reads it
+    // there (a short dependent load instead of a trip to L1 / L2); the loads go out with the prologue's
+    __shared__ double sct[256];  // F110_SINCOS_TAB_N x 4 doubles, padded to 4 per thread
+    {
+        static_assert(F110_SINCOS_TAB_N * 4 <= 256, "the LDS copy holds the table");
+        constexpr int NT = F110_SINCOS_TAB_N * 4;
+        const double *src = &kSinCosTab[0][0];
+        double v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = (int)threadIdx.x + 64 * i;
+            v[i] = src[k < NT ? k : NT - 1];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sct[threadIdx.x + 64 * i] = v[i];
+        __syncthreads();
+    }
+    const double(*tab)[4] = reinterpret_cast<const double(*)[4]>(sct);
+#ifdef F110_AGENTS_PHASES  // timing build (scripts/agents_phases.py): counters 8-12 = s_memrealtime ticks per phase
+    // and wave, summed (prologue + reset, update_pose, scan pose + first lookup, beam runs: 8-11), 13 = waves
+    uint64_t tph = __builtin_amdgcn_s_memrealtime();
+    auto aphase = [&](int k) {
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        if ((threadIdx.x & 63) == 0)
+            atomicAdd(a.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride + 8 + k, (unsigned long long)(t - tph));
+        tph = t;
+        __builtin_amdgcn_sched_barrier(0);
+    };
+#else
+    auto aphase = [](int) {};
+#endif
     // the car's update (its returns leave the lambda: the hand-off poses below need every thread)
     int do_reset = 0;
     bool act = false;
@@ -266,14 +298,16 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
     // the reference's NaN)
     const bool no_offset = a.lidar_dist == 0.0 && isfinite(s[4]);
     double sy4 = 0.0, cy4 = 1.0;
-    if (!no_offset) cr_sincos(s[4], sy4, cy4);
+    if (!no_offset) cr_sincos(s[4], sy4, cy4, tab);
     const double sx = no_offset ? s[0] + 0.0 : s[0] + a.lidar_dist * cy4;
     const double sy = no_offset ? s[1] + 0.0 : s[1] + a.lidar_dist * sy4;
     a.ray0[g] = sx;
     a.ray0[EA + g] = sy;
     a.ray0[2 * EA + g] = a.map.dt[cell_index(a.map, sx, sy)];  // first lookup (laser_models.py:129)
+    aphase(2);
     double t0 = first_theta_index(s[4], a.fov, a.theta_dis);
-    a.nruns[g] = build_beam_runs(t0, a.inc, a.theta_dis, a.B, a.runs + (size_t)g * kMaxSeg, kMaxSeg);
+    a.nruns[g] = build_beam_runs_fast(t0, a.inc, a.theta_dis, a.B, a.runs + (size_t)g * kMaxSeg, kMaxSeg);
+    aphase(3);
     a.ttc_hit[g] = 0;
     if (ag == 0) {
         a.reset_flag[e] = (uint8_t)do_reset;
@@ -325,7 +359,7 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
                 a.start_rot[a.E + e] = (double)np_sincosf(nt, false);
             } else {
                 double sr, crr;
-                cr_sincos(-pth, sr, crr);
+                cr_sincos(-pth, sr, crr, tab);
                 a.start_rot[e] = crr;
                 a.start_rot[a.E + e] = sr;
             }
@@ -335,11 +369,16 @@ __global__ void __launch_bounds__(64) k_agents(StepArgs a) {
         a.lap_times[g] = 0.0f;
         a.lap_counts[g] = 0.0f;
     }
-    update_pose(s, b0, b1, cnt, raw_steer, vel, a.pa[ag], a.dt, a.integrator);  // RaceCar.params (per agent)
+    aphase(0);
+    update_pose(s, b0, b1, cnt, raw_steer, vel, a.pa[ag], a.dt, a.integrator, tab);  // RaceCar.params (per agent)
+    aphase(1);
     act = true;
     if (!HMASK) tail();
     };
     car();
+#ifdef F110_AGENTS_PHASES
+    if ((threadIdx.x & 63) == 0) atomicAdd(a.ctr + (size_t)(blockIdx.x % kCtrSlots) * kCtrStride + 13, 1ull);
+#endif
     if (HMASK) {
         // the hand-off mask's poses (every car of the block, the new or the unchanged ones), shared
         // before the state stores so that the barrier waits on no memory operation

@@ -147,6 +147,9 @@ F110_API void f110_host_tables(int32_t theta_dis, int32_t n_beams, double fov, c
  * use.  Returns the number of runs (>0) or a negative error. */
 F110_API int f110_host_beam_indices(double yaw, double fov, int32_t theta_dis, int32_t n_beams,
                                     double *theta_index_out);
+/* 1 when k_agents' run builder (build_beam_runs_fast) gives the same runs as
+ * build_beam_runs at yaw, 0 when not, < 0 on error (host). */
+F110_API int f110_host_beam_runs_agree(double yaw, double fov, int32_t theta_dis, int32_t n_beams);
 
 /* xy_2_rc's cell (laser_models.py:55-104) for n points xy [n][2] on an H x W
  * map, through the three device mappings: lin_out[n][3] = row-major index

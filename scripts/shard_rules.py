@@ -48,6 +48,8 @@ def main():
             if E % S:
                 continue
             kw = dict(n_agents=A, device=dev, seed=12345, noise_std=0.01, autoreset=True, spawn_poses=spawn)
+            if os.environ.get("SR_INTEGRATOR"):  # 1: RK4, 2: Euler (probe of k_agents' share of a small shard's step)
+                kw["integrator"] = int(os.environ["SR_INTEGRATOR"])
             runs = {}
             for lanes, refill in choices:
                 name = f"lanes{lanes}_refill{refill}" if lanes else f"shared_refill{refill}"

@@ -120,6 +120,17 @@ def test_beam_index_runs_other_configs(L, fov, td, nb):
         assert np.array_equal(out, _seq_indices(y, fov, td, nb))
 
 
+@pytest.mark.parametrize("fov,td,nb", [(4.7, 2000, 1080), (6.2, 2000, 1080), (3.14159, 2000, 271),
+                                       (4.7, 1000, 1080), (0.5, 2000, 64), (4.7, 4096, 2160), (6.28, 360, 3),
+                                       (4.7, 3, 1080), (1.0, 7, 1081)])
+def test_beam_runs_fast_builder_agrees(L, fov, td, nb):
+    """k_agents' run builder (approximate quotient + exact fixups) gives build_beam_runs' runs."""
+    rng = np.random.default_rng(2)
+    yaws = np.concatenate([rng.uniform(-20, 20, 2000), np.linspace(-np.pi, np.pi, 501), [0.0, 2.35, -2.35, 1e-300]])
+    for y in yaws:
+        assert L.f110_host_beam_runs_agree(float(y), fov, td, nb) == 1, (y, fov, td, nb)
+
+
 def test_create_validates_without_gpu(L):
     """No GPU here: f110_create must fail loudly (no CPU fallback)."""
     from f110_gymnasium_ros2_jazzy_amd import _lib
