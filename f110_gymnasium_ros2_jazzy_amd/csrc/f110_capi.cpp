@@ -984,6 +984,10 @@ extern "C" void f110_host_sincos(const double *x, int64_t n, double *sn, double 
     for (int64_t i = 0; i < n; ++i) cr_sincos(x[i], sn[i], cs[i]);
 }
 
+extern "C" void f110_host_sincos_fast(const double *x, int64_t n, double *sn, double *cs, uint8_t *ok) {
+    for (int64_t i = 0; i < n; ++i) ok[i] = cr_sincos_fast(x[i], sn[i], cs[i]) ? 1 : 0;
+}
+
 extern "C" void f110_host_sincos_series(const double *x, int64_t n, double *sn, double *cs) {
     for (int64_t i = 0; i < n; ++i) cr_sincos_series(x[i], sn[i], cs[i]);
 }

@@ -152,9 +152,12 @@ constexpr double kSinCosTab[F110_SINCOS_TAB_N][4] = {F110_SINCOS_TAB_DATA};
 // series path (about 0.1 % of the values).  Where it returns true the result
 // is the one sincos_series gives (both round the same certain value), which
 // tests/test_host_lib.py checks over a few million arguments.
-F110_HD bool sincos_table(DD r, double &s, double &c, const double (*tab)[4] = kSinCosTab) {
+// The table path without a branch: returns whether the rounding is certain (s, c are then the
+// correctly rounded values).  |r.h| >= 1 (not a reduced argument) reads entry 0 and returns garbage.
+F110_HD bool sincos_table_nb(DD r, double &s, double &c, const double (*tab)[4]) {
     const bool neg = r.h < 0.0;
-    const double ah = fabs(r.h), al = neg ? -r.l : r.l;
+    const double ah0 = fabs(r.h), al = neg ? -r.l : r.l;
+    const double ah = ah0 < 1.0 ? ah0 : 0.0;  // (NaN too) keeps the index in the table
     const int i = (int)rint(ah * 64.0);
     const double *T = tab[i];
     const double th = ah - (double)i * 0.015625;  // exact (Sterbenz)
@@ -184,14 +187,51 @@ F110_HD bool sincos_table(DD r, double &s, double &c, const double (*tab)[4] = k
     const double es = fabs(sa.h) * 0x1p-64, ec = 0x1p-64;  // |cos a| > 0.7
     const double s_up = sa.h + (sl + es), s_dn = sa.h + (sl - es);
     const double c_up = ca.h + (cl2 + ec), c_dn = ca.h + (cl2 - ec);
-    if (s_up != s_dn || c_up != c_dn) return false;
     s = neg ? -s_up : s_up;
     c = c_up;
+    return (s_up == s_dn) & (c_up == c_dn);
+}
+
+F110_HD bool sincos_table(DD r, double &s, double &c, const double (*tab)[4] = kSinCosTab) {
+    double s2, c2;
+    if (!sincos_table_nb(r, s2, c2, tab)) return false;
+    s = s2;
+    c = c2;
     return true;
 }
 
-// tab: kSinCosTab or a copy of it (k_agents reads an LDS copy: one short dependent load per call)
+// cr_sincos's common case without a branch: the reduction, the table path and the quadrant as
+// selects, +-0 included.  Returns false where cr_sincos takes another path (|x| >= 2^20, NaN, an
+// uncertain rounding); where it returns true sn / cs are cr_sincos's values.  Straight-line code,
+// so independent evaluations (and the arithmetic around them) can overlap; the caller runs
+// cr_sincos itself on false, after the rest of its work.
+F110_HD bool cr_sincos_fast(double x, double &sn, double &cs, const double (*tab)[4] = kSinCosTab) {
+    const bool in = fabs(x) < 1048576.0;
+    double k;
+    const DD r = sincos_reduce(in ? x : 1.0, k);
+    double s, c;
+    const bool cert = sincos_table_nb(r, s, c, tab);
+    const int q = (int)((int64_t)k & 3);
+    const double a = q == 0 ? s : q == 1 ? c : q == 2 ? -s : -c;
+    const double b = q == 0 ? c : q == 1 ? -s : q == 2 ? -c : s;
+    const bool zero = x == 0.0;
+    sn = zero ? x : a;
+    cs = zero ? 1.0 : b;
+    return zero | (cert & in);
+}
+
+// tab: kSinCosTab or a copy of it (k_agents reads an LDS copy: one short dependent load per call).
+// The branch-free common case inline, the rest (library calls, the series) out of line: one copy
+// of it per kernel instead of one per call site (k_agents' code is read once per wave from L2).
+__host__ __device__ __attribute__((noinline)) inline void cr_sincos_slow(double x, double &sn, double &cs,
+                                                                          const double (*tab)[4]);
+
 F110_HD void cr_sincos(double x, double &sn, double &cs, const double (*tab)[4] = kSinCosTab) {
+    if (!cr_sincos_fast(x, sn, cs, tab)) cr_sincos_slow(x, sn, cs, tab);
+}
+
+__host__ __device__ __attribute__((noinline)) inline void cr_sincos_slow(double x, double &sn, double &cs,
+                                                                          const double (*tab)[4]) {
     if (!(fabs(x) < 1048576.0)) {  // NaN, inf, or beyond the exact reduction
         sn = sin(x);
         cs = cos(x);
@@ -284,9 +324,10 @@ F110_HD void vehicle_dynamics_ks(const double x[5], double u0_in, double u1_in, 
 }
 
 // vehicle_dynamics_st, dynamic_models.py:123-176 (KS branch :152-160 via
-// vehicle_dynamics_ks :90-121).  Python's left-to-right order kept.
-F110_HD void vehicle_dynamics_st(const double x[7], double u0_in, double u1_in, const f110_params &p,
-                                 double f[7], const double (*tab)[4] = kSinCosTab) {
+// vehicle_dynamics_ks :90-121).  Python's left-to-right order kept.  tn, c2: tan(x[2]) and
+// cr_cos(x[2]), the kinematic model's (the caller may have them already, see update_pose_impl).
+F110_HD void vehicle_dynamics_st_tc(const double x[7], double u0_in, double u1_in, const f110_params &p,
+                                    double f[7], const double (*tab)[4], double tn, double c2) {
     const double mu = p.mu, C_Sf = p.C_Sf, C_Sr = p.C_Sr, lf = p.lf, lr = p.lr, h = p.h, m = p.m, I = p.I;
     double u0 = steering_constraint(x[2], u0_in, p.s_min, p.s_max, p.sv_min, p.sv_max);
     double u1 = accl_constraints(x[3], u1_in, p.v_switch, p.a_max, p.v_min, p.v_max);
@@ -297,14 +338,13 @@ F110_HD void vehicle_dynamics_st(const double x[7], double u0_in, double u1_in, 
     // sum (this launch is latency-bound: one wave per SIMD).  f[0], f[1] take
     // one sincos of the car's own angle (the yaw, or yaw + slip).
     const bool kinematic = fabs(x[3]) < 0.5;
+    const double ang = kinematic ? x[4] : x[6] + x[4];
     double sy, cy;
-    cr_sincos(kinematic ? x[4] : x[6] + x[4], sy, cy, tab);
+    const bool sc_ok = cr_sincos_fast(ang, sy, cy, tab);  // (cr_sincos below when not certain)
     // kinematic (vehicle_dynamics_ks re-applies the (idempotent) constraints to u)
     const double lwb = lf + lr;
     const double k0 = steering_constraint(x[2], u0, p.s_min, p.s_max, p.sv_min, p.sv_max);
     const double k1 = accl_constraints(x[3], u1, p.v_switch, p.a_max, p.v_min, p.v_max);
-    const double tn = tan(x[2]);
-    const double c2 = cr_cos(x[2], tab);
     const double kf4 = x[3] / lwb * tn;
     const double kf5 = u1 / lwb * tn + x[3] / (lwb * (c2 * c2)) * u0;
     // single track
@@ -317,6 +357,7 @@ F110_HD void vehicle_dynamics_st(const double x[7], double u0_in, double u1_in, 
     const double s1 = (mu / (x[3] * x[3] * lrlf) * (C_Sr * glf_p * lr - C_Sf * glr_m * lf) - 1) * x[5];
     const double s2 = mu / (x[3] * lrlf) * (C_Sr * glf_p + C_Sf * glr_m) * x[6];
     const double s3 = mu / (x[3] * lrlf) * (C_Sf * glr_m) * x[2];
+    if (!sc_ok) cr_sincos(ang, sy, cy, tab);  // rare: after the independent work above
     f[0] = x[3] * cy;
     f[1] = x[3] * sy;
     f[2] = kinematic ? k0 : u0;
@@ -324,6 +365,47 @@ F110_HD void vehicle_dynamics_st(const double x[7], double u0_in, double u1_in, 
     f[4] = kinematic ? kf4 : x[5];
     f[5] = kinematic ? kf5 : t1 + t2 + t3;
     f[6] = kinematic ? 0.0 : s1 - s2 + s3;
+}
+
+F110_HD void vehicle_dynamics_st(const double x[7], double u0_in, double u1_in, const f110_params &p,
+                                 double f[7], const double (*tab)[4] = kSinCosTab) {
+    vehicle_dynamics_st_tc(x, u0_in, u1_in, p, f, tab, tan(x[2]), cr_cos(x[2], tab));
+}
+
+// The steering angle and speed of RK4's four stages (xs[2], xs[3] of update_pose_impl) depend
+// only on themselves: f[2] and f[3] are the constrained inputs, and the model choice |v| < 0.5
+// reads the speed.  Their chains are a few compares and products, so they run first, and the
+// kinematic model's tan / cos of the four steering angles -- a stage's largest independent work --
+// are issued together (k_agents is one wave per SIMD: issue- and latency-bound) instead of one
+// pair per stage.  Same operations as vehicle_dynamics_st's, so the same values.
+F110_HD void steer_stage_trig(double s2, double s3, double sv, double accl, const f110_params &p, double dt,
+                              const double (*tab)[4], double tn[4], double c2[4]) {
+    double x2[4], x3[4];
+    x2[0] = s2;
+    x3[0] = s3;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const double u0 = steering_constraint(x2[j], sv, p.s_min, p.s_max, p.sv_min, p.sv_max);
+        const double u1 = accl_constraints(x3[j], accl, p.v_switch, p.a_max, p.v_min, p.v_max);
+        const bool kinematic = fabs(x3[j]) < 0.5;
+        const double k0 = steering_constraint(x2[j], u0, p.s_min, p.s_max, p.sv_min, p.sv_max);
+        const double k1 = accl_constraints(x3[j], u1, p.v_switch, p.a_max, p.v_min, p.v_max);
+        const double f2 = kinematic ? k0 : u0, f3 = kinematic ? k1 : u1;
+        x2[j + 1] = j < 2 ? s2 + dt * (f2 / 2) : s2 + dt * f2;  // the stages' xs = s + dt k/2, s + dt k
+        x3[j + 1] = j < 2 ? s3 + dt * (f3 / 2) : s3 + dt * f3;
+    }
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // the four cos as one straight-line block
+        double sj;
+        ok = ok & cr_sincos_fast(x2[j], sj, c2[j], tab);
+    }
+#pragma unroll 1
+    for (int j = 0; j < 4; ++j) tn[j] = tan(x2[j]);  // (one copy of the library's tan)
+    if (!ok) {  // rare: an uncertain rounding
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c2[j] = cr_cos(x2[j], tab);
+    }
 }
 
 // pid, dynamic_models.py:178-221 (v_min = 1e-8 braking quirk included).
@@ -371,25 +453,22 @@ F110_HD void update_pose_impl(V s, V acc, double &b0, double &b1, int &cnt, doub
         // k1 + 2*k2 + 2*k3 + k4 is summed left to right as the stages come
         // (((k1 + 2k2) + 2k3) + k4: the reference's rounding order), so only
         // one stage's k is live at a time
-        vehicle_dynamics_st(xs, sv, accl, p, k, tab);
+        double tn[4], c2[4];
+        steer_stage_trig(s[2], s[3], sv, accl, p, dt, tab, tn, c2);
+        // the four stages as one loop body (one copy of the model's code: k_agents' instructions are
+        // read from L2 once per wave), the same operations in the same order as written out
+#pragma unroll 1
+        for (int st = 0; st < 4; ++st) {
+            const double tns = st == 0 ? tn[0] : st == 1 ? tn[1] : st == 2 ? tn[2] : tn[3];
+            const double c2s = st == 0 ? c2[0] : st == 1 ? c2[1] : st == 2 ? c2[2] : c2[3];
+            vehicle_dynamics_st_tc(xs, sv, accl, p, k, tab, tns, c2s);
+            if (st == 3) break;
 #pragma unroll
-        for (int i = 0; i < 7; ++i) {
-            acc[i] = k[i];
-            xs[i] = s[i] + dt * (k[i] / 2);
+            for (int i = 0; i < 7; ++i) {
+                acc[i] = st == 0 ? k[i] : acc[i] + 2 * k[i];
+                xs[i] = st < 2 ? s[i] + dt * (k[i] / 2) : s[i] + dt * k[i];
+            }
         }
-        vehicle_dynamics_st(xs, sv, accl, p, k, tab);
-#pragma unroll
-        for (int i = 0; i < 7; ++i) {
-            acc[i] = acc[i] + 2 * k[i];
-            xs[i] = s[i] + dt * (k[i] / 2);
-        }
-        vehicle_dynamics_st(xs, sv, accl, p, k, tab);
-#pragma unroll
-        for (int i = 0; i < 7; ++i) {
-            acc[i] = acc[i] + 2 * k[i];
-            xs[i] = s[i] + dt * k[i];
-        }
-        vehicle_dynamics_st(xs, sv, accl, p, k, tab);
         const double w = dt * (1.0 / 6.0);
 #pragma unroll
         for (int i = 0; i < 7; ++i) s[i] = s[i] + w * (acc[i] + k[i]);

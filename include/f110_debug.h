@@ -149,6 +149,9 @@ F110_API int f110_host_beam_indices(double yaw, double fov, int32_t theta_dis, i
                                     double *theta_index_out);
 /* 1 when k_agents' run builder (build_beam_runs_fast) gives the same runs as
  * build_beam_runs at yaw, 0 when not, < 0 on error (host). */
+/* cr_sincos's branch-free common case (k_agents' dynamics): ok[i] = 1 where it applies, and
+ * there sn / cs are cr_sincos's values (host). */
+F110_API void f110_host_sincos_fast(const double *x, int64_t n, double *sn, double *cs, uint8_t *ok);
 F110_API int f110_host_beam_runs_agree(double yaw, double fov, int32_t theta_dis, int32_t n_beams);
 
 /* xy_2_rc's cell (laser_models.py:55-104) for n points xy [n][2] on an H x W

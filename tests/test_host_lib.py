@@ -131,6 +131,27 @@ def test_beam_runs_fast_builder_agrees(L, fov, td, nb):
         assert L.f110_host_beam_runs_agree(float(y), fov, td, nb) == 1, (y, fov, td, nb)
 
 
+def test_sincos_fast_path_matches_cr_sincos(L):
+    """The branch-free common case of cr_sincos (k_agents) gives cr_sincos's bits wherever it
+    claims to apply, and claims it for almost every argument."""
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.uniform(-8, 8, 400000), rng.uniform(-0.42, 0.42, 200000),
+                        rng.uniform(-3000, 3000, 100000), 10.0 ** rng.uniform(-300, 5.9, 50000),
+                        [0.0, -0.0, np.pi / 4, -np.pi / 4, 1048575.9, 1048576.0, 1e300, np.inf, -np.inf, np.nan,
+                         5e-324, -5e-324]])
+    n = x.size
+    s0, c0 = np.empty(n), np.empty(n)
+    s1, c1 = np.empty(n), np.empty(n)
+    ok = np.zeros(n, np.uint8)
+    L.f110_host_sincos(x.ctypes.data, n, s0.ctypes.data, c0.ctypes.data)
+    L.f110_host_sincos_fast(x.ctypes.data, n, s1.ctypes.data, c1.ctypes.data, ok.ctypes.data)
+    m = ok.astype(bool)
+    assert np.array_equal(s1[m].view(np.uint64), s0[m].view(np.uint64))
+    assert np.array_equal(c1[m].view(np.uint64), c0[m].view(np.uint64))
+    assert not m[-7:-2].any() and m[-12] and m[-11]  # 2^20, 1e300, +-inf, NaN fall back; +-0 do not
+    assert m.mean() > 0.995
+
+
 def test_create_validates_without_gpu(L):
     """No GPU here: f110_create must fail loudly (no CPU fallback)."""
     from f110_gymnasium_ros2_jazzy_amd import _lib
