@@ -1823,10 +1823,15 @@ __global__ void __launch_bounds__(64) k_post_single(StepArgs a) {
     }
     if (a.out.obs) {
         float *o = a.out.obs + (size_t)e * obs_row(a) + a.B;
-        o[0] = (float)stl[0];
-        o[1] = (float)stl[1];
-        o[2] = (float)wrap_angle(yaw);
-        o[3] = col ? 1.0f : 0.0f;
+        const float4 v = make_float4((float)stl[0], (float)stl[1], (float)wrap_angle(yaw), col ? 1.0f : 0.0f);
+        if ((reinterpret_cast<uintptr_t>(o) & 15u) == 0) {  // one 16-byte store (the default obs row is aligned)
+            *reinterpret_cast<float4 *>(o) = v;
+        } else {
+            o[0] = v.x;
+            o[1] = v.y;
+            o[2] = v.z;
+            o[3] = v.w;
+        }
     }
     if (a.out.collisions) a.out.collisions[e] = (uint8_t)col;
     env_epilogue(a, e, stl, 2, &col, do_reset, env, &car);
