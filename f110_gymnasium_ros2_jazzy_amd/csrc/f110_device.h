@@ -46,8 +46,15 @@ F110_HD double pymod(double a, double b) {
     return mod;
 }
 
+// pymod for 0 <= a < b (the yaw wraps' common case): a itself, +0 for a zero of either sign --
+// what fmod and the sign fix-up give there -- without the library's fmod loop.
+F110_HD double pymod_fast(double a, double b) {
+    if (b > 0.0 && a >= 0.0 && a < b) return a == 0.0 ? 0.0 : a;
+    return pymod(a, b);
+}
+
 // F110Env._wrap_angle / update_pose yaw wrap: ((a + pi) % 2pi) - pi.
-F110_HD double wrap_angle(double a) { return pymod(a + kPi, kTwoPi) - kPi; }
+F110_HD double wrap_angle(double a) { return pymod_fast(a + kPi, kTwoPi) - kPi; }
 
 // ------------------------------------------------ correctly rounded sin/cos --
 // The reference's np.sin / np.cos (and Numba's libm calls) are glibc's, which

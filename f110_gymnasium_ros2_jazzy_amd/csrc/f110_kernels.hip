@@ -1743,7 +1743,8 @@ __device__ __forceinline__ void epilogue_load_env(const StepArgs &a, int e, EpiE
     v.ct = a.start_rot[e];  // cos(-th), sin(-th) of the ego start yaw
     v.st = a.start_rot[a.E + e];
     v.nstep = a.noise_step[e];  // written by this step's k_agents
-    v.episode = a.mode == 0 ? a.episode[e] : 0u;
+    const uint32_t ep = a.episode[e];  // (loaded whatever the mode: one round trip with the others)
+    v.episode = a.mode == 0 ? ep : 0u;
 }
 
 // stl: post-TTC state rows of its A agents (x at [i*stride], y at
