@@ -347,7 +347,9 @@ def auto_streams(envs, agents=1):
     in cars (envs x agents).  Round 2, end (k_rays_fxn / k_rays_fxr): 16384 envs
     61.3 / 63.1 M at S = 2 / 4 (fxn), 65.3 M at S = 4 with k_rays_fxr
     (profiles/r02_refill_small/): S = 4 up to 16384 cars.  Round 3 (k_rays_fxs): 32768 envs 76.7 M at
-    S = 2, 78.7 / 75.8 M at S = 4 on two boxes (profiles/r03_ab/e32768_*.json): no change."""
+    S = 2, 78.7 / 75.8 M at S = 4 on two boxes (profiles/r03_ab/e32768_*.json): no change.  Round 6
+    (profiles/r06/shard_rules_streams_large_sizes.jsonl, S = 1 / 2 / 4): 65536 90.4 / 101.9 / 99.0 M,
+    32768 80.2 / 100.0 / 98.3 M, 16384 66.2 / 82.0 / 85.7 M: the rule stands."""
     return 4 if envs * agents <= 16384 else 2
 
 
