@@ -1,5 +1,5 @@
 """A/B of two libf110 builds in one process (GPU box): the current build and
-an alternate one (AB_LIB, e.g. ab_libs/head.so built from the previous
+an alternate one (AB_LIB, e.g. ab_libs/head.so from scripts/build_ab_lib.sh: an earlier
 commit), each loaded once (ctypes, local symbols), their contexts stepped in
 interleaved rounds on the same poses and actions.  Per build and size: the
 per-kernel times of the one-context runner (HIP events on each kernel's own
