@@ -1466,15 +1466,15 @@ __global__ void __launch_bounds__(LDS ? 64 * kFxsWaves : 64, 8) k_rays_fxs(RayAr
     int pnext = wj;       // position of this wave's next chunk in the car's chunk order
     int kinfo = 0;        // lane k < nch: the run holding beam 64 k (one divergent search per car)
     uint32_t srch = 0;    // the search's vector loads past the LDS copy (their wave-level count is the max)
-    if (lane < nch) {
+    if (nr <= kRunsLds) {  // wave-uniform: the LDS copy holds every run; the last run starting at or
+        // before beam 64 lane, by counting (unrolled over the copy: no search loop; lanes >= nch unused)
+        int cnt = 0;
+#pragma unroll
+        for (int j = 1; j < kRunsLds; ++j) cnt += (j < nr && RL[j].start <= lane * 64) ? 1 : 0;
+        kinfo = cnt;
+    } else if (lane < nch) {
         int lo = 0, hi = nr - 1;
-        if (nr <= kRunsLds) {  // wave-uniform: the LDS copy holds every run
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (RL[mid].start <= lane * 64) lo = mid;
-                else hi = mid - 1;
-            }
-        } else {
+        {
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
                 if (RG[mid].start <= lane * 64) lo = mid;
