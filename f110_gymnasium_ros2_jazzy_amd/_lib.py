@@ -68,7 +68,7 @@ INTEGRATOR_EULER = 2
 EXPORTS = [
     "f110_abi_version", "f110_last_error", "f110_default_params", "f110_default_config", "f110_edt_k",
     "f110_create", "f110_destroy", "f110_reset", "f110_step", "f110_get_state", "f110_set_state",
-    "f110_scan_batch", "f110_dynamics_batch", "f110_read_counters", "f110_reset_counters", "f110_debug_read_simt", "f110_debug_set_simt", "f110_debug_set_handoff_check", "f110_debug_profile_stamps", "f110_host_beam_runs_agree", "f110_host_sincos_fast",
+    "f110_scan_batch", "f110_dynamics_batch", "f110_read_counters", "f110_reset_counters", "f110_debug_read_simt", "f110_debug_set_simt", "f110_debug_set_handoff_check", "f110_debug_profile_stamps", "f110_host_beam_runs_agree", "f110_host_sincos_fast", "f110_host_tan_cos_fast",
     "f110_profile_begin", "f110_profile_end", "f110_host_tables", "f110_host_beam_indices",
     "f110_set_scan_noise", "f110_set_params", "f110_host_cell_index", "f110_gap_follow",
     "f110_host_window_ranges", "f110_track_create", "f110_track_destroy", "f110_track_arrays",
@@ -155,6 +155,7 @@ def load(build_if_missing: bool = True):
     L.f110_debug_set_handoff_check.argtypes = [_P, ctypes.c_int32]
     L.f110_host_beam_runs_agree.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int32, ctypes.c_int32]
     L.f110_host_sincos_fast.argtypes = [_P, i64, _P, _P, _P]
+    L.f110_host_tan_cos_fast.argtypes = [_P, i64, _P, _P, _P, _P]
     L.f110_debug_profile_stamps.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]
     L.f110_set_scan_noise.argtypes = [_P, _P]
     L.f110_host_window_ranges.argtypes = [ctypes.c_double, ctypes.c_double, i32, ctypes.c_double, ctypes.c_double,

@@ -984,6 +984,16 @@ extern "C" void f110_host_sincos(const double *x, int64_t n, double *sn, double 
     for (int64_t i = 0; i < n; ++i) cr_sincos(x[i], sn[i], cs[i]);
 }
 
+extern "C" void f110_host_tan_cos_fast(const double *x, int64_t n, double *t, double *c, uint8_t *ok_t,
+                                       uint8_t *ok_c) {
+    for (int64_t i = 0; i < n; ++i) {
+        bool a, b;
+        tan_cos_fast(x[i], kSinCosTab, t[i], c[i], a, b);
+        ok_t[i] = a ? 1 : 0;
+        ok_c[i] = b ? 1 : 0;
+    }
+}
+
 extern "C" void f110_host_sincos_fast(const double *x, int64_t n, double *sn, double *cs, uint8_t *ok) {
     for (int64_t i = 0; i < n; ++i) ok[i] = cr_sincos_fast(x[i], sn[i], cs[i]) ? 1 : 0;
 }

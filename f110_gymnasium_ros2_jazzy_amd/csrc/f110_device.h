@@ -161,7 +161,14 @@ constexpr double kSinCosTab[F110_SINCOS_TAB_N][4] = {F110_SINCOS_TAB_DATA};
 // tests/test_host_lib.py checks over a few million arguments.
 // The table path without a branch: returns whether the rounding is certain (s, c are then the
 // correctly rounded values).  |r.h| >= 1 (not a reduced argument) reads entry 0 and returns garbage.
-F110_HD bool sincos_table_nb(DD r, double &s, double &c, const double (*tab)[4]) {
+// The table path's double-double sin / cos of |r| (before the rounding) and their rounding bounds.
+struct SinCosDD {
+    double sh, sl, ch, cl;           // sin |r| = sh + sl, cos |r| = ch + cl (relative error < ~2^-68)
+    double s_up, s_dn, c_up, c_dn;   // the roundings at +- the error bound: certain where equal
+    bool neg;                        // r < 0
+};
+
+F110_HD SinCosDD sincos_table_core(DD r, const double (*tab)[4]) {
     const bool neg = r.h < 0.0;
     const double ah0 = fabs(r.h), al = neg ? -r.l : r.l;
     const double ah = ah0 < 1.0 ? ah0 : 0.0;  // (NaN too) keeps the index in the table
@@ -194,9 +201,14 @@ F110_HD bool sincos_table_nb(DD r, double &s, double &c, const double (*tab)[4])
     const double es = fabs(sa.h) * 0x1p-64, ec = 0x1p-64;  // |cos a| > 0.7
     const double s_up = sa.h + (sl + es), s_dn = sa.h + (sl - es);
     const double c_up = ca.h + (cl2 + ec), c_dn = ca.h + (cl2 - ec);
-    s = neg ? -s_up : s_up;
-    c = c_up;
-    return (s_up == s_dn) & (c_up == c_dn);
+    return {sa.h, sl, ca.h, cl2, s_up, s_dn, c_up, c_dn, neg};
+}
+
+F110_HD bool sincos_table_nb(DD r, double &s, double &c, const double (*tab)[4]) {
+    const SinCosDD v = sincos_table_core(r, tab);
+    s = v.neg ? -v.s_up : v.s_up;
+    c = v.c_up;
+    return (v.s_up == v.s_dn) & (v.c_up == v.c_dn);
 }
 
 F110_HD bool sincos_table(DD r, double &s, double &c, const double (*tab)[4] = kSinCosTab) {
@@ -225,6 +237,42 @@ F110_HD bool cr_sincos_fast(double x, double &sn, double &cs, const double (*tab
     sn = zero ? x : a;
     cs = zero ? 1.0 : b;
     return zero | (cert & in);
+}
+
+// tan x and cos x from one table evaluation (the kinematic model's pair, vehicle_dynamics_st).
+// cos: cr_sincos's value where ok_c.  tan: sin / cos in double-double, rounded once at a 2^-64
+// relative bound -- the correctly rounded tan where ok_t (glibc's tan, which the reference's
+// Numba code calls, is correctly rounded on all but ~0.4 % of arguments; the device library's
+// differs more often).  Where a flag is false the caller takes cr_cos / the library tan.
+F110_HD void tan_cos_fast(double x, const double (*tab)[4], double &t, double &c, bool &ok_t, bool &ok_c) {
+    const bool in = fabs(x) < 1048576.0;
+    double k;
+    const DD r = sincos_reduce(in ? x : 1.0, k);
+    const SinCosDD v = sincos_table_core(r, tab);
+    const int q = (int)((int64_t)k & 3);
+    const double s_r = v.neg ? -v.s_up : v.s_up, c_r = v.c_up;
+    const bool s_ok = v.s_up == v.s_dn, c_ok = v.c_up == v.c_dn;
+    const bool zero = x == 0.0;
+    const double cq = q == 0 ? c_r : q == 1 ? -s_r : q == 2 ? -c_r : s_r;  // cos(r + q pi/2)
+    c = zero ? 1.0 : cq;
+    ok_c = zero | (in & ((q & 1) ? s_ok : c_ok));
+    // tan(r + q pi/2) = sin r / cos r (q even), -cos r / sin r (q odd)
+    // (the table path's low parts carry the t^3 / t^2 terms: up to ~2^-22 of the high parts, so both
+    // are renormalised before the division, whose correction divides by the high part only)
+    const DD Sn = dd_fast(v.neg ? -v.sh : v.sh, v.neg ? -v.sl : v.sl), Cn = dd_fast(v.ch, v.cl);
+    const double nh = (q & 1) ? Cn.h : Sn.h, nl = (q & 1) ? Cn.l : Sn.l;
+    const double dh = (q & 1) ? Sn.h : Cn.h, dl = (q & 1) ? Sn.l : Cn.l;
+    const double q0 = nh / dh;
+    const double rr = (fma(-q0, dh, nh) + nl) - q0 * dl;  // N - q0 D (the product's error exact)
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double q1 = rr * __builtin_amdgcn_rcp(dh);  // a correction below an ulp of q0: a rough quotient
+#else
+    const double q1 = rr / dh;
+#endif
+    const double et = fabs(q0) * 0x1p-64;
+    const double t_up = q0 + (q1 + et), t_dn = q0 + (q1 - et);
+    t = zero ? x : ((q & 1) ? -t_up : t_up);
+    ok_t = zero | (in & (t_up == t_dn) & (dh != 0.0));
 }
 
 // tab: kSinCosTab or a copy of it (k_agents reads an LDS copy: one short dependent load per call).
@@ -327,7 +375,11 @@ F110_HD void vehicle_dynamics_ks(const double x[5], double u0_in, double u1_in, 
     f[1] = x[3] * s4;
     f[2] = u0;
     f[3] = u1;
-    f[4] = x[3] / lwb * tan(x[2]);
+    double tn, c2;
+    bool ok_t, ok_c;
+    tan_cos_fast(x[2], kSinCosTab, tn, c2, ok_t, ok_c);
+    if (!ok_t) tn = tan(x[2]);
+    f[4] = x[3] / lwb * tn;
 }
 
 // vehicle_dynamics_st, dynamic_models.py:123-176 (KS branch :152-160 via
@@ -376,7 +428,12 @@ F110_HD void vehicle_dynamics_st_tc(const double x[7], double u0_in, double u1_i
 
 F110_HD void vehicle_dynamics_st(const double x[7], double u0_in, double u1_in, const f110_params &p,
                                  double f[7], const double (*tab)[4] = kSinCosTab) {
-    vehicle_dynamics_st_tc(x, u0_in, u1_in, p, f, tab, tan(x[2]), cr_cos(x[2], tab));
+    double tn, c2;
+    bool ok_t, ok_c;
+    tan_cos_fast(x[2], tab, tn, c2, ok_t, ok_c);
+    if (!ok_t) tn = tan(x[2]);
+    if (!ok_c) c2 = cr_cos(x[2], tab);
+    vehicle_dynamics_st_tc(x, u0_in, u1_in, p, f, tab, tn, c2);
 }
 
 // The steering angle and speed of RK4's four stages (xs[2], xs[3] of update_pose_impl) depend
@@ -401,17 +458,18 @@ F110_HD void steer_stage_trig(double s2, double s3, double sv, double accl, cons
         x2[j + 1] = j < 2 ? s2 + dt * (f2 / 2) : s2 + dt * f2;  // the stages' xs = s + dt k/2, s + dt k
         x3[j + 1] = j < 2 ? s3 + dt * (f3 / 2) : s3 + dt * f3;
     }
-    bool ok = true;
+    bool okt[4], okc[4], ok = true;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {  // the four cos as one straight-line block
-        double sj;
-        ok = ok & cr_sincos_fast(x2[j], sj, c2[j], tab);
+    for (int j = 0; j < 4; ++j) {  // the four (tan, cos) as one straight-line block
+        tan_cos_fast(x2[j], tab, tn[j], c2[j], okt[j], okc[j]);
+        ok = ok & okt[j] & okc[j];
     }
-#pragma unroll 1
-    for (int j = 0; j < 4; ++j) tn[j] = tan(x2[j]);  // (one copy of the library's tan)
     if (!ok) {  // rare: an uncertain rounding
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c2[j] = cr_cos(x2[j], tab);
+#pragma unroll 1
+        for (int j = 0; j < 4; ++j) {
+            if (!okt[j]) tn[j] = tan(x2[j]);
+            if (!okc[j]) c2[j] = cr_cos(x2[j], tab);
+        }
     }
 }
 

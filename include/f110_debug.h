@@ -152,6 +152,9 @@ F110_API int f110_host_beam_indices(double yaw, double fov, int32_t theta_dis, i
 /* cr_sincos's branch-free common case (k_agents' dynamics): ok[i] = 1 where it applies, and
  * there sn / cs are cr_sincos's values (host). */
 F110_API void f110_host_sincos_fast(const double *x, int64_t n, double *sn, double *cs, uint8_t *ok);
+/* The kinematic model's (tan, cos) from one table evaluation: where ok_t the correctly rounded
+ * tan, where ok_c cr_sincos's cos (host). */
+F110_API void f110_host_tan_cos_fast(const double *x, int64_t n, double *t, double *c, uint8_t *ok_t, uint8_t *ok_c);
 F110_API int f110_host_beam_runs_agree(double yaw, double fov, int32_t theta_dis, int32_t n_beams);
 
 /* xy_2_rc's cell (laser_models.py:55-104) for n points xy [n][2] on an H x W

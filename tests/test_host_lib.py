@@ -152,6 +152,47 @@ def test_sincos_fast_path_matches_cr_sincos(L):
     assert m.mean() > 0.995
 
 
+def _tan_cr(x):
+    """tan(x) correctly rounded to double: 40-digit sin / cos series (|x| < 3.2)."""
+    from decimal import Decimal, getcontext
+    getcontext().prec = 40
+    d = Decimal(float(x))  # exact
+    s, c, term, k = Decimal(0), Decimal(0), Decimal(1), 0
+    while True:  # term = x^k / k!
+        if k % 4 == 0: c += term
+        elif k % 4 == 1: s += term
+        elif k % 4 == 2: c -= term
+        else: s -= term
+        k += 1
+        term = term * d / k
+        if abs(term) < Decimal(10) ** -38:
+            break
+    return float(s / c)
+
+
+def test_tan_cos_fast_is_correctly_rounded(L):
+    """k_agents' tan (one table evaluation with the cos): the correctly rounded tan where it
+    claims certainty, cr_sincos's cos where it claims that, both for nearly every argument."""
+    rng = np.random.default_rng(4)
+    x = np.concatenate([rng.uniform(-0.42, 0.42, 3000), rng.uniform(-3.1, 3.1, 1000), 10.0 ** rng.uniform(-12, -1, 300),
+                        [0.0, -0.0, 0.4189, -0.4189, 1.0, np.pi / 4]])
+    n = x.size
+    t, c = np.empty(n), np.empty(n)
+    okt, okc = np.zeros(n, np.uint8), np.zeros(n, np.uint8)
+    L.f110_host_tan_cos_fast(x.ctypes.data, n, t.ctypes.data, c.ctypes.data, okt.ctypes.data, okc.ctypes.data)
+    s0, c0 = np.empty(n), np.empty(n)
+    L.f110_host_sincos(x.ctypes.data, n, s0.ctypes.data, c0.ctypes.data)
+    mc = okc.astype(bool)
+    assert np.array_equal(c[mc].view(np.uint64), c0[mc].view(np.uint64))
+    mt = okt.astype(bool)
+    assert mt.mean() > 0.99 and mc.mean() > 0.99
+    ref = np.array([_tan_cr(v) if v != 0.0 else v for v in x[mt]])  # tan(+-0) = +-0
+    assert np.array_equal(t[mt].view(np.uint64), ref.view(np.uint64))
+    assert np.signbit(t[-5]) and not np.signbit(t[-6])  # tan(-0) = -0
+    # the reference's libm tan agrees on all but a fraction of a percent
+    assert np.mean(t[mt] != np.tan(x[mt])) < 0.01
+
+
 def test_create_validates_without_gpu(L):
     """No GPU here: f110_create must fail loudly (no CPU fallback)."""
     from f110_gymnasium_ros2_jazzy_amd import _lib
