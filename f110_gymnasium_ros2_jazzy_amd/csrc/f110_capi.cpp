@@ -631,6 +631,9 @@ extern "C" int f110_create(f110_ctx **out, int32_t device, const f110_config *cf
         return fail(F110_E_INVALID, "f110_create: map too large (the EDT tables are addressed by 32-bit byte offsets)");
     if (!(C.fov > 0) || !(C.fov < 2 * kPi))
         return fail(F110_E_INVALID, "f110_create: fov must be in (0, 2*pi) (one index wrap per scan)");
+    if (max_beam_runs((double)C.theta_dis * (C.fov / (double)(C.n_beams - 1)) / (2. * kPi), C.theta_dis) > kMaxSeg)
+        return fail(F110_E_INVALID, "f110_create: theta_dis / (fov / n_beams) too large for the beam-index runs "
+                                    "(f110_device.h max_beam_runs <= 80)");
     if (C.ego_idx < 0 || C.ego_idx >= C.n_agents) return fail(F110_E_INVALID, "f110_create: bad ego_idx");
     if (C.integrator != F110_INTEGRATOR_RK4 && C.integrator != F110_INTEGRATOR_EULER)
         return fail(F110_E_INVALID, "f110_create: Invalid Integrator Specified (base_classes.py:399)");

@@ -735,7 +735,12 @@ __device__ __forceinline__ double tiled_lookup(const TiledMapView &m, double x, 
 // wraps.  A run {start, count, t0, delta} holds t_{start+k} = t0 + k*delta
 // (exact in fp64).  Ties (inc exactly half-way on the u grid) round to even:
 // once t/u is even the increment is constant again, so an odd start is one
-// single step.  Bound for fov < 2*pi (one wrap): < 80 runs.
+// single step.  t = 0 and t below kRunTMin (where the ulp grid and the tie
+// test's half-ulp reach the subnormals) are single-beam runs.  Runs per scan:
+// at most two per binade the indices pass through (a tie's odd start), over
+// the binades from inc to theta_dis (twice: before and after the one wrap of
+// fov < 2*pi), plus the wrapped start's own binade: max_beam_runs() bounds it
+// and f110_create rejects a scan configuration whose bound exceeds kMaxSeg.
 struct BeamRun {
     int32_t start, count;
     double t0, delta;
@@ -749,6 +754,19 @@ F110_HD double first_theta_index(double yaw, double fov, int theta_dis) {
     return t;
 }
 
+constexpr double kRunTMin = 0x1p-960;
+
+// Upper bound of build_beam_runs' count for any yaw: per part (before and after the wrap)
+// two runs per binade from the one holding inc up to theta_dis, one for a start below inc
+// and one at the wrap.
+inline int max_beam_runs(double inc, int theta_dis) {
+    int e_inc, e_td;
+    frexp(inc, &e_inc);
+    frexp((double)theta_dis, &e_td);
+    const int binades = e_td - e_inc + 1;
+    return 2 * (2 * binades + 2);
+}
+
 // Returns the number of runs written, or -1 if max_runs is too small.
 F110_HD int build_beam_runs(double t, double inc, int theta_dis, int B, BeamRun *runs, int max_runs) {
     const double td = (double)theta_dis;
@@ -757,7 +775,7 @@ F110_HD int build_beam_runs(double t, double inc, int theta_dis, int B, BeamRun 
         if (n >= max_runs) return -1;
         int run = 1;
         double delta = 0.0;
-        if (t >= 1.0 && t < td) {
+        if (t >= kRunTMin && t < td) {
             int e;
             frexp(t, &e);  // t in [2^(e-1), 2^e)
             double lim = ldexp(1.0, e);
@@ -811,7 +829,7 @@ F110_HD int build_beam_runs_fast(double t, double inc, int theta_dis, int B, Bea
         if (n >= max_runs) return -1;
         int run = 1;
         double delta = 0.0;
-        if (t >= 1.0 && t < td) {
+        if (t >= kRunTMin && t < td) {
             int e;
             frexp(t, &e);  // t in [2^(e-1), 2^e)
             double lim = ldexp(1.0, e);
@@ -829,9 +847,10 @@ F110_HD int build_beam_runs_fast(double t, double inc, int theta_dis, int B, Bea
 #else
                     const double qa = span / delta;
 #endif
-                    // (int)qa is kmax - 1, kmax or kmax + 1 (qa within 2^-20 relative of q < 2^31):
+                    // (int)qa is kmax - 1, kmax or kmax + 1 (qa within 2^-20 relative of q); a
+                    // quotient beyond 2^30 (> B) is clamped there, where kmax > B - i - 1 anyway:
                     // one exact test each way, branch-free
-                    int k = (int)qa;
+                    int k = (int)(qa < 0x1p30 ? qa : 0x1p30);
                     k -= fma((double)k, delta, -span) >= 0.0 ? 1 : 0;
                     k += fma((double)(k + 1), delta, -span) < 0.0 ? 1 : 0;
                     const int left = B - i - 1;

@@ -99,6 +99,64 @@ def test_step_rotated_origin_vs_oracle(rotated, gpu, oracle_mod, monkeypatch, A)
             assert np.array_equal(sc[live], ref[live])
 
 
+@pytest.mark.parametrize("td,B", [(7, 1080), (100, 2048), (3, 333)])
+def test_small_theta_dis_vs_oracle(gpu, tracks, oracle_mod, monkeypatch, td, B):
+    """ScanSimulator2D's theta_dis (laser_models.py:360, the C-ABI's f110_config.theta_dis)
+    small enough that the beam indices spend a large part of the scan below 1: the beam-index
+    runs then cover the binades below 1 (before, every such beam was a run of its own and a
+    scan could exceed the 80-run table).  scan_batch and steps through k_rays_fxs, k_rays_fxn
+    and the tiled kernel (F110_RAY_KERNEL=1) against the oracle scanner with the same
+    theta_dis, poses with yaws all round the circle."""
+    import os
+    from conftest import MAPS
+    from f110_gymnasium_ros2_jazzy_amd import _lib
+    from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns
+    from f110_gymnasium_ros2_jazzy_amd.sim import BatchSim
+    free, res, org = oracle_mod.load_map(os.path.join(MAPS, "Spielberg_map.yaml"))
+    osc = oracle_mod.OracleScanner(free, res, org, num_beams=B, theta_dis=td)
+    base_cfg = _lib.default_config
+
+    def cfg():
+        c = base_cfg()
+        c.theta_dis = td
+        return c
+    monkeypatch.setattr(_lib, "default_config", cfg)
+    E = 96
+    rng = np.random.default_rng(td)
+    sp = centerline_spawns("Spielberg", 1)
+    poses = sp[rng.integers(0, sp.shape[0], E)].copy()
+    poses[:, 0, 2] = rng.uniform(-np.pi, np.pi, E)
+    acts = np.stack([rng.uniform(-0.4189, 0.4189, (4, E, 1)), rng.uniform(0, 3, (4, E, 1))], -1).astype(np.float32)
+    outs = []
+    for kern, refill in (("3", None), ("3", 0), ("1", None)):
+        monkeypatch.setenv("F110_RAY_KERNEL", kern)
+        sim = BatchSim(tracks("Spielberg_map"), n_envs=E, n_agents=1, device=gpu, noise_std=0.0, num_beams=B,
+                       keep_f64_scans=True)
+        assert sim.cfg.theta_dis == td
+        if refill is not None:
+            sim.set_ray_refill(refill)
+        if kern == "3":
+            assert sim.ray_kernel == 3 and (sim.ray_refill > 0) == (refill is None)
+        got = sim.scan_batch(poses[:, 0]).cpu().numpy()
+        assert np.array_equal(got, osc.scan(poses[:, 0]))
+        rec = [sim.reset(poses).scans_f64.cpu().numpy()[:, 0]]
+        sts = [poses[:, 0].copy()]
+        for t in range(4):
+            o = sim.step(acts[t])
+            rec.append(o.scans_f64.cpu().numpy()[:, 0])
+            st = sim.agent_states().cpu().numpy()[:, 0]
+            sts.append(np.stack([st[:, 0], st[:, 1], st[:, 4]], 1))
+        outs.append(rec)
+        sim.close()
+        for sc, p in zip(rec, sts):
+            live = p[:, 2] != 0  # TTC-collided cars have yaw zeroed after their scan
+            assert live.sum() > E // 2
+            assert np.array_equal(sc[live], osc.scan(p)[live])
+    for rec in outs[1:]:
+        for a, b in zip(outs[0], rec):
+            assert np.array_equal(a, b)
+
+
 def test_scan_batch_random_poses_vs_oracle(sims, oracle_scanners):
     from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns
     sp = centerline_spawns("Spielberg", 1)[:, 0]

@@ -110,11 +110,14 @@ def test_beam_index_runs_spielberg_config(L, oracle_scanners):
 
 
 @pytest.mark.parametrize("fov,td,nb", [(6.2, 2000, 1080), (3.14159, 2000, 271), (4.7, 1000, 1080),
-                                       (0.5, 2000, 64), (4.7, 4096, 2160), (6.28, 360, 3)])
+                                       (0.5, 2000, 64), (4.7, 4096, 2160), (6.28, 360, 3),
+                                       (4.7, 7, 1080), (4.7, 2, 1080), (6.2, 100, 2048), (4.7, 2000, 65536)])
 def test_beam_index_runs_other_configs(L, fov, td, nb):
+    """Runs against the sequential accumulation; small theta_dis (indices below 1 over a large part
+    of the scan) and fine scans included: there the runs cover binades below 1 too."""
     rng = np.random.default_rng(1)
     out = np.empty(nb)
-    for y in rng.uniform(-10, 10, 200):
+    for y in rng.uniform(-10, 10, 200 if nb <= 4096 else 20):
         n = L.f110_host_beam_indices(float(y), fov, td, nb, out.ctypes.data)
         assert 0 < n <= 80
         assert np.array_equal(out, _seq_indices(y, fov, td, nb))
