@@ -326,6 +326,55 @@ def _adversarial_poses(rng, E, A, sp):
     return out
 
 
+@pytest.mark.parametrize("B", [2, 3, 63, 4096])
+@pytest.mark.parametrize("A", [1, 2])
+def test_beam_counts_lockstep_vs_oracle(sims, oracle_mod, A, B):
+    """Scan sizes away from 1080 (ScanSimulator2D(num_beams), laser_models.py:360): two and three
+    beams (one 64-beam chunk, mostly idle), 63, and 4096 (past the fixed-point kernels' 2048: the
+    tiled kernel over 64 chunks), one and two agents with the adversarial opponent poses, 4 steps
+    in lock-step with the oracle: scans and collisions bit-exact against the oracle with the
+    device's correctly rounded sin / cos, within 1e-9 of the glibc one; no hand-off
+    read outside the mask."""
+    import os
+    from conftest import MAPS
+    from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns
+    O = oracle_mod
+    E = 48
+    rng = np.random.default_rng(B * 10 + A)
+    poses = _adversarial_poses(rng, E, A, centerline_spawns("Spielberg", 1))
+    free, res, org = O.load_map(os.path.join(MAPS, "Spielberg_map.yaml"))
+    osc = O.OracleScanner(free, res, org, num_beams=B)
+    sim = sims("Spielberg_map", E, A, num_beams=B)
+    if B > 2048:
+        assert sim.ray_kernel == 1
+    if A > 1:
+        sim.set_handoff_check(1)
+    sim.reset_counters()
+    ref, refd = O.OracleSim(osc, E, A), O.OracleSim(osc, E, A)
+    sim.reset(poses)
+    ref.reset(poses)
+    rs, rc = ref.step(np.zeros((E, A, 2)))
+    with O.device_trig():
+        refd.reset(poses)
+        rd, _ = refd.step(np.zeros((E, A, 2)))
+    for t in range(4):
+        g = sim.out.scans_f64.cpu().numpy()
+        assert g.shape == (E, A, B)
+        assert np.array_equal(g, rd), f"step {t}"
+        np.testing.assert_allclose(g, rs, rtol=1e-9, atol=1e-9)
+        np.testing.assert_array_equal(sim.out.collisions.cpu().numpy(), rc.astype(np.uint8))
+        act = np.stack([rng.uniform(-0.3, 0.3, (E, A)), rng.uniform(0, 5, (E, A))], -1)
+        ref.state[:] = sim.agent_states().cpu().numpy().reshape(E * A, 7)
+        refd.state[:] = ref.state
+        sim.step(act)
+        rs, rc = ref.step(act)
+        with O.device_trig():
+            rd, _ = refd.step(act)
+    if A > 1:
+        assert sim.read_counter(6) == 0, "k_post_multi read hand-off beams outside the mask"
+        sim.set_handoff_check(0)
+
+
 @pytest.mark.parametrize("A", [2, 3])
 def test_agent_ray_cast_adversarial_vs_oracle(sims, oracle_scanners, A, nonexact_budget):
     """Agent ray_cast (base_classes.py:206-227, laser_models.py:318-346) with
