@@ -326,15 +326,19 @@ def _adversarial_poses(rng, E, A, sp):
     return out
 
 
-@pytest.mark.parametrize("B", [2, 3, 63, 4096])
-@pytest.mark.parametrize("A", [1, 2])
-def test_beam_counts_lockstep_vs_oracle(sims, oracle_mod, A, B):
-    """Scan sizes away from 1080 (ScanSimulator2D(num_beams), laser_models.py:360): two and three
-    beams (one 64-beam chunk, mostly idle), 63, and 4096 (past the fixed-point kernels' 2048: the
-    tiled kernel over 64 chunks), one and two agents with the adversarial opponent poses, 4 steps
-    in lock-step with the oracle: scans and collisions bit-exact against the oracle with the
-    device's correctly rounded sin / cos, within 1e-9 of the glibc one; no hand-off
-    read outside the mask."""
+@pytest.mark.parametrize("A,B,fov,ld", [(1, 2, 4.7, 0.0), (1, 3, 4.7, 0.0), (1, 63, 4.7, 0.0), (1, 4096, 4.7, 0.0),
+                                        (2, 2, 4.7, 0.0), (2, 3, 4.7, 0.0), (2, 63, 4.7, 0.0), (2, 4096, 4.7, 0.0),
+                                        (8, 333, 4.7, 0.0), (1, 1080, 4.7, 0.275), (2, 1080, 6.2, 0.275),
+                                        (2, 720, 1.0, -0.1), (1, 256, 0.05, 0.0)])
+def test_beam_counts_lockstep_vs_oracle(sims, oracle_mod, A, B, fov, ld):
+    """Scan configurations away from the default (ScanSimulator2D(num_beams, fov),
+    laser_models.py:360; RaceCar's lidar_dist, base_classes.py:420-422): two and three beams (one
+    64-beam chunk, mostly idle), 63, and 4096 (past the fixed-point kernels' 2048: the tiled
+    kernel over 64 chunks); eight agents; the scan origin ahead of / behind the car; a wide, a
+    narrow and a very narrow fov.  Adversarial opponent poses, 4 steps in lock-step with the
+    oracle: scans and collisions bit-exact against the oracle with the device's correctly
+    rounded sin / cos, within 1e-9 of the glibc one; no hand-off read outside the
+    mask."""
     import os
     from conftest import MAPS
     from f110_gymnasium_ros2_jazzy_amd.maps import centerline_spawns
@@ -343,14 +347,14 @@ def test_beam_counts_lockstep_vs_oracle(sims, oracle_mod, A, B):
     rng = np.random.default_rng(B * 10 + A)
     poses = _adversarial_poses(rng, E, A, centerline_spawns("Spielberg", 1))
     free, res, org = O.load_map(os.path.join(MAPS, "Spielberg_map.yaml"))
-    osc = O.OracleScanner(free, res, org, num_beams=B)
-    sim = sims("Spielberg_map", E, A, num_beams=B)
+    osc = O.OracleScanner(free, res, org, num_beams=B, fov=fov)
+    sim = sims("Spielberg_map", E, A, num_beams=B, fov=fov, lidar_dist=ld)
     if B > 2048:
         assert sim.ray_kernel == 1
     if A > 1:
         sim.set_handoff_check(1)
     sim.reset_counters()
-    ref, refd = O.OracleSim(osc, E, A), O.OracleSim(osc, E, A)
+    ref, refd = O.OracleSim(osc, E, A, lidar_dist=ld), O.OracleSim(osc, E, A, lidar_dist=ld)
     sim.reset(poses)
     ref.reset(poses)
     rs, rc = ref.step(np.zeros((E, A, 2)))
