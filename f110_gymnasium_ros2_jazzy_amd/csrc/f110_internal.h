@@ -287,6 +287,10 @@ struct RewardArgs {
 constexpr int kTieCap = 4096;        // keys equal to the selection threshold kept for the tie break
 constexpr int kReplayMaxGrid = 1024; // blocks of the streaming replay kernels
 constexpr int kReplayMaxBatch = 8192;
+// Copies of the radix select's global histograms: block b adds into copy b % kHistRep (consecutive
+// blocks land on different XCDs), so each bin's device-scope atomics are spread over 8 addresses;
+// the consumer sums the copies.  Layout hist[(copy * 4 + pass) * 256 + bin].
+constexpr int kHistRep = 8;
 
 // Device header of a replay buffer (one per f110_replay).
 struct ReplayHdr {
@@ -301,6 +305,8 @@ struct ReplayHdr {
     uint32_t n_lt, n_tie;  // keys below / equal to the threshold (n_tie zeroed by k_finish)
     uint32_t overflow;  // samples whose tie list overflowed kTieCap
     uint32_t pad_;
+    uint32_t sel_prefix[4], sel_kleft[4];  // the select through digit q (written by the kernel after
+                                           // pass q's histogram, read by the next one)
 };
 
 struct ReplayView {

@@ -17,7 +17,7 @@
 //           numpy's Generator.choice(replace=False, p=...) returns (it draws,
 //           drops repeats in draw order and redraws the rest from the
 //           renormalised p).  The B smallest 32-bit key patterns are found by
-//           a 4-pass radix select (8-bit digits, LDS histograms; each pass's blocks pick the digits so far from the global histograms themselves); ties at the
+//           a 4-pass radix select (8-bit digits, LDS histograms; each pass's blocks pick the last digit from its global histogram, the earlier ones from the header); ties at the
 //           threshold go to the lowest indices; the selection is compacted in
 //           index order (two passes, no sort) and one workgroup computes the
 //           IS weights.  As a set the batch has the distribution of the
@@ -271,39 +271,54 @@ __global__ void __launch_bounds__(kKB) k_keys(ReplayView v, int32_t batch, int v
         for (int w = 0; w < kRB / 64; ++w) tsum += sh[threadIdx.x * (kRB / 64) + w];
         v.den_part[blockIdx.x * Q + threadIdx.x] = tsum;
     }
-    if (threadIdx.x < 256 && hist[threadIdx.x]) atomicAdd(&v.hist[threadIdx.x], hist[threadIdx.x]);
+    if (threadIdx.x < 256 && hist[threadIdx.x])
+        atomicAdd(&v.hist[(blockIdx.x % kHistRep) * 4 * 256 + threadIdx.x], hist[threadIdx.x]);
 }
 
-// The digits of the batch-th smallest key from the histograms of passes
-// 0 .. npass-1 (every block of a consumer computes them itself: no one-block
-// select launch between the passes).  Per pass an inclusive scan of its 256
-// bins; the digit is the bin where the running count reaches kleft.
-__device__ void select_digits(const ReplayView &v, int32_t batch, int npass, uint32_t &prefix, uint32_t &kleft) {
-    __shared__ uint32_t inc[256];
+// Digit q of the batch-th smallest key from pass q's histogram, given the
+// digits before it (prefix) and the rank still to select among the keys that
+// share them (kleft): an inclusive scan of the 256 bins (one bin per thread, a
+// shuffle scan per wave, the waves' totals added in order); the digit is the
+// bin where the running count reaches kleft.  Every block of a consumer
+// computes it itself (no one-block select launch between the passes); block
+// 0 records the result in the header for the next kernel, so each kernel
+// scans one histogram.
+__device__ void select_digit(const ReplayView &v, int q, uint32_t &prefix, uint32_t &kleft) {
+    __shared__ uint32_t wtot[kRB / 64];
     __shared__ uint32_t res[2];
     const int t = threadIdx.x;  // blockDim.x == 256
-    prefix = 0u;
-    kleft = (uint32_t)batch;
-    for (int p = 0; p < npass; ++p) {
-        const int shift = 24 - 8 * p;
-        inc[t] = v.hist[p * 256 + t];
-        __syncthreads();
-        for (int o = 1; o < 256; o <<= 1) {
-            const uint32_t add = t >= o ? inc[t - o] : 0u;
-            __syncthreads();
-            inc[t] += add;
-            __syncthreads();
-        }
-        const uint32_t below = t ? inc[t - 1] : 0u;
-        if (inc[t] >= kleft && below < kleft) {
-            res[0] = prefix | ((uint32_t)t << shift);
-            res[1] = kleft - below;
-        }
-        __syncthreads();
-        prefix = res[0];
-        kleft = res[1];
-        __syncthreads();
+    const int lane = t & 63, wave = t >> 6;
+    uint32_t x = 0;
+#pragma unroll
+    for (int c = 0; c < kHistRep; ++c) x += v.hist[(c * 4 + q) * 256 + t];
+    uint32_t inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
+        inc += lane >= o ? y : 0u;
     }
+    if (lane == 63) wtot[wave] = inc;
+    __syncthreads();
+    for (int w = 0; w < wave; ++w) inc += wtot[w];
+    const uint32_t below = inc - x;
+    if (inc >= kleft && below < kleft) {
+        res[0] = prefix | ((uint32_t)t << (24 - 8 * q));
+        res[1] = kleft - below;
+    }
+    __syncthreads();
+    prefix = res[0];
+    kleft = res[1];
+    if (blockIdx.x == 0 && t == 0) {
+        v.hdr->sel_prefix[q] = prefix;
+        v.hdr->sel_kleft[q] = kleft;
+    }
+}
+
+// The select through digit q - 1, as the previous kernel recorded it (q = 0: none yet).
+__device__ __forceinline__ void select_so_far(const ReplayView &v, int32_t batch, int q, uint32_t &prefix,
+                                              uint32_t &kleft) {
+    prefix = q > 0 ? v.hdr->sel_prefix[q - 1] : 0u;
+    kleft = q > 0 ? v.hdr->sel_kleft[q - 1] : (uint32_t)batch;
 }
 
 // Passes 1..3: histogram of digit `pass` over the keys whose higher digits
@@ -314,7 +329,8 @@ __global__ void __launch_bounds__(kRB) k_hist(ReplayView v, int32_t batch, int p
     if (len < batch) return;
     const int shift = 24 - 8 * pass;
     uint32_t prefix, kleft;
-    select_digits(v, batch, pass, prefix, kleft);
+    select_so_far(v, batch, pass - 1, prefix, kleft);
+    select_digit(v, pass - 1, prefix, kleft);
     const uint32_t want = prefix >> (shift + 8);
     hist[threadIdx.x] = 0;
     __syncthreads();
@@ -323,7 +339,8 @@ __global__ void __launch_bounds__(kRB) k_hist(ReplayView v, int32_t batch, int p
         if ((key >> (shift + 8)) == want) atomicAdd(&hist[(key >> shift) & 255u], 1u);
     }
     __syncthreads();
-    if (hist[threadIdx.x]) atomicAdd(&v.hist[pass * 256 + threadIdx.x], hist[threadIdx.x]);
+    if (hist[threadIdx.x])
+        atomicAdd(&v.hist[((blockIdx.x % kHistRep) * 4 + pass) * 256 + threadIdx.x], hist[threadIdx.x]);
 }
 
 // The selection: every key below the threshold key T, plus the lowest-index
@@ -341,7 +358,8 @@ __global__ void __launch_bounds__(kRB) k_count(ReplayView v, int32_t batch, int 
     const int64_t len = v.hdr->length;
     if (len < batch) return;
     uint32_t T, kleft;
-    select_digits(v, batch, 4, T, kleft);
+    select_so_far(v, batch, 3, T, kleft);
+    select_digit(v, 3, T, kleft);
     if (blockIdx.x == 0) {  // for k_place / k_finish: the threshold, and den (k_keys' partials, fixed order)
         double acc = 0.0;
         for (int k = threadIdx.x; k < n_part; k += kRB) acc += v.den_part[k];
@@ -375,8 +393,9 @@ __global__ void __launch_bounds__(kRB) k_place(ReplayView v, int32_t batch) {
     const int64_t len = v.hdr->length;
     if (len < batch) return;
     const uint32_t T = v.hdr->prefix;
-    if (blockIdx.x == 0)  // the four passes' histograms, consumed: zero for the next sample
-        for (int k = threadIdx.x; k < 4 * 256; k += kRB) v.hist[k] = 0u;
+    // the four passes' histograms (all copies), consumed: zero for the next sample
+    for (int k = (int)blockIdx.x * kRB + (int)threadIdx.x; k < kHistRep * 4 * 256; k += (int)gridDim.x * kRB)
+        v.hist[k] = 0u;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     {  // this block's offset: the counts of the blocks before it
         uint32_t acc = 0;

@@ -70,7 +70,7 @@ extern "C" int f110_replay_create(f110_replay **out, int32_t device, int64_t cap
     if (e == hipSuccess) e = rb->alloc(&v.prio, cap);
     if (e == hipSuccess) e = rb->alloc(&v.wt, cap);
     if (e == hipSuccess) e = rb->alloc(&v.keys, cap);
-    if (e == hipSuccess) e = rb->alloc(&v.hist, 4 * 256);
+    if (e == hipSuccess) e = rb->alloc(&v.hist, (size_t)kHistRep * 4 * 256);
     if (e == hipSuccess) e = rb->alloc(&v.den_part, kReplayMaxGrid);
     if (e == hipSuccess) e = rb->alloc(&v.part, kReplayMaxGrid);
     if (e == hipSuccess) e = rb->alloc(&v.sel, kReplayMaxBatch);
@@ -79,7 +79,7 @@ extern "C" int f110_replay_create(f110_replay **out, int32_t device, int64_t cap
     if (e == hipSuccess) e = hipMemset(v.hdr, 0, sizeof(ReplayHdr));
     if (e == hipSuccess) e = hipMemset(v.prio, 0, cap * sizeof(float));
     if (e == hipSuccess) e = hipMemset(v.wt, 0, cap * sizeof(double));
-    if (e == hipSuccess) e = hipMemset(v.hist, 0, 4 * 256 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(v.hist, 0, (size_t)kHistRep * 4 * 256 * sizeof(uint32_t));
     if (e == hipSuccess) e = prepare_replay(max_batch);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
