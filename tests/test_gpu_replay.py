@@ -245,22 +245,25 @@ def test_learner_graphs_match_eager(gpu):
     torch.testing.assert_close(runs[0][2], runs[1][2], rtol=1e-3, atol=1e-6)
 
 
-def test_flat_adam_matches_torch_adam(gpu):
+@pytest.mark.parametrize("n", [5000, 345_000])
+def test_flat_adam_matches_torch_adam(gpu, n):
     """f110_adam_step over a flat buffer == torch.optim.Adam's single-tensor
     update (agent.py:187-188) on CPU, five steps, float32 tolerance; its fused
-    soft target update == target.lerp_(param, tau) after each step."""
+    soft target update == target.lerp_(param, tau) after each step.  2 blocks,
+    and the critic's size (337 blocks taking tickets: the step counter advances
+    once per launch and the ticket word is re-armed to 0)."""
     import ctypes
     from f110_gymnasium_ros2_jazzy_amd import _lib
     L = _lib.load()
     g = torch.Generator().manual_seed(0)
-    p0 = torch.randn(5000, generator=g)
-    grads = [torch.randn(5000, generator=g) * 10 ** (k - 2) for k in range(5)]
+    p0 = torch.randn(n, generator=g)
+    grads = [torch.randn(n, generator=g) * 10 ** (k - 2) for k in range(5)]
     ref = p0.clone().requires_grad_(True)
     opt = torch.optim.Adam([ref], lr=1e-3)
     dev = p0.cuda()
     m, v = torch.zeros_like(dev), torch.zeros_like(dev)
     state = torch.zeros(2, dtype=torch.int64, device="cuda")
-    tgt_ref = torch.randn(5000, generator=g)
+    tgt_ref = torch.randn(n, generator=g)
     tgt = tgt_ref.cuda()
     vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     for gr in grads:
@@ -271,7 +274,8 @@ def test_flat_adam_matches_torch_adam(gpu):
         gd = gr.cuda()
         _lib.check(L.f110_adam_step(vp(dev), vp(m), vp(v), vp(gd), dev.numel(), 1e-3, 0.9, 0.999, 1e-8, vp(state),
                                     vp(tgt), 0.005, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "adam")
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        assert int(state[1]) == 0
     assert int(state[0]) == 5
     torch.testing.assert_close(tgt.cpu(), tgt_ref, rtol=2e-6, atol=1e-7)
     torch.testing.assert_close(dev.cpu(), ref.detach(), rtol=2e-6, atol=1e-7)
