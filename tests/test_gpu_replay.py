@@ -279,7 +279,9 @@ def test_flat_adam_matches_torch_adam(gpu, n):
     assert int(state[0]) == 5
     torch.testing.assert_close(tgt.cpu(), tgt_ref, rtol=2e-6, atol=1e-7)
     torch.testing.assert_close(dev.cpu(), ref.detach(), rtol=2e-6, atol=1e-7)
-    torch.testing.assert_close(m.cpu(), opt.state[ref]["exp_avg"], rtol=1e-5, atol=1e-7)  # CPU lerp may fuse (1 ulp)
+    # CPU lerp may fuse: an ulp or two of (1 - beta1) * g, which is all of m where m cancels to ~0
+    atol = 4 * torch.finfo(torch.float32).eps * 0.1 * max(float(gr.abs().max()) for gr in grads)
+    torch.testing.assert_close(m.cpu(), opt.state[ref]["exp_avg"], rtol=1e-5, atol=max(atol, 1e-7))
 
 
 def test_replay_add_env_matches_add(gpu):
