@@ -213,7 +213,13 @@ def test_create_validates_without_gpu(L):
     rc = L.f110_create(ctypes.byref(ctx), 0, ctypes.byref(c), ctypes.byref(p), k.ctypes.data, 4, 4, 0.05,
                        origin, None, 0)
     assert rc == -1
-    c.fov = 4.7
+    # a scan so fine against theta_dis that its beam-index runs could overflow the 80-run table
+    # (f110_device.h max_beam_runs): rejected before any device call
+    c.fov, c.theta_dis, c.n_beams = 0.001, 2, 2048
+    rc = L.f110_create(ctypes.byref(ctx), 0, ctypes.byref(c), ctypes.byref(p), k.ctypes.data, 4, 4, 0.05,
+                       origin, None, 0)
+    assert rc == -1 and b"beam-index runs" in L.f110_last_error()
+    c.fov, c.theta_dis, c.n_beams = 4.7, 2000, 1080
     rc = L.f110_create(ctypes.byref(ctx), 0, ctypes.byref(c), ctypes.byref(p), k.ctypes.data, 4, 4, 0.05,
                        origin, None, 0)
     import torch
